@@ -1,0 +1,367 @@
+#!/usr/bin/env python3
+"""Training-throughput benchmark of the station-graph GNN on MI355X.
+
+Metric (BASELINE.json): training graphs/s (+ edges aggregated/s), 24h_mixed config.
+One step = one full training step exactly as train.py:55-74 does it -- DeepSet + dim_red +
+4 GINE layers (HIP engine) + head + PostProcess + MixedLoss + backward + AdamW -- on one
+pre-collated batch resident in HBM.  N=1 runs configs[1] (500-station k=10 graphs, 32 per
+GPU); with N>1 every rank runs its own 32 graphs (weak scaling) and the gradient is
+averaged with one RCCL all-reduce per step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  Per-kernel timings (HIP events on the launch stream) and the
+CPU baseline (oracle, rank 0, N=1 only) are measured in the same process.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "raincast-gnn_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from raincast_gnn import functional as Fn  # noqa: E402
+from raincast_gnn.data import synthetic_batch  # noqa: E402
+from raincast_gnn.distributed import FlatGradReducer, broadcast_parameters, env_rank  # noqa: E402
+from raincast_gnn.graph import get_graph  # noqa: E402
+from raincast_gnn.models import gnn_from_params  # noqa: E402
+from raincast_gnn.params import BENCH_CONFIGS  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix peak (dense)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(BENCH_CONFIGS))
+    ap.add_argument("--no-graph", action="store_true", help="eager steps (no HIP graph)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target duration of the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=50)
+    return ap.parse_args()
+
+
+# -----------------------------------------------------------------------------------------
+# training step
+# -----------------------------------------------------------------------------------------
+class Trainer:
+    def __init__(self, cfg, device, rank, world, graphs_per_rank):
+        self.cfg, self.device, self.world = cfg, device, world
+        params = cfg.params()
+        self.params = params
+        torch.manual_seed(42)
+        self.model = gnn_from_params(params).to(device).train()
+        broadcast_parameters(self.model)
+        self.batch = synthetic_batch(cfg.num_stations, graphs_per_rank, k=cfg.k,
+                                     seed=1000 + rank).to(device)
+        self.reducer = FlatGradReducer(self.model.parameters())
+        self.opt = torch.optim.AdamW(self.model.parameters(), lr=params["lr"], capturable=True,
+                                     foreach=True)
+        self.graph_fb = self.graph_opt = None
+        self.loss = None
+
+    def fwd_bwd(self):
+        self.reducer.zero_()
+        pred = self.model(self.batch)
+        loss = self.model.loss_fn.crps(pred, self.batch.y)
+        loss.backward()
+        return loss
+
+    def eager_step(self):
+        loss = self.fwd_bwd()
+        self.reducer.all_reduce_()
+        self.opt.step()
+        return loss
+
+    def capture(self):
+        """fwd+bwd (+ optimizer when there is no collective) as HIP graphs."""
+        self.graph_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_fb):
+            self.loss = self.fwd_bwd()
+            if self.world == 1:
+                self.opt.step()
+        if self.world > 1:
+            self.graph_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_opt):
+                self.opt.step()
+        assert self.reducer.check_views()
+
+    def step(self):
+        if self.graph_fb is None:
+            return self.eager_step()
+        self.graph_fb.replay()
+        if self.world > 1:
+            self.reducer.all_reduce_()
+            self.graph_opt.replay()
+        return self.loss
+
+
+# -----------------------------------------------------------------------------------------
+# per-kernel timing (HIP events on the stream the kernels are launched on)
+# -----------------------------------------------------------------------------------------
+def time_kernels(tr: Trainer, reps: int):
+    dev = tr.device
+    b = tr.batch
+    conv = tr.model.conv.convolutions[1]
+    N, D = b.num_nodes, tr.params["gnn_hidden"]
+    E = b.edge_index.size(1)
+    g = get_graph(b.edge_index, b.edge_attr.float(), N)
+    torch.manual_seed(0)
+    x = torch.randn(N, D, device=dev)
+    dz = torch.randn(N, D, device=dev)
+    lw = conv.lin.weight.detach().reshape(-1).contiguous()
+    lb = conv.lin.bias.detach().contiguous()
+    ep = conv.eps.detach().contiguous()
+    l1, bn, _, l2 = conv.nn
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    from raincast_gnn._lib import call, ptr
+    P = Fn._count("gine_mlp_num_partials", N, D)
+    partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
+    a1 = torch.empty_like(x)
+    y = torch.empty_like(x)
+    dbn = torch.empty_like(x)
+    mask = torch.empty(N, D, dtype=torch.uint8, device=dev)
+    bn_save = torch.empty(4, D, device=dev)
+    coef = torch.empty(3, D, device=dev)
+    w1, b1, w2, b2 = (t.detach().contiguous() for t in (l1.weight, l1.bias, l2.weight, l2.bias))
+    C = Fn._count("gine_mlp_wgrad_num_chunks", N, D)
+    slab = torch.empty(2 * C * (D * D + D), device=dev)
+    dw1, dw2 = torch.empty(D, D, device=dev), torch.empty(D, D, device=dev)
+    db1, db2 = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    Pm = Fn._count("gine_mp_bwd_num_partials", N, D)
+    mp_part = torch.empty(Pm, 3, D, dtype=torch.float64, device=dev)
+    dx = torch.empty_like(x)
+    z = Fn.mp_forward(x, g, lw, lb, ep)
+    rm = torch.zeros(D, device=dev)
+    rv = torch.ones(D, device=dev)
+    call("gine_mlp_fwd1", ptr(z), ptr(w1), ptr(b1), ptr(a1), ptr(partials), N, D, sh)
+    call("gine_bn_fwd_finalize", ptr(partials), P, ptr(bn.weight), ptr(bn.bias), ptr(rm),
+         ptr(rv), None, ptr(bn_save), N, D, 0.1, 1e-5, 1, 0, sh)
+    call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2), ptr(b2), ptr(x), ptr(y), ptr(mask),
+         N, D, 2, sh)
+    call("gine_mlp_bwd2", ptr(dz), None, ptr(mask), ptr(a1), ptr(bn_save), ptr(w2), ptr(dbn),
+         ptr(partials), N, D, 2, sh)
+    call("gine_bn_bwd_finalize", ptr(partials), P, ptr(bn.weight), ptr(bn_save), None, None,
+         ptr(coef), N, D, 1, sh)
+
+    kernels = {
+        "gine_mp_fwd": (lambda: call("gine_mp_fwd", ptr(x), ptr(g.in_rowptr), ptr(g.in_src),
+                                     ptr(g.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(z), N, D, sh),
+                        {"bytes": 4 * (2 * N * D + 2 * E + N + 1)}),
+        "gine_mp_bwd": (lambda: call("gine_mp_bwd", ptr(dz), ptr(x), ptr(g.out_rowptr),
+                                     ptr(g.out_dst), ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep),
+                                     ptr(dz), ptr(dx), ptr(mp_part), N, D, 1, sh),
+                        {"bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D}),
+        "gine_mlp_fwd1": (lambda: call("gine_mlp_fwd1", ptr(z), ptr(w1), ptr(b1), ptr(a1),
+                                       ptr(partials), N, D, sh),
+                          {"flops": 2 * N * D * D, "bytes": 8 * N * D}),
+        "gine_mlp_fwd2": (lambda: call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2), ptr(b2),
+                                       ptr(x), ptr(y), ptr(mask), N, D, 2, sh),
+                          {"flops": 2 * N * D * D, "bytes": 13 * N * D}),
+        "gine_mlp_bwd2": (lambda: call("gine_mlp_bwd2", ptr(dz), None, ptr(mask), ptr(a1),
+                                       ptr(bn_save), ptr(w2), ptr(dbn), ptr(partials), N, D, 2,
+                                       sh),
+                          {"flops": 2 * N * D * D, "bytes": 13 * N * D}),
+        "gine_mlp_bwd1": (lambda: call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save),
+                                       ptr(coef), ptr(w1), ptr(dx), N, D, sh),
+                          {"flops": 2 * N * D * D, "bytes": 12 * N * D}),
+        "gine_mlp_wgrad": (lambda: call("gine_mlp_wgrad", ptr(dz), None, ptr(mask), ptr(a1),
+                                        ptr(bn_save), ptr(dbn), ptr(coef), ptr(z), ptr(slab),
+                                        ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), N, D, 2, sh),
+                           {"flops": 4 * N * D * D, "bytes": 4 * 4 * N * D + 5 * N * D}),
+    }
+    out = {}
+    for name, (fn, work) in kernels.items():
+        for _ in range(3):
+            fn()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(reps):
+            fn()
+        ev1.record(stream)
+        ev1.synchronize()
+        us = ev0.elapsed_time(ev1) * 1e3 / reps
+        rec = {"us": round(us, 3)}
+        if "bytes" in work:
+            rec["alg_bytes"] = work["bytes"]
+            rec["GBps"] = round(work["bytes"] / us * 1e-3, 1)
+        if "flops" in work:
+            rec["alg_flops"] = work["flops"]
+            rec["TFLOPps"] = round(work["flops"] / us * 1e-6, 2)
+        out[name] = rec
+    return out
+
+
+def roofline_for(kernels: dict, layers: int):
+    # launches per step: every kernel once per layer
+    dominant = max(kernels, key=lambda k: kernels[k]["us"])
+    rec = kernels[dominant]
+    if "flops" in rec or "alg_flops" in rec:
+        achieved = rec["TFLOPps"]
+        roof = {"kernel": dominant, "bound": "mfma", "achieved": achieved,
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
+    else:
+        achieved = rec["GBps"]
+        roof = {"kernel": dominant, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    roof["avg_us"] = rec["us"]
+    roof["launches_per_step"] = layers
+    roof["traffic"] = pmc_traffic(dominant)
+    return roof
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (FETCH_SIZE x2 on
+    gfx950 + WRITE_SIZE, KB units) for this kernel, if one was collected; else None."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if kernel in d:
+                return d[kernel]
+        except (OSError, ValueError):
+            continue
+    return None
+
+
+# -----------------------------------------------------------------------------------------
+# CPU baseline (oracle, rank 0, N=1)
+# -----------------------------------------------------------------------------------------
+def cpu_baseline(cfg, graphs, seconds):
+    from oracle import gine_cpu as O
+    params = cfg.params()
+    torch.manual_seed(42)
+    model = O.OracleGNN(35, params["gnn_hidden"], params["gnn_layers"], params["loss"],
+                        params["grad_u"], params["u"], params["xi"]).train()
+    opt = torch.optim.AdamW(model.parameters(), lr=params["lr"])
+    batch = synthetic_batch(cfg.num_stations, graphs, k=cfg.k, seed=1000)
+
+    def step():
+        opt.zero_grad()
+        loss = model.crps(model(batch), batch.y)
+        loss.backward()
+        opt.step()
+
+    step()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 200:
+            break
+    return {"value": round(graphs * n / el, 3), "unit": "graphs/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} full training steps (oracle CPU restatement, fp32) on the cfg "
+                      f"{cfg.name} batch of {graphs} graphs x {cfg.num_stations} stations, "
+                      f"after 1 warm-up step; {el:.1f} s; cpu={platform.processor() or platform.machine()}",
+            "ms_per_step": round(el / n * 1e3, 2)}
+
+
+# -----------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    rank, local_rank, world = env_rank()
+    if world > 1:
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    cfg = BENCH_CONFIGS[args.config]
+    if args.config == 4:  # global batch fixed -> strong scaling
+        graphs_per_rank = cfg.graphs_per_gpu // world
+        scaling = "strong"
+    else:
+        graphs_per_rank = cfg.graphs_per_gpu
+        scaling = "weak"
+    tr = Trainer(cfg, device, rank, world, graphs_per_rank)
+    layers = tr.params["gnn_layers"]
+    E_rank = tr.batch.edge_index.size(1)
+
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        for _ in range(max(args.warmup, 2)):
+            tr.eager_step()
+    torch.cuda.current_stream(device).wait_stream(side)
+    torch.cuda.synchronize(device)
+    if not args.no_graph:
+        tr.capture()
+        for _ in range(2):
+            tr.step()
+    torch.cuda.synchronize(device)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_val = float(tr.loss.item()) if tr.loss is not None else float("nan")
+
+    graphs_global = graphs_per_rank * world
+    edges_global = E_rank * world
+    ms = elapsed / args.steps * 1e3
+    value = graphs_global * args.steps / elapsed
+    edges_per_s = edges_global * layers * args.steps / elapsed
+
+    kernels = time_kernels(tr, args.kernel_reps) if rank == 0 else {}
+    result = None
+    if rank == 0:
+        roof = roofline_for(kernels, layers)
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(cfg, graphs_per_rank, args.cpu_seconds)
+        result = {
+            "metric": "training graphs/s (24h_mixed GNN, full train step)",
+            "value": round(value, 2), "unit": "graphs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (k-NN station graphs, random-init weights)",
+            "config": {"workload": f"{cfg.name}: {cfg.experiment}, {graphs_global} graphs x "
+                                   f"{cfg.num_stations} stations, k={cfg.k}, "
+                                   f"{layers} GINE layers, D={tr.params['gnn_hidden']}",
+                       "global_batch": graphs_global, "graphs_per_gpu": graphs_per_rank,
+                       "nodes_per_gpu": tr.batch.num_nodes, "edges_per_gpu": E_rank,
+                       "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
+            "edges_aggregated_per_s": round(edges_per_s, 1),
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+            "final_loss": loss_val,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+/*
+ * gine_hip.h -- C ABI of the MI355X (gfx950) GINEConv message-passing engine.
+ *
+ * This is the drop-in boundary for the hot path of SohirMaskey/raincast-gnn:
+ *   models/gnn.py:20-29   ResGnn builds GINEConv(nn=Linear->BatchNorm1d->ReLU->Linear,
+ *                          train_eps=True, edge_dim=1)
+ *   models/gnn.py:41,44   conv(x, edge_index, edge_attr)   (called once per layer per step)
+ * The arithmetic behind that call lives in torch_geometric (GINEConv.message /
+ * MessagePassing.propagate / SumAggregation -> scatter_add_), which is not vendored in the
+ * reference (environment.yml:29-31).  Every entry point below names the reference-side
+ * operation it replaces.
+ *
+ * Conventions
+ *   - All tensors are device pointers (HBM), row-major, contiguous, fp32 unless stated.
+ *   - Every buffer (outputs and workspace) is allocated by the caller; no entry point
+ *     allocates, frees or synchronises, so every call is legal inside hipGraph capture.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).
+ *   - Return value: GINE_OK, a GINE_ERR_* code, or GINE_ERR_HIP_BASE + hipError_t.
+ *   - No hidden global state: the library holds nothing but its immutable kernels, so
+ *     calls are re-entrant from any host thread (PyTorch runs backward on its autograd
+ *     device thread).
+ */
+#ifndef GINE_HIP_H_
+#define GINE_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GINE_ABI_VERSION 1
+
+#define GINE_OK 0
+#define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
+#define GINE_ERR_DIM 2        /* unsupported channel count */
+#define GINE_ERR_WORKSPACE 3  /* workspace smaller than gine_graph_workspace_bytes() */
+#define GINE_ERR_TOO_LARGE 4  /* num_nodes or num_edges >= 2^31 */
+#define GINE_ERR_HIP_BASE 1000
+
+/* Library identity. */
+int gine_abi_version(void);
+const char* gine_status_string(int status);
+
+/* ------------------------------------------------------------------------------------
+ * Graph preparation.  Replaces the implicit per-call work of PyG's gather/scatter
+ * (x.index_select(0, edge_index[0]) and zeros.scatter_add_(0, edge_index[1], .)) with
+ * two stable counting structures built once per distinct edge_index:
+ *   CSR by destination (in-edges):  in_rowptr[N+1], in_src[E], in_attr[E]
+ *   CSR by source      (out-edges): out_rowptr[N+1], out_dst[E], out_attr[E]
+ * Within a node's segment edges keep their original order (stable), which is exactly
+ * the order in which CPU scatter_add_ / index_add_ accumulate.
+ *   edge_index: int64 [2, E] (row 0 = source j, row 1 = target i; flow source_to_target)
+ *   edge_attr : fp32 [E] (edge_dim = 1) or NULL (then in_attr/out_attr are not written)
+ *   d_error   : device int32, OR-ed with 1 when an index lies outside [0, N); the caller
+ *               zeroes it before the call and reads it when convenient.
+ * Reference: utils/data.py:261-284 (edge layout), models/gnn.py:41,44 (consumer).
+ * ---------------------------------------------------------------------------------- */
+int gine_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges, size_t* bytes);
+int gine_graph_build(const int64_t* edge_index, const float* edge_attr, int64_t num_nodes,
+                     int64_t num_edges, int32_t* in_rowptr, int32_t* in_src, float* in_attr,
+                     int32_t* out_rowptr, int32_t* out_dst, float* out_attr, int32_t* d_error,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Message passing forward.  Replaces GINEConv.forward up to (excluding) self.nn:
+ *   m_e  = relu(x[src_e] + fma(a_e, lin_w, lin_b))        (GINEConv.message, lin=Linear(1,D))
+ *   agg_i = sum over in-edges of i, original edge order   (SumAggregation / scatter_add_)
+ *   z_i  = agg_i + (1 + eps) * x_i                         (out + (1 + self.eps) * x_r)
+ * Bit-identical to the CPU path (sequential per-destination order, single-rounding fma
+ * for the K=1 Linear, no contraction elsewhere).
+ *   x [N, D], lin_w [D] (Linear(1,D).weight flattened), lin_b [D], eps [1] (device), z [N, D]
+ * Supported D: multiple of 4, 4 <= D <= 1024.
+ * ---------------------------------------------------------------------------------- */
+int gine_mp_fwd(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                const float* in_attr, const float* lin_w, const float* lin_b, const float* eps,
+                float* z, int64_t num_nodes, int32_t channels, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Message passing backward (autograd of gine_mp_fwd), over the out-edge CSR:
+ *   dm_e   = dz[dst_e] * 1[x[j] + fma(a_e, lin_w, lin_b) > 0]      (gather + relu bwd)
+ *   dx_j   = sum over out-edges of j in original order of dm_e   (index_add_, bit-exact)
+ *            [+ (1 + eps) * dz_j  if flags & GINE_MP_BWD_SELF]
+ *            [+ dres_j            if dres != NULL]
+ *   partials[b] (fp64, [3][D] per block b): sum dm*a, sum dm, sum dz*x for the block
+ * gine_mp_bwd_finalize reduces the partials in fixed block order into
+ *   dlin_w [D], dlin_b [D], deps [1].
+ * ---------------------------------------------------------------------------------- */
+#define GINE_MP_BWD_SELF 1
+int gine_mp_bwd_num_partials(int64_t num_nodes, int32_t channels, int32_t* num_partials);
+int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_rowptr,
+                const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                const float* lin_b, const float* eps, const float* dres, float* dx,
+                double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                void* stream);
+int gine_mp_bwd_finalize(const double* partials, int32_t num_partials, int32_t channels,
+                         float* dlin_w, float* dlin_b, float* deps, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Node MLP  nn = Sequential(Linear(D,D), BatchNorm1d(D), ReLU(), Linear(D,D))
+ * (models/gnn.py:21-26), plus the ResGnn epilogue (models/gnn.py:38-44).
+ * fp32 MFMA (v_mfma_f32_32x32x2_f32) row-tile GEMMs with fused prologues/epilogues.
+ * Supported D: 32, 64, 128, 256.
+ *
+ * Forward, training mode:
+ *   gine_mlp_fwd1:      a1 = z W1^T + b1; per-block fp64 partial sums of a1 and a1^2
+ *   gine_bn_fwd_finalize: mean, biased var -> invstd; running stats update
+ *                       (momentum, unbiased var); bn_save = [mean | invstd | alpha | shift]
+ *                       with alpha = gamma*invstd, shift = beta - mean*alpha
+ *                       (eval mode: from running stats, partials unused)
+ *   gine_mlp_fwd2:      r = relu(a1*alpha + shift); o = r W2^T + b2;
+ *                       y = o | relu(o) | x + relu(o)   (epilogue 0 | 1 | 2)
+ *                       mask[n,c] = (o > 0) stored as uint8 for epilogue 2 (may be NULL else)
+ * Backward:
+ *   gine_mlp_bwd2:      do = dy*1[o>0] (per epilogue); dr = do W2; dbn = dr*1[bn>0];
+ *                       partials of sum dbn, sum dbn*xhat
+ *   gine_bn_bwd_finalize: dgamma, dbeta, and coef = [c1 | c2 | c3] with
+ *                       da1 = c1*dbn + c2*xhat + c3
+ *   gine_mlp_bwd1:      dz = da1 W1
+ *   gine_mlp_wgrad:     dW2 = do^T r, db2 = sum do, dW1 = da1^T z, db1 = sum da1
+ *                       (split over row chunks; fp32 partial slabs reduced in fixed order)
+ * ---------------------------------------------------------------------------------- */
+#define GINE_EPI_NONE 0
+#define GINE_EPI_RELU 1
+#define GINE_EPI_RESIDUAL_RELU 2
+
+int gine_mlp_num_partials(int64_t num_nodes, int32_t channels, int32_t* num_partials);
+int gine_mlp_fwd1(const float* z, const float* w1, const float* b1, float* a1, double* partials,
+                  int64_t num_nodes, int32_t channels, void* stream);
+int gine_bn_fwd_finalize(const double* partials, int32_t num_partials, const float* gamma,
+                         const float* beta, float* running_mean, float* running_var,
+                         int64_t* num_batches_tracked, float* bn_save, int64_t num_nodes,
+                         int32_t channels, float momentum, float bn_eps, int32_t training,
+                         int32_t update_running, void* stream);
+int gine_mlp_fwd2(const float* a1, const float* bn_save, const float* w2, const float* b2,
+                  const float* x, float* y, uint8_t* mask, int64_t num_nodes, int32_t channels,
+                  int32_t epilogue, void* stream);
+
+int gine_mlp_bwd2(const float* dy, const float* y, const uint8_t* mask, const float* a1,
+                  const float* bn_save, const float* w2, float* dbn, double* partials,
+                  int64_t num_nodes, int32_t channels, int32_t epilogue, void* stream);
+int gine_bn_bwd_finalize(const double* partials, int32_t num_partials, const float* gamma,
+                         const float* bn_save, float* dgamma, float* dbeta, float* coef,
+                         int64_t num_nodes, int32_t channels, int32_t training, void* stream);
+int gine_mlp_bwd1(const float* dbn, const float* a1, const float* bn_save, const float* coef,
+                  const float* w1, float* dz, int64_t num_nodes, int32_t channels,
+                  void* stream);
+int gine_mlp_wgrad_num_chunks(int64_t num_nodes, int32_t channels, int32_t* num_chunks);
+int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* mask, const float* a1,
+                   const float* bn_save, const float* dbn, const float* coef, const float* z,
+                   float* slab, float* dw1, float* db1, float* dw2, float* db2,
+                   int64_t num_nodes, int32_t channels, int32_t epilogue, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GINE_HIP_H_ */

@@ -1,0 +1,251 @@
+"""ORACLE -- test infrastructure only.  CPU restatement of the reference's hot path.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / the timed CPU baseline.  The product path
+(``raincast_gnn``) never imports it and has no CPU fallback.
+
+What is restated, and from where
+--------------------------------
+* GINEConv (torch_geometric, NOT vendored in /root/reference and not installed here;
+  environment.yml:31 leaves it unpinned, README.md:73 says "2.3.1+"; the semantics below
+  are identical across 2.3-2.6).  Its published algorithm, in the ATen ops PyG dispatches
+  to on CPU for a plain-Tensor ``edge_index`` and ``aggr='add'``:
+    - ``MessagePassing._collect``:   ``x_j = x.index_select(0, edge_index[0])``
+    - ``GINEConv.message``:          ``(x_j + self.lin(edge_attr)).relu()``, lin = Linear(1, D)
+    - ``SumAggregation`` -> ``utils.scatter(reduce='sum')``:
+                                     ``x.new_zeros(N, D).scatter_add_(0, index.expand, m)``
+    - ``GINEConv.forward``:          ``out = out + (1 + self.eps) * x_r; return self.nn(out)``
+  Call sites anchoring it: models/gnn.py:5 (import), :28 (construction), :41,44 (calls).
+* ResGnn / DeepSetEncoder / GNN: models/gnn.py:10-141.
+* PostProcess: models/model_utils.py:42-113.   Losses: models/loss.py:6-68, 71-272, 335-369.
+* Graph layout: utils/data.py:261-284 (``build_edge_index_and_attr``).
+
+Pinning
+-------
+* GINE path: **parity unpinned** -- the reference ships no test, fixture or golden vector
+  for GINEConv and torch_geometric cannot be imported here.  The
+  restatement is cross-checked against an independent per-edge Python loop
+  (:func:`gine_aggregate_loops`) and its CPU summation order is verified in tests.
+* PostProcess and the CRPS losses: pinned -- ``tests/golden/reference_heads.npz`` holds
+  outputs of the reference's own models/model_utils.py and models/loss.py, generated in the
+  build container by ``tests/golden/make_reference_heads.py``.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+# ---------------------------------------------------------------------------------------
+# GINEConv (PyG semantics)
+# ---------------------------------------------------------------------------------------
+
+
+def gine_aggregate(x, edge_index, edge_attr, lin_w, lin_b, eps):
+    """z = scatter_add(relu(x[src] + lin(a)), dst) + (1 + eps) * x  (PyG op sequence)."""
+    src, dst = edge_index[0], edge_index[1]
+    x_j = x.index_select(0, src)
+    e = F.linear(edge_attr.reshape(-1, lin_w.size(1)), lin_w, lin_b)
+    m = (x_j + e).relu()
+    agg = x.new_zeros(x.size(0), m.size(1)).scatter_add_(0, dst.view(-1, 1).expand_as(m), m)
+    return agg + (1 + eps) * x
+
+
+def gine_aggregate_loops(x, edge_index, edge_attr, lin_w, lin_b, eps):
+    """Independent per-edge restatement (small inputs only): sequential float32 sums in
+    original edge order, fma for the K=1 Linear (np.float32 arithmetic per element)."""
+    xn = x.detach().numpy().astype(np.float32)
+    ei = edge_index.numpy()
+    a = edge_attr.detach().reshape(-1).numpy().astype(np.float32)
+    w = lin_w.detach().reshape(-1).numpy().astype(np.float32)
+    b = lin_b.detach().reshape(-1).numpy().astype(np.float32)
+    ope = np.float32(1) + np.float32(eps.detach().reshape(-1)[0].item())
+    N, D = xn.shape
+    agg = np.zeros((N, D), dtype=np.float32)
+    for e in range(ei.shape[1]):
+        s, d = ei[0, e], ei[1, e]
+        lin = (np.float64(a[e]) * np.float64(w) + np.float64(b)).astype(np.float32)  # one rounding
+        pre = (xn[s] + lin).astype(np.float32)
+        m = np.where(pre > 0, pre, np.float32(0)).astype(np.float32)
+        agg[d] = (agg[d] + m).astype(np.float32)
+    return torch.from_numpy((agg + (ope * xn).astype(np.float32)).astype(np.float32))
+
+
+class OracleGINEConv(nn.Module):
+    """CPU GINEConv with PyG's attributes and state_dict keys (nn.*, eps, lin.*)."""
+
+    def __init__(self, nn_module, eps=0.0, train_eps=False, edge_dim=None):
+        super().__init__()
+        self.nn = nn_module
+        self.initial_eps = eps
+        if train_eps:
+            self.eps = nn.Parameter(torch.empty(1))
+        else:
+            self.register_buffer("eps", torch.empty(1))
+        self.lin = None
+        if edge_dim is not None:
+            first = self.nn[0] if isinstance(self.nn, nn.Sequential) else self.nn
+            self.lin = nn.Linear(edge_dim, first.in_features)
+        self.eps.data.fill_(eps)
+
+    def aggregate(self, x, edge_index, edge_attr):
+        return gine_aggregate(x, edge_index, edge_attr, self.lin.weight, self.lin.bias, self.eps)
+
+    def forward(self, x, edge_index, edge_attr):
+        return self.nn(self.aggregate(x, edge_index, edge_attr))
+
+
+class OracleResGnn(nn.Module):
+    """models/gnn.py:10-45 on OracleGINEConv."""
+
+    def __init__(self, in_channels, out_channels, num_layers, hidden_channels):
+        super().__init__()
+        self.convolutions = nn.ModuleList()
+        for _ in range(num_layers):
+            mlp = nn.Sequential(nn.Linear(in_channels, hidden_channels),
+                                nn.BatchNorm1d(hidden_channels), nn.ReLU(),
+                                nn.Linear(hidden_channels, hidden_channels))
+            self.convolutions.append(OracleGINEConv(mlp, train_eps=True, edge_dim=1))
+        self.relu = nn.ReLU()
+
+    def forward(self, x, edge_index, edge_attr):
+        x = x.float()
+        edge_attr = edge_attr.float()
+        for i, conv in enumerate(self.convolutions):
+            h = self.relu(conv(x, edge_index, edge_attr))
+            x = h if i == 0 else x + h
+        return x
+
+
+class OracleDeepSet(nn.Module):
+    def __init__(self, d_in, hidden, out):
+        super().__init__()
+        self.phi = nn.Sequential(nn.Linear(d_in, hidden), nn.ReLU(), nn.Linear(hidden, hidden))
+        self.rho = nn.Sequential(nn.Linear(hidden, hidden), nn.ReLU(), nn.Linear(hidden, out))
+
+    def forward(self, ens):
+        return self.rho(self.phi(ens).sum(dim=1))
+
+
+# ---------------------------------------------------------------------------------------
+# Heads: PostProcess and CRPS losses (reference semantics, boolean-mask NaN handling)
+# ---------------------------------------------------------------------------------------
+_EPS = 1e-6
+
+
+def postprocess(x, loss, grad_u):
+    cols = list(torch.split(x, 1, dim=-1))
+    if loss == "NormalCRPS":
+        cols[1] = F.softplus(cols[1]) + _EPS
+    elif loss == "MixedNormalCRPS":
+        cols[1] = F.softplus(cols[1]) + _EPS
+        cols[2] = torch.sigmoid(cols[2])
+    elif loss == "MixedLoss":
+        cols[1] = F.softplus(cols[1]) + _EPS
+        cols[2] = torch.sigmoid(cols[2])
+        cols[3] = F.softplus(cols[3]) + _EPS
+        if grad_u == "True":
+            cols[4] = torch.sigmoid(cols[4]) * 2.12
+    return torch.cat(cols, dim=-1)
+
+
+def _Phi(v):
+    return torch.distributions.Normal(loc=0, scale=1).cdf(v)
+
+
+def _phi(v):
+    return torch.distributions.Normal(loc=0, scale=1).log_prob(v).exp()
+
+
+def crps_normal(pred, y):
+    keep = ~torch.isnan(y)
+    mu, sigma = (t[keep] for t in torch.split(pred, 1, dim=1))
+    yy = y.unsqueeze(1)[keep]
+    z = (yy - mu) / sigma
+    inv_sqrt_pi = 1 / torch.sqrt(torch.tensor(np.pi))
+    dist = torch.distributions.Normal(loc=0.0, scale=1.0)
+    val = sigma * (z * (2.0 * dist.cdf(z) - 1.0) + 2.0 * torch.exp(dist.log_prob(z)) - inv_sqrt_pi)
+    return val.mean()
+
+
+def crps_mixed_normal(pred, y, c=np.log(0.01)):
+    keep = ~torch.isnan(y)
+    mu, sigma, p = (t[keep] for t in torch.split(pred, 1, dim=1))
+    yy = y.unsqueeze(1)[keep]
+    ct = (torch.tensor([c]) - mu) / sigma
+    yt = (yy - mu) / sigma
+    mass_c = p + (1 - p) * _Phi(ct)
+    body = (yt * (2 * (p + (1 - p) * _Phi(yt)) - 1) - ct * mass_c ** 2
+            - 2 * (1 - p) * _phi(ct) * mass_c + 2 * (1 - p) * _phi(yt)
+            - (1 - p) ** 2 / math.sqrt(math.pi) * (1 - _Phi(math.sqrt(2) * ct)))
+    return (sigma * body).mean()
+
+
+def _gpd_crps(y, u, m, s, xi):
+    t = (y - u) / s
+    G = torch.where(t <= 0, 0, 1 - (1 + xi * t).pow(-1 / xi))
+    return s * (t.abs() - 2 * (1 - m) / (1 - xi) * (1 - (1 - G).pow(1 - xi))
+                + (1 - m) ** 2 / (2 - xi))
+
+
+def crps_mixed(pred, y, grad_u, u=None, xi=0.5, t=5, c=np.log(0.01)):
+    keep = ~torch.isnan(y)
+    cols = torch.split(pred, 1, dim=1)
+    if grad_u:
+        mu, sigma, p, su, uu = (v[keep] for v in cols)
+    else:
+        mu, sigma, p, su = (v[keep] for v in cols)
+        uu = torch.tensor([u])
+    yy = y.unsqueeze(1)[keep]
+    xit = torch.tensor([xi])
+    ct = (torch.tensor([c]) - mu) / sigma
+    ut = (uu - mu) / sigma
+    yt = (yy - mu) / sigma
+    m_u = p + (1 - p) * _Phi(ut)
+    mass_c = p + (1 - p) * _Phi(ct)
+    mass_u = (1 - p) * (1 - _Phi(ut))
+    shared = (-ct * mass_c ** 2 + ut * mass_u ** 2
+              - 2 * (1 - p) * _phi(ct) * mass_c - 2 * (1 - p) * _phi(ut) * mass_u
+              - (1 - p) ** 2 / math.sqrt(math.pi) * (_Phi(math.sqrt(2) * ut)
+                                                      - _Phi(math.sqrt(2) * ct)))
+    below = sigma * (yt * (2 * (p + (1 - p) * _Phi(yt)) - 1) + 2 * (1 - p) * _phi(yt) + shared)
+    above = sigma * (ut + 2 * ((1 - p) * _phi(ut) - ut * mass_u) + shared)
+    loss_1 = below + _gpd_crps(uu, uu, m_u, su, xit)
+    loss_2 = _gpd_crps(yy, uu, m_u, su, xit) + above
+    if grad_u:
+        val = torch.sigmoid((uu - yy) * t) * (loss_1 - loss_2) + loss_2
+    else:
+        val = torch.where(yy < uu, loss_1, loss_2)
+    return val.mean()
+
+
+def make_crps(loss, grad_u, u, xi):
+    if loss == "NormalCRPS":
+        return crps_normal, 2
+    if loss == "MixedNormalCRPS":
+        return crps_mixed_normal, 3
+    if grad_u == "True":
+        return (lambda pr, y: crps_mixed(pr, y, True, xi=xi)), 5
+    return (lambda pr, y: crps_mixed(pr, y, False, u=u, xi=xi)), 4
+
+
+class OracleGNN(nn.Module):
+    """models/gnn.py:70-141 on CPU; state_dict keys identical to the reference."""
+
+    def __init__(self, in_channels, hidden, num_layers, loss="MixedLoss", grad_u="False",
+                 u=1.71, xi=0.5):
+        super().__init__()
+        self.loss, self.grad_u = loss, grad_u
+        self.crps, out = make_crps(loss, grad_u, u, xi)
+        self.deepset = OracleDeepSet(in_channels, hidden, hidden)
+        self.dim_red = nn.Linear(in_channels + hidden, hidden)
+        self.conv = OracleResGnn(hidden, hidden, num_layers, hidden)
+        self.aggr = nn.Linear(hidden, out)
+
+    def forward(self, data):
+        h = self.dim_red(torch.cat([data.x, self.deepset(data.ensemble)], dim=1))
+        h = self.conv(h, data.edge_index, data.edge_attr)
+        return postprocess(self.aggr(h), self.loss, self.grad_u)

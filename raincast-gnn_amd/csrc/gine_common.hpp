@@ -1,0 +1,57 @@
+// Shared device/host helpers for the gfx950 GINEConv engine.
+// Everything in this directory is compiled with -ffp-contract=off: the message-passing
+// kernels reproduce the CPU rounding sequence exactly, so the only fused multiply-adds are
+// the explicit __builtin_fmaf calls (CPU Linear(1,D) rounds once, like an fma) and the MFMA
+// accumulation chains of the node-MLP GEMMs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gine_hip.h"
+
+#define GINE_RETURN_IF_HIP(expr)                                  \
+  do {                                                            \
+    hipError_t gine_e_ = (expr);                                  \
+    if (gine_e_ != hipSuccess) return GINE_ERR_HIP_BASE + (int)gine_e_; \
+  } while (0)
+
+#define GINE_LAUNCH_STATUS() \
+  do {                                                            \
+    hipError_t gine_e_ = hipGetLastError();                       \
+    if (gine_e_ != hipSuccess) return GINE_ERR_HIP_BASE + (int)gine_e_; \
+  } while (0)
+
+namespace gine {
+
+constexpr int kWave = 64;   // CDNA wavefront width
+constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, each with a private 4 MiB L2
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Blocks are dealt round-robin over the 8 XCDs (blocks b and b+8 share one).  Remap the
+// hardware block id so that every XCD walks one contiguous range of tiles: neighbouring
+// destinations gather neighbouring source rows (graphs are block-diagonal batches of
+// station graphs), so a contiguous range keeps those rows in that XCD's L2.  Bijective for
+// any grid size (remainder-aware); a placement other than round-robin only costs speed.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int q = nblocks / kNumXcd, r = nblocks % kNumXcd;
+  const int xcd = bid % kNumXcd, pos = bid / kNumXcd;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + pos;
+}
+
+__device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+// relu with ATen's NaN propagation (clamp_min keeps NaN); the sign of a zero result never
+// changes a sum that starts from +0, so 0 vs -0 is immaterial.
+__device__ __forceinline__ float relu_nan(float v) { return (v <= 0.f) ? 0.f : v; }
+
+// Double-precision block reduction helper over the 32 lanes of one MFMA column half.
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+  return __shfl_xor(v, m, kWave);
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace gine

@@ -1,0 +1,176 @@
+// Graph preparation: int64 edge_index -> two stable CSR structures (by destination and by
+// source).  Built once per distinct static station graph (utils/data.py:300 shares one
+// edge_index across every sample; a batch is a block-diagonal union, PyG collate), then
+// reused by every layer of every step.
+//
+// Stable LSD radix sort (hipCUB) on 32-bit keys keeps the original edge order inside each
+// node's segment -- the order CPU scatter_add_ (forward) and index_add_ (backward of
+// index_select) accumulate in -- which is what makes the aggregation bit-identical.
+#include <hipcub/hipcub.hpp>
+
+#include "gine_common.hpp"
+
+namespace gine {
+namespace {
+
+constexpr size_t kAlign = 256;
+
+inline size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+inline int key_bits(int64_t num_nodes) {
+  int bits = 1;
+  while (bits < 31 && (int64_t(1) << bits) < num_nodes) ++bits;
+  return bits;
+}
+
+__global__ void k_split_edges(const int64_t* __restrict__ ei, int64_t E, int64_t N,
+                              int32_t* __restrict__ src32, int32_t* __restrict__ dst32,
+                              int32_t* __restrict__ ids, int32_t* __restrict__ err) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  int64_t s = ei[e];
+  int64_t d = ei[E + e];
+  const bool bad = (s < 0) | (s >= N) | (d < 0) | (d >= N);
+  if (bad) {
+    atomicOr(err, 1);
+    s = 0;  // keep every downstream access in bounds; the caller raises on *err
+    d = 0;
+  }
+  src32[e] = (int32_t)s;
+  dst32[e] = (int32_t)d;
+  ids[e] = (int32_t)e;
+}
+
+__global__ void k_gather_segment(const int32_t* __restrict__ perm,
+                                 const int32_t* __restrict__ other_end,
+                                 const float* __restrict__ attr, int64_t E,
+                                 int32_t* __restrict__ seg_other, float* __restrict__ seg_attr) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= E) return;
+  const int32_t e = perm[p];
+  seg_other[p] = other_end[e];
+  if (attr != nullptr) seg_attr[p] = attr[e];
+}
+
+// rowptr[i] = first position whose sorted key >= i  (lower bound), rowptr[N] = E.
+__global__ void k_rowptr(const int32_t* __restrict__ sorted_keys, int64_t E, int64_t N,
+                         int32_t* __restrict__ rowptr) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i > N) return;
+  int64_t lo = 0, hi = E;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)sorted_keys[mid] < i) lo = mid + 1; else hi = mid;
+  }
+  rowptr[i] = (int32_t)lo;
+}
+
+struct Layout {
+  size_t src32, dst32, ids, keys_out, perm, temp, temp_bytes, total;
+};
+
+int plan(int64_t N, int64_t E, Layout* L) {
+  const size_t eb = align_up(sizeof(int32_t) * (size_t)(E > 0 ? E : 1));
+  L->src32 = 0;
+  L->dst32 = L->src32 + eb;
+  L->ids = L->dst32 + eb;
+  L->keys_out = L->ids + eb;
+  L->perm = L->keys_out + eb;
+  L->temp = L->perm + eb;
+  size_t temp_bytes = 0;
+  if (E > 0) {
+    GINE_RETURN_IF_HIP(hipcub::DeviceRadixSort::SortPairs(
+        nullptr, temp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+        (const int32_t*)nullptr, (int32_t*)nullptr, (int)E, 0, key_bits(N)));
+  }
+  L->temp_bytes = align_up(temp_bytes > 0 ? temp_bytes : 1);
+  L->total = L->temp + L->temp_bytes;
+  return GINE_OK;
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_graph_workspace_bytes(int64_t num_nodes, int64_t num_edges, size_t* bytes) {
+  if (bytes == nullptr || num_nodes < 0 || num_edges < 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31) || num_edges >= (int64_t(1) << 31))
+    return GINE_ERR_TOO_LARGE;
+  Layout L;
+  const int st = plan(num_nodes, num_edges, &L);
+  if (st != GINE_OK) return st;
+  *bytes = L.total;
+  return GINE_OK;
+}
+
+extern "C" int gine_graph_build(const int64_t* edge_index, const float* edge_attr,
+                                int64_t num_nodes, int64_t num_edges, int32_t* in_rowptr,
+                                int32_t* in_src, float* in_attr, int32_t* out_rowptr,
+                                int32_t* out_dst, float* out_attr, int32_t* d_error,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  if (num_nodes < 0 || num_edges < 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31) || num_edges >= (int64_t(1) << 31))
+    return GINE_ERR_TOO_LARGE;
+  if (in_rowptr == nullptr || out_rowptr == nullptr || d_error == nullptr)
+    return GINE_ERR_INVALID;
+  if (num_edges > 0 && (edge_index == nullptr || in_src == nullptr || out_dst == nullptr ||
+                        workspace == nullptr))
+    return GINE_ERR_INVALID;
+  if (edge_attr != nullptr && num_edges > 0 && (in_attr == nullptr || out_attr == nullptr))
+    return GINE_ERR_INVALID;
+  Layout L;
+  int st = plan(num_nodes, num_edges, &L);
+  if (st != GINE_OK) return st;
+  if (num_edges > 0 && workspace_bytes < L.total) return GINE_ERR_WORKSPACE;
+
+  hipStream_t s = as_stream(stream);
+  const int64_t E = num_edges, N = num_nodes;
+  const int threads = 256;
+  if (E == 0) {
+    hipLaunchKernelGGL(k_rowptr, dim3((unsigned)ceil_div(N + 1, threads)), dim3(threads), 0, s,
+                       (const int32_t*)nullptr, (int64_t)0, N, in_rowptr);
+    GINE_LAUNCH_STATUS();
+    hipLaunchKernelGGL(k_rowptr, dim3((unsigned)ceil_div(N + 1, threads)), dim3(threads), 0, s,
+                       (const int32_t*)nullptr, (int64_t)0, N, out_rowptr);
+    GINE_LAUNCH_STATUS();
+    return GINE_OK;
+  }
+  char* ws = static_cast<char*>(workspace);
+  int32_t* src32 = reinterpret_cast<int32_t*>(ws + L.src32);
+  int32_t* dst32 = reinterpret_cast<int32_t*>(ws + L.dst32);
+  int32_t* ids = reinterpret_cast<int32_t*>(ws + L.ids);
+  int32_t* keys_out = reinterpret_cast<int32_t*>(ws + L.keys_out);
+  int32_t* perm = reinterpret_cast<int32_t*>(ws + L.perm);
+  void* temp = ws + L.temp;
+  size_t temp_bytes = L.temp_bytes;
+  const int bits = key_bits(N);
+  const unsigned eg = (unsigned)ceil_div(E, threads);
+  const unsigned ng = (unsigned)ceil_div(N + 1, threads);
+
+  hipLaunchKernelGGL(k_split_edges, dim3(eg), dim3(threads), 0, s, edge_index, E, N, src32,
+                     dst32, ids, d_error);
+  GINE_LAUNCH_STATUS();
+
+  // In-edges: stable sort by destination.
+  GINE_RETURN_IF_HIP(hipcub::DeviceRadixSort::SortPairs(
+      temp, temp_bytes, reinterpret_cast<const uint32_t*>(dst32),
+      reinterpret_cast<uint32_t*>(keys_out), ids, perm, (int)E, 0, bits, s));
+  hipLaunchKernelGGL(k_gather_segment, dim3(eg), dim3(threads), 0, s, perm, src32, edge_attr, E,
+                     in_src, in_attr);
+  GINE_LAUNCH_STATUS();
+  hipLaunchKernelGGL(k_rowptr, dim3(ng), dim3(threads), 0, s, keys_out, E, N, in_rowptr);
+  GINE_LAUNCH_STATUS();
+
+  // Out-edges: stable sort by source.
+  temp_bytes = L.temp_bytes;
+  GINE_RETURN_IF_HIP(hipcub::DeviceRadixSort::SortPairs(
+      temp, temp_bytes, reinterpret_cast<const uint32_t*>(src32),
+      reinterpret_cast<uint32_t*>(keys_out), ids, perm, (int)E, 0, bits, s));
+  hipLaunchKernelGGL(k_gather_segment, dim3(eg), dim3(threads), 0, s, perm, dst32, edge_attr, E,
+                     out_dst, out_attr);
+  GINE_LAUNCH_STATUS();
+  hipLaunchKernelGGL(k_rowptr, dim3(ng), dim3(threads), 0, s, keys_out, E, N, out_rowptr);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

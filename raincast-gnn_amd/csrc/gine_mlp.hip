@@ -1,0 +1,608 @@
+// Node MLP of the GINE layer on gfx950 fp32 matrix cores.
+//
+// Replaces nn = Sequential(Linear(D,D), BatchNorm1d(D), ReLU(), Linear(D,D))
+// (models/gnn.py:21-26) applied by GINEConv to z, plus ResGnn's outer ReLU / residual
+// (models/gnn.py:38-44), forward (train and eval BN) and backward.
+//
+// All four node GEMMs are [N x D] x [D x D] with D <= 256: tall-skinny.  One kernel shape
+// serves them all (k_rowgemm): a workgroup of D/32 waves, wave w owns output columns
+// [32w, 32w+32); the whole [D x 32] slice of the weight for that wave lives in VGPRs as
+// v_mfma_f32_32x32x2_f32 B fragments (D/2 registers), loaded once per workgroup; 32-row
+// tiles of the activation are staged through LDS by the workgroup with the elementwise
+// prologue fused (BN-normalise + ReLU, ReLU-mask of the upstream gradient, BN backward),
+// and the epilogue is fused too (bias, BN statistics, ReLU / residual, ReLU mask).
+//
+// The contraction index k is split between the two lane halves of the MFMA operand
+// (lane half h takes k in [h*D/2, (h+1)*D/2)); A and B use the same permutation so the
+// product is unchanged, and each lane's A fragments become contiguous in LDS, so four
+// k-steps are fetched with one ds_read_b128 (row stride D+4 floats: conflict-free).
+//
+// Weight gradients (K = N rows) use k_wgrad: 64x64 output blocks x row chunks, fp32
+// partial slabs, reduced in fixed chunk order in fp64 by k_slab_reduce -> deterministic.
+#include "gine_common.hpp"
+
+namespace gine {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ floatx16 zero16() {
+  floatx16 v;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = 0.f;
+  return v;
+}
+
+constexpr int kRowTile = 32;
+constexpr int kMaxRowBlocks = 1024;
+constexpr int kChunkTarget = 64;
+
+enum Pro { PRO_PLAIN = 0, PRO_BNRELU = 1, PRO_DO = 2, PRO_DA1 = 3 };
+enum Epi { EPI_A1STATS = 0, EPI_OUT = 1, EPI_DBN = 2, EPI_PLAIN = 3 };
+
+// bn_save layout: [mean | invstd | alpha | shift], each [D]
+struct BnView {
+  const float* mean;
+  const float* invstd;
+  const float* alpha;
+  const float* shift;
+};
+__device__ __forceinline__ BnView bn_view(const float* s, int D) {
+  return BnView{s, s + D, s + 2 * D, s + 3 * D};
+}
+
+struct ProArgs {
+  const float* x;        // primary [N][D]: z | a1 | dy | dbn
+  const float* aux;      // a1 for PRO_DA1; y for PRO_DO with the ReLU epilogue
+  const uint8_t* mask;   // PRO_DO, residual epilogue
+  const float* bn;       // bn_save
+  const float* coef;     // [c1 | c2 | c3] (PRO_DA1)
+  int epi;               // GINE_EPI_* of the forward output (PRO_DO)
+};
+
+// Same rounding sequence wherever bn is recomputed (forward GEMM2 prologue, backward
+// ReLU mask, dW2 prologue): mul then add, no contraction.
+__device__ __forceinline__ float bn_apply(float a, float alpha, float shift) {
+  return a * alpha + shift;
+}
+
+// Prologue value of float4 column-group q of row n.
+template <int PRO>
+__device__ __forceinline__ float4 prologue(const ProArgs& p, int D, int64_t n, int q) {
+  const int64_t off = n * D + 4 * q;
+  const float4 v = *reinterpret_cast<const float4*>(p.x + off);
+  if constexpr (PRO == PRO_PLAIN) {
+    return v;
+  } else if constexpr (PRO == PRO_BNRELU) {
+    const BnView b = bn_view(p.bn, D);
+    const float4 al = *reinterpret_cast<const float4*>(b.alpha + 4 * q);
+    const float4 sh = *reinterpret_cast<const float4*>(b.shift + 4 * q);
+    return make_float4(relu_nan(bn_apply(v.x, al.x, sh.x)), relu_nan(bn_apply(v.y, al.y, sh.y)),
+                       relu_nan(bn_apply(v.z, al.z, sh.z)), relu_nan(bn_apply(v.w, al.w, sh.w)));
+  } else if constexpr (PRO == PRO_DO) {
+    if (p.epi == GINE_EPI_RELU) {
+      const float4 y = *reinterpret_cast<const float4*>(p.aux + off);
+      return make_float4(y.x > 0.f ? v.x : 0.f, y.y > 0.f ? v.y : 0.f, y.z > 0.f ? v.z : 0.f,
+                         y.w > 0.f ? v.w : 0.f);
+    } else if (p.epi == GINE_EPI_RESIDUAL_RELU) {
+      const uchar4 m = *reinterpret_cast<const uchar4*>(p.mask + off);
+      return make_float4(m.x ? v.x : 0.f, m.y ? v.y : 0.f, m.z ? v.z : 0.f, m.w ? v.w : 0.f);
+    }
+    return v;
+  } else {  // PRO_DA1: da1 = c1*dbn + c2*xhat + c3, xhat = (a1 - mean)*invstd
+    const BnView b = bn_view(p.bn, D);
+    const float4 a1 = *reinterpret_cast<const float4*>(p.aux + off);
+    const float4 mu = *reinterpret_cast<const float4*>(b.mean + 4 * q);
+    const float4 is = *reinterpret_cast<const float4*>(b.invstd + 4 * q);
+    const float4 c1 = *reinterpret_cast<const float4*>(p.coef + 4 * q);
+    const float4 c2 = *reinterpret_cast<const float4*>(p.coef + D + 4 * q);
+    const float4 c3 = *reinterpret_cast<const float4*>(p.coef + 2 * D + 4 * q);
+    float4 r;
+    r.x = c1.x * v.x + c2.x * ((a1.x - mu.x) * is.x) + c3.x;
+    r.y = c1.y * v.y + c2.y * ((a1.y - mu.y) * is.y) + c3.y;
+    r.z = c1.z * v.z + c2.z * ((a1.z - mu.z) * is.z) + c3.z;
+    r.w = c1.w * v.w + c2.w * ((a1.w - mu.w) * is.w) + c3.w;
+    return r;
+  }
+}
+
+struct EpiArgs {
+  const float* bias;   // b1 (A1STATS) / b2 (OUT)
+  float* out;          // a1 | y | dbn | dz
+  uint8_t* mask_out;   // OUT, residual epilogue
+  const float* resid;  // OUT, residual epilogue: the layer input x
+  const float* a1;     // DBN
+  const float* bn;     // DBN
+  double* partials;    // A1STATS / DBN: [grid][2][D]
+  int mode;            // OUT: GINE_EPI_*
+};
+
+// Tiles of one XCD form a contiguous range; its blocks stride that range.
+struct TileRange {
+  int first, end, step;
+};
+__device__ __forceinline__ TileRange xcd_tile_range(int num_tiles) {
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
+  const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
+  const int span = (num_tiles + kNumXcd - 1) / kNumXcd;
+  const int b = xcd * span;
+  return TileRange{b + pos, min(num_tiles, b + span), here};
+}
+
+// ----------------------------------------------------------------------------------------
+// Row-tile GEMM: out[n][j] = epi( sum_k pro(X)[n][k] * B[k][j] )
+//   BT = true : B[k][j] = W[j][k]   (Y = X W^T, forward Linear)
+//   BT = false: B[k][j] = W[k][j]   (dX = dY W, backward Linear)
+// ----------------------------------------------------------------------------------------
+template <int D, int PRO, int EPI, bool BT>
+__global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, ProArgs pa,
+                                                   EpiArgs ea, int64_t N, int num_tiles) {
+  constexpr int NT = 2 * D;      // threads: D/32 waves
+  constexpr int KS = D / 2;      // k-steps per lane half
+  constexpr int LD = D + 4;      // padded LDS row (floats)
+  constexpr int D4 = D / 4;
+  constexpr int ITEMS = kRowTile * D4 / NT;  // float4 staged per thread (= 4)
+  __shared__ __attribute__((aligned(16))) float s_x[kRowTile * LD];
+
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int col = wave * 32 + c32;
+
+  float bf[KS];
+  if constexpr (BT) {
+    const float4* wr = reinterpret_cast<const float4*>(W + (size_t)col * D + h * KS);
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const float4 v = wr[q];
+      bf[4 * q] = v.x;
+      bf[4 * q + 1] = v.y;
+      bf[4 * q + 2] = v.z;
+      bf[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bf[s] = W[(size_t)(h * KS + s) * D + col];
+  }
+
+  float bias = 0.f;
+  if constexpr (EPI == EPI_A1STATS || EPI == EPI_OUT) bias = ea.bias[col];
+  float alpha = 0.f, shift = 0.f, mean = 0.f, invstd = 0.f;
+  if constexpr (EPI == EPI_DBN) {
+    const BnView b = bn_view(ea.bn, D);
+    alpha = b.alpha[col];
+    shift = b.shift[col];
+    mean = b.mean[col];
+    invstd = b.invstd[col];
+  }
+  double st1 = 0.0, st2 = 0.0;
+
+  const TileRange tr = xcd_tile_range(num_tiles);
+  for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+    const int64_t n0 = (int64_t)tile * kRowTile;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int idx = threadIdx.x + i * NT;
+      const int r = idx / D4, q = idx % D4;
+      const int64_t n = n0 + r;
+      float4 v = prologue<PRO>(pa, D, n < N ? n : N - 1, q);  // clamped: load always issued
+      if (n >= N) v = f4_zero();
+      *reinterpret_cast<float4*>(&s_x[r * LD + 4 * q]) = v;
+    }
+    __syncthreads();
+    floatx16 acc = zero16();
+    const float* arow = &s_x[c32 * LD + h * KS];
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+    }
+    __syncthreads();  // s_x is restaged by the next tile
+
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (n >= N) continue;
+      const int64_t off = n * D + col;
+      const float v = acc[r];
+      if constexpr (EPI == EPI_A1STATS) {
+        const float a1 = v + bias;
+        ea.out[off] = a1;
+        st1 += (double)a1;
+        st2 += (double)a1 * (double)a1;
+      } else if constexpr (EPI == EPI_OUT) {
+        const float o = v + bias;
+        float y;
+        if (ea.mode == GINE_EPI_NONE) {
+          y = o;
+        } else if (ea.mode == GINE_EPI_RELU) {
+          y = relu_nan(o);
+        } else {
+          y = ea.resid[off] + relu_nan(o);
+          ea.mask_out[off] = (o > 0.f) ? 1 : 0;
+        }
+        ea.out[off] = y;
+      } else if constexpr (EPI == EPI_DBN) {
+        const float a1 = ea.a1[off];
+        const float bn = bn_apply(a1, alpha, shift);
+        const float dbn = (bn > 0.f) ? v : 0.f;
+        ea.out[off] = dbn;
+        const double xhat = (double)((a1 - mean) * invstd);
+        st1 += (double)dbn;
+        st2 += (double)dbn * xhat;
+      } else {
+        ea.out[off] = v;
+      }
+    }
+  }
+
+  if constexpr (EPI == EPI_A1STATS || EPI == EPI_DBN) {
+    st1 += shfl_xor_d(st1, 32);
+    st2 += shfl_xor_d(st2, 32);
+    if (h == 0) {
+      double* p = ea.partials + (size_t)blockIdx.x * 2 * D;
+      p[col] = st1;
+      p[D + col] = st2;
+    }
+  }
+}
+
+inline int rowgemm_grid(int64_t N) {
+  const int64_t tiles = ceil_div(N, kRowTile);
+  const int64_t g = tiles < kMaxRowBlocks ? tiles : kMaxRowBlocks;
+  return (int)(g > 0 ? g : 1);
+}
+
+template <int PRO, int EPI, bool BT>
+int launch_rowgemm(int D, const float* W, const ProArgs& pa, const EpiArgs& ea, int64_t N,
+                   hipStream_t s) {
+  const int grid = rowgemm_grid(N);
+  const int tiles = (int)ceil_div(N, kRowTile);
+  switch (D) {
+    case 32:
+      hipLaunchKernelGGL((k_rowgemm<32, PRO, EPI, BT>), dim3(grid), dim3(64), 0, s, W, pa, ea,
+                         N, tiles);
+      break;
+    case 64:
+      hipLaunchKernelGGL((k_rowgemm<64, PRO, EPI, BT>), dim3(grid), dim3(128), 0, s, W, pa, ea,
+                         N, tiles);
+      break;
+    case 128:
+      hipLaunchKernelGGL((k_rowgemm<128, PRO, EPI, BT>), dim3(grid), dim3(256), 0, s, W, pa,
+                         ea, N, tiles);
+      break;
+    case 256:
+      hipLaunchKernelGGL((k_rowgemm<256, PRO, EPI, BT>), dim3(grid), dim3(512), 0, s, W, pa,
+                         ea, N, tiles);
+      break;
+    default:
+      return GINE_ERR_DIM;
+  }
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+// ----------------------------------------------------------------------------------------
+// BatchNorm1d finalize kernels (one thread per channel, partials summed in fixed order)
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bn_fwd_finalize(
+    const double* __restrict__ partials, int P, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+    int64_t* __restrict__ nbt, float* __restrict__ bn_save, int64_t N, int D, float momentum,
+    float bn_eps, int training, int update_running) {
+  __shared__ double s_factor;
+  if (threadIdx.x == 0) {
+    double f = (double)momentum;
+    if (training && update_running && nbt != nullptr) {
+      const int64_t t = nbt[0] + 1;
+      nbt[0] = t;
+      if (momentum < 0.f) f = 1.0 / (double)t;  // momentum=None: cumulative average
+    }
+    s_factor = f;
+  }
+  __syncthreads();
+  const double factor = s_factor;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    double mean, var;
+    if (training) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int p = 0; p < P; ++p) {
+        s1 += partials[(size_t)p * 2 * D + c];
+        s2 += partials[(size_t)p * 2 * D + D + c];
+      }
+      mean = s1 / (double)N;
+      var = s2 / (double)N - mean * mean;
+      if (var < 0.0) var = 0.0;
+      if (update_running && rmean != nullptr) {
+        const double unbiased = N > 1 ? var * (double)N / (double)(N - 1) : var;
+        rmean[c] = (float)(factor * mean + (1.0 - factor) * (double)rmean[c]);
+        rvar[c] = (float)(factor * unbiased + (1.0 - factor) * (double)rvar[c]);
+      }
+    } else {
+      mean = (double)rmean[c];
+      var = (double)rvar[c];
+    }
+    const double invstd = 1.0 / sqrt(var + (double)bn_eps);
+    const double g = gamma ? (double)gamma[c] : 1.0;
+    const double bt = beta ? (double)beta[c] : 0.0;
+    const double alpha = g * invstd;
+    bn_save[c] = (float)mean;
+    bn_save[D + c] = (float)invstd;
+    bn_save[2 * D + c] = (float)alpha;
+    bn_save[3 * D + c] = (float)(bt - mean * alpha);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bn_bwd_finalize(
+    const double* __restrict__ partials, int P, const float* __restrict__ gamma,
+    const float* __restrict__ bn_save, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ coef, int64_t N, int D, int training) {
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    double sd = 0.0, sx = 0.0;
+    for (int p = 0; p < P; ++p) {
+      sd += partials[(size_t)p * 2 * D + c];
+      sx += partials[(size_t)p * 2 * D + D + c];
+    }
+    if (dgamma) dgamma[c] = (float)sx;
+    if (dbeta) dbeta[c] = (float)sd;
+    const double g = gamma ? (double)gamma[c] : 1.0;
+    const double c1 = g * (double)bn_save[D + c];
+    coef[c] = (float)c1;
+    coef[D + c] = training ? (float)(-c1 * sx / (double)N) : 0.f;
+    coef[2 * D + c] = training ? (float)(-c1 * sd / (double)N) : 0.f;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Weight gradients: dW[o][i] = sum_n P[n][o] * Q[n][i], db[o] = sum_n P[n][o]
+//   z = 0: P = do (PRO_DO of dy), Q = r = relu(bn(a1))  -> dW2, db2
+//   z = 1: P = da1 (PRO_DA1 of dbn), Q = z               -> dW1, db1
+// grid = (chunks, 64x64 output blocks, 2); 4 waves per block, one 32x32 tile per wave.
+// ----------------------------------------------------------------------------------------
+struct WgradArgs {
+  ProArgs p_do, q_r, p_da1, q_z;
+  float* slab;  // [2][chunks][D*D + D]
+  int chunks, rows_per_chunk;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void k_wgrad(WgradArgs wa, int64_t N) {
+  constexpr int BW = D < 64 ? D : 64;    // block tile width (o and i)
+  constexpr int NBI = D / BW;            // block tiles along i
+  constexpr int LDW = BW + 1;
+  constexpr int BW4 = BW / 4;
+  __shared__ float sP[kRowTile * LDW];
+  __shared__ float sQ[kRowTile * LDW];
+
+  const int chunk = blockIdx.x, bt = blockIdx.y, zsel = blockIdx.z;
+  const int o0 = (bt / NBI) * BW, i0 = (bt % NBI) * BW;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int wr = wave >> 1, wc = wave & 1;
+  const bool active = (32 * wr < BW) && (32 * wc < BW);
+  const bool do_bias = active && wc == 0 && i0 == 0;
+  const ProArgs& P = zsel == 0 ? wa.p_do : wa.p_da1;
+  const ProArgs& Q = zsel == 0 ? wa.q_r : wa.q_z;
+
+  const int64_t r_begin = (int64_t)chunk * wa.rows_per_chunk;
+  const int64_t r_end = min<int64_t>(N, r_begin + wa.rows_per_chunk);
+  floatx16 acc = zero16();
+  double bsum = 0.0;
+
+  for (int64_t n0 = r_begin; n0 < r_end; n0 += kRowTile) {
+    for (int idx = threadIdx.x; idx < kRowTile * BW4; idx += 256) {
+      const int r = idx / BW4, q = idx % BW4;
+      const int64_t n = n0 + r;
+      const int64_t nc = n < r_end ? n : r_end - 1;
+      float4 vp = zsel == 0 ? prologue<PRO_DO>(P, D, nc, o0 / 4 + q)
+                            : prologue<PRO_DA1>(P, D, nc, o0 / 4 + q);
+      float4 vq = zsel == 0 ? prologue<PRO_BNRELU>(Q, D, nc, i0 / 4 + q)
+                            : prologue<PRO_PLAIN>(Q, D, nc, i0 / 4 + q);
+      if (n >= r_end) vp = vq = f4_zero();
+      float* dp = &sP[r * LDW + 4 * q];
+      float* dq = &sQ[r * LDW + 4 * q];
+      dp[0] = vp.x; dp[1] = vp.y; dp[2] = vp.z; dp[3] = vp.w;
+      dq[0] = vq.x; dq[1] = vq.y; dq[2] = vq.z; dq[3] = vq.w;
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int s = 0; s < kRowTile / 2; ++s) {
+        const int rr = h * (kRowTile / 2) + s;
+        const float a = sP[rr * LDW + 32 * wr + c32];
+        const float b = sQ[rr * LDW + 32 * wc + c32];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        if (do_bias) bsum += (double)a;
+      }
+    }
+    __syncthreads();
+  }
+
+  float* slab = wa.slab + ((size_t)zsel * wa.chunks + chunk) * (size_t)(D * D + D);
+  if (active) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = o0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int i = i0 + 32 * wc + c32;
+      slab[(size_t)o * D + i] = acc[r];
+    }
+  }
+  bsum += shfl_xor_d(bsum, 32);
+  if (do_bias && h == 0) slab[(size_t)D * D + o0 + 32 * wr + c32] = (float)bsum;
+}
+
+__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int chunks,
+                                                     int D, float* __restrict__ dw2,
+                                                     float* __restrict__ db2,
+                                                     float* __restrict__ dw1,
+                                                     float* __restrict__ db1) {
+  const int per = D * D + D;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2 * per) return;
+  const int zsel = e / per, r = e % per;
+  const float* base = slab + (size_t)zsel * chunks * per + r;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += (double)base[(size_t)c * per];
+  float* w = zsel == 0 ? dw2 : dw1;
+  float* b = zsel == 0 ? db2 : db1;
+  if (r < D * D) {
+    if (w) w[r] = (float)s;
+  } else {
+    if (b) b[r - D * D] = (float)s;
+  }
+}
+
+inline bool mlp_dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
+
+inline void wgrad_plan(int64_t N, int* chunks, int* rows) {
+  int64_t tiles = ceil_div(N, kRowTile);
+  if (tiles < 1) tiles = 1;
+  const int64_t per = ceil_div(tiles, kChunkTarget);  // tiles per chunk
+  *rows = (int)(per * kRowTile);
+  *chunks = (int)ceil_div(N > 0 ? N : 1, *rows);
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_mlp_num_partials(int64_t num_nodes, int32_t channels,
+                                     int32_t* num_partials) {
+  if (!num_partials || num_nodes < 0) return GINE_ERR_INVALID;
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  *num_partials = rowgemm_grid(num_nodes);
+  return GINE_OK;
+}
+
+extern "C" int gine_mlp_fwd1(const float* z, const float* w1, const float* b1, float* a1,
+                             double* partials, int64_t num_nodes, int32_t channels,
+                             void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !z || !w1 || !b1 || !a1 || !partials) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  ProArgs pa{z, nullptr, nullptr, nullptr, nullptr, 0};
+  EpiArgs ea{b1, a1, nullptr, nullptr, nullptr, nullptr, partials, 0};
+  return launch_rowgemm<PRO_PLAIN, EPI_A1STATS, true>(channels, w1, pa, ea, num_nodes,
+                                                      as_stream(stream));
+}
+
+extern "C" int gine_bn_fwd_finalize(const double* partials, int32_t num_partials,
+                                    const float* gamma, const float* beta, float* running_mean,
+                                    float* running_var, int64_t* num_batches_tracked,
+                                    float* bn_save, int64_t num_nodes, int32_t channels,
+                                    float momentum, float bn_eps, int32_t training,
+                                    int32_t update_running, void* stream) {
+  if (channels <= 0 || !bn_save || num_nodes <= 0) return GINE_ERR_INVALID;
+  if (training && (!partials || num_partials <= 0)) return GINE_ERR_INVALID;
+  if (!training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
+  if (update_running && training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3(1), dim3(256), 0, as_stream(stream), partials,
+                     num_partials, gamma, beta, running_mean, running_var, num_batches_tracked,
+                     bn_save, num_nodes, channels, momentum, bn_eps, training, update_running);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_mlp_fwd2(const float* a1, const float* bn_save, const float* w2,
+                             const float* b2, const float* x, float* y, uint8_t* mask,
+                             int64_t num_nodes, int32_t channels, int32_t epilogue,
+                             void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !a1 || !bn_save || !w2 || !b2 || !y) return GINE_ERR_INVALID;
+  if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && (!x || !mask)) return GINE_ERR_INVALID;
+  ProArgs pa{a1, nullptr, nullptr, bn_save, nullptr, 0};
+  EpiArgs ea{b2, y, mask, x, nullptr, nullptr, nullptr, epilogue};
+  return launch_rowgemm<PRO_BNRELU, EPI_OUT, true>(channels, w2, pa, ea, num_nodes,
+                                                   as_stream(stream));
+}
+
+extern "C" int gine_mlp_bwd2(const float* dy, const float* y, const uint8_t* mask,
+                             const float* a1, const float* bn_save, const float* w2, float* dbn,
+                             double* partials, int64_t num_nodes, int32_t channels,
+                             int32_t epilogue, void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !dy || !a1 || !bn_save || !w2 || !dbn || !partials)
+    return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
+  ProArgs pa{dy, y, mask, nullptr, nullptr, epilogue};
+  EpiArgs ea{nullptr, dbn, nullptr, nullptr, a1, bn_save, partials, 0};
+  return launch_rowgemm<PRO_DO, EPI_DBN, false>(channels, w2, pa, ea, num_nodes,
+                                                as_stream(stream));
+}
+
+extern "C" int gine_bn_bwd_finalize(const double* partials, int32_t num_partials,
+                                    const float* gamma, const float* bn_save, float* dgamma,
+                                    float* dbeta, float* coef, int64_t num_nodes,
+                                    int32_t channels, int32_t training, void* stream) {
+  if (channels <= 0 || !partials || num_partials <= 0 || !bn_save || !coef || num_nodes <= 0)
+    return GINE_ERR_INVALID;
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(1), dim3(256), 0, as_stream(stream), partials,
+                     num_partials, gamma, bn_save, dgamma, dbeta, coef, num_nodes, channels,
+                     training);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_mlp_bwd1(const float* dbn, const float* a1, const float* bn_save,
+                             const float* coef, const float* w1, float* dz, int64_t num_nodes,
+                             int32_t channels, void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !dbn || !a1 || !bn_save || !coef || !w1 || !dz)
+    return GINE_ERR_INVALID;
+  ProArgs pa{dbn, a1, nullptr, bn_save, coef, 0};
+  EpiArgs ea{nullptr, dz, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  return launch_rowgemm<PRO_DA1, EPI_PLAIN, false>(channels, w1, pa, ea, num_nodes,
+                                                   as_stream(stream));
+}
+
+extern "C" int gine_mlp_wgrad_num_chunks(int64_t num_nodes, int32_t channels,
+                                         int32_t* num_chunks) {
+  if (!num_chunks || num_nodes < 0) return GINE_ERR_INVALID;
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  int chunks, rows;
+  wgrad_plan(num_nodes, &chunks, &rows);
+  *num_chunks = chunks;
+  return GINE_OK;
+}
+
+extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* mask,
+                              const float* a1, const float* bn_save, const float* dbn,
+                              const float* coef, const float* z, float* slab, float* dw1,
+                              float* db1, float* dw2, float* db2, int64_t num_nodes,
+                              int32_t channels, int32_t epilogue, void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !dy || !a1 || !bn_save || !dbn || !coef || !z || !slab)
+    return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
+  const int D = channels;
+  WgradArgs wa;
+  wa.p_do = ProArgs{dy, y, mask, nullptr, nullptr, epilogue};
+  wa.q_r = ProArgs{a1, nullptr, nullptr, bn_save, nullptr, 0};
+  wa.p_da1 = ProArgs{dbn, a1, nullptr, bn_save, coef, 0};
+  wa.q_z = ProArgs{z, nullptr, nullptr, nullptr, nullptr, 0};
+  wa.slab = slab;
+  wgrad_plan(num_nodes, &wa.chunks, &wa.rows_per_chunk);
+  const int bw = D < 64 ? D : 64;
+  const int nbt = (D / bw) * (D / bw);
+  hipStream_t s = as_stream(stream);
+  const dim3 grid(wa.chunks, nbt, 2);
+  switch (D) {
+    case 32: hipLaunchKernelGGL(k_wgrad<32>, grid, dim3(256), 0, s, wa, num_nodes); break;
+    case 64: hipLaunchKernelGGL(k_wgrad<64>, grid, dim3(256), 0, s, wa, num_nodes); break;
+    case 128: hipLaunchKernelGGL(k_wgrad<128>, grid, dim3(256), 0, s, wa, num_nodes); break;
+    default: hipLaunchKernelGGL(k_wgrad<256>, grid, dim3(256), 0, s, wa, num_nodes); break;
+  }
+  GINE_LAUNCH_STATUS();
+  const int total = 2 * (D * D + D);
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, slab,
+                     wa.chunks, D, dw2, db2, dw1, db1);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

@@ -1,0 +1,439 @@
+// GINEConv message passing on gfx950: gather -> edge-MLP -> deterministic scatter-add.
+//
+// Replaces (torch_geometric, called from models/gnn.py:41,44):
+//   x_j = x.index_select(0, edge_index[0])                 MessagePassing._collect
+//   m   = (x_j + Linear(1,D)(edge_attr)).relu()            GINEConv.message
+//   agg = zeros(N,D).scatter_add_(0, edge_index[1], m)     SumAggregation
+//   z   = agg + (1 + eps) * x                              GINEConv.forward
+// and the autograd of that chain.
+//
+// Layout: one "row group" of L lanes owns one node; lane t holds float4 chunks
+// t, t+L, ... of the node's D channels, so every row read/written is a run of D*4
+// contiguous bytes (512 B at D=128: two nodes per wave, 16 B per lane).  The node's edge
+// list (neighbour id + edge attribute) is staged through LDS (one coalesced load by the
+// group's lanes, then broadcast reads), and U neighbour rows are kept in flight per lane
+// before the sequential accumulation, so the gather is latency-hidden without splitting a
+// destination's sum.  Accumulation order is the CSR order = original edge order, hence
+// bit-identical to CPU scatter_add_ / index_add_.
+#include "gine_common.hpp"
+
+namespace gine {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+
+template <int C>
+struct MpUnroll {
+  static constexpr int value = C == 1 ? 8 : (C == 2 ? 4 : 2);
+};
+
+// ----------------------------------------------------------------------------------------
+// Forward
+// ----------------------------------------------------------------------------------------
+template <int L, int C>
+__global__ __launch_bounds__(kThreads) void k_mp_fwd(
+    const float4* __restrict__ x4, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ nbr, const float* __restrict__ attr,
+    const float4* __restrict__ lw4, const float4* __restrict__ lb4,
+    const float* __restrict__ eps, float4* __restrict__ z4, int64_t N, int D4) {
+  constexpr int GPW = kWave / L;  // nodes per wave
+  constexpr int U = MpUnroll<C>::value;
+  __shared__ int32_t s_nbr[kWaves][kWave];
+  __shared__ float s_attr[kWaves][kWave];
+
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int g = lane / L, t = lane % L;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t node = (int64_t)tile * (kWaves * GPW) + wave * GPW + g;
+  if (node >= N) return;  // whole row group leaves together; no block barrier below
+
+  // Lanes past the last float4 (D/4 not a multiple of L) duplicate the last chunk so that
+  // every load is issued unconditionally; only their stores are masked.
+  float4 w[C], b[C], self[C], acc[C];
+  int qc[C];
+  const int64_t row = node * D4;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    qc[c] = min(t + c * L, D4 - 1);
+    acc[c] = f4_zero();
+    w[c] = lw4[qc[c]];
+    b[c] = lb4[qc[c]];
+    self[c] = x4[row + qc[c]];
+  }
+  const float ope = 1.0f + eps[0];
+  const int beg = rowptr[node], end = rowptr[node + 1];
+  int32_t* my_nbr = &s_nbr[wave][g * L];
+  float* my_attr = &s_attr[wave][g * L];
+
+  for (int base = beg; base < end; base += L) {
+    const int cnt = min(L, end - base);
+    if (t < cnt) {
+      my_nbr[t] = nbr[base + t];
+      my_attr[t] = attr[base + t];
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int j = 0; j < cnt; j += U) {
+      float4 r[U][C];
+      float a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = min(j + u, cnt - 1);  // clamp: loads are always issued (no branch)
+        const int64_t src_row = (int64_t)my_nbr[jj] * D4;
+        a[u] = my_attr[jj];
+#pragma unroll
+        for (int c = 0; c < C; ++c) r[u][c] = x4[src_row + qc[c]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (j + u < cnt) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            // m = relu(x_j + (a*W + b)); the K=1 Linear rounds once (fma), the add rounds
+            // once, the sum rounds once per edge in edge order.
+            acc[c].x = acc[c].x + relu_nan(r[u][c].x + __builtin_fmaf(a[u], w[c].x, b[c].x));
+            acc[c].y = acc[c].y + relu_nan(r[u][c].y + __builtin_fmaf(a[u], w[c].y, b[c].y));
+            acc[c].z = acc[c].z + relu_nan(r[u][c].z + __builtin_fmaf(a[u], w[c].z, b[c].z));
+            acc[c].w = acc[c].w + relu_nan(r[u][c].w + __builtin_fmaf(a[u], w[c].w, b[c].w));
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int q = t + c * L;
+    if (q < D4) {
+      float4 o;
+      o.x = acc[c].x + ope * self[c].x;
+      o.y = acc[c].y + ope * self[c].y;
+      o.z = acc[c].z + ope * self[c].z;
+      o.w = acc[c].w + ope * self[c].w;
+      z4[row + q] = o;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Backward over the out-edge CSR (source-sorted, stable)
+// ----------------------------------------------------------------------------------------
+template <int L, int C>
+__global__ __launch_bounds__(kThreads) void k_mp_bwd(
+    const float4* __restrict__ dz4, const float4* __restrict__ x4,
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ nbr,
+    const float* __restrict__ attr, const float4* __restrict__ lw4,
+    const float4* __restrict__ lb4, const float* __restrict__ eps,
+    const float4* __restrict__ dres4, float4* __restrict__ dx4, double* __restrict__ partials,
+    int64_t N, int D4, int num_tiles, int flags) {
+  constexpr int GPW = kWave / L;
+  constexpr int U = MpUnroll<C>::value;
+  __shared__ int32_t s_nbr[kWaves][kWave];
+  __shared__ float s_attr[kWaves][kWave];
+  extern __shared__ __attribute__((aligned(16))) double s_red[];  // [3][D]
+
+  const int D = D4 * 4;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int g = lane / L, t = lane % L;
+  const float ope = 1.0f + eps[0];
+  const bool add_self = (flags & GINE_MP_BWD_SELF) != 0;
+
+  float4 w[C], b[C];
+  int qc[C];
+  double pw[C][4], pb[C][4], pe[C][4];  // sum dm*a, sum dm, sum dz*x
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    qc[c] = min(t + c * L, D4 - 1);
+    w[c] = lw4[qc[c]];
+    b[c] = lb4[qc[c]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pw[c][k] = pb[c][k] = pe[c][k] = 0.0;
+  }
+  int32_t* my_nbr = &s_nbr[wave][g * L];
+  float* my_attr = &s_attr[wave][g * L];
+
+  // Tiles are split into 8 contiguous XCD ranges; the blocks of one XCD stride its range.
+  const int nb = gridDim.x;
+  const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
+  const int blocks_here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
+  const int span = (num_tiles + kNumXcd - 1) / kNumXcd;
+  const int t_begin = xcd * span, t_end = min(num_tiles, t_begin + span);
+
+  for (int tile = t_begin + pos; tile < t_end; tile += blocks_here) {
+    const int64_t node = (int64_t)tile * (kWaves * GPW) + wave * GPW + g;
+    if (node >= N) continue;
+    const int64_t row = node * D4;
+    float4 h[C], g_self[C], acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      acc[c] = f4_zero();
+      h[c] = x4[row + qc[c]];
+      g_self[c] = dz4[row + qc[c]];
+    }
+    // pre-activation of this node's outgoing messages: h + (a*W + b) depends on the edge
+    // only through a, so h is loaded once per source node.
+    const int beg = rowptr[node], end = rowptr[node + 1];
+    for (int base = beg; base < end; base += L) {
+      const int cnt = min(L, end - base);
+      if (t < cnt) {
+        my_nbr[t] = nbr[base + t];
+        my_attr[t] = attr[base + t];
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (int j = 0; j < cnt; j += U) {
+        float4 r[U][C];
+        float a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int jj = min(j + u, cnt - 1);
+          const int64_t dst_row = (int64_t)my_nbr[jj] * D4;
+          a[u] = my_attr[jj];
+#pragma unroll
+          for (int c = 0; c < C; ++c) r[u][c] = dz4[dst_row + qc[c]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (j + u < cnt) {
+            const double ad = (double)a[u];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+              float dm[4];
+              dm[0] = (h[c].x + __builtin_fmaf(a[u], w[c].x, b[c].x) > 0.f) ? r[u][c].x : 0.f;
+              dm[1] = (h[c].y + __builtin_fmaf(a[u], w[c].y, b[c].y) > 0.f) ? r[u][c].y : 0.f;
+              dm[2] = (h[c].z + __builtin_fmaf(a[u], w[c].z, b[c].z) > 0.f) ? r[u][c].z : 0.f;
+              dm[3] = (h[c].w + __builtin_fmaf(a[u], w[c].w, b[c].w) > 0.f) ? r[u][c].w : 0.f;
+              acc[c].x = acc[c].x + dm[0];
+              acc[c].y = acc[c].y + dm[1];
+              acc[c].z = acc[c].z + dm[2];
+              acc[c].w = acc[c].w + dm[3];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                pw[c][k] += (double)dm[k] * ad;
+                pb[c][k] += (double)dm[k];
+              }
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int q = t + c * L;
+      if (q < D4) {
+        float4 o = acc[c];
+        if (add_self) {
+          o.x = o.x + ope * g_self[c].x;
+          o.y = o.y + ope * g_self[c].y;
+          o.z = o.z + ope * g_self[c].z;
+          o.w = o.w + ope * g_self[c].w;
+        }
+        if (dres4 != nullptr) {
+          const float4 d = dres4[row + q];
+          o.x = o.x + d.x;
+          o.y = o.y + d.y;
+          o.z = o.z + d.z;
+          o.w = o.w + d.w;
+        }
+        dx4[row + q] = o;
+        pe[c][0] += (double)g_self[c].x * (double)h[c].x;
+        pe[c][1] += (double)g_self[c].y * (double)h[c].y;
+        pe[c][2] += (double)g_self[c].z * (double)h[c].z;
+        pe[c][3] += (double)g_self[c].w * (double)h[c].w;
+      }
+    }
+  }
+
+  // Block reduction of the parameter-gradient partials: row groups of a wave first
+  // (butterfly over lanes t, t+L, ...), then the waves in fixed order through LDS.
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int m = L; m < kWave; m <<= 1) {
+        pw[c][k] += shfl_xor_d(pw[c][k], m);
+        pb[c][k] += shfl_xor_d(pb[c][k], m);
+        pe[c][k] += shfl_xor_d(pe[c][k], m);
+      }
+    }
+  }
+  for (int wv = 0; wv < kWaves; ++wv) {
+    if (wave == wv && g == 0) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int q = t + c * L;
+        if (q < D4) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int ch = q * 4 + k;
+            if (wv == 0) {
+              s_red[ch] = pw[c][k];
+              s_red[D + ch] = pb[c][k];
+              s_red[2 * D + ch] = pe[c][k];
+            } else {
+              s_red[ch] += pw[c][k];
+              s_red[D + ch] += pb[c][k];
+              s_red[2 * D + ch] += pe[c][k];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  double* out = partials + (size_t)blockIdx.x * 3 * D;
+  for (int i = threadIdx.x; i < 3 * D; i += kThreads) out[i] = s_red[i];
+}
+
+__global__ __launch_bounds__(kThreads) void k_mp_bwd_finalize(
+    const double* __restrict__ partials, int P, int D, float* __restrict__ dlin_w,
+    float* __restrict__ dlin_b, float* __restrict__ deps) {
+  __shared__ double s_eps[kThreads];
+  double e_acc = 0.0;
+  for (int c = threadIdx.x; c < D; c += kThreads) {
+    double sw = 0.0, sb = 0.0, se = 0.0;
+    for (int p = 0; p < P; ++p) {
+      const double* row = partials + (size_t)p * 3 * D;
+      sw += row[c];
+      sb += row[D + c];
+      se += row[2 * D + c];
+    }
+    dlin_w[c] = (float)sw;
+    dlin_b[c] = (float)sb;
+    e_acc += se;
+  }
+  s_eps[threadIdx.x] = e_acc;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) s_eps[threadIdx.x] += s_eps[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) deps[0] = (float)s_eps[0];
+}
+
+// ----------------------------------------------------------------------------------------
+// Host dispatch
+// ----------------------------------------------------------------------------------------
+struct Shape {
+  int L, C;
+};
+
+inline bool pick_shape(int D, Shape* s) {
+  if (D <= 0 || D % 4 != 0 || D > 1024) return false;
+  const int D4 = D / 4;
+  if (D4 <= 64) {
+    int L = 1;
+    while (L < D4) L <<= 1;
+    s->L = L;
+    s->C = 1;
+  } else {
+    s->L = 64;
+    s->C = (D4 + 63) / 64;
+  }
+  return true;
+}
+
+inline int nodes_per_block(const Shape& s) { return kWaves * (kWave / s.L); }
+
+constexpr int kMaxBwdBlocks = 1024;
+
+inline int bwd_grid(int64_t N, const Shape& s) {
+  const int64_t tiles = ceil_div(N, nodes_per_block(s));
+  int64_t g = tiles < kMaxBwdBlocks ? tiles : kMaxBwdBlocks;
+  return (int)(g > 0 ? g : 1);
+}
+
+#define GINE_MP_DISPATCH(SHAPE, MACRO)                                          \
+  switch ((SHAPE).C) {                                                          \
+    case 1:                                                                     \
+      switch ((SHAPE).L) {                                                      \
+        case 1: MACRO(1, 1); break;                                             \
+        case 2: MACRO(2, 1); break;                                             \
+        case 4: MACRO(4, 1); break;                                             \
+        case 8: MACRO(8, 1); break;                                             \
+        case 16: MACRO(16, 1); break;                                           \
+        case 32: MACRO(32, 1); break;                                           \
+        default: MACRO(64, 1); break;                                           \
+      }                                                                         \
+      break;                                                                    \
+    case 2: MACRO(64, 2); break;                                                \
+    case 3: MACRO(64, 3); break;                                                \
+    default: MACRO(64, 4); break;                                               \
+  }
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_mp_fwd(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                           const float* in_attr, const float* lin_w, const float* lin_b,
+                           const float* eps, float* z, int64_t num_nodes, int32_t channels,
+                           void* stream) {
+  Shape sh;
+  if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
+  if (num_nodes < 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (num_nodes == 0) return GINE_OK;
+  if (!x || !in_rowptr || !lin_w || !lin_b || !eps || !z) return GINE_ERR_INVALID;
+  const int D4 = channels / 4;
+  const int64_t tiles = ceil_div(num_nodes, nodes_per_block(sh));
+  hipStream_t s = as_stream(stream);
+#define LAUNCH_FWD(L_, C_)                                                                  \
+  hipLaunchKernelGGL((k_mp_fwd<L_, C_>), dim3((unsigned)tiles), dim3(kThreads), 0, s,      \
+                     (const float4*)x, in_rowptr, in_src, in_attr, (const float4*)lin_w,    \
+                     (const float4*)lin_b, eps, (float4*)z, num_nodes, D4)
+  GINE_MP_DISPATCH(sh, LAUNCH_FWD);
+#undef LAUNCH_FWD
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_mp_bwd_num_partials(int64_t num_nodes, int32_t channels,
+                                        int32_t* num_partials) {
+  Shape sh;
+  if (!num_partials) return GINE_ERR_INVALID;
+  if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
+  if (num_nodes < 0) return GINE_ERR_INVALID;
+  *num_partials = bwd_grid(num_nodes, sh);
+  return GINE_OK;
+}
+
+extern "C" int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_rowptr,
+                           const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                           const float* lin_b, const float* eps, const float* dres, float* dx,
+                           double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                           void* stream) {
+  Shape sh;
+  if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
+  if (num_nodes < 0 || (flags & ~GINE_MP_BWD_SELF) != 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (!dz || !x || !out_rowptr || !lin_w || !lin_b || !eps || !dx || !partials)
+    return GINE_ERR_INVALID;
+  const int D4 = channels / 4;
+  const int grid = bwd_grid(num_nodes, sh);
+  const int tiles = (int)ceil_div(num_nodes, nodes_per_block(sh));
+  const size_t smem = sizeof(double) * 3 * (size_t)channels;
+  hipStream_t s = as_stream(stream);
+#define LAUNCH_BWD(L_, C_)                                                                   \
+  hipLaunchKernelGGL((k_mp_bwd<L_, C_>), dim3((unsigned)grid), dim3(kThreads), smem, s,     \
+                     (const float4*)dz, (const float4*)x, out_rowptr, out_dst, out_attr,     \
+                     (const float4*)lin_w, (const float4*)lin_b, eps, (const float4*)dres,   \
+                     (float4*)dx, partials, num_nodes, D4, tiles, flags)
+  GINE_MP_DISPATCH(sh, LAUNCH_BWD);
+#undef LAUNCH_BWD
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_mp_bwd_finalize(const double* partials, int32_t num_partials,
+                                    int32_t channels, float* dlin_w, float* dlin_b,
+                                    float* deps, void* stream) {
+  if (num_partials < 0 || channels <= 0) return GINE_ERR_INVALID;
+  if (!partials || !dlin_w || !dlin_b || !deps) return GINE_ERR_INVALID;
+  hipLaunchKernelGGL(k_mp_bwd_finalize, dim3(1), dim3(kThreads), 0, as_stream(stream),
+                     partials, num_partials, channels, dlin_w, dlin_b, deps);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

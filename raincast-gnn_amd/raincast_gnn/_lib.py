@@ -1,0 +1,111 @@
+"""ctypes binding of ``libgine_hip.so`` (the C ABI declared in ``include/gine_hip.h``).
+
+The library is loaded lazily on first use and never replaced by a fallback: when it is
+missing or a device is absent every op raises.  ``torch`` is imported first on purpose --
+its bundled ``libamdhip64.so`` (SONAME ``libamdhip64.so.7``) must be the runtime our library
+binds to, so both share one HIP runtime, one set of streams and one caching allocator.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (load order: torch's HIP runtime first)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GINE_HIP_LIB", os.path.join(_HERE, "_native", "libgine_hip.so"))
+
+GINE_OK = 0
+GINE_ERR_HIP_BASE = 1000
+GINE_MP_BWD_SELF = 1
+EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
+ABI_VERSION = 1
+
+_c_void_p = ctypes.c_void_p
+_i32, _i64, _f32, _size = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+
+# name -> argtypes (every entry point returns int status)
+_SIGNATURES = {
+    "gine_graph_workspace_bytes": [_i64, _i64, ctypes.POINTER(_size)],
+    "gine_graph_build": [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p,
+                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size, _c_void_p],
+    "gine_mp_fwd": [_c_void_p] * 8 + [_i64, _i32, _c_void_p],
+    "gine_mp_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
+    "gine_mp_bwd": [_c_void_p] * 11 + [_i64, _i32, _i32, _c_void_p],
+    "gine_mp_bwd_finalize": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "gine_mlp_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
+    "gine_mlp_fwd1": [_c_void_p] * 5 + [_i64, _i32, _c_void_p],
+    "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,
+                                                                   _i32, _c_void_p],
+    "gine_mlp_fwd2": [_c_void_p] * 7 + [_i64, _i32, _i32, _c_void_p],
+    "gine_mlp_bwd2": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
+    "gine_bn_bwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 5 + [_i64, _i32, _i32, _c_void_p],
+    "gine_mlp_bwd1": [_c_void_p] * 6 + [_i64, _i32, _c_void_p],
+    "gine_mlp_wgrad_num_chunks": [_i64, _i32, ctypes.POINTER(_i32)],
+    "gine_mlp_wgrad": [_c_void_p] * 13 + [_i64, _i32, _i32, _c_void_p],
+}
+
+EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)
+
+_lock = threading.Lock()
+_lib = None
+
+
+class GineError(RuntimeError):
+    """A native entry point returned a non-zero status."""
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load and type the shared library (idempotent).  Raises when it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise GineError(
+                f"native GINE library not found at {p}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        lib = ctypes.CDLL(p)
+        lib.gine_abi_version.restype = ctypes.c_int
+        lib.gine_abi_version.argtypes = []
+        lib.gine_status_string.restype = ctypes.c_char_p
+        lib.gine_status_string.argtypes = [ctypes.c_int]
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = ctypes.c_int
+            fn.argtypes = argtypes
+        if lib.gine_abi_version() != ABI_VERSION:
+            raise GineError(f"ABI mismatch: library {lib.gine_abi_version()} != {ABI_VERSION}")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != GINE_OK:
+        msg = load().gine_status_string(status).decode()
+        raise GineError(f"{what} failed with status {status}: {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def ptr(t) -> int | None:
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise GineError(
+            f"{what}: the MI355X GINE engine runs on HIP devices only (got a {t.device} tensor); "
+            "there is no CPU fallback")

@@ -1,0 +1,186 @@
+"""Autograd bindings of the gfx950 GINE kernels.
+
+Two functions sit behind ``GINEConv``:
+
+* :class:`GineMessagePassing` -- ``z = scatter_add(relu(x[src] + lin(a))) + (1 + eps) * x``,
+  i.e. PyG ``GINEConv.forward`` up to ``self.nn`` (upstream gine_conv.py; call sites
+  models/gnn.py:41,44).  Used with any ``nn``.
+* :class:`GineLayer` -- the same plus the node MLP ``Linear -> BatchNorm1d -> ReLU -> Linear``
+  (models/gnn.py:21-26) and optionally ResGnn's outer ReLU / residual (models/gnn.py:38-44),
+  all in HIP.  Used when ``nn`` has exactly that structure.
+
+Every kernel launch goes to the current HIP stream of the tensors' device; backward runs on
+PyTorch's autograd device thread and touches no thread-local state.  Nothing here falls
+back to CPU: a tensor on another device raises.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = _lib.EPI_NONE, _lib.EPI_RELU, _lib.EPI_RESIDUAL_RELU
+
+
+def _count(fn: str, n: int, d: int) -> int:
+    out = ctypes.c_int32(0)
+    call(fn, n, d, ctypes.byref(out))
+    return int(out.value)
+
+
+def _as_vec(p: torch.Tensor) -> torch.Tensor:
+    """Linear(1, D).weight [D, 1] / bias [D] -> contiguous fp32 [D] view."""
+    return p.detach().reshape(-1).contiguous()
+
+
+def mp_forward(x, graph, lin_w, lin_b, eps):
+    N, D = x.shape
+    z = torch.empty_like(x)
+    if N == 0:
+        return z
+    call("gine_mp_fwd", ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
+         ptr(lin_w), ptr(lin_b), ptr(eps), ptr(z), N, D, _lib.stream_handle(x.device))
+    return z
+
+
+def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True):
+    """Returns (dx, dlin_w[D], dlin_b[D], deps[1])."""
+    N, D = x.shape
+    dev = x.device
+    dx = torch.empty_like(x)
+    dlw = torch.empty(D, dtype=torch.float32, device=dev)
+    dlb = torch.empty(D, dtype=torch.float32, device=dev)
+    deps = torch.empty(1, dtype=torch.float32, device=dev)
+    if N == 0:
+        return dx, dlw.zero_(), dlb.zero_(), deps.zero_()
+    P = _count("gine_mp_bwd_num_partials", N, D)
+    partials = torch.empty(P, 3, D, dtype=torch.float64, device=dev)
+    stream = _lib.stream_handle(dev)
+    call("gine_mp_bwd", ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst),
+         ptr(graph.out_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx),
+         ptr(partials), N, D, _lib.GINE_MP_BWD_SELF if self_term else 0, stream)
+    call("gine_mp_bwd_finalize", ptr(partials), P, D, ptr(dlw), ptr(dlb), ptr(deps), stream)
+    return dx, dlw, dlb, deps
+
+
+class GineMessagePassing(torch.autograd.Function):
+    """z = sum_{e: dst_e = i} relu(x[src_e] + a_e * W_e + b_e) + (1 + eps) * x_i."""
+
+    @staticmethod
+    def forward(ctx, x, lin_w, lin_b, eps, graph):
+        x = x.contiguous()
+        lw, lb, ep = _as_vec(lin_w), _as_vec(lin_b), eps.detach().contiguous()
+        z = mp_forward(x, graph, lw, lb, ep)
+        ctx.save_for_backward(x, lw, lb, ep)
+        ctx.graph = graph
+        ctx.lin_w_shape = lin_w.shape
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, lw, lb, ep = ctx.saved_tensors
+        dx, dlw, dlb, deps = mp_backward(dz.contiguous(), x, ctx.graph, lw, lb, ep)
+        return dx, dlw.view(ctx.lin_w_shape), dlb, deps.view_as(ep), None
+
+
+class BnConfig:
+    """What GineLayer needs from a BatchNorm1d module (torch semantics)."""
+
+    __slots__ = ("running_mean", "running_var", "num_batches_tracked", "momentum", "eps",
+                 "use_batch_stats", "update_running")
+
+    def __init__(self, bn: torch.nn.BatchNorm1d):
+        self.running_mean = bn.running_mean
+        self.running_var = bn.running_var
+        self.num_batches_tracked = bn.num_batches_tracked
+        self.momentum = -1.0 if bn.momentum is None else float(bn.momentum)
+        self.eps = float(bn.eps)
+        # torch: batch statistics in training mode, or when no running stats are tracked
+        self.use_batch_stats = bn.training or (bn.running_mean is None and bn.running_var is None)
+        self.update_running = bn.training and bn.track_running_stats
+
+
+class GineLayer(torch.autograd.Function):
+    """y = epilogue( Linear2( ReLU( BN( Linear1( z ) ) ) ) ),  z = GINE message passing.
+
+    epilogue: EPI_NONE -> o, EPI_RELU -> relu(o), EPI_RESIDUAL_RELU -> x + relu(o).
+    """
+
+    @staticmethod
+    def forward(ctx, x, lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2, graph, bn, epilogue):
+        x = x.contiguous()
+        N, D = x.shape
+        dev = x.device
+        stream = _lib.stream_handle(dev)
+        lw, lb, ep = _as_vec(lin_w), _as_vec(lin_b), eps.detach().contiguous()
+        w1c, b1c, w2c, b2c = (t.detach().contiguous() for t in (w1, b1, w2, b2))
+        g = gamma.detach().contiguous() if gamma is not None else None
+        bt = beta.detach().contiguous() if beta is not None else None
+        if bn.use_batch_stats and N <= 1:
+            raise ValueError(
+                f"Expected more than 1 value per channel when training, got input size "
+                f"{torch.Size([N, D])}")
+
+        z = mp_forward(x, graph, lw, lb, ep)
+        a1 = torch.empty_like(x)
+        P = _count("gine_mlp_num_partials", N, D)
+        partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
+        call("gine_mlp_fwd1", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), ptr(partials), N, D, stream)
+        bn_save = torch.empty(4, D, dtype=torch.float32, device=dev)
+        call("gine_bn_fwd_finalize", ptr(partials), P, ptr(g), ptr(bt), ptr(bn.running_mean),
+             ptr(bn.running_var), ptr(bn.num_batches_tracked) if bn.update_running else None,
+             ptr(bn_save), N, D, bn.momentum, bn.eps, int(bn.use_batch_stats),
+             int(bn.update_running and bn.running_mean is not None), stream)
+        y = torch.empty_like(x)
+        mask = (torch.empty(N, D, dtype=torch.uint8, device=dev)
+                if epilogue == EPI_RESIDUAL_RELU else None)
+        call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2c), ptr(b2c), ptr(x), ptr(y),
+             ptr(mask), N, D, epilogue, stream)
+
+        ctx.save_for_backward(x, z, a1, y if epilogue == EPI_RELU else None, mask, bn_save,
+                              lw, lb, ep, w1c, w2c, g)
+        ctx.graph, ctx.epilogue = graph, epilogue
+        ctx.use_batch_stats = bn.use_batch_stats
+        ctx.shapes = (lin_w.shape, gamma is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, a1, y, mask, bn_save, lw, lb, ep, w1c, w2c, g = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, D = x.shape
+        dev = x.device
+        stream = _lib.stream_handle(dev)
+        epi = ctx.epilogue
+
+        dbn = torch.empty_like(x)
+        P = _count("gine_mlp_num_partials", N, D)
+        partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
+        call("gine_mlp_bwd2", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save), ptr(w2c),
+             ptr(dbn), ptr(partials), N, D, epi, stream)
+        dgamma = torch.empty(D, dtype=torch.float32, device=dev)
+        dbeta = torch.empty(D, dtype=torch.float32, device=dev)
+        coef = torch.empty(3, D, dtype=torch.float32, device=dev)
+        call("gine_bn_bwd_finalize", ptr(partials), P, ptr(g), ptr(bn_save), ptr(dgamma),
+             ptr(dbeta), ptr(coef), N, D, int(ctx.use_batch_stats), stream)
+        dz = torch.empty_like(x)
+        call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save), ptr(coef), ptr(w1c), ptr(dz), N,
+             D, stream)
+        C = _count("gine_mlp_wgrad_num_chunks", N, D)
+        slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
+        dw1 = torch.empty(D, D, dtype=torch.float32, device=dev)
+        dw2 = torch.empty(D, D, dtype=torch.float32, device=dev)
+        db1 = torch.empty(D, dtype=torch.float32, device=dev)
+        db2 = torch.empty(D, dtype=torch.float32, device=dev)
+        call("gine_mlp_wgrad", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save), ptr(dbn),
+             ptr(coef), ptr(z), ptr(slab), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), N, D, epi,
+             stream)
+        dres = dy if epi == EPI_RESIDUAL_RELU else None
+        dx, dlw, dlb, deps = mp_backward(dz, x, ctx.graph, lw, lb, ep, dres=dres)
+        lin_w_shape, affine = ctx.shapes
+        return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1,
+                dgamma if affine else None, dbeta if affine else None, dw2, db2,
+                None, None, None)

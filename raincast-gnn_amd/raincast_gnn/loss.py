@@ -1,0 +1,173 @@
+"""CRPS losses of the reference (models/loss.py), restated for device execution.
+
+Same closed forms, same dtype promotions (the censoring point ``c = log(0.01)`` is a float64
+tensor, so every term that touches it -- and the loss -- is float64, loss.py:33-34,
+230-231), same NaN semantics: rows whose target is NaN do not contribute.  The reference
+drops them with boolean indexing (``mu[mask]``, loss.py:39-42, 234-239), which needs a
+device->host sync for the result shape; here NaN targets are replaced by 0 before the
+closed form and the mean is taken over the valid rows with a masked sum, so a training
+step contains no host sync and can be captured in a HIP graph.  The masked rows get exactly
+zero gradient, as in the reference.  ``torch.distributions.Normal`` (which validates its
+arguments with a host sync) is replaced by its own cdf/log_prob formulas for loc 0, scale 1.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+_LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
+# NormalCRPS keeps 1/sqrt(pi) as an fp32 tensor (loss.py:343): same value as a Python float
+_INV_SQRT_PI_F32 = float(1 / torch.sqrt(torch.tensor(np.pi)))
+
+
+def _cdf(v: torch.Tensor) -> torch.Tensor:
+    # Normal(0, 1).cdf: 0.5 * (1 + erf((v - loc) * scale.reciprocal() / sqrt(2)))
+    return 0.5 * (1 + torch.erf(v / math.sqrt(2)))
+
+
+def _pdf(v: torch.Tensor) -> torch.Tensor:
+    # Normal(0, 1).log_prob(v).exp(): -(v - loc)**2 / (2 var) - log(scale) - log(sqrt(2 pi))
+    return torch.exp(-(v ** 2) / 2 - _LOG_SQRT_2PI)
+
+
+class _Consts:
+    """Per-device 1-element constant tensors, created once (a host->device copy inside a
+    captured step would be illegal), with the reference's dtypes: ``torch.tensor([c])`` of
+    a Python/NumPy float gives float64 for np.float64 and float32 for a plain float."""
+
+    def __init__(self):
+        self._cache = {}
+
+    def get(self, value, device) -> torch.Tensor:
+        key = (repr(value), type(value).__name__, str(device))
+        t = self._cache.get(key)
+        if t is None:
+            t = torch.tensor([value], device=device)
+            self._cache[key] = t
+        return t
+
+
+_consts = _Consts()
+
+
+def _finish(crps: torch.Tensor, mask: torch.Tensor, reduce: bool) -> torch.Tensor:
+    if not reduce:  # reference shape: only the rows with a target, [M, 1]
+        return crps[mask]
+    return _masked_mean(crps, mask)
+
+
+def _masked_mean(values: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    m = mask.reshape(values.shape)
+    total = torch.where(m, values, torch.zeros_like(values)).sum()
+    return total / m.sum().to(values.dtype)
+
+
+def _prepare(prediction: torch.Tensor, y: torch.Tensor, width: int):
+    mask = ~torch.isnan(y)
+    cols = torch.split(prediction, 1, dim=1)
+    if len(cols) != width:
+        raise ValueError(f"prediction must have {width} columns, got {prediction.size(1)}")
+    y_safe = torch.where(mask, y, torch.zeros_like(y)).unsqueeze(1)
+    return mask, cols, y_safe
+
+
+class NormalCRPS(torch.nn.Module):
+    """models/loss.py:335-369."""
+
+    def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        mask, (mu, sigma), y1 = _prepare(prediction, y, 2)
+        z = (y1 - mu) / sigma
+        crps = sigma * (z * (2.0 * _cdf(z) - 1.0) + 2.0 * _pdf(z) - _INV_SQRT_PI_F32)
+        return _finish(crps, mask, True)
+
+
+class MixedNormalCRPS(torch.nn.Module):
+    """Censored normal with a point mass p at c, models/loss.py:6-68."""
+
+    def __init__(self, reduce: bool = True, c: float = np.log(0.01)):
+        super().__init__()
+        self.reduce = reduce
+        self.c = c
+
+    def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        mask, (mu, sigma, p), y1 = _prepare(prediction, y, 3)
+        c = _consts.get(self.c, y.device)  # float64: np.float64 is a float
+        y_t = (y1 - mu) / sigma
+        c_t = (c - mu) / sigma
+        P_c = p + (1 - p) * _cdf(c_t)
+        t1 = y_t * (2 * (p + (1 - p) * _cdf(y_t)) - 1)
+        t2 = -c_t * torch.pow(P_c, 2)
+        t3 = 2 * (1 - p) * (-_pdf(c_t)) * P_c
+        t4 = -2 * (1 - p) * (-_pdf(y_t))
+        t5 = (2 * torch.pow(1 - p, 2) * (-1 / (2 * math.sqrt(math.pi)))
+              * (1 - _cdf(math.sqrt(2) * c_t)))
+        crps = sigma * (t1 + t2 + t3 + t4 + t5)
+        return _finish(crps, mask, self.reduce)
+
+
+class MixedLoss(torch.nn.Module):
+    """Censored normal body + generalised Pareto tail above u, models/loss.py:71-272."""
+
+    def __init__(self, grad_u: bool, xi: float, u=None, reduce: bool = True, t: float = 5,
+                 c=np.log(0.01)):
+        super().__init__()
+        self.reduce, self.c, self.grad_u, self.u, self.xi, self.t = reduce, c, grad_u, u, xi, t
+
+    @staticmethod
+    def _gpd(x_re, xi):
+        return torch.where(x_re <= 0, 0, 1 - (1 + xi * x_re).pow(-1 / xi))
+
+    @staticmethod
+    def _delta_u(u_t, p):
+        return p + (1 - p) * _cdf(u_t)
+
+    def _pareto_crps(self, y, u, m, sigma, xi):
+        y_t = (y - u) / sigma
+        cdf = self._gpd(y_t, xi)
+        return sigma * (torch.abs(y_t) - 2 * (1 - m) / (1 - xi) * (1 - torch.pow(1 - cdf, 1 - xi))
+                        + torch.pow(1 - m, 2) / (2 - xi))
+
+    @staticmethod
+    def _body(p, c_t, u_t):
+        P_c = p + (1 - p) * _cdf(c_t)
+        P_u = (1 - p) * (1 - _cdf(u_t))
+        t2 = -c_t * torch.pow(P_c, 2) + u_t * torch.pow(P_u, 2)
+        t3 = 2 * (1 - p) * (-_pdf(c_t)) * P_c + 2 * (1 - p) * (-_pdf(u_t)) * P_u
+        t5 = (2 * torch.pow(1 - p, 2) * (-1 / (2 * math.sqrt(math.pi)))
+              * (_cdf(math.sqrt(2) * u_t) - _cdf(math.sqrt(2) * c_t)))
+        return P_u, t2, t3, t5
+
+    def _mixed_normal_crps(self, y_t, p, c_t, u_t, sigma):
+        _, t2, t3, t5 = self._body(p, c_t, u_t)
+        t1 = y_t * (2 * (p + (1 - p) * _cdf(y_t)) - 1)
+        t4 = -2 * (1 - p) * (-_pdf(y_t))
+        return sigma * (t1 + t2 + t3 + t4 + t5)
+
+    def _mixed_normal_crps_upper(self, p, c_t, u_t, sigma):
+        P_u, t2, t3, t5 = self._body(p, c_t, u_t)
+        t4 = -2 * ((1 - p) * (-_pdf(u_t)) + u_t * P_u)
+        return sigma * (u_t + t2 + t3 + t4 + t5)
+
+    def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if self.grad_u == True:  # noqa: E712  (reference compares with == True, loss.py:227)
+            mask, (mu, sigma, p, sigma_u, u), y1 = _prepare(prediction, y, 5)
+        else:
+            mask, (mu, sigma, p, sigma_u), y1 = _prepare(prediction, y, 4)
+            u = _consts.get(self.u, y.device)
+        c = _consts.get(self.c, y.device)
+        xi = _consts.get(self.xi, y.device)
+        c_t = (c - mu) / sigma
+        u_t = (u - mu) / sigma
+        y_t = (y1 - mu) / sigma
+        m_u = self._delta_u(u_t, p)
+        loss_1 = (self._mixed_normal_crps(y_t, p, c_t, u_t, sigma)
+                  + self._pareto_crps(u, u, m_u, sigma_u, xi))
+        loss_2 = (self._pareto_crps(y1, u, m_u, sigma_u, xi)
+                  + self._mixed_normal_crps_upper(p, c_t, u_t, sigma))
+        if self.grad_u:
+            crps = torch.sigmoid((u - y1) * self.t) * (loss_1 - loss_2) + loss_2
+        else:
+            crps = torch.where(y1 < u, loss_1, loss_2)
+        return _finish(crps, mask, self.reduce)

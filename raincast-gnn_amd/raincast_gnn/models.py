@@ -1,0 +1,114 @@
+"""The station-graph GNN of models/gnn.py on the MI355X GINE engine.
+
+Structure, constructor arguments and state_dict keys follow models/gnn.py exactly, so a
+checkpoint saved by the reference (train.py:203) loads here and vice versa; the only change
+is that ``GINEConv`` comes from this package instead of torch_geometric (gnn.py:5), and
+ResGnn's outer ReLU / residual add are fused into the last GEMM of each GINE layer.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+from torch.nn import Linear, ModuleList, ReLU
+
+from .loss import MixedLoss, MixedNormalCRPS, NormalCRPS
+from .nn import GINEConv
+from .postprocess import PostProcess
+
+
+class ResGnn(nn.Module):
+    """models/gnn.py:10-45: a stack of GINEConv(Linear-BN-ReLU-Linear) with residuals."""
+
+    def __init__(self, in_channels: int, out_channels: int, num_layers: int,
+                 hidden_channels: int):
+        super().__init__()
+        assert num_layers > 0, "num_layers must be > 0."
+        self.convolutions = ModuleList()
+        out = hidden_channels
+        for layer in range(num_layers):
+            mlp = nn.Sequential(Linear(in_channels, hidden_channels),
+                                nn.BatchNorm1d(hidden_channels), ReLU(),
+                                Linear(hidden_channels, out))
+            self.convolutions.append(GINEConv(nn=mlp, train_eps=True, edge_dim=1))
+            if layer == num_layers - 1:  # kept for parity; has no effect
+                out = out_channels
+        self.relu = ReLU()
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor,
+                edge_attr: torch.Tensor) -> torch.Tensor:
+        x = x.float()
+        edge_attr = edge_attr.float()
+        for i, conv in enumerate(self.convolutions):
+            if i == 0:
+                x = conv.forward_relu(x, edge_index, edge_attr)            # relu(conv(x))
+            else:
+                x = conv.forward_residual_relu(x, edge_index, edge_attr)   # x + relu(conv(x))
+        return x
+
+
+class DeepSetEncoder(nn.Module):
+    """models/gnn.py:48-68: phi per member, sum over members, rho."""
+
+    def __init__(self, ensemble_in_dim, hidden_channels, out_channels):
+        super().__init__()
+        self.phi = nn.Sequential(nn.Linear(ensemble_in_dim, hidden_channels), nn.ReLU(),
+                                 nn.Linear(hidden_channels, hidden_channels))
+        self.rho = nn.Sequential(nn.Linear(hidden_channels, hidden_channels), nn.ReLU(),
+                                 nn.Linear(hidden_channels, out_channels))
+
+    def forward(self, ensemble_feats):
+        return self.rho(self.phi(ensemble_feats).sum(dim=1))
+
+
+def make_loss(loss: str, grad_u, u, xi):
+    """gnn.py:91-103: loss object and number of distribution parameters."""
+    if loss == "NormalCRPS":
+        return NormalCRPS(), 2
+    if loss == "MixedNormalCRPS":
+        return MixedNormalCRPS(), 3
+    if loss == "MixedLoss":
+        if grad_u == "True":
+            return MixedLoss(grad_u=True, xi=xi), 5
+        return MixedLoss(grad_u=False, u=u, xi=xi), 4
+    raise ValueError(f"unknown loss '{loss}'")
+
+
+class GNN(nn.Module):
+    """models/gnn.py:70-141 (the Lightning-style helpers at gnn.py:143-168 are dead code in
+    the reference -- nn.Module has no ``log`` -- and are not reproduced)."""
+
+    def __init__(self, in_channels, hidden_channels_gnn, out_channels_gnn, num_layers_gnn,
+                 optimizer_class=None, optimizer_params=None, loss="MixedLoss", grad_u=False,
+                 u=0.5, xi=0.5):
+        super().__init__()
+        self.loss, self.grad_u, self.u, self.xi = loss, grad_u, u, xi
+        self.loss_fn, self.out_channels = make_loss(loss, grad_u, u, xi)
+        self.deepset = DeepSetEncoder(ensemble_in_dim=in_channels,
+                                      hidden_channels=hidden_channels_gnn,
+                                      out_channels=hidden_channels_gnn)
+        self.dim_red = Linear(in_channels + hidden_channels_gnn, hidden_channels_gnn)
+        self.conv = ResGnn(in_channels=hidden_channels_gnn, hidden_channels=hidden_channels_gnn,
+                           out_channels=hidden_channels_gnn, num_layers=num_layers_gnn)
+        self.aggr = nn.Linear(out_channels_gnn, self.out_channels)
+        self.postprocess = PostProcess(self.loss, self.grad_u)
+        self.optimizer_class = optimizer_class
+        self.optimizer_params = optimizer_params
+
+    def forward(self, data):
+        emb = self.deepset(data.ensemble)
+        h = self.dim_red(torch.cat([data.x, emb], dim=1))
+        h = self.conv(h, data.edge_index, data.edge_attr)
+        return self.postprocess(self.aggr(h))
+
+    def configure_optimizers(self):
+        return self.optimizer_class(self.parameters(), **self.optimizer_params)
+
+
+def gnn_from_params(params: dict, in_channels: int = 35, **overrides) -> GNN:
+    """Build the model the way train.py:168-179 does from a params.json dict."""
+    cfg = dict(params)
+    cfg.update(overrides)
+    return GNN(in_channels=in_channels, hidden_channels_gnn=cfg["gnn_hidden"],
+               out_channels_gnn=cfg["gnn_hidden"], num_layers_gnn=cfg["gnn_layers"],
+               optimizer_class=torch.optim.AdamW, optimizer_params={"lr": cfg["lr"]},
+               loss=cfg["loss"], grad_u=cfg["grad_u"], u=cfg["u"], xi=cfg["xi"])

@@ -1,0 +1,64 @@
+"""CPU: the C-ABI library loads and exports every symbol include/gine_hip.h declares.
+
+No compute calls (no GPU here); only the host-side argument validation, which returns
+before any HIP call.
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+from raincast_gnn import _lib
+
+HEADER = os.path.join(ROOT, "include", "gine_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(gine_\w+)\s*\(", text, re.M)))
+
+
+def test_header_and_binding_agree():
+    decl = declared_symbols()
+    assert len(decl) >= 17
+    assert sorted(_lib.EXPORTED_SYMBOLS) == decl
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.gine_abi_version() == _lib.ABI_VERSION
+    out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
+    exported = set(re.findall(r"\bT (gine_\w+)", out))
+    assert set(declared_symbols()) <= exported
+
+
+def test_status_strings():
+    lib = _lib.load()
+    assert lib.gine_status_string(0) == b"ok"
+    assert b"channel" in lib.gine_status_string(2)
+    assert lib.gine_status_string(12345) != b""
+
+
+def test_host_validation_without_device():
+    lib = _lib.load()
+    # unsupported channel counts are rejected before any HIP call
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 10, 6, None) == 2
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 10, 2048, None) == 2
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, -1, 8, None) == 1
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 0, 8, None) == 0
+    n = ctypes.c_int32(0)
+    assert lib.gine_mlp_num_partials(1000, 48, ctypes.byref(n)) == 2
+    assert lib.gine_mlp_num_partials(1000, 128, ctypes.byref(n)) == 0 and n.value > 0
+    assert lib.gine_mp_bwd_num_partials(16000, 128, ctypes.byref(n)) == 0 and n.value > 0
+    assert lib.gine_mlp_wgrad_num_chunks(16000, 128, ctypes.byref(n)) == 0 and n.value > 0
+    with pytest.raises(_lib.GineError, match="channel"):
+        _lib.check(2, "probe")
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(_lib.GineError, match="not found"):
+        _lib.load(str(tmp_path / "nope.so"))

@@ -1,0 +1,337 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bit-exact: graph build, message-passing forward z, message-passing backward dx (index_add_
+order).  Everything with a reduction over nodes or a GEMM: max-norm relative 1e-5 vs the
+fp32 CPU oracle, with an fp64 oracle tie-break (tests/helpers.py).
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import assert_close_tiebreak, knn_batch_graph, random_graph, rel_err, special_graphs
+from oracle import gine_cpu as O
+from raincast_gnn import GINEConv, _lib, functional as Fn
+from raincast_gnn.graph import GineGraph
+from raincast_gnn.models import GNN, ResGnn
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL = 1e-5
+
+
+def _mp_params(D, seed=0, eps=0.1):
+    g = torch.Generator().manual_seed(seed)
+    lw = torch.randn(D, 1, generator=g) * 0.5
+    lb = torch.randn(D, generator=g) * 0.5
+    return lw, lb, torch.tensor([eps])
+
+
+# ---------------------------------------------------------------------------------------
+# graph build
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case", special_graphs(), ids=lambda c: c[0])
+def test_graph_build_matches_stable_sort(case):
+    _, ei, ea, n = case
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    E = ei.size(1)
+    for key, other, rowptr, nbr, attr in ((1, 0, g.in_rowptr, g.in_src, g.in_attr),
+                                          (0, 1, g.out_rowptr, g.out_dst, g.out_attr)):
+        perm = np.argsort(ei[key].numpy(), kind="stable")
+        counts = np.bincount(ei[key].numpy(), minlength=n)
+        exp_rowptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+        assert np.array_equal(rowptr.cpu().numpy(), exp_rowptr)
+        if E:
+            assert np.array_equal(nbr.cpu().numpy()[:E], ei[other].numpy()[perm].astype(np.int32))
+            assert np.array_equal(attr.cpu().numpy()[:E], ea.reshape(-1).numpy()[perm])
+
+
+def test_graph_build_rejects_out_of_range():
+    ei = torch.tensor([[0, 1, 5], [1, 2, 0]], device=DEV)
+    with pytest.raises(IndexError):
+        GineGraph(ei, torch.ones(3, 1, device=DEV), 3)
+    ei = torch.tensor([[0, -1], [1, 0]], device=DEV)
+    with pytest.raises(IndexError):
+        GineGraph(ei, torch.ones(2, 1, device=DEV), 3)
+
+
+# ---------------------------------------------------------------------------------------
+# message passing: bit-exact
+# ---------------------------------------------------------------------------------------
+@pytest.mark.parametrize("case", special_graphs(), ids=lambda c: c[0])
+@pytest.mark.parametrize("D", [4, 64, 128, 96, 260])
+def test_mp_forward_bit_exact(case, D):
+    _, ei, ea, n = case
+    torch.manual_seed(D)
+    x = torch.randn(n, D)
+    lw, lb, eps = _mp_params(D, seed=D)
+    z_ref = O.gine_aggregate(x, ei, ea, lw, lb, eps)
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    z = Fn.mp_forward(x.to(DEV), g, lw.reshape(-1).to(DEV), lb.to(DEV), eps.to(DEV))
+    assert torch.equal(z.cpu(), z_ref), f"max diff {(z.cpu() - z_ref).abs().max().item()}"
+
+
+def test_mp_forward_matches_loop_restatement():
+    ei, ea, n = random_graph(30, 200, seed=9)
+    x = torch.randn(n, 8)
+    lw, lb, eps = _mp_params(8, seed=2, eps=-0.3)
+    z_loop = O.gine_aggregate_loops(x, ei, ea, lw, lb, eps)
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    z = Fn.mp_forward(x.to(DEV), g, lw.reshape(-1).to(DEV), lb.to(DEV), eps.to(DEV))
+    assert torch.equal(z.cpu(), z_loop)
+
+
+@pytest.mark.parametrize("case", special_graphs(), ids=lambda c: c[0])
+@pytest.mark.parametrize("D", [64, 128, 36])
+def test_mp_backward(case, D):
+    _, ei, ea, n = case
+    torch.manual_seed(100 + D)
+    x = torch.randn(n, D, requires_grad=True)
+    lw, lb, eps = _mp_params(D, seed=D + 1, eps=0.25)
+    lw.requires_grad_(True)
+    lb.requires_grad_(True)
+    eps.requires_grad_(True)
+    z = O.gine_aggregate(x, ei, ea, lw, lb, eps)
+    dz = torch.randn_like(z)
+    z.backward(dz)
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    xd = x.detach().to(DEV)
+    dx, dlw, dlb, deps = Fn.mp_backward(dz.to(DEV), xd, g, lw.detach().reshape(-1).to(DEV),
+                                        lb.detach().to(DEV), eps.detach().to(DEV))
+    # index_add_ order + two-term sum with (1+eps)*dz: bit-identical to CPU autograd
+    assert torch.equal(dx.cpu(), x.grad), f"max diff {(dx.cpu() - x.grad).abs().max().item()}"
+    # fp64 reference for the parameter reductions
+    x64 = x.detach().double().requires_grad_(False)
+    lw64, lb64, e64 = (t.detach().double().requires_grad_(True) for t in (lw, lb, eps))
+    O.gine_aggregate(x64, ei, ea.double(), lw64, lb64, e64).backward(dz.double())
+    for name, got, ref32, ref64 in (("dlin_w", dlw, lw.grad.reshape(-1), lw64.grad.reshape(-1)),
+                                    ("dlin_b", dlb, lb.grad, lb64.grad),
+                                    ("deps", deps, eps.grad, e64.grad)):
+        if ref32.abs().max() == 0:
+            assert got.abs().max().item() == 0
+            continue
+        assert_close_tiebreak(got.cpu(), ref32, ref64, TOL, name)
+
+
+def test_mp_deterministic():
+    ei, ea, n = random_graph(3000, 60000, seed=11)
+    x = torch.randn(n, 128, device=DEV)
+    lw, lb, eps = (t.to(DEV) for t in _mp_params(128))
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    dz = torch.randn(n, 128, device=DEV)
+    r1 = Fn.mp_backward(dz, x, g, lw.reshape(-1), lb, eps)
+    r2 = Fn.mp_backward(dz, x, g, lw.reshape(-1), lb, eps)
+    z1 = Fn.mp_forward(x, g, lw.reshape(-1), lb, eps)
+    z2 = Fn.mp_forward(x, g, lw.reshape(-1), lb, eps)
+    assert torch.equal(z1, z2)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------------------------------
+# GINE layer with the fused node MLP
+# ---------------------------------------------------------------------------------------
+def _make_pair(D, seed):
+    torch.manual_seed(seed)
+    mlp = torch.nn.Sequential(torch.nn.Linear(D, D), torch.nn.BatchNorm1d(D), torch.nn.ReLU(),
+                              torch.nn.Linear(D, D))
+    conv = GINEConv(nn=mlp, train_eps=True, edge_dim=1)
+    with torch.no_grad():
+        conv.eps.fill_(0.125)
+        mlp[1].weight.uniform_(0.5, 1.5)
+        mlp[1].bias.uniform_(-0.2, 0.2)
+        mlp[1].running_mean.uniform_(-0.1, 0.1)
+        mlp[1].running_var.uniform_(0.5, 2.0)
+    ref = O.OracleGINEConv(copy.deepcopy(mlp), train_eps=True, edge_dim=1)
+    ref.load_state_dict(conv.state_dict())
+    return conv.to(DEV), ref
+
+
+def _oracle_layer(ref, x, ei, ea, epilogue, dtype):
+    r = copy.deepcopy(ref).to(dtype)
+    xx = x.detach().to(dtype).requires_grad_(True)
+    o = r(xx, ei, ea.to(dtype))
+    if epilogue == "relu":
+        o = torch.relu(o)
+    elif epilogue == "residual":
+        o = xx + torch.relu(o)
+    return r, xx, o
+
+
+@pytest.mark.parametrize("D", [128, 64, 32, 256])
+@pytest.mark.parametrize("epilogue", ["none", "relu", "residual"])
+@pytest.mark.parametrize("training", [True, False])
+def test_gine_layer_fused(D, epilogue, training):
+    ei, ea, n = knn_batch_graph(300, 8, 2, seed=D)
+    conv, ref = _make_pair(D, seed=D + len(epilogue))
+    conv.train(training)
+    ref.train(training)
+    x = torch.randn(n, D)
+    dy = torch.randn(n, D)
+    outs = {}
+    for dtype in (torch.float32, torch.float64):
+        r, xx, o = _oracle_layer(ref, x, ei, ea, epilogue, dtype)
+        o.backward(dy.to(dtype))
+        outs[dtype] = (r, xx, o)
+    xd = x.to(DEV).requires_grad_(True)
+    eid, ead = ei.to(DEV), ea.to(DEV)
+    fn = {"none": conv.forward, "relu": conv.forward_relu,
+          "residual": conv.forward_residual_relu}[epilogue]
+    y = fn(xd, eid, ead)
+    y.backward(dy.to(DEV))
+    r32, x32, o32 = outs[torch.float32]
+    r64, x64, o64 = outs[torch.float64]
+    assert_close_tiebreak(y.detach().cpu(), o32.detach(), o64.detach(), TOL, "y")
+    assert_close_tiebreak(xd.grad.cpu(), x32.grad, x64.grad, TOL, "dx")
+    p_gpu = dict(conv.named_parameters())
+    p32, p64 = dict(r32.named_parameters()), dict(r64.named_parameters())
+    for name in p32:
+        assert_close_tiebreak(p_gpu[name].grad.cpu(), p32[name].grad, p64[name].grad, TOL, name)
+    bn_gpu, bn32 = conv.nn[1], r32.nn[1]
+    for buf in ("running_mean", "running_var"):
+        assert rel_err(getattr(bn_gpu, buf).cpu(), getattr(bn32, buf)) <= TOL, buf
+    assert int(bn_gpu.num_batches_tracked) == int(bn32.num_batches_tracked)
+
+
+def test_generic_nn_path():
+    """An nn the fused path does not cover (D=48, GELU): HIP message passing + torch nn."""
+    D = 48
+    ei, ea, n = knn_batch_graph(100, 6, 1, seed=5)
+    torch.manual_seed(0)
+    mlp = torch.nn.Sequential(torch.nn.Linear(D, 24), torch.nn.GELU(), torch.nn.Linear(24, 16))
+    conv = GINEConv(nn=mlp, train_eps=True, edge_dim=1)
+    ref = O.OracleGINEConv(copy.deepcopy(mlp), train_eps=True, edge_dim=1)
+    ref.load_state_dict(conv.state_dict())
+    conv = conv.to(DEV)
+    x = torch.randn(n, D)
+    xd = x.to(DEV).requires_grad_(True)
+    out = conv(xd, ei.to(DEV), ea.to(DEV))
+    xr = x.clone().requires_grad_(True)
+    outr = ref(xr, ei, ea)
+    assert rel_err(out.cpu(), outr) <= TOL
+    g = torch.randn_like(outr)
+    out.backward(g.to(DEV))
+    outr.backward(g)
+    assert rel_err(xd.grad.cpu(), xr.grad) <= TOL
+
+
+def test_layer_deterministic_and_errors():
+    conv, _ = _make_pair(128, seed=1)
+    ei, ea, n = knn_batch_graph(500, 10, 4, seed=1)
+    x = torch.randn(n, 128, device=DEV, requires_grad=True)
+    eid, ead = ei.to(DEV), ea.to(DEV)
+    conv.eval()  # no running-stat drift between the two runs
+    res = []
+    for _ in range(2):
+        x.grad = None
+        conv.zero_grad()
+        y = conv.forward_residual_relu(x, eid, ead)
+        y.square().sum().backward()
+        res.append([y.detach().clone(), x.grad.clone()] +
+                   [p.grad.clone() for p in conv.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    with pytest.raises(_lib.GineError):
+        conv(x.detach().cpu(), ei, ea)
+    conv.train()
+    with pytest.raises(ValueError):
+        conv(x[:1].detach(), torch.zeros(2, 0, dtype=torch.long, device=DEV),
+             torch.zeros(0, 1, device=DEV))
+
+
+# ---------------------------------------------------------------------------------------
+# full models
+# ---------------------------------------------------------------------------------------
+def _oracle_gnn_from(model: GNN, params) -> O.OracleGNN:
+    ref = O.OracleGNN(35, params["gnn_hidden"], params["gnn_layers"], params["loss"],
+                      params["grad_u"], params["u"], params["xi"])
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()},
+                        strict=True)
+    return ref
+
+
+@pytest.mark.parametrize("experiment", ["24h_mixed", "72h_mixed_u", "120h_normal_mixed",
+                                        "24h_normal"])
+def test_training_step_matches_oracle(experiment):
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.params import EXPERIMENTS
+    params = dict(EXPERIMENTS[experiment])
+    torch.manual_seed(42)
+    model = GNN(35, params["gnn_hidden"], params["gnn_hidden"], params["gnn_layers"],
+                loss=params["loss"], grad_u=params["grad_u"], u=params["u"], xi=params["xi"])
+    ref = _oracle_gnn_from(model, params)
+    batch = synthetic_batch(500, 2, k=10, seed=7)
+    model = model.to(DEV).train()
+    ref.train()
+    pred = model(batch.to(DEV))
+    loss = model.loss_fn.crps(pred, batch.y.to(DEV))
+    loss.backward()
+    pred_r = ref(batch)
+    loss_r = ref.crps(pred_r, batch.y)
+    loss_r.backward()
+    assert loss.dtype == loss_r.dtype
+    assert rel_err(pred.detach().cpu(), pred_r.detach()) <= 1e-4
+    assert abs(loss.item() - loss_r.item()) <= 1e-5 * abs(loss_r.item())
+    pr = dict(ref.named_parameters())
+    worst = 0.0
+    for name, p in model.named_parameters():
+        e = rel_err(p.grad.cpu(), pr[name].grad)
+        worst = max(worst, e)
+        assert e <= 1e-4, f"{name}: {e:.3e}"
+    print(f"{experiment}: worst grad rel err {worst:.2e}")
+
+
+def test_resgnn_stack_matches_oracle():
+    ei, ea, n = knn_batch_graph(500, 10, 3, seed=2)
+    torch.manual_seed(3)
+    net = ResGnn(128, 128, 4, 128)
+    ref = O.OracleResGnn(128, 128, 4, 128)
+    ref.load_state_dict(net.state_dict())
+    net = net.to(DEV)
+    x = torch.randn(n, 128)
+    y = net(x.to(DEV), ei.to(DEV), ea.to(DEV))
+    yr = ref(x, ei, ea)
+    ref64 = copy.deepcopy(ref).double()
+    y64 = ref64(x.double(), ei, ea.double())
+    assert_close_tiebreak(y.detach().cpu(), yr.detach(), y64.detach(), TOL, "resgnn")
+
+
+def test_graph_capture_replay_matches_eager():
+    """Whole training step (fwd + loss + bwd + AdamW) captured in one HIP graph: replays
+    follow the same trajectory as eager steps from the same initial state."""
+    from raincast_gnn.data import synthetic_batch
+    torch.manual_seed(0)
+    base = GNN(35, 128, 128, 4, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5)
+    batch = synthetic_batch(500, 4, k=10, seed=1).to(DEV)
+
+    def make():
+        m = copy.deepcopy(base).to(DEV)
+        return m, torch.optim.AdamW(m.parameters(), lr=1e-3, capturable=True)
+
+    def step(m, opt):
+        opt.zero_grad(set_to_none=False)
+        loss = m.loss_fn.crps(m(batch), batch.y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    m_e, o_e = make()
+    eager = [step(m_e, o_e).item() for _ in range(5)]
+
+    m_g, o_g = make()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        warm = [step(m_g, o_g).item() for _ in range(2)]
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_loss = step(m_g, o_g)
+    replayed = []
+    for _ in range(3):
+        g.replay()
+        replayed.append(static_loss.item())
+    got = warm + replayed
+    for a, b in zip(got, eager):
+        assert abs(a - b) <= 1e-6 * abs(b), (got, eager)

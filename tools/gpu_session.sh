@@ -1,0 +1,39 @@
+#!/usr/bin/env bash
+# One GPU session on the gpurun box: each GPU step has its own time limit; a crash-class exit
+# (fault/abort/segv/timeout) ends the session, ordinary test failures do not.
+#   tools/gpu_session.sh <tag> [steps...]   steps: tests smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-run}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+STEPS=${*:-tests smoke bench prof}
+
+run() {  # run <name> <seconds> cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))" | tee -a "$OUT/session.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(date +%T))" | tee -a "$OUT/session.log"
+  tail -5 "$OUT/$name.log" | tee -a "$OUT/session.log"
+  case $rc in
+    0|1) return 0 ;;   # pass / test failures: keep going
+    *) echo "crash-class exit $rc: stopping session" | tee -a "$OUT/session.log"; exit $rc ;;
+  esac
+}
+
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+               python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -- \
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -- \
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ;;
+  esac
+done
+echo "session done" | tee -a "$OUT/session.log"
