@@ -136,6 +136,7 @@ def time_kernels(tr: Trainer, reps: int):
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     from raincast_gnn._lib import call, ptr
+    lin = Fn.edge_linear_flag()
     P = Fn._count("gine_mlp_num_partials", N, D)
     partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
     a1 = torch.empty_like(x)
@@ -167,11 +168,12 @@ def time_kernels(tr: Trainer, reps: int):
 
     kernels = {
         "gine_mp_fwd": (lambda: call("gine_mp_fwd", ptr(x), ptr(g.in_rowptr), ptr(g.in_src),
-                                     ptr(g.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(z), N, D, sh),
+                                     ptr(g.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(z), N, D,
+                                     lin, sh),
                         {"bytes": 4 * (2 * N * D + 2 * E + N + 1)}),
         "gine_mp_bwd": (lambda: call("gine_mp_bwd", ptr(dz), ptr(x), ptr(g.out_rowptr),
                                      ptr(g.out_dst), ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep),
-                                     ptr(dz), ptr(dx), ptr(mp_part), N, D, 1, sh),
+                                     ptr(dz), ptr(dx), ptr(mp_part), N, D, 1 | lin, sh),
                         {"bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D}),
         "gine_mlp_fwd1": (lambda: call("gine_mlp_fwd1", ptr(z), ptr(w1), ptr(b1), ptr(a1),
                                        ptr(partials), N, D, sh),

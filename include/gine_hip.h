@@ -65,25 +65,29 @@ int gine_graph_build(const int64_t* edge_index, const float* edge_attr, int64_t 
 
 /* ------------------------------------------------------------------------------------
  * Message passing forward.  Replaces GINEConv.forward up to (excluding) self.nn:
- *   m_e  = relu(x[src_e] + fma(a_e, lin_w, lin_b))        (GINEConv.message, lin=Linear(1,D))
+ *   m_e  = relu(x[src_e] + lin(a_e))                      (GINEConv.message, lin=Linear(1,D))
  *   agg_i = sum over in-edges of i, original edge order   (SumAggregation / scatter_add_)
  *   z_i  = agg_i + (1 + eps) * x_i                         (out + (1 + self.eps) * x_r)
- * Bit-identical to the CPU path (sequential per-destination order, single-rounding fma
- * for the K=1 Linear, no contraction elsewhere).
+ * Bit-identical to the CPU path (sequential per-destination order, no contraction).
+ * The K=1 Linear's rounding is host-dependent in the reference itself: MKL's sgemm rounds
+ * a*w+b once (fma) on Intel CPUs and twice (mul, then add) on AMD EPYC hosts, so the mode
+ * is a flag: GINE_MP_LIN_MULADD selects mul-then-add, otherwise fma.
  *   x [N, D], lin_w [D] (Linear(1,D).weight flattened), lin_b [D], eps [1] (device), z [N, D]
  * Supported D: multiple of 4, 4 <= D <= 1024.
  * ---------------------------------------------------------------------------------- */
+#define GINE_MP_LIN_MULADD 2
 int gine_mp_fwd(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                 const float* in_attr, const float* lin_w, const float* lin_b, const float* eps,
-                float* z, int64_t num_nodes, int32_t channels, void* stream);
+                float* z, int64_t num_nodes, int32_t channels, int32_t flags, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Message passing backward (autograd of gine_mp_fwd), over the out-edge CSR:
- *   dm_e   = dz[dst_e] * 1[x[j] + fma(a_e, lin_w, lin_b) > 0]      (gather + relu bwd)
+ *   dm_e   = dz[dst_e] * 1[x[j] + lin(a_e) > 0]                    (gather + relu bwd)
  *   dx_j   = sum over out-edges of j in original order of dm_e   (index_add_, bit-exact)
  *            [+ (1 + eps) * dz_j  if flags & GINE_MP_BWD_SELF]
  *            [+ dres_j            if dres != NULL]
  *   partials[b] (fp64, [3][D] per block b): sum dm*a, sum dm, sum dz*x for the block
+ *   flags may also carry GINE_MP_LIN_MULADD (must match the forward).
  * gine_mp_bwd_finalize reduces the partials in fixed block order into
  *   dlin_w [D], dlin_b [D], deps [1].
  * ---------------------------------------------------------------------------------- */

@@ -54,9 +54,11 @@ def gine_aggregate(x, edge_index, edge_attr, lin_w, lin_b, eps):
     return agg + (1 + eps) * x
 
 
-def gine_aggregate_loops(x, edge_index, edge_attr, lin_w, lin_b, eps):
+def gine_aggregate_loops(x, edge_index, edge_attr, lin_w, lin_b, eps, rounding="fma"):
     """Independent per-edge restatement (small inputs only): sequential float32 sums in
-    original edge order, fma for the K=1 Linear (np.float32 arithmetic per element)."""
+    original edge order (np.float32 arithmetic per element).  ``rounding`` is how the host's
+    CPU Linear(1, D) rounds a*w+b: "fma" (one rounding; MKL on Intel) or "muladd" (two;
+    MKL on AMD EPYC) -- see tools/probe_cpu_rounding.py."""
     xn = x.detach().numpy().astype(np.float32)
     ei = edge_index.numpy()
     a = edge_attr.detach().reshape(-1).numpy().astype(np.float32)
@@ -67,7 +69,10 @@ def gine_aggregate_loops(x, edge_index, edge_attr, lin_w, lin_b, eps):
     agg = np.zeros((N, D), dtype=np.float32)
     for e in range(ei.shape[1]):
         s, d = ei[0, e], ei[1, e]
-        lin = (np.float64(a[e]) * np.float64(w) + np.float64(b)).astype(np.float32)  # one rounding
+        if rounding == "fma":
+            lin = (np.float64(a[e]) * np.float64(w) + np.float64(b)).astype(np.float32)
+        else:
+            lin = ((a[e] * w).astype(np.float32) + b).astype(np.float32)
         pre = (xn[s] + lin).astype(np.float32)
         m = np.where(pre > 0, pre, np.float32(0)).astype(np.float32)
         agg[d] = (agg[d] + m).astype(np.float32)
@@ -112,8 +117,10 @@ class OracleResGnn(nn.Module):
         self.relu = nn.ReLU()
 
     def forward(self, x, edge_index, edge_attr):
-        x = x.float()
-        edge_attr = edge_attr.float()
+        # models/gnn.py:36-37 casts to fp32; the fp64 tie-break copy keeps its own dtype
+        dt = self.convolutions[0].lin.weight.dtype
+        x = x.to(dt)
+        edge_attr = edge_attr.to(dt)
         for i, conv in enumerate(self.convolutions):
             h = self.relu(conv(x, edge_index, edge_attr))
             x = h if i == 0 else x + h
@@ -199,7 +206,7 @@ def crps_mixed(pred, y, grad_u, u=None, xi=0.5, t=5, c=np.log(0.01)):
     else:
         mu, sigma, p, su = (v[keep] for v in cols)
         uu = torch.tensor([u])
-    yy = y.unsqueeze(1)[keep]
+    yy = y.unsqueeze(1)[keep].to(pred.dtype)
     xit = torch.tensor([xi])
     ct = (torch.tensor([c]) - mu) / sigma
     ut = (uu - mu) / sigma

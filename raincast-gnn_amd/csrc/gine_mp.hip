@@ -23,6 +23,13 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
 
+// Edge Linear(1, D): a*w + b, rounded like the host CPU's PyG path (see gine_hip.h).
+template <bool FMA>
+__device__ __forceinline__ float edge_lin(float a, float w, float b) {
+  if constexpr (FMA) return __builtin_fmaf(a, w, b);
+  return a * w + b;  // -ffp-contract=off: two roundings
+}
+
 template <int C>
 struct MpUnroll {
   static constexpr int value = C == 1 ? 8 : (C == 2 ? 4 : 2);
@@ -31,7 +38,7 @@ struct MpUnroll {
 // ----------------------------------------------------------------------------------------
 // Forward
 // ----------------------------------------------------------------------------------------
-template <int L, int C>
+template <int L, int C, bool FMA>
 __global__ __launch_bounds__(kThreads) void k_mp_fwd(
     const float4* __restrict__ x4, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ nbr, const float* __restrict__ attr,
@@ -89,12 +96,12 @@ __global__ __launch_bounds__(kThreads) void k_mp_fwd(
         if (j + u < cnt) {
 #pragma unroll
           for (int c = 0; c < C; ++c) {
-            // m = relu(x_j + (a*W + b)); the K=1 Linear rounds once (fma), the add rounds
-            // once, the sum rounds once per edge in edge order.
-            acc[c].x = acc[c].x + relu_nan(r[u][c].x + __builtin_fmaf(a[u], w[c].x, b[c].x));
-            acc[c].y = acc[c].y + relu_nan(r[u][c].y + __builtin_fmaf(a[u], w[c].y, b[c].y));
-            acc[c].z = acc[c].z + relu_nan(r[u][c].z + __builtin_fmaf(a[u], w[c].z, b[c].z));
-            acc[c].w = acc[c].w + relu_nan(r[u][c].w + __builtin_fmaf(a[u], w[c].w, b[c].w));
+            // m = relu(x_j + lin(a)); the add rounds once, the sum rounds once per edge in
+            // edge order.
+            acc[c].x = acc[c].x + relu_nan(r[u][c].x + edge_lin<FMA>(a[u], w[c].x, b[c].x));
+            acc[c].y = acc[c].y + relu_nan(r[u][c].y + edge_lin<FMA>(a[u], w[c].y, b[c].y));
+            acc[c].z = acc[c].z + relu_nan(r[u][c].z + edge_lin<FMA>(a[u], w[c].z, b[c].z));
+            acc[c].w = acc[c].w + relu_nan(r[u][c].w + edge_lin<FMA>(a[u], w[c].w, b[c].w));
           }
         }
       }
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_fwd(
 // ----------------------------------------------------------------------------------------
 // Backward over the out-edge CSR (source-sorted, stable)
 // ----------------------------------------------------------------------------------------
-template <int L, int C>
+template <int L, int C, bool FMA>
 __global__ __launch_bounds__(kThreads) void k_mp_bwd(
     const float4* __restrict__ dz4, const float4* __restrict__ x4,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ nbr,
@@ -198,10 +205,10 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
 #pragma unroll
             for (int c = 0; c < C; ++c) {
               float dm[4];
-              dm[0] = (h[c].x + __builtin_fmaf(a[u], w[c].x, b[c].x) > 0.f) ? r[u][c].x : 0.f;
-              dm[1] = (h[c].y + __builtin_fmaf(a[u], w[c].y, b[c].y) > 0.f) ? r[u][c].y : 0.f;
-              dm[2] = (h[c].z + __builtin_fmaf(a[u], w[c].z, b[c].z) > 0.f) ? r[u][c].z : 0.f;
-              dm[3] = (h[c].w + __builtin_fmaf(a[u], w[c].w, b[c].w) > 0.f) ? r[u][c].w : 0.f;
+              dm[0] = (h[c].x + edge_lin<FMA>(a[u], w[c].x, b[c].x) > 0.f) ? r[u][c].x : 0.f;
+              dm[1] = (h[c].y + edge_lin<FMA>(a[u], w[c].y, b[c].y) > 0.f) ? r[u][c].y : 0.f;
+              dm[2] = (h[c].z + edge_lin<FMA>(a[u], w[c].z, b[c].z) > 0.f) ? r[u][c].z : 0.f;
+              dm[3] = (h[c].w + edge_lin<FMA>(a[u], w[c].w, b[c].w) > 0.f) ? r[u][c].w : 0.f;
               acc[c].x = acc[c].x + dm[0];
               acc[c].y = acc[c].y + dm[1];
               acc[c].z = acc[c].z + dm[2];
@@ -344,22 +351,29 @@ inline int bwd_grid(int64_t N, const Shape& s) {
   return (int)(g > 0 ? g : 1);
 }
 
-#define GINE_MP_DISPATCH(SHAPE, MACRO)                                          \
+#define GINE_MP_DISPATCH_L(SHAPE, MACRO, F)                                     \
   switch ((SHAPE).C) {                                                          \
     case 1:                                                                     \
       switch ((SHAPE).L) {                                                      \
-        case 1: MACRO(1, 1); break;                                             \
-        case 2: MACRO(2, 1); break;                                             \
-        case 4: MACRO(4, 1); break;                                             \
-        case 8: MACRO(8, 1); break;                                             \
-        case 16: MACRO(16, 1); break;                                           \
-        case 32: MACRO(32, 1); break;                                           \
-        default: MACRO(64, 1); break;                                           \
+        case 1: MACRO(1, 1, F); break;                                          \
+        case 2: MACRO(2, 1, F); break;                                          \
+        case 4: MACRO(4, 1, F); break;                                          \
+        case 8: MACRO(8, 1, F); break;                                          \
+        case 16: MACRO(16, 1, F); break;                                        \
+        case 32: MACRO(32, 1, F); break;                                        \
+        default: MACRO(64, 1, F); break;                                        \
       }                                                                         \
       break;                                                                    \
-    case 2: MACRO(64, 2); break;                                                \
-    case 3: MACRO(64, 3); break;                                                \
-    default: MACRO(64, 4); break;                                               \
+    case 2: MACRO(64, 2, F); break;                                             \
+    case 3: MACRO(64, 3, F); break;                                             \
+    default: MACRO(64, 4, F); break;                                            \
+  }
+
+#define GINE_MP_DISPATCH(SHAPE, FMA_FLAG, MACRO)                                \
+  if (FMA_FLAG) {                                                               \
+    GINE_MP_DISPATCH_L(SHAPE, MACRO, true)                                      \
+  } else {                                                                      \
+    GINE_MP_DISPATCH_L(SHAPE, MACRO, false)                                     \
   }
 
 }  // namespace
@@ -370,21 +384,22 @@ using namespace gine;
 extern "C" int gine_mp_fwd(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                            const float* in_attr, const float* lin_w, const float* lin_b,
                            const float* eps, float* z, int64_t num_nodes, int32_t channels,
-                           void* stream) {
+                           int32_t flags, void* stream) {
   Shape sh;
   if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
-  if (num_nodes < 0) return GINE_ERR_INVALID;
+  if (num_nodes < 0 || (flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
   if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   if (num_nodes == 0) return GINE_OK;
   if (!x || !in_rowptr || !lin_w || !lin_b || !eps || !z) return GINE_ERR_INVALID;
   const int D4 = channels / 4;
   const int64_t tiles = ceil_div(num_nodes, nodes_per_block(sh));
   hipStream_t s = as_stream(stream);
-#define LAUNCH_FWD(L_, C_)                                                                  \
-  hipLaunchKernelGGL((k_mp_fwd<L_, C_>), dim3((unsigned)tiles), dim3(kThreads), 0, s,      \
+  const bool fma = (flags & GINE_MP_LIN_MULADD) == 0;
+#define LAUNCH_FWD(L_, C_, F_)                                                              \
+  hipLaunchKernelGGL((k_mp_fwd<L_, C_, F_>), dim3((unsigned)tiles), dim3(kThreads), 0, s,      \
                      (const float4*)x, in_rowptr, in_src, in_attr, (const float4*)lin_w,    \
                      (const float4*)lin_b, eps, (float4*)z, num_nodes, D4)
-  GINE_MP_DISPATCH(sh, LAUNCH_FWD);
+  GINE_MP_DISPATCH(sh, fma, LAUNCH_FWD);
 #undef LAUNCH_FWD
   GINE_LAUNCH_STATUS();
   return GINE_OK;
@@ -407,7 +422,8 @@ extern "C" int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_r
                            void* stream) {
   Shape sh;
   if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
-  if (num_nodes < 0 || (flags & ~GINE_MP_BWD_SELF) != 0) return GINE_ERR_INVALID;
+  if (num_nodes < 0 || (flags & ~(GINE_MP_BWD_SELF | GINE_MP_LIN_MULADD)) != 0)
+    return GINE_ERR_INVALID;
   if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   if (!dz || !x || !out_rowptr || !lin_w || !lin_b || !eps || !dx || !partials)
     return GINE_ERR_INVALID;
@@ -416,12 +432,13 @@ extern "C" int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_r
   const int tiles = (int)ceil_div(num_nodes, nodes_per_block(sh));
   const size_t smem = sizeof(double) * 3 * (size_t)channels;
   hipStream_t s = as_stream(stream);
-#define LAUNCH_BWD(L_, C_)                                                                   \
-  hipLaunchKernelGGL((k_mp_bwd<L_, C_>), dim3((unsigned)grid), dim3(kThreads), smem, s,     \
+  const bool fma = (flags & GINE_MP_LIN_MULADD) == 0;
+#define LAUNCH_BWD(L_, C_, F_)                                                               \
+  hipLaunchKernelGGL((k_mp_bwd<L_, C_, F_>), dim3((unsigned)grid), dim3(kThreads), smem, s,     \
                      (const float4*)dz, (const float4*)x, out_rowptr, out_dst, out_attr,     \
                      (const float4*)lin_w, (const float4*)lin_b, eps, (const float4*)dres,   \
                      (float4*)dx, partials, num_nodes, D4, tiles, flags)
-  GINE_MP_DISPATCH(sh, LAUNCH_BWD);
+  GINE_MP_DISPATCH(sh, fma, LAUNCH_BWD);
 #undef LAUNCH_BWD
   GINE_LAUNCH_STATUS();
   return GINE_OK;

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("GINE_HIP_LIB", os.path.join(_HERE, "_native", "libgin
 GINE_OK = 0
 GINE_ERR_HIP_BASE = 1000
 GINE_MP_BWD_SELF = 1
+GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 ABI_VERSION = 1
 
@@ -30,7 +31,7 @@ _SIGNATURES = {
     "gine_graph_workspace_bytes": [_i64, _i64, ctypes.POINTER(_size)],
     "gine_graph_build": [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p,
                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size, _c_void_p],
-    "gine_mp_fwd": [_c_void_p] * 8 + [_i64, _i32, _c_void_p],
+    "gine_mp_fwd": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
     "gine_mp_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mp_bwd": [_c_void_p] * 11 + [_i64, _i32, _i32, _c_void_p],
     "gine_mp_bwd_finalize": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p],

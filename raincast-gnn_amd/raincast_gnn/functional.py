@@ -16,6 +16,8 @@ back to CPU: a tensor on another device raises.
 from __future__ import annotations
 
 import ctypes
+import os
+import warnings
 
 import torch
 
@@ -23,6 +25,45 @@ from . import _lib
 from ._lib import call, ptr
 
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = _lib.EPI_NONE, _lib.EPI_RELU, _lib.EPI_RESIDUAL_RELU
+
+
+_LIN_FLAG = None
+
+
+def edge_linear_flag() -> int:
+    """Rounding of the K=1 edge Linear, matched to what PyG's CPU path does on THIS host.
+
+    CPU ``Linear(1, D)`` is an MKL sgemm with K=1; MKL rounds ``a*w + b`` once (fma) on Intel
+    CPUs and twice (mul, then add) on AMD EPYC CPUs, so the reference's own result is
+    host-dependent.  ``GINE_EDGE_LINEAR_ROUNDING`` = ``fma`` | ``muladd`` | ``auto`` (default:
+    probe torch's CPU Linear once and match it, so the HIP result is bit-identical to the
+    reference run on the same machine).
+    """
+    global _LIN_FLAG
+    if _LIN_FLAG is not None:
+        return _LIN_FLAG
+    mode = os.environ.get("GINE_EDGE_LINEAR_ROUNDING", "auto").lower()
+    if mode == "fma":
+        _LIN_FLAG = 0
+    elif mode == "muladd":
+        _LIN_FLAG = _lib.GINE_MP_LIN_MULADD
+    elif mode == "auto":
+        g = torch.Generator().manual_seed(7)
+        a = torch.randn(4096, 1, generator=g) * 3
+        w = torch.randn(32, 1, generator=g)
+        b = torch.randn(32, generator=g)
+        lin = torch.nn.functional.linear(a, w, b)
+        fma = (a.double() * w.double().T + b.double()).float()
+        muladd = a * w.T + b
+        miss_fma = int((lin != fma).sum())
+        miss_muladd = int((lin != muladd).sum())
+        _LIN_FLAG = 0 if miss_fma <= miss_muladd else _lib.GINE_MP_LIN_MULADD
+        if min(miss_fma, miss_muladd) > 2:
+            warnings.warn("host CPU Linear(1,D) rounding is neither fma nor mul+add; "
+                          "using the closer one", RuntimeWarning)
+    else:
+        raise ValueError(f"GINE_EDGE_LINEAR_ROUNDING={mode!r}: expected fma, muladd or auto")
+    return _LIN_FLAG
 
 
 def _count(fn: str, n: int, d: int) -> int:
@@ -36,17 +77,18 @@ def _as_vec(p: torch.Tensor) -> torch.Tensor:
     return p.detach().reshape(-1).contiguous()
 
 
-def mp_forward(x, graph, lin_w, lin_b, eps):
+def mp_forward(x, graph, lin_w, lin_b, eps, lin_flag=None):
     N, D = x.shape
     z = torch.empty_like(x)
     if N == 0:
         return z
+    flag = edge_linear_flag() if lin_flag is None else lin_flag
     call("gine_mp_fwd", ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
-         ptr(lin_w), ptr(lin_b), ptr(eps), ptr(z), N, D, _lib.stream_handle(x.device))
+         ptr(lin_w), ptr(lin_b), ptr(eps), ptr(z), N, D, flag, _lib.stream_handle(x.device))
     return z
 
 
-def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True):
+def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_flag=None):
     """Returns (dx, dlin_w[D], dlin_b[D], deps[1])."""
     N, D = x.shape
     dev = x.device
@@ -59,9 +101,11 @@ def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True):
     P = _count("gine_mp_bwd_num_partials", N, D)
     partials = torch.empty(P, 3, D, dtype=torch.float64, device=dev)
     stream = _lib.stream_handle(dev)
+    flags = (_lib.GINE_MP_BWD_SELF if self_term else 0) | (
+        edge_linear_flag() if lin_flag is None else lin_flag)
     call("gine_mp_bwd", ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst),
          ptr(graph.out_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx),
-         ptr(partials), N, D, _lib.GINE_MP_BWD_SELF if self_term else 0, stream)
+         ptr(partials), N, D, flags, stream)
     call("gine_mp_bwd_finalize", ptr(partials), P, D, ptr(dlw), ptr(dlb), ptr(deps), stream)
     return dx, dlw, dlb, deps
 

@@ -46,10 +46,11 @@ def test_status_strings():
 def test_host_validation_without_device():
     lib = _lib.load()
     # unsupported channel counts are rejected before any HIP call
-    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 10, 6, None) == 2
-    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 10, 2048, None) == 2
-    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, -1, 8, None) == 1
-    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 0, 8, None) == 0
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 10, 6, 0, None) == 2
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 10, 2048, 0, None) == 2
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, -1, 8, 0, None) == 1
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 0, 8, 0, None) == 0
+    assert lib.gine_mp_fwd(None, None, None, None, None, None, None, None, 5, 8, 4, None) == 1
     n = ctypes.c_int32(0)
     assert lib.gine_mlp_num_partials(1000, 48, ctypes.byref(n)) == 2
     assert lib.gine_mlp_num_partials(1000, 128, ctypes.byref(n)) == 0 and n.value > 0

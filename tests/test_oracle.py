@@ -26,7 +26,9 @@ def test_scatter_add_is_sequential_edge_order():
     ei, ea, n = random_graph(40, 4000, seed=1)  # ~100 in-edges per node: order matters
     x = torch.randn(n, 16) * torch.logspace(-3, 3, 16)
     lw, lb, eps = _params(16, 0)
-    ref = O.gine_aggregate_loops(x, ei, ea, lw, lb, eps)
+    from raincast_gnn.functional import edge_linear_flag
+    ref = O.gine_aggregate_loops(x, ei, ea, lw, lb, eps,
+                                 "fma" if edge_linear_flag() == 0 else "muladd")
     old = torch.get_num_threads()
     try:
         for threads in (1, max(2, old)):
@@ -56,15 +58,19 @@ def test_index_add_backward_is_sequential_edge_order():
     assert torch.equal(x.grad, expect)
 
 
-def test_linear_k1_rounds_like_fma():
-    """CPU Linear(1, D) rounds once (fma); the kernel uses __builtin_fmaf for it."""
+def test_linear_k1_rounding_is_fma_or_muladd():
+    """CPU Linear(1, D) rounds a*w+b either once (fma: MKL on Intel) or twice (mul, add: MKL on
+    AMD EPYC); the kernel implements both and the host side probes which one applies."""
+    from raincast_gnn.functional import edge_linear_flag
     g = torch.Generator().manual_seed(5)
     a = torch.randn(20000, 1, generator=g) * 3
     w = torch.randn(64, 1, generator=g)
     b = torch.randn(64, generator=g)
     got = torch.nn.functional.linear(a, w, b)
     fma = (a.double() * w.double().T + b.double()).float()  # exact product+sum, one rounding
-    assert torch.equal(got, fma)
+    muladd = a * w.T + b
+    assert torch.equal(got, fma) or torch.equal(got, muladd)
+    assert edge_linear_flag() == (0 if torch.equal(got, fma) else 2)
 
 
 def test_oracle_knn_layer_runs_and_is_deterministic():
