@@ -76,7 +76,7 @@ def test_dp_allreduce_equals_mean_of_shard_grads(tmp_path):
         grads.append(_shard_grads(model, collate(samples[lo:hi])))
     expect = torch.stack(grads).mean(0)
     err = (res[0]["flat"] - expect).abs().max() / expect.abs().max()
-    assert err <= 1e-6, err
+    assert err <= 1e-5, err  # thread-count-dependent CPU BLAS sums between processes
 
 
 def test_shard_range_covers_batch():
