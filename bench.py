@@ -37,6 +37,7 @@ from raincast_gnn.data import synthetic_batch  # noqa: E402
 from raincast_gnn.distributed import FlatGradReducer, broadcast_parameters, env_rank  # noqa: E402
 from raincast_gnn.graph import get_graph  # noqa: E402
 from raincast_gnn.models import gnn_from_params  # noqa: E402
+from raincast_gnn.optim import FlatAdamW  # noqa: E402
 from raincast_gnn.params import BENCH_CONFIGS  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -74,14 +75,15 @@ class Trainer:
         broadcast_parameters(self.model)
         self.batch = synthetic_batch(cfg.num_stations, graphs_per_rank, k=cfg.k,
                                      seed=1000 + rank).to(device)
-        self.reducer = FlatGradReducer(self.model.parameters())
-        self.opt = torch.optim.AdamW(self.model.parameters(), lr=params["lr"], capturable=True,
-                                     foreach=True)
+        # AdamW (train.py:185, torch defaults betas/eps/weight_decay) over one flat buffer;
+        # the same flat gradient buffer is what the data-parallel all-reduce reduces
+        self.opt = FlatAdamW(self.model.parameters(), lr=params["lr"])
+        self.reducer = FlatGradReducer(self.model.parameters(), flat=self.opt.flat_grad)
         self.graph_fb = self.graph_opt = None
         self.loss = None
 
     def fwd_bwd(self):
-        self.reducer.zero_()
+        self.opt.zero_grad()
         pred = self.model(self.batch)
         loss = self.model.loss_fn.crps(pred, self.batch.y)
         loss.backward()
@@ -104,7 +106,7 @@ class Trainer:
             self.graph_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_opt):
                 self.opt.step()
-        assert self.reducer.check_views()
+        assert self.opt.views_intact()
 
     def step(self):
         if self.graph_fb is None:

@@ -156,6 +156,16 @@ int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* mask, const f
                    float* slab, float* dw1, float* db1, float* dw2, float* db2,
                    int64_t num_nodes, int32_t channels, int32_t epilogue, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * AdamW over one flat fp32 parameter buffer (the optimizer of the benchmarked training
+ * step, train.py:67-69 with torch.optim.AdamW, lr from params.json).  Bumps the device
+ * step counter `step` (fp32 [1]) and updates param / exp_avg / exp_avg_sq in place with
+ * torch.optim.AdamW's default (amsgrad=False) formulation.  Two launches, graph-safe.
+ * ---------------------------------------------------------------------------------- */
+int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                    float* step, int64_t n, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

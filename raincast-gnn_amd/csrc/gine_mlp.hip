@@ -20,6 +20,7 @@
 // Weight gradients (K = N rows) use k_wgrad: 64x64 output blocks x row chunks, fp32
 // partial slabs, reduced in fixed chunk order in fp64 by k_slab_reduce -> deterministic.
 #include "gine_common.hpp"
+#include "gine_reduce.hpp"
 
 namespace gine {
 namespace {
@@ -288,12 +289,15 @@ int launch_rowgemm(int D, const float* W, const ProArgs& pa, const EpiArgs& ea, 
 // ----------------------------------------------------------------------------------------
 // BatchNorm1d finalize kernels (one thread per channel, partials summed in fixed order)
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_bn_fwd_finalize(
+__global__ __launch_bounds__(kColsumThreads) void k_bn_fwd_finalize(
     const double* __restrict__ partials, int P, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     int64_t* __restrict__ nbt, float* __restrict__ bn_save, int64_t N, int D, float momentum,
     float bn_eps, int training, int update_running) {
+  __shared__ double s_tmp[kColsumThreads];
+  __shared__ double s_sum[2 * 256];  // [sum | sumsq], D <= 256
   __shared__ double s_factor;
+  if (training) block_colsum(partials, P, 2 * D, 2 * D, s_tmp, s_sum);
   if (threadIdx.x == 0) {
     double f = (double)momentum;
     if (training && update_running && nbt != nullptr) {
@@ -308,13 +312,8 @@ __global__ __launch_bounds__(256) void k_bn_fwd_finalize(
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
     double mean, var;
     if (training) {
-      double s1 = 0.0, s2 = 0.0;
-      for (int p = 0; p < P; ++p) {
-        s1 += partials[(size_t)p * 2 * D + c];
-        s2 += partials[(size_t)p * 2 * D + D + c];
-      }
-      mean = s1 / (double)N;
-      var = s2 / (double)N - mean * mean;
+      mean = s_sum[c] / (double)N;
+      var = s_sum[D + c] / (double)N - mean * mean;
       if (var < 0.0) var = 0.0;
       if (update_running && rmean != nullptr) {
         const double unbiased = N > 1 ? var * (double)N / (double)(N - 1) : var;
@@ -336,16 +335,15 @@ __global__ __launch_bounds__(256) void k_bn_fwd_finalize(
   }
 }
 
-__global__ __launch_bounds__(256) void k_bn_bwd_finalize(
+__global__ __launch_bounds__(kColsumThreads) void k_bn_bwd_finalize(
     const double* __restrict__ partials, int P, const float* __restrict__ gamma,
     const float* __restrict__ bn_save, float* __restrict__ dgamma, float* __restrict__ dbeta,
     float* __restrict__ coef, int64_t N, int D, int training) {
+  __shared__ double s_tmp[kColsumThreads];
+  __shared__ double s_sum[2 * 256];  // [sum dbn | sum dbn*xhat]
+  block_colsum(partials, P, 2 * D, 2 * D, s_tmp, s_sum);
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    double sd = 0.0, sx = 0.0;
-    for (int p = 0; p < P; ++p) {
-      sd += partials[(size_t)p * 2 * D + c];
-      sx += partials[(size_t)p * 2 * D + D + c];
-    }
+    const double sd = s_sum[c], sx = s_sum[D + c];
     if (dgamma) dgamma[c] = (float)sx;
     if (dbeta) dbeta[c] = (float)sd;
     const double g = gamma ? (double)gamma[c] : 1.0;
@@ -444,8 +442,16 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
   if (e >= 2 * per) return;
   const int zsel = e / per, r = e % per;
   const float* base = slab + (size_t)zsel * chunks * per + r;
-  double s = 0.0;
-  for (int c = 0; c < chunks; ++c) s += (double)base[(size_t)c * per];
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int c = 0;
+  for (; c + 3 < chunks; c += 4) {
+    a0 += (double)base[(size_t)c * per];
+    a1 += (double)base[(size_t)(c + 1) * per];
+    a2 += (double)base[(size_t)(c + 2) * per];
+    a3 += (double)base[(size_t)(c + 3) * per];
+  }
+  for (; c < chunks; ++c) a0 += (double)base[(size_t)c * per];
+  const double s = (a0 + a1) + (a2 + a3);
   float* w = zsel == 0 ? dw2 : dw1;
   float* b = zsel == 0 ? db2 : db1;
   if (r < D * D) {
@@ -500,7 +506,9 @@ extern "C" int gine_bn_fwd_finalize(const double* partials, int32_t num_partials
   if (training && (!partials || num_partials <= 0)) return GINE_ERR_INVALID;
   if (!training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
   if (update_running && training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
-  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3(1), dim3(256), 0, as_stream(stream), partials,
+  if (channels > 256) return GINE_ERR_DIM;
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3(1), dim3(kColsumThreads), 0, as_stream(stream),
+                     partials,
                      num_partials, gamma, beta, running_mean, running_var, num_batches_tracked,
                      bn_save, num_nodes, channels, momentum, bn_eps, training, update_running);
   GINE_LAUNCH_STATUS();
@@ -542,7 +550,9 @@ extern "C" int gine_bn_bwd_finalize(const double* partials, int32_t num_partials
                                     int32_t channels, int32_t training, void* stream) {
   if (channels <= 0 || !partials || num_partials <= 0 || !bn_save || !coef || num_nodes <= 0)
     return GINE_ERR_INVALID;
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(1), dim3(256), 0, as_stream(stream), partials,
+  if (channels > 256) return GINE_ERR_DIM;
+  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(1), dim3(kColsumThreads), 0, as_stream(stream),
+                     partials,
                      num_partials, gamma, bn_save, dgamma, dbeta, coef, num_nodes, channels,
                      training);
   GINE_LAUNCH_STATUS();

@@ -16,6 +16,7 @@
 // destination's sum.  Accumulation order is the CSR order = original edge order, hence
 // bit-identical to CPU scatter_add_ / index_add_.
 #include "gine_common.hpp"
+#include "gine_reduce.hpp"
 
 namespace gine {
 namespace {
@@ -293,30 +294,18 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
   for (int i = threadIdx.x; i < 3 * D; i += kThreads) out[i] = s_red[i];
 }
 
-__global__ __launch_bounds__(kThreads) void k_mp_bwd_finalize(
+__global__ __launch_bounds__(kColsumThreads) void k_mp_bwd_finalize(
     const double* __restrict__ partials, int P, int D, float* __restrict__ dlin_w,
     float* __restrict__ dlin_b, float* __restrict__ deps) {
-  __shared__ double s_eps[kThreads];
-  double e_acc = 0.0;
-  for (int c = threadIdx.x; c < D; c += kThreads) {
-    double sw = 0.0, sb = 0.0, se = 0.0;
-    for (int p = 0; p < P; ++p) {
-      const double* row = partials + (size_t)p * 3 * D;
-      sw += row[c];
-      sb += row[D + c];
-      se += row[2 * D + c];
-    }
-    dlin_w[c] = (float)sw;
-    dlin_b[c] = (float)sb;
-    e_acc += se;
+  __shared__ double s_tmp[kColsumThreads];
+  extern __shared__ __attribute__((aligned(16))) double s_out[];  // [3D]
+  block_colsum(partials, P, 3 * D, 3 * D, s_tmp, s_out);
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    dlin_w[c] = (float)s_out[c];
+    dlin_b[c] = (float)s_out[D + c];
   }
-  s_eps[threadIdx.x] = e_acc;
-  __syncthreads();
-  for (int s = kThreads / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) s_eps[threadIdx.x] += s_eps[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) deps[0] = (float)s_eps[0];
+  block_tree_sum(s_out + 2 * D, D);  // sum over channels of sum dz*x
+  if (threadIdx.x == 0) deps[0] = (float)s_out[2 * D];
 }
 
 // ----------------------------------------------------------------------------------------
@@ -449,8 +438,11 @@ extern "C" int gine_mp_bwd_finalize(const double* partials, int32_t num_partials
                                     float* deps, void* stream) {
   if (num_partials < 0 || channels <= 0) return GINE_ERR_INVALID;
   if (!partials || !dlin_w || !dlin_b || !deps) return GINE_ERR_INVALID;
-  hipLaunchKernelGGL(k_mp_bwd_finalize, dim3(1), dim3(kThreads), 0, as_stream(stream),
-                     partials, num_partials, channels, dlin_w, dlin_b, deps);
+  int m = 1;
+  while (m < channels) m <<= 1;  // tree-sum scratch beyond 3D
+  const size_t smem = sizeof(double) * (size_t)(2 * channels + m);
+  hipLaunchKernelGGL(k_mp_bwd_finalize, dim3(1), dim3(kColsumThreads), smem,
+                     as_stream(stream), partials, num_partials, channels, dlin_w, dlin_b, deps);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

@@ -1,0 +1,69 @@
+// AdamW over ONE flat fp32 buffer holding every parameter of the model (the benchmarked
+// training step, train.py:67-69: zero_grad / backward / AdamW.step, lr from params.json).
+//
+// torch.optim.AdamW (amsgrad=False, maximize=False) per element, default (non-capturable)
+// formulation, with the scalar bias corrections computed in double and applied in fp32 the
+// way torch applies Python scalars to fp32 tensors:
+//   step += 1
+//   p  *= 1 - lr*wd
+//   m   = m + (1-b1)*(g - m)                 (lerp, weight < 0.5 branch)
+//   v   = v*b2 + (1-b2)*g*g
+//   p  += -(lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// The step counter lives on the device (a separate 1-thread launch bumps it first), so the
+// update is legal inside a captured HIP graph and replays correctly.
+#include "gine_common.hpp"
+
+namespace gine {
+namespace {
+
+__global__ void k_adamw_tick(float* __restrict__ step) { step[0] = step[0] + 1.0f; }
+
+__global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
+                                               float* __restrict__ m, float* __restrict__ v,
+                                               const float* __restrict__ step, int64_t n,
+                                               float lr, float beta1, float beta2, float eps,
+                                               float weight_decay) {
+  const double t = (double)step[0];
+  const float decay = (float)(1.0 - (double)lr * (double)weight_decay);
+  const float neg_step_size = (float)(-((double)lr / (1.0 - pow((double)beta1, t))));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, t));
+  const float w1 = 1.0f - beta1;
+  const float w2 = 1.0f - beta2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i];
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = mi + w1 * (gi - mi);
+    float vi = v[i] * beta2;
+    vi = vi + w2 * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi + neg_step_size * (mi / denom);  // addcdiv: p + value * (m / denom)
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_adamw_step(float* param, const float* grad, float* exp_avg,
+                               float* exp_avg_sq, float* step, int64_t n, float lr,
+                               float beta1, float beta2, float eps, float weight_decay,
+                               void* stream) {
+  if (n < 0 || !step) return GINE_ERR_INVALID;
+  if (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)) return GINE_ERR_INVALID;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(k_adamw_tick, dim3(1), dim3(1), 0, s, step);
+  GINE_LAUNCH_STATUS();
+  if (n == 0) return GINE_OK;
+  int64_t blocks = ceil_div(n, 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_adamw, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg,
+                     exp_avg_sq, step, n, lr, beta1, beta2, eps, weight_decay);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

@@ -45,6 +45,7 @@ _SIGNATURES = {
     "gine_mlp_bwd1": [_c_void_p] * 6 + [_i64, _i32, _c_void_p],
     "gine_mlp_wgrad_num_chunks": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_wgrad": [_c_void_p] * 13 + [_i64, _i32, _i32, _c_void_p],
+    "gine_adamw_step": [_c_void_p] * 5 + [_i64, _f32, _f32, _f32, _f32, _f32, _c_void_p],
 }
 
 EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)

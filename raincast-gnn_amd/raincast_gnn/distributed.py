@@ -30,14 +30,19 @@ class FlatGradReducer:
     single collective.  Optimisers see ordinary ``.grad`` tensors.
     """
 
-    def __init__(self, params, group=None):
+    def __init__(self, params, group=None, flat: torch.Tensor | None = None):
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("no trainable parameters")
         dev = self.params[0].device
         total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.group = group
+        if flat is not None:  # gradients already live in this buffer (e.g. FlatAdamW's)
+            if flat.numel() != total:
+                raise ValueError("flat gradient buffer does not match the parameters")
+            self.flat = flat
+            return
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         off = 0
         for p in self.params:
             if p.dtype != torch.float32:

@@ -1,0 +1,66 @@
+"""Flat-buffer AdamW for the benchmarked training step (train.py:67-69).
+
+The reference steps ``torch.optim.AdamW(model.parameters(), lr=params["lr"])`` (train.py:185)
+over ~40 small parameter tensors (209,800 fp32 values for 24h_mixed): on a GPU that is a
+few hundred tiny launches per step.  :class:`FlatAdamW` re-points every parameter at a view
+of ONE contiguous buffer (and every ``.grad`` at a view of one contiguous gradient buffer --
+the same buffer the data-parallel all-reduce uses), then updates all of them with one HIP
+kernel (``gine_adamw_step``, include/gine_hip.h) that reproduces torch's AdamW arithmetic.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+class FlatAdamW:
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("no trainable parameters")
+        dev = self.params[0].device
+        _lib.require_device(self.params[0], "FlatAdamW")
+        if any(p.dtype != torch.float32 or p.device != dev for p in self.params):
+            raise TypeError("FlatAdamW needs fp32 parameters on one device")
+        self.lr, self.betas, self.eps, self.weight_decay = float(lr), betas, float(eps), \
+            float(weight_decay)
+        n = sum(p.numel() for p in self.params)
+        self.flat_param = torch.empty(n, dtype=torch.float32, device=dev)
+        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                view = self.flat_param[off:off + k].view_as(p)
+                view.copy_(p)
+                p.data = view
+                p.grad = self.flat_grad[off:off + k].view_as(p)
+                off += k
+        self.exp_avg = torch.zeros_like(self.flat_param)
+        self.exp_avg_sq = torch.zeros_like(self.flat_param)
+        self.step_count = torch.zeros(1, dtype=torch.float32, device=dev)
+
+    @property
+    def numel(self) -> int:
+        return self.flat_param.numel()
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        if set_to_none:
+            raise ValueError("FlatAdamW keeps gradients in its flat buffer (set_to_none=False)")
+        self.flat_grad.zero_()
+
+    @torch.no_grad()
+    def step(self) -> None:
+        b1, b2 = self.betas
+        _lib.call("gine_adamw_step", _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad),
+                  _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), _lib.ptr(self.step_count),
+                  self.numel, self.lr, float(b1), float(b2), self.eps, self.weight_decay,
+                  _lib.stream_handle(self.flat_param.device))
+
+    def views_intact(self) -> bool:
+        """True while every parameter and gradient still aliases the flat buffers."""
+        pb, gb = self.flat_param.data_ptr(), self.flat_grad.data_ptr()
+        end_p, end_g = pb + 4 * self.numel, gb + 4 * self.numel
+        return all(pb <= p.data_ptr() < end_p and p.grad is not None
+                   and gb <= p.grad.data_ptr() < end_g for p in self.params)

@@ -28,7 +28,7 @@ for s in $STEPS; do
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -- \
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
