@@ -257,8 +257,11 @@ def _oracle_gnn_from(model: GNN, params) -> O.OracleGNN:
     return ref
 
 
-def _oracle_step(ref, batch, dtype):
+def _oracle_step(ref, batch, dtype, record=False):
     r = copy.deepcopy(ref).to(dtype)
+    if record:
+        for conv in r.conv.convolutions:
+            conv.record = []
     b = copy.copy(batch)
     b.x, b.ensemble, b.edge_attr = (t.to(dtype) for t in (batch.x, batch.ensemble,
                                                           batch.edge_attr))
@@ -287,7 +290,7 @@ def test_training_step_matches_oracle(experiment):
     loss = model.loss_fn.crps(pred, batch.y.to(DEV))
     loss.backward()
     r32, pred32, loss32 = _oracle_step(ref, batch, torch.float32)
-    r64, pred64, loss64 = _oracle_step(ref, batch, torch.float64)
+    r64, pred64, loss64 = _oracle_step(ref, batch, torch.float64, record=True)
     assert loss.dtype == loss32.dtype
     assert_close_tiebreak(pred.detach().cpu(), pred32.detach(), pred64.detach(), TOL, "pred")
     assert_close_tiebreak(loss.detach().cpu().reshape(1), loss32.detach().reshape(1),
@@ -295,6 +298,17 @@ def test_training_step_matches_oracle(experiment):
     p32, p64 = dict(r32.named_parameters()), dict(r64.named_parameters())
     worst = 0.0
     for name, p in model.named_parameters():
+        if name.endswith(".eps"):
+            # d eps = sum_{n,c} dz*x: one cancelling reduction over N*D terms, whose relative
+            # error is ill-conditioned in any fp32 implementation (the fp32 CPU oracle itself
+            # is up to ~1e-4 off the exact value).  Check it against its condition scale:
+            # |gpu - exact| <= TOL * sum |dz*x|  (exact = fp64 oracle).
+            i = int(name.split(".")[2])
+            x64, dz64 = r64.conv.convolutions[i].record[0]
+            scale = (dz64 * x64).abs().sum().item()
+            err = abs(p.grad.item() - p64[name].grad.item())
+            assert err <= TOL * scale, f"{name}: |err| {err:.3e} > {TOL} * {scale:.3e}"
+            continue
         e = assert_close_tiebreak(p.grad.cpu(), p32[name].grad, p64[name].grad, TOL, name)
         worst = max(worst, e)
     print(f"{experiment}: worst grad rel err vs fp32 oracle {worst:.2e}")
