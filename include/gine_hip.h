@@ -166,6 +166,30 @@ int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_
                     float* step, int64_t n, float lr, float beta1, float beta2, float eps,
                     float weight_decay, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Fused CRPS losses (models/loss.py) over the post-processed predictions pred [N, K]
+ * (models/model_utils.py PostProcess output) and targets y [N] (NaN = missing):
+ *   GINE_LOSS_NORMAL        NormalCRPS.crps         (loss.py:335-369)   K = 2
+ *   GINE_LOSS_MIXED_NORMAL  MixedNormalCRPS.crps    (loss.py:6-68)      K = 3
+ *   GINE_LOSS_MIXED         MixedLoss(grad_u=False) (loss.py:71-272)    K = 4, u fixed
+ *   GINE_LOSS_MIXED_U       MixedLoss(grad_u=True)                      K = 5, u learned
+ * gine_crps_fwd: per node the closed form and its exact gradient w.r.t. pred (fp64
+ * forward-mode duals) into dpred [N, K]; per-block partials [P][2]; loss_out[0] = mean over
+ * non-NaN targets, count_out[0] = their number.  c = censoring point (log 0.01), t =
+ * sigmoid temperature of grad_u, xi = GPD shape, u = fixed threshold.
+ * gine_crps_bwd: grad_pred = gloss[0] * dpred / count (fp32).
+ * ---------------------------------------------------------------------------------- */
+#define GINE_LOSS_NORMAL 0
+#define GINE_LOSS_MIXED_NORMAL 1
+#define GINE_LOSS_MIXED 2
+#define GINE_LOSS_MIXED_U 3
+int gine_crps_num_partials(int64_t num_nodes, int32_t* num_partials);
+int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t kind, double u,
+                  double xi, double c, double t, double* dpred, double* partials,
+                  double* loss_out, double* count_out, void* stream);
+int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
+                  int64_t num_nodes, int32_t kind, float* grad_pred, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

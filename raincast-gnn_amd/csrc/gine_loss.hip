@@ -1,0 +1,337 @@
+// Fused CRPS losses of the reference (models/loss.py) on gfx950: one pass computes, per
+// station-node, the closed-form CRPS and its exact gradient w.r.t. the K distribution
+// parameters (forward-mode dual numbers), then the NaN-masked mean over nodes.
+//
+// Replaces the ~700 elementwise launches per training step that the torch formulation of
+// MixedLoss.crps (loss.py:203-272) + its autograd takes.  Evaluated in fp64 (the reference
+// promotes the mixed losses to fp64 through c = tensor([log 0.01]), loss.py:33-34,230-231;
+// its remaining fp32 sub-expressions are reproduced to within their fp32 rounding).
+//   NormalCRPS      loss.py:335-369   pred = [mu, sigma]
+//   MixedNormalCRPS loss.py:6-68      pred = [mu, sigma, p]
+//   MixedLoss       loss.py:71-272    pred = [mu, sigma, p, sigma_u] (+ u if grad_u)
+#include "gine_common.hpp"
+#include "gine_reduce.hpp"
+
+namespace gine {
+namespace {
+
+constexpr double kInvSqrtPi = 0.56418958354775628695;   // 1/sqrt(pi)
+constexpr double kLogSqrt2Pi = 0.91893853320467274178;  // log(sqrt(2 pi))
+constexpr double kSqrt2 = 1.41421356237309504880;
+constexpr int kThreads = 256;
+
+// ---------------------------------------------------------------------------------------
+// forward-mode dual numbers: value + gradient w.r.t. the K prediction columns
+// ---------------------------------------------------------------------------------------
+template <int K>
+struct Dual {
+  double v;
+  double d[K];
+};
+
+template <int K>
+__device__ __forceinline__ Dual<K> cst(double v) {
+  Dual<K> r;
+  r.v = v;
+#pragma unroll
+  for (int i = 0; i < K; ++i) r.d[i] = 0.0;
+  return r;
+}
+template <int K>
+__device__ __forceinline__ Dual<K> var(double v, int i) {
+  Dual<K> r = cst<K>(v);
+  r.d[i] = 1.0;
+  return r;
+}
+// f(x) with derivative f'(x): chain rule
+template <int K>
+__device__ __forceinline__ Dual<K> apply(const Dual<K>& x, double f, double df) {
+  Dual<K> r;
+  r.v = f;
+#pragma unroll
+  for (int i = 0; i < K; ++i) r.d[i] = df * x.d[i];
+  return r;
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator+(const Dual<K>& a, const Dual<K>& b) {
+  Dual<K> r;
+  r.v = a.v + b.v;
+#pragma unroll
+  for (int i = 0; i < K; ++i) r.d[i] = a.d[i] + b.d[i];
+  return r;
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator-(const Dual<K>& a, const Dual<K>& b) {
+  Dual<K> r;
+  r.v = a.v - b.v;
+#pragma unroll
+  for (int i = 0; i < K; ++i) r.d[i] = a.d[i] - b.d[i];
+  return r;
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator-(const Dual<K>& a) {
+  return apply(a, -a.v, -1.0);
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator*(const Dual<K>& a, const Dual<K>& b) {
+  Dual<K> r;
+  r.v = a.v * b.v;
+#pragma unroll
+  for (int i = 0; i < K; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
+  return r;
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator/(const Dual<K>& a, const Dual<K>& b) {
+  Dual<K> r;
+  r.v = a.v / b.v;
+  const double inv = 1.0 / b.v;
+#pragma unroll
+  for (int i = 0; i < K; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) * inv;
+  return r;
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator*(double s, const Dual<K>& a) {
+  return apply(a, s * a.v, s);
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator+(double s, const Dual<K>& a) {
+  return apply(a, s + a.v, 1.0);
+}
+template <int K>
+__device__ __forceinline__ Dual<K> operator-(double s, const Dual<K>& a) {
+  return apply(a, s - a.v, -1.0);
+}
+template <int K>
+__device__ __forceinline__ Dual<K> sq(const Dual<K>& a) {
+  return apply(a, a.v * a.v, 2.0 * a.v);
+}
+template <int K>
+__device__ __forceinline__ Dual<K> dabs(const Dual<K>& a) {  // torch: d|x| = sign(x)
+  return apply(a, fabs(a.v), a.v > 0.0 ? 1.0 : (a.v < 0.0 ? -1.0 : 0.0));
+}
+template <int K>
+__device__ __forceinline__ Dual<K> powc(const Dual<K>& a, double c) {  // constant exponent
+  const double p = pow(a.v, c);
+  return apply(a, p, c * pow(a.v, c - 1.0));
+}
+// standard normal cdf / pdf (torch.distributions.Normal(0, 1))
+template <int K>
+__device__ __forceinline__ Dual<K> Phi(const Dual<K>& z) {
+  const double pdf = exp(-0.5 * z.v * z.v - kLogSqrt2Pi);
+  return apply(z, 0.5 * (1.0 + erf(z.v / kSqrt2)), pdf);
+}
+template <int K>
+__device__ __forceinline__ Dual<K> phi(const Dual<K>& z) {
+  const double pdf = exp(-0.5 * z.v * z.v - kLogSqrt2Pi);
+  return apply(z, pdf, -z.v * pdf);
+}
+template <int K>
+__device__ __forceinline__ Dual<K> sigmoid(const Dual<K>& a) {
+  const double s = 1.0 / (1.0 + exp(-a.v));
+  return apply(a, s, s * (1.0 - s));
+}
+template <int K>
+__device__ __forceinline__ Dual<K> select(bool c, const Dual<K>& a, const Dual<K>& b) {
+  return c ? a : b;  // torch.where: gradient flows to the selected branch only
+}
+
+// ---------------------------------------------------------------------------------------
+// closed forms (restated from models/loss.py)
+// ---------------------------------------------------------------------------------------
+template <int K>
+__device__ Dual<K> crps_normal(const Dual<K>& mu, const Dual<K>& sigma, double y) {
+  const Dual<K> z = (cst<K>(y) - mu) / sigma;
+  return sigma * (z * (2.0 * Phi(z) - cst<K>(1.0)) + 2.0 * phi(z) - cst<K>(kInvSqrtPi));
+}
+
+template <int K>
+__device__ Dual<K> crps_mixed_normal(const Dual<K>& mu, const Dual<K>& sigma, const Dual<K>& p,
+                                     double y, double c) {
+  const Dual<K> yt = (cst<K>(y) - mu) / sigma;
+  const Dual<K> ct = (cst<K>(c) - mu) / sigma;
+  const Dual<K> q = 1.0 - p;
+  const Dual<K> Pc = p + q * Phi(ct);
+  const Dual<K> t1 = yt * (2.0 * (p + q * Phi(yt)) - cst<K>(1.0));
+  const Dual<K> t2 = -(ct * sq(Pc));
+  const Dual<K> t3 = 2.0 * (q * (-phi(ct)) * Pc);
+  const Dual<K> t4 = -2.0 * (q * (-phi(yt)));
+  const Dual<K> t5 = (-kInvSqrtPi) * (sq(q) * (1.0 - Phi(kSqrt2 * ct)));
+  return sigma * (t1 + t2 + t3 + t4 + t5);
+}
+
+template <int K>
+__device__ Dual<K> pareto_crps(const Dual<K>& y, const Dual<K>& u, const Dual<K>& m,
+                               const Dual<K>& s, double xi) {
+  const Dual<K> yt = (y - u) / s;
+  const Dual<K> cdf = select(yt.v <= 0.0, cst<K>(0.0), 1.0 - powc(1.0 + xi * yt, -1.0 / xi));
+  const Dual<K> om = 1.0 - m;
+  return s * (dabs(yt) - (2.0 / (1.0 - xi)) * (om * (1.0 - powc(1.0 - cdf, 1.0 - xi))) +
+              (1.0 / (2.0 - xi)) * sq(om));
+}
+
+template <int K, bool GRAD_U>
+__device__ Dual<K> crps_mixed(const Dual<K>& mu, const Dual<K>& sigma, const Dual<K>& p,
+                              const Dual<K>& su, const Dual<K>& u, double y, double c,
+                              double xi, double t) {
+  const Dual<K> yy = cst<K>(y);
+  const Dual<K> ct = (cst<K>(c) - mu) / sigma;
+  const Dual<K> ut = (u - mu) / sigma;
+  const Dual<K> yt = (yy - mu) / sigma;
+  const Dual<K> q = 1.0 - p;
+  const Dual<K> m_u = p + q * Phi(ut);
+  const Dual<K> Pc = p + q * Phi(ct);
+  const Dual<K> Pu = q * (1.0 - Phi(ut));
+  const Dual<K> t2 = ut * sq(Pu) - ct * sq(Pc);
+  const Dual<K> t3 = -2.0 * (q * phi(ct) * Pc + q * phi(ut) * Pu);
+  const Dual<K> t5 = (-kInvSqrtPi) * (sq(q) * (Phi(kSqrt2 * ut) - Phi(kSqrt2 * ct)));
+  const Dual<K> mixed = sigma * (yt * (2.0 * (p + q * Phi(yt)) - cst<K>(1.0)) + t2 + t3 +
+                                 2.0 * (q * phi(yt)) + t5);
+  const Dual<K> upper = sigma * (ut + t2 + t3 + (-2.0) * (q * (-phi(ut)) + ut * Pu) + t5);
+  const Dual<K> loss1 = mixed + pareto_crps(u, u, m_u, su, xi);
+  const Dual<K> loss2 = pareto_crps(yy, u, m_u, su, xi) + upper;
+  if constexpr (GRAD_U) {
+    return sigmoid(t * (u - yy)) * (loss1 - loss2) + loss2;
+  } else {
+    return select(y < u.v, loss1, loss2);
+  }
+}
+
+template <int KIND>
+struct LossK {
+  static constexpr int value = KIND == GINE_LOSS_NORMAL ? 2
+                               : KIND == GINE_LOSS_MIXED_NORMAL ? 3
+                               : KIND == GINE_LOSS_MIXED ? 4 : 5;
+};
+
+// One thread per node.  Writes d crps_n / d pred_n (0 for NaN targets) and per-block
+// [sum crps, count] partials.
+template <int KIND>
+__global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pred,
+                                                   const float* __restrict__ y, int64_t n,
+                                                   double u_fixed, double xi, double c,
+                                                   double t, double* __restrict__ dpred,
+                                                   double* __restrict__ partials) {
+  constexpr int K = LossK<KIND>::value;
+  __shared__ double s_sum[kThreads];
+  __shared__ double s_cnt[kThreads];
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  double val = 0.0, cnt = 0.0;
+  if (i < n) {
+    const float yf = y[i];
+    double g[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) g[k] = 0.0;
+    if (yf == yf) {  // NaN targets are masked out (loss.py:22,220)
+      const double yy = (double)yf;
+      Dual<K> v[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) v[k] = var<K>((double)pred[i * K + k], k);
+      Dual<K> r;
+      if constexpr (KIND == GINE_LOSS_NORMAL) {
+        r = crps_normal(v[0], v[1], yy);
+      } else if constexpr (KIND == GINE_LOSS_MIXED_NORMAL) {
+        r = crps_mixed_normal(v[0], v[1], v[2], yy, c);
+      } else if constexpr (KIND == GINE_LOSS_MIXED) {
+        r = crps_mixed<K, false>(v[0], v[1], v[2], v[3], cst<K>(u_fixed), yy, c, xi, t);
+      } else {
+        r = crps_mixed<K, true>(v[0], v[1], v[2], v[3], v[4], yy, c, xi, t);
+      }
+      val = r.v;
+      cnt = 1.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) g[k] = r.d[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) dpred[i * K + k] = g[k];
+  }
+  s_sum[threadIdx.x] = val;
+  s_cnt[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {  // fixed-order tree
+    if (threadIdx.x < s) {
+      s_sum[threadIdx.x] += s_sum[threadIdx.x + s];
+      s_cnt[threadIdx.x] += s_cnt[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = s_sum[0];
+    partials[2 * blockIdx.x + 1] = s_cnt[0];
+  }
+}
+
+// loss = sum / count (NaN when no target is valid, like torch.mean of an empty tensor)
+__global__ __launch_bounds__(kColsumThreads) void k_crps_finalize(
+    const double* __restrict__ partials, int P, double* __restrict__ loss_out,
+    double* __restrict__ count_out) {
+  __shared__ double s_tmp[kColsumThreads];
+  __shared__ double s_out[2];
+  block_colsum(partials, P, 2, 2, s_tmp, s_out);
+  if (threadIdx.x == 0) {
+    loss_out[0] = s_out[0] / s_out[1];
+    count_out[0] = s_out[1];
+  }
+}
+
+// grad_pred = gloss * dpred / count
+__global__ __launch_bounds__(kThreads) void k_crps_bwd(const double* __restrict__ dpred,
+                                                       const double* __restrict__ count,
+                                                       const double* __restrict__ gloss,
+                                                       int64_t total, float* __restrict__ grad) {
+  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  if (i >= total) return;
+  grad[i] = (float)(gloss[0] * dpred[i] / count[0]);
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_crps_num_partials(int64_t num_nodes, int32_t* num_partials) {
+  if (!num_partials || num_nodes < 0) return GINE_ERR_INVALID;
+  const int64_t p = ceil_div(num_nodes, kThreads);
+  *num_partials = (int32_t)(p > 0 ? p : 1);
+  return GINE_OK;
+}
+
+extern "C" int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
+                             double u, double xi, double c, double t, double* dpred,
+                             double* partials, double* loss_out, double* count_out,
+                             void* stream) {
+  if (num_nodes < 0 || !partials || !loss_out || !count_out) return GINE_ERR_INVALID;
+  if (num_nodes > 0 && (!pred || !y || !dpred)) return GINE_ERR_INVALID;
+  if (kind < GINE_LOSS_NORMAL || kind > GINE_LOSS_MIXED_U) return GINE_ERR_INVALID;
+  hipStream_t s = as_stream(stream);
+  const int64_t blocks = ceil_div(num_nodes, kThreads) > 0 ? ceil_div(num_nodes, kThreads) : 1;
+#define LAUNCH_CRPS(KIND_)                                                                  \
+  hipLaunchKernelGGL(k_crps<KIND_>, dim3((unsigned)blocks), dim3(kThreads), 0, s, pred, y,  \
+                     num_nodes, u, xi, c, t, dpred, partials)
+  switch (kind) {
+    case GINE_LOSS_NORMAL: LAUNCH_CRPS(GINE_LOSS_NORMAL); break;
+    case GINE_LOSS_MIXED_NORMAL: LAUNCH_CRPS(GINE_LOSS_MIXED_NORMAL); break;
+    case GINE_LOSS_MIXED: LAUNCH_CRPS(GINE_LOSS_MIXED); break;
+    default: LAUNCH_CRPS(GINE_LOSS_MIXED_U); break;
+  }
+#undef LAUNCH_CRPS
+  GINE_LAUNCH_STATUS();
+  hipLaunchKernelGGL(k_crps_finalize, dim3(1), dim3(kColsumThreads), 0, s, partials,
+                     (int)blocks, loss_out, count_out);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
+                             int64_t num_nodes, int32_t kind, float* grad_pred, void* stream) {
+  if (num_nodes < 0 || !count || !gloss) return GINE_ERR_INVALID;
+  if (kind < GINE_LOSS_NORMAL || kind > GINE_LOSS_MIXED_U) return GINE_ERR_INVALID;
+  const int K = kind == GINE_LOSS_NORMAL ? 2 : kind == GINE_LOSS_MIXED_NORMAL ? 3
+              : kind == GINE_LOSS_MIXED ? 4 : 5;
+  const int64_t total = num_nodes * K;
+  if (total == 0) return GINE_OK;
+  if (!dpred || !grad_pred) return GINE_ERR_INVALID;
+  hipLaunchKernelGGL(k_crps_bwd, dim3((unsigned)ceil_div(total, kThreads)), dim3(kThreads), 0,
+                     as_stream(stream), dpred, count, gloss, total, grad_pred);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

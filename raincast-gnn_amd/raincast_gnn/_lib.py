@@ -21,10 +21,12 @@ GINE_ERR_HIP_BASE = 1000
 GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
+LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
 ABI_VERSION = 1
 
 _c_void_p = ctypes.c_void_p
 _i32, _i64, _f32, _size = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+_f64 = ctypes.c_double
 
 # name -> argtypes (every entry point returns int status)
 _SIGNATURES = {
@@ -46,6 +48,10 @@ _SIGNATURES = {
     "gine_mlp_wgrad_num_chunks": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_wgrad": [_c_void_p] * 13 + [_i64, _i32, _i32, _c_void_p],
     "gine_adamw_step": [_c_void_p] * 5 + [_i64, _f32, _f32, _f32, _f32, _f32, _c_void_p],
+    "gine_crps_num_partials": [_i64, ctypes.POINTER(_i32)],
+    "gine_crps_fwd": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64, _c_void_p,
+                      _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "gine_crps_bwd": [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
 }
 
 EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)

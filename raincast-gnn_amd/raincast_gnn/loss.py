@@ -1,5 +1,10 @@
 """CRPS losses of the reference (models/loss.py), restated for device execution.
 
+On a HIP device the reduced loss runs as ONE fused kernel pass (``gine_crps_fwd`` /
+``gine_crps_bwd``, csrc/gine_loss.hip: closed form + exact per-node gradient by fp64
+forward-mode duals, NaN-masked mean).  The torch formulation below is kept for CPU tensors
+and ``reduce=False``; both are pinned to the reference's own outputs (tests/golden/).
+
 Same closed forms, same dtype promotions (the censoring point ``c = log(0.01)`` is a float64
 tensor, so every term that touches it -- and the loss -- is float64, loss.py:33-34,
 230-231), same NaN semantics: rows whose target is NaN do not contribute.  The reference
@@ -12,10 +17,13 @@ arguments with a host sync) is replaced by its own cdf/log_prob formulas for loc
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
 import torch
+
+from . import _lib
 
 _LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
 # NormalCRPS keeps 1/sqrt(pi) as an fp32 tensor (loss.py:343): same value as a Python float
@@ -64,6 +72,49 @@ def _masked_mean(values: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return total / m.sum().to(values.dtype)
 
 
+class _FusedCRPS(torch.autograd.Function):
+    """Reduced CRPS of ``pred [N, K]`` vs ``y [N]`` in one HIP pass (fp64 result)."""
+
+    @staticmethod
+    def forward(ctx, pred, y, kind, u, xi, c, t):
+        pred = pred.detach().float().contiguous()
+        y = y.detach().float().contiguous()
+        N, K = pred.shape
+        dev = pred.device
+        n_part = ctypes.c_int32(0)
+        _lib.call("gine_crps_num_partials", N, ctypes.byref(n_part))
+        dpred = torch.empty(N, K, dtype=torch.float64, device=dev)
+        partials = torch.empty(n_part.value, 2, dtype=torch.float64, device=dev)
+        loss = torch.empty((), dtype=torch.float64, device=dev)
+        count = torch.empty(1, dtype=torch.float64, device=dev)
+        _lib.call("gine_crps_fwd", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c, t,
+                  _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss), _lib.ptr(count),
+                  _lib.stream_handle(dev))
+        ctx.save_for_backward(dpred, count)
+        ctx.kind = kind
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        dpred, count = ctx.saved_tensors
+        N = dpred.size(0)
+        g = gloss.detach().to(torch.float64).reshape(1).contiguous()
+        grad = torch.empty(dpred.shape, dtype=torch.float32, device=dpred.device)
+        _lib.call("gine_crps_bwd", _lib.ptr(dpred), _lib.ptr(count), _lib.ptr(g), N, ctx.kind,
+                  _lib.ptr(grad), _lib.stream_handle(dpred.device))
+        return grad, None, None, None, None, None, None
+
+
+def _fused(prediction, y, kind, u=0.0, xi=0.5, c=float(np.log(0.01)), t=5.0):
+    if prediction.dim() != 2:
+        raise ValueError("prediction must be [N, K]")
+    return _FusedCRPS.apply(prediction, y, kind, float(u), float(xi), float(c), float(t))
+
+
+def _use_fused(prediction: torch.Tensor, reduce: bool = True) -> bool:
+    return reduce and prediction.is_cuda
+
+
 def _prepare(prediction: torch.Tensor, y: torch.Tensor, width: int):
     mask = ~torch.isnan(y)
     cols = torch.split(prediction, 1, dim=1)
@@ -77,6 +128,8 @@ class NormalCRPS(torch.nn.Module):
     """models/loss.py:335-369."""
 
     def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if _use_fused(prediction):  # the reference's NormalCRPS stays fp32 (loss.py:358-369)
+            return _fused(prediction, y, _lib.LOSS_NORMAL).to(torch.float32)
         mask, (mu, sigma), y1 = _prepare(prediction, y, 2)
         z = (y1 - mu) / sigma
         crps = sigma * (z * (2.0 * _cdf(z) - 1.0) + 2.0 * _pdf(z) - _INV_SQRT_PI_F32)
@@ -92,6 +145,8 @@ class MixedNormalCRPS(torch.nn.Module):
         self.c = c
 
     def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if _use_fused(prediction, self.reduce):
+            return _fused(prediction, y, _lib.LOSS_MIXED_NORMAL, c=float(self.c))
         mask, (mu, sigma, p), y1 = _prepare(prediction, y, 3)
         c = _consts.get(self.c, y.device)  # float64: np.float64 is a float
         y_t = (y1 - mu) / sigma
@@ -151,6 +206,12 @@ class MixedLoss(torch.nn.Module):
         return sigma * (u_t + t2 + t3 + t4 + t5)
 
     def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if _use_fused(prediction, self.reduce):
+            # u / xi are fp32 tensors in the reference (torch.tensor([python float]))
+            kind = _lib.LOSS_MIXED_U if self.grad_u else _lib.LOSS_MIXED
+            u = 0.0 if self.grad_u else float(np.float32(self.u))
+            return _fused(prediction, y, kind, u=u, xi=float(np.float32(self.xi)),
+                          c=float(self.c), t=float(self.t))
         if self.grad_u == True:  # noqa: E712  (reference compares with == True, loss.py:227)
             mask, (mu, sigma, p, sigma_u, u), y1 = _prepare(prediction, y, 5)
         else:

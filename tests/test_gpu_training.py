@@ -61,3 +61,68 @@ def test_bench_trainer_graph_step_runs():
         losses.append(tr.step().item())
     assert all(map(lambda v: v == v, losses))  # finite / not NaN
     assert losses[-1] < losses[0]              # training makes progress (lr 1e-4, 6 steps)
+
+
+CASES = [("normal", "NormalCRPS", "False"), ("normal_mixed", "MixedNormalCRPS", "False"),
+         ("mixed", "MixedLoss", "False"), ("mixed_u", "MixedLoss", "True")]
+
+
+@pytest.mark.parametrize("name,loss,grad_u", CASES)
+def test_fused_crps_matches_reference_golden(name, loss, grad_u):
+    """The fused HIP loss (value + gradient through PostProcess) vs outputs of the
+    reference's own models/loss.py + models/model_utils.py (tests/golden/)."""
+    import os
+
+    import numpy as np
+
+    from conftest import GOLDEN
+    from raincast_gnn.models import make_loss
+    from raincast_gnn.postprocess import PostProcess
+    d = np.load(os.path.join(GOLDEN, "reference_heads.npz"))
+    raw = torch.from_numpy(d[f"{name}_raw"]).to(DEV).requires_grad_(True)
+    y = torch.from_numpy(d[f"{name}_y"]).to(DEV)
+    fn, _ = make_loss(loss, grad_u, 1.71, 0.5)
+    val = fn.crps(PostProcess(loss, grad_u)(raw), y)
+    assert str(val.dtype) == str(d[f"{name}_loss_dtype"][0])
+    ref = d[f"{name}_loss"][0]
+    assert abs(val.item() - ref) <= 1e-6 * abs(ref), (val.item(), ref)
+    val.backward()
+    g, gr = raw.grad.cpu().numpy(), d[f"{name}_grad"]
+    assert np.abs(g - gr).max() <= 1e-5 * np.abs(gr).max()
+
+
+@pytest.mark.parametrize("name,loss,grad_u", CASES)
+def test_fused_crps_matches_torch_formulation(name, loss, grad_u):
+    from raincast_gnn.models import make_loss
+    from raincast_gnn.postprocess import PostProcess
+    from raincast_gnn.data import synthetic_targets
+    import numpy as np
+    torch.manual_seed(3)
+    K = {"NormalCRPS": 2, "MixedNormalCRPS": 3, "MixedLoss": 4 + (grad_u == "True")}[loss]
+    raw = torch.randn(20000, K)
+    y = torch.from_numpy(synthetic_targets(np.random.default_rng(1), 20000, nan_frac=0.05))
+    fn, _ = make_loss(loss, grad_u, 1.71, 0.5)
+    pp = PostProcess(loss, grad_u)
+    xg = raw.to(DEV).requires_grad_(True)
+    v = fn.crps(pp(xg), y.to(DEV))          # fused HIP path
+    v.backward()
+    xc = raw.clone().requires_grad_(True)
+    vc = fn.crps(pp(xc), y)                  # torch formulation (CPU)
+    vc.backward()
+    assert v.dtype == vc.dtype
+    assert abs(v.item() - vc.item()) <= 1e-6 * abs(vc.item())
+    assert rel_err(xg.grad.cpu(), xc.grad) <= 1e-5
+
+
+def test_fused_crps_nan_handling():
+    from raincast_gnn.loss import MixedLoss
+    fn = MixedLoss(grad_u=False, u=1.71, xi=0.5)
+    pred = torch.rand(50, 4, device=DEV) + 0.1
+    y = torch.full((50,), float("nan"), device=DEV)
+    y[7] = 0.3
+    pred.requires_grad_(True)
+    v = fn.crps(pred, y)
+    v.backward()
+    assert torch.isfinite(v)
+    assert torch.count_nonzero(pred.grad.abs().sum(1)) == 1  # only row 7 has a gradient
+    assert torch.isnan(fn.crps(pred.detach(), torch.full((50,), float("nan"), device=DEV)))
