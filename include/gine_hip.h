@@ -190,6 +190,19 @@ int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t 
 int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
                   int64_t num_nodes, int32_t kind, float* grad_pred, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Weight/bias gradient of a plain Linear y = x W^T + b over many rows (the DeepSet,
+ * dim_red and aggr layers around the GINE stack, models/gnn.py:48-68,112-123):
+ *   dw [O, I] = dy^T x,  db [O] = sum_rows dy  (db may be NULL)
+ * dy [rows, O], x [rows, I] row-major fp32.  Rows are split into chunks
+ * (gine_linear_wgrad_num_chunks); slab holds chunks * (O*I + O) floats of partials,
+ * reduced in fixed order (deterministic).
+ * ---------------------------------------------------------------------------------- */
+int gine_linear_wgrad_num_chunks(int64_t rows, int32_t out_features, int32_t in_features,
+                                 int32_t* num_chunks);
+int gine_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out_features,
+                      int32_t in_features, float* slab, float* dw, float* db, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

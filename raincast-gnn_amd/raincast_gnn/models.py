@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 from torch.nn import Linear, ModuleList, ReLU
 
+from .linear import Linear as RowLinear
 from .loss import MixedLoss, MixedNormalCRPS, NormalCRPS
 from .nn import GINEConv
 from .postprocess import PostProcess
@@ -57,15 +58,15 @@ class DeepSetEncoder(nn.Module):
 
     def __init__(self, ensemble_in_dim, hidden_channels, out_channels):
         super().__init__()
-        self.phi = nn.Sequential(nn.Linear(ensemble_in_dim, hidden_channels), nn.ReLU(),
-                                 nn.Linear(hidden_channels, hidden_channels))
-        self.rho = nn.Sequential(nn.Linear(hidden_channels, hidden_channels), nn.ReLU(),
-                                 nn.Linear(hidden_channels, out_channels))
+        self.phi = nn.Sequential(RowLinear(ensemble_in_dim, hidden_channels), nn.ReLU(),
+                                 RowLinear(hidden_channels, hidden_channels))
+        self.rho = nn.Sequential(RowLinear(hidden_channels, hidden_channels), nn.ReLU(),
+                                 RowLinear(hidden_channels, out_channels))
 
     def forward(self, ensemble_feats):
         lin1, act, lin2 = self.phi
         r = act(lin1(ensemble_feats)).sum(dim=1)                       # [N, H]
-        phi_sum = torch.nn.functional.linear(r, lin2.weight) + ensemble_feats.size(1) * lin2.bias
+        phi_sum = lin2(r) + (ensemble_feats.size(1) - 1) * lin2.bias   # = sum_m lin2(r_m)
         return self.rho(phi_sum)
 
 
@@ -95,10 +96,10 @@ class GNN(nn.Module):
         self.deepset = DeepSetEncoder(ensemble_in_dim=in_channels,
                                       hidden_channels=hidden_channels_gnn,
                                       out_channels=hidden_channels_gnn)
-        self.dim_red = Linear(in_channels + hidden_channels_gnn, hidden_channels_gnn)
+        self.dim_red = RowLinear(in_channels + hidden_channels_gnn, hidden_channels_gnn)
         self.conv = ResGnn(in_channels=hidden_channels_gnn, hidden_channels=hidden_channels_gnn,
                            out_channels=hidden_channels_gnn, num_layers=num_layers_gnn)
-        self.aggr = nn.Linear(out_channels_gnn, self.out_channels)
+        self.aggr = RowLinear(out_channels_gnn, self.out_channels)
         self.postprocess = PostProcess(self.loss, self.grad_u)
         self.optimizer_class = optimizer_class
         self.optimizer_params = optimizer_params

@@ -126,3 +126,22 @@ def test_fused_crps_nan_handling():
     assert torch.isfinite(v)
     assert torch.count_nonzero(pred.grad.abs().sum(1)) == 1  # only row 7 has a gradient
     assert torch.isnan(fn.crps(pred.detach(), torch.full((50,), float("nan"), device=DEV)))
+
+
+@pytest.mark.parametrize("rows,O,I", [(176000, 128, 35), (16000, 128, 163), (16000, 4, 128),
+                                      (1000, 128, 128), (37, 5, 3), (0, 8, 8)])
+def test_linear_wgrad_kernel(rows, O, I):
+    from raincast_gnn.linear import Linear
+    torch.manual_seed(rows + O)
+    lin = Linear(I, O).to(DEV)
+    x = torch.randn(rows, I, device=DEV)
+    dy = torch.randn(rows, O, device=DEV)
+    lin(x).backward(dy)
+    dw64 = dy.double().T @ x.double()
+    db64 = dy.double().sum(0)
+    scale_w = (dy.double().abs().T @ x.double().abs()).max().item() or 1.0
+    assert (lin.weight.grad.double() - dw64).abs().max().item() <= 1e-6 * scale_w
+    if rows:
+        assert (lin.bias.grad.double() - db64).abs().max().item() <= 1e-6 * dy.abs().sum(0).max().item()
+    else:
+        assert torch.count_nonzero(lin.weight.grad) == 0
