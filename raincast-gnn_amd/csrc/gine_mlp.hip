@@ -390,22 +390,41 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs wa, int64_t N) {
   floatx16 acc = zero16();
   double bsum = 0.0;
 
-  for (int64_t n0 = r_begin; n0 < r_end; n0 += kRowTile) {
-    for (int idx = threadIdx.x; idx < kRowTile * BW4; idx += 256) {
+  // Software pipeline: the next 32-row sub-tile's prologue values are loaded into
+  // registers while the current sub-tile's MFMAs run.
+  constexpr int ITEMS = (kRowTile * BW4 + 255) / 256;
+  float4 vp[ITEMS], vq[ITEMS];
+  auto load = [&](int64_t n0) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = threadIdx.x + k * 256;
       const int r = idx / BW4, q = idx % BW4;
       const int64_t n = n0 + r;
       const int64_t nc = n < r_end ? n : r_end - 1;
-      float4 vp = zsel == 0 ? prologue<PRO_DO>(P, D, nc, o0 / 4 + q)
-                            : prologue<PRO_DA1>(P, D, nc, o0 / 4 + q);
-      float4 vq = zsel == 0 ? prologue<PRO_BNRELU>(Q, D, nc, i0 / 4 + q)
-                            : prologue<PRO_PLAIN>(Q, D, nc, i0 / 4 + q);
-      if (n >= r_end) vp = vq = f4_zero();
-      float* dp = &sP[r * LDW + 4 * q];
-      float* dq = &sQ[r * LDW + 4 * q];
-      dp[0] = vp.x; dp[1] = vp.y; dp[2] = vp.z; dp[3] = vp.w;
-      dq[0] = vq.x; dq[1] = vq.y; dq[2] = vq.z; dq[3] = vq.w;
+      float4 a = zsel == 0 ? prologue<PRO_DO>(P, D, nc, o0 / 4 + q)
+                           : prologue<PRO_DA1>(P, D, nc, o0 / 4 + q);
+      float4 b = zsel == 0 ? prologue<PRO_BNRELU>(Q, D, nc, i0 / 4 + q)
+                           : prologue<PRO_PLAIN>(Q, D, nc, i0 / 4 + q);
+      if (n >= r_end || idx >= kRowTile * BW4) a = b = f4_zero();
+      vp[k] = a;
+      vq[k] = b;
+    }
+  };
+  load(r_begin);
+  for (int64_t n0 = r_begin; n0 < r_end; n0 += kRowTile) {
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = threadIdx.x + k * 256;
+      if (idx < kRowTile * BW4) {
+        const int r = idx / BW4, q = idx % BW4;
+        float* dp = &sP[r * LDW + 4 * q];
+        float* dq = &sQ[r * LDW + 4 * q];
+        dp[0] = vp[k].x; dp[1] = vp[k].y; dp[2] = vp[k].z; dp[3] = vp[k].w;
+        dq[0] = vq[k].x; dq[1] = vq[k].y; dq[2] = vq[k].z; dq[3] = vq[k].w;
+      }
     }
     __syncthreads();
+    if (n0 + kRowTile < r_end) load(n0 + kRowTile);
     if (active) {
 #pragma unroll
       for (int s = 0; s < kRowTile / 2; ++s) {
