@@ -83,10 +83,11 @@ class Trainer:
         self.loss = None
 
     def fwd_bwd(self):
-        self.opt.zero_grad()
+        self.opt.zero_grad()            # set_to_none: kernels write grads into flat slices
         pred = self.model(self.batch)
         loss = self.model.loss_fn.crps(pred, self.batch.y)
         loss.backward()
+        self.opt.gather_grads()         # flat_grad complete before the all-reduce
         return loss
 
     def eager_step(self):

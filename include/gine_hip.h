@@ -89,7 +89,8 @@ int gine_mp_fwd(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
  *   partials[b] (fp64, [3][D] per block b): sum dm*a, sum dm, sum dz*x for the block
  *   flags may also carry GINE_MP_LIN_MULADD (must match the forward).
  * gine_mp_bwd_finalize reduces the partials in fixed block order into
- *   dlin_w [D], dlin_b [D], deps [1].
+ *   dlin_w [D], dlin_b [D], deps [1].  Finalize calls reduce IN PLACE: the partials
+ *   buffer is consumed (overwritten) -- true of every *_finalize below too.
  * ---------------------------------------------------------------------------------- */
 #define GINE_MP_BWD_SELF 1
 int gine_mp_bwd_num_partials(int64_t num_nodes, int32_t channels, int32_t* num_partials);

@@ -126,28 +126,29 @@ __global__ __launch_bounds__(256) void k_linear_wgrad(const float* __restrict__ 
   if (do_bias && h == 0 && ob < O) out[(size_t)O * I + ob] = (float)bsum;
 }
 
+// 64 consecutive slab elements x 4 chunk groups per workgroup (fixed order, see gine_mlp).
 __global__ __launch_bounds__(256) void k_linear_slab_reduce(const float* __restrict__ slab,
                                                             int chunks, int64_t per,
                                                             int64_t wsize,
                                                             float* __restrict__ dw,
                                                             float* __restrict__ db) {
-  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (e >= per) return;
-  const float* base = slab + e;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int c = 0;
-  for (; c + 3 < chunks; c += 4) {
-    a0 += (double)base[(size_t)c * per];
-    a1 += (double)base[(size_t)(c + 1) * per];
-    a2 += (double)base[(size_t)(c + 2) * per];
-    a3 += (double)base[(size_t)(c + 3) * per];
+  __shared__ double s_part[4][64];
+  const int64_t e = blockIdx.x * (int64_t)64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  double acc = 0.0;
+  if (e < per) {
+    const float* base = slab + e;
+    for (int c = g; c < chunks; c += 4) acc += (double)base[(size_t)c * per];
   }
-  for (; c < chunks; ++c) a0 += (double)base[(size_t)c * per];
-  const float s = (float)((a0 + a1) + (a2 + a3));
+  s_part[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g != 0 || e >= per) return;
+  const int j = threadIdx.x & 63;
+  const float v = (float)((s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]));
   if (e < wsize) {
-    dw[e] = s;
+    dw[e] = v;
   } else if (db != nullptr) {
-    db[e - wsize] = s;
+    db[e - wsize] = v;
   }
 }
 
@@ -181,7 +182,7 @@ extern "C" int gine_linear_wgrad(const float* dy, const float* x, int64_t rows,
                        dy, x, rows, O, I, p.rows_per_chunk, p.tiles_i, slab);
     GINE_LAUNCH_STATUS();
   }
-  hipLaunchKernelGGL(k_linear_slab_reduce, dim3((unsigned)ceil_div(per, 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_linear_slab_reduce, dim3((unsigned)ceil_div(per, 64)), dim3(256), 0, s,
                      slab, rows == 0 ? 1 : p.chunks, per, (int64_t)O * I, dw, db);
   GINE_LAUNCH_STATUS();
   return GINE_OK;

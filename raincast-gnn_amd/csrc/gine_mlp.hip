@@ -297,7 +297,7 @@ __global__ __launch_bounds__(kColsumThreads) void k_bn_fwd_finalize(
   __shared__ double s_tmp[kColsumThreads];
   __shared__ double s_sum[2 * 256];  // [sum | sumsq], D <= 256
   __shared__ double s_factor;
-  if (training) block_colsum(partials, P, 2 * D, 2 * D, s_tmp, s_sum);
+  if (training) block_colsum(partials, P, 2 * D, 2 * D * kSliceRows, s_tmp, s_sum);
   if (threadIdx.x == 0) {
     double f = (double)momentum;
     if (training && update_running && nbt != nullptr) {
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kColsumThreads) void k_bn_bwd_finalize(
     float* __restrict__ coef, int64_t N, int D, int training) {
   __shared__ double s_tmp[kColsumThreads];
   __shared__ double s_sum[2 * 256];  // [sum dbn | sum dbn*xhat]
-  block_colsum(partials, P, 2 * D, 2 * D, s_tmp, s_sum);
+  block_colsum(partials, P, 2 * D, 2 * D * kSliceRows, s_tmp, s_sum);
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
     const double sd = s_sum[c], sx = s_sum[D + c];
     if (dgamma) dgamma[c] = (float)sx;
@@ -451,32 +451,35 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs wa, int64_t N) {
   if (do_bias && h == 0) slab[(size_t)D * D + o0 + 32 * wr + c32] = (float)bsum;
 }
 
+// Sum the chunk slabs: workgroup = 64 consecutive elements x 4 chunk groups (chunk c goes
+// to group c % 4, summed in chunk order), groups combined in fixed order through LDS.
 __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int chunks,
                                                      int D, float* __restrict__ dw2,
                                                      float* __restrict__ db2,
                                                      float* __restrict__ dw1,
                                                      float* __restrict__ db1) {
+  __shared__ double s_part[4][64];
   const int per = D * D + D;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= 2 * per) return;
-  const int zsel = e / per, r = e % per;
-  const float* base = slab + (size_t)zsel * chunks * per + r;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int c = 0;
-  for (; c + 3 < chunks; c += 4) {
-    a0 += (double)base[(size_t)c * per];
-    a1 += (double)base[(size_t)(c + 1) * per];
-    a2 += (double)base[(size_t)(c + 2) * per];
-    a3 += (double)base[(size_t)(c + 3) * per];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  double acc = 0.0;
+  if (e < 2 * per) {
+    const int zsel = e / per, r = e % per;
+    const float* base = slab + (size_t)zsel * chunks * per + r;
+    for (int c = g; c < chunks; c += 4) acc += (double)base[(size_t)c * per];
   }
-  for (; c < chunks; ++c) a0 += (double)base[(size_t)c * per];
-  const double s = (a0 + a1) + (a2 + a3);
+  s_part[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g != 0 || e >= 2 * per) return;
+  const int j = threadIdx.x & 63;
+  const float v = (float)((s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]));
+  const int zsel = e / per, r = e % per;
   float* w = zsel == 0 ? dw2 : dw1;
   float* b = zsel == 0 ? db2 : db1;
   if (r < D * D) {
-    if (w) w[r] = (float)s;
+    if (w) w[r] = v;
   } else {
-    if (b) b[r - D * D] = (float)s;
+    if (b) b[r - D * D] = v;
   }
 }
 
@@ -526,9 +529,15 @@ extern "C" int gine_bn_fwd_finalize(const double* partials, int32_t num_partials
   if (!training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
   if (update_running && training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
   if (channels > 256) return GINE_ERR_DIM;
+  int S = 0;
+  if (training) {  // stage 1 of the partial reduction; stage 2 inside the finalize
+    S = launch_colsum_slices(const_cast<double*>(partials), num_partials, 2 * channels,
+                             as_stream(stream));
+    GINE_LAUNCH_STATUS();
+  }
   hipLaunchKernelGGL(k_bn_fwd_finalize, dim3(1), dim3(kColsumThreads), 0, as_stream(stream),
                      partials,
-                     num_partials, gamma, beta, running_mean, running_var, num_batches_tracked,
+                     S, gamma, beta, running_mean, running_var, num_batches_tracked,
                      bn_save, num_nodes, channels, momentum, bn_eps, training, update_running);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
@@ -570,9 +579,12 @@ extern "C" int gine_bn_bwd_finalize(const double* partials, int32_t num_partials
   if (channels <= 0 || !partials || num_partials <= 0 || !bn_save || !coef || num_nodes <= 0)
     return GINE_ERR_INVALID;
   if (channels > 256) return GINE_ERR_DIM;
+  const int S = launch_colsum_slices(const_cast<double*>(partials), num_partials, 2 * channels,
+                                     as_stream(stream));
+  GINE_LAUNCH_STATUS();
   hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(1), dim3(kColsumThreads), 0, as_stream(stream),
                      partials,
-                     num_partials, gamma, bn_save, dgamma, dbeta, coef, num_nodes, channels,
+                     S, gamma, bn_save, dgamma, dbeta, coef, num_nodes, channels,
                      training);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
@@ -630,7 +642,7 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   }
   GINE_LAUNCH_STATUS();
   const int total = 2 * (D * D + D);
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, slab,
+  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)ceil_div(total, 64)), dim3(256), 0, s, slab,
                      wa.chunks, D, dw2, db2, dw1, db1);
   GINE_LAUNCH_STATUS();
   return GINE_OK;

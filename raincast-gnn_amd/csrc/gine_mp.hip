@@ -295,11 +295,12 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
 }
 
 __global__ __launch_bounds__(kColsumThreads) void k_mp_bwd_finalize(
-    const double* __restrict__ partials, int P, int D, float* __restrict__ dlin_w,
+    const double* __restrict__ partials, int S, int D, float* __restrict__ dlin_w,
     float* __restrict__ dlin_b, float* __restrict__ deps) {
   __shared__ double s_tmp[kColsumThreads];
   extern __shared__ __attribute__((aligned(16))) double s_out[];  // [3D]
-  block_colsum(partials, P, 3 * D, 3 * D, s_tmp, s_out);
+  // stage 2: the S slice heads left by k_colsum_slices (row stride kSliceRows rows)
+  block_colsum(partials, S, 3 * D, 3 * D * kSliceRows, s_tmp, s_out);
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
     dlin_w[c] = (float)s_out[c];
     dlin_b[c] = (float)s_out[D + c];
@@ -441,8 +442,11 @@ extern "C" int gine_mp_bwd_finalize(const double* partials, int32_t num_partials
   int m = 1;
   while (m < channels) m <<= 1;  // tree-sum scratch beyond 3D
   const size_t smem = sizeof(double) * (size_t)(2 * channels + m);
-  hipLaunchKernelGGL(k_mp_bwd_finalize, dim3(1), dim3(kColsumThreads), smem,
-                     as_stream(stream), partials, num_partials, channels, dlin_w, dlin_b, deps);
+  hipStream_t s = as_stream(stream);
+  const int S = launch_colsum_slices(const_cast<double*>(partials), num_partials, 3 * channels, s);
+  GINE_LAUNCH_STATUS();
+  hipLaunchKernelGGL(k_mp_bwd_finalize, dim3(1), dim3(kColsumThreads), smem, s, partials, S,
+                     channels, dlin_w, dlin_b, deps);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

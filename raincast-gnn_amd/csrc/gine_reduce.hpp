@@ -47,6 +47,44 @@ __device__ inline void block_colsum(const double* __restrict__ a, int P, int W, 
   }
 }
 
+// Stage 1 of a two-stage fixed-order column reduction of a row-major [P][W] fp64 matrix:
+// workgroup (column slab x, row slice y) sums rows [y*L, y*L+L) of 64 columns and writes
+// the result IN PLACE into row y*L (the first row of its own slice -- no other workgroup
+// reads it).  Stage 2 then reduces the S = ceil(P/L) slice heads with block_colsum using
+// row stride L*W.  Pulls the partials through many CUs instead of one.
+constexpr int kSliceRows = 32;
+
+namespace {  // one private copy of the kernel per translation unit
+
+__global__ __launch_bounds__(256) void k_colsum_slices(double* __restrict__ a, int P, int W) {
+  __shared__ double s_part[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane4 = threadIdx.x >> 6;  // 4 row lanes
+  const int r0 = blockIdx.y * kSliceRows;
+  const int r1 = min(P, r0 + kSliceRows);
+  double acc = 0.0;
+  if (c < W) {
+    for (int r = r0 + lane4; r < r1; r += 4) acc += a[(size_t)r * W + c];
+  }
+  s_part[lane4][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (lane4 == 0 && c < W) {
+    const int j = threadIdx.x & 63;
+    a[(size_t)r0 * W + c] = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
+  }
+}
+
+inline int colsum_slices(int P) { return (P + kSliceRows - 1) / kSliceRows; }
+
+// Launch stage 1 on `s`; returns the number of slice heads (stage-2 rows).
+inline int launch_colsum_slices(double* a, int P, int W, hipStream_t s) {
+  const int S = colsum_slices(P);
+  hipLaunchKernelGGL(k_colsum_slices, dim3((W + 63) / 64, S), dim3(256), 0, s, a, P, W);
+  return S;
+}
+
+}  // namespace
+
 // Fixed-order tree sum of v[0..n) (LDS, clobbered) by one workgroup; result in v[0].
 __device__ inline void block_tree_sum(double* v, int n) {
   int m = 1;

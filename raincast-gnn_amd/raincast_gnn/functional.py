@@ -23,6 +23,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr
+from .gradbuf import grad_out
 
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = _lib.EPI_NONE, _lib.EPI_RELU, _lib.EPI_RESIDUAL_RELU
 
@@ -88,14 +89,17 @@ def mp_forward(x, graph, lin_w, lin_b, eps, lin_flag=None):
     return z
 
 
-def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_flag=None):
-    """Returns (dx, dlin_w[D], dlin_b[D], deps[1])."""
+def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_flag=None,
+                params=(None, None, None)):
+    """Returns (dx, dlin_w, dlin_b, deps); ``params`` = the (lin.weight, lin.bias, eps)
+    Parameters, whose gradients then go straight to their flat-buffer slices if any."""
     N, D = x.shape
     dev = x.device
     dx = torch.empty_like(x)
-    dlw = torch.empty(D, dtype=torch.float32, device=dev)
-    dlb = torch.empty(D, dtype=torch.float32, device=dev)
-    deps = torch.empty(1, dtype=torch.float32, device=dev)
+    p_w, p_b, p_e = params
+    dlw = grad_out(p_w, (D,), dev) if p_w is not None else torch.empty(D, device=dev)
+    dlb = grad_out(p_b, (D,), dev) if p_b is not None else torch.empty(D, device=dev)
+    deps = grad_out(p_e, (1,), dev) if p_e is not None else torch.empty(1, device=dev)
     if N == 0:
         return dx, dlw.zero_(), dlb.zero_(), deps.zero_()
     P = _count("gine_mp_bwd_num_partials", N, D)
@@ -121,12 +125,14 @@ class GineMessagePassing(torch.autograd.Function):
         ctx.save_for_backward(x, lw, lb, ep)
         ctx.graph = graph
         ctx.lin_w_shape = lin_w.shape
+        ctx.params = (lin_w, lin_b, eps)
         return z
 
     @staticmethod
     def backward(ctx, dz):
         x, lw, lb, ep = ctx.saved_tensors
-        dx, dlw, dlb, deps = mp_backward(dz.contiguous(), x, ctx.graph, lw, lb, ep)
+        dx, dlw, dlb, deps = mp_backward(dz.contiguous(), x, ctx.graph, lw, lb, ep,
+                                         params=ctx.params)
         return dx, dlw.view(ctx.lin_w_shape), dlb, deps.view_as(ep), None
 
 
@@ -188,6 +194,7 @@ class GineLayer(torch.autograd.Function):
                               lw, lb, ep, w1c, w2c, g)
         ctx.graph, ctx.epilogue = graph, epilogue
         ctx.use_batch_stats = bn.use_batch_stats
+        ctx.params = (lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2)
         ctx.shapes = (lin_w.shape, gamma is not None)
         return y
 
@@ -205,8 +212,9 @@ class GineLayer(torch.autograd.Function):
         partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
         call("gine_mlp_bwd2", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save), ptr(w2c),
              ptr(dbn), ptr(partials), N, D, epi, stream)
-        dgamma = torch.empty(D, dtype=torch.float32, device=dev)
-        dbeta = torch.empty(D, dtype=torch.float32, device=dev)
+        p_lw, p_lb, p_eps, p_w1, p_b1, p_g, p_bt, p_w2, p_b2 = ctx.params
+        dgamma = grad_out(p_g, (D,), dev) if p_g is not None else None
+        dbeta = grad_out(p_bt, (D,), dev) if p_bt is not None else None
         coef = torch.empty(3, D, dtype=torch.float32, device=dev)
         call("gine_bn_bwd_finalize", ptr(partials), P, ptr(g), ptr(bn_save), ptr(dgamma),
              ptr(dbeta), ptr(coef), N, D, int(ctx.use_batch_stats), stream)
@@ -215,16 +223,14 @@ class GineLayer(torch.autograd.Function):
              D, stream)
         C = _count("gine_mlp_wgrad_num_chunks", N, D)
         slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
-        dw1 = torch.empty(D, D, dtype=torch.float32, device=dev)
-        dw2 = torch.empty(D, D, dtype=torch.float32, device=dev)
-        db1 = torch.empty(D, dtype=torch.float32, device=dev)
-        db2 = torch.empty(D, dtype=torch.float32, device=dev)
+        dw1, db1 = grad_out(p_w1, (D, D), dev), grad_out(p_b1, (D,), dev)
+        dw2, db2 = grad_out(p_w2, (D, D), dev), grad_out(p_b2, (D,), dev)
         call("gine_mlp_wgrad", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save), ptr(dbn),
              ptr(coef), ptr(z), ptr(slab), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), N, D, epi,
              stream)
         dres = dy if epi == EPI_RESIDUAL_RELU else None
-        dx, dlw, dlb, deps = mp_backward(dz, x, ctx.graph, lw, lb, ep, dres=dres)
+        dx, dlw, dlb, deps = mp_backward(dz, x, ctx.graph, lw, lb, ep, dres=dres,
+                                         params=(p_lw, p_lb, p_eps))
         lin_w_shape, affine = ctx.shapes
-        return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1,
-                dgamma if affine else None, dbeta if affine else None, dw2, db2,
-                None, None, None)
+        return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1, dgamma, dbeta,
+                dw2, db2, None, None, None)

@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from .gradbuf import grad_out
 
 
 class _RowLinearFn(torch.autograd.Function):
@@ -22,6 +23,7 @@ class _RowLinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -37,8 +39,8 @@ class _RowLinearFn(torch.autograd.Function):
             chunks = ctypes.c_int32(0)
             _lib.call("gine_linear_wgrad_num_chunks", R, O, I, ctypes.byref(chunks))
             slab = torch.empty(chunks.value * (O * I + O), dtype=torch.float32, device=dy.device)
-            dw = torch.empty(O, I, dtype=torch.float32, device=dy.device)
-            db = torch.empty(O, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
+            dw = grad_out(ctx.params[0], (O, I), dy.device)
+            db = grad_out(ctx.params[1], (O,), dy.device) if ctx.has_bias else None
             _lib.call("gine_linear_wgrad", _lib.ptr(dy2), _lib.ptr(x2), R, O, I, _lib.ptr(slab),
                       _lib.ptr(dw), _lib.ptr(db), _lib.stream_handle(dy.device))
         return dx, dw, db

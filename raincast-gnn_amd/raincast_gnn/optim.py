@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
+from . import _lib, gradbuf
 
 
 class FlatAdamW:
@@ -26,6 +26,7 @@ class FlatAdamW:
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), betas, float(eps), \
             float(weight_decay)
         n = sum(p.numel() for p in self.params)
+        self._offsets = []
         self.flat_param = torch.empty(n, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
         off = 0
@@ -35,7 +36,8 @@ class FlatAdamW:
                 view = self.flat_param[off:off + k].view_as(p)
                 view.copy_(p)
                 p.data = view
-                p.grad = self.flat_grad[off:off + k].view_as(p)
+                gradbuf.register(p, self.flat_grad, off)
+                self._offsets.append(off)
                 off += k
         self.exp_avg = torch.zeros_like(self.flat_param)
         self.exp_avg_sq = torch.zeros_like(self.flat_param)
@@ -45,13 +47,41 @@ class FlatAdamW:
     def numel(self) -> int:
         return self.flat_param.numel()
 
-    def zero_grad(self, set_to_none: bool = False) -> None:
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """Release the gradients.  The HIP backward kernels then write each parameter's
+        gradient straight into its slice of ``flat_grad`` (raincast_gnn/gradbuf.py);
+        ``set_to_none=False`` instead keeps ``.grad`` as slice views and zeroes them
+        (gradients are then accumulated by autograd, one add per parameter)."""
         if set_to_none:
-            raise ValueError("FlatAdamW keeps gradients in its flat buffer (set_to_none=False)")
-        self.flat_grad.zero_()
+            for p in self.params:
+                p.grad = None
+            gradbuf.new_step(self.params)
+        else:
+            for p, off in zip(self.params, self._offsets):
+                if p.grad is None or p.grad.data_ptr() != self.flat_grad[off:].data_ptr():
+                    p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            self.flat_grad.zero_()
+
+    @torch.no_grad()
+    def gather_grads(self) -> None:
+        """Make ``flat_grad`` hold every gradient: parameters whose ``.grad`` is not their
+        slice (a CPU-side or generic-torch backward produced it) are copied in, unused ones
+        zeroed.  Host-side pointer checks only when everything already landed in place."""
+        base = self.flat_grad.data_ptr()
+        for p, off in zip(self.params, self._offsets):
+            g = p.grad
+            if g is not None and g.data_ptr() == base + 4 * off:
+                continue
+            sl = self.flat_grad[off:off + p.numel()]
+            if g is None:
+                sl.zero_()
+            else:
+                sl.copy_(g.reshape(-1))
+            p.grad = sl.view_as(p)
 
     @torch.no_grad()
     def step(self) -> None:
+        self.gather_grads()
         b1, b2 = self.betas
         _lib.call("gine_adamw_step", _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad),
                   _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), _lib.ptr(self.step_count),

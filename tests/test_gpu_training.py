@@ -145,3 +145,28 @@ def test_linear_wgrad_kernel(rows, O, I):
         assert (lin.bias.grad.double() - db64).abs().max().item() <= 1e-6 * dy.abs().sum(0).max().item()
     else:
         assert torch.count_nonzero(lin.weight.grad) == 0
+
+
+def test_grads_land_in_flat_buffer_without_copies():
+    """Backward kernels write every parameter gradient straight into its FlatAdamW slice,
+    and the resulting training trajectory equals torch.optim.AdamW's on ordinary grads."""
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.models import GNN
+    torch.manual_seed(5)
+    base = GNN(35, 128, 128, 4, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5)
+    batch = synthetic_batch(300, 2, k=8, seed=2).to(DEV)
+    m1, m2 = copy.deepcopy(base).to(DEV), copy.deepcopy(base).to(DEV)
+    opt1 = FlatAdamW(m1.parameters(), lr=1e-3)
+    opt2 = torch.optim.AdamW(m2.parameters(), lr=1e-3, foreach=False)
+    for step in range(3):
+        opt1.zero_grad()
+        m1.loss_fn.crps(m1(batch), batch.y).backward()
+        base_ptr = opt1.flat_grad.data_ptr()
+        for p, off in zip(opt1.params, opt1._offsets):
+            assert p.grad.data_ptr() == base_ptr + 4 * off   # adopted, not copied
+        opt1.step()
+        opt2.zero_grad()
+        m2.loss_fn.crps(m2(batch), batch.y).backward()
+        opt2.step()
+    for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert rel_err(p.detach(), q.detach()) <= 1e-5, n

@@ -12,7 +12,7 @@ import statistics
 
 
 def family(name: str) -> str:
-    n = re.sub(r"\(.*", "", name).replace("void ", "")
+    n = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "")).replace("void ", "")
     n = re.sub(r"<.*", "", n) if n.startswith("at::") else n
     if n.startswith("Cijk_"):
         return "rocBLAS/hipBLASLt GEMM " + re.search(r"MT\w+?_", n).group(0)[:-1]
