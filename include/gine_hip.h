@@ -194,7 +194,8 @@ int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
 /* ------------------------------------------------------------------------------------
  * Weight/bias gradient of a plain Linear y = x W^T + b over many rows (the DeepSet,
  * dim_red and aggr layers around the GINE stack, models/gnn.py:48-68,112-123):
- *   dw [O, I] = dy^T x,  db [O] = sum_rows dy  (db may be NULL)
+ *   dw [O, I] = dy^T x,  db [O] = bias_scale * sum_rows dy  (db may be NULL)
+ * (bias_scale: y = x W^T + bias_scale * b, e.g. the DeepSet member sum of a bias)
  * dy [rows, O], x [rows, I] row-major fp32.  Rows are split into chunks
  * (gine_linear_wgrad_num_chunks); slab holds chunks * (O*I + O) floats of partials,
  * reduced in fixed order (deterministic).
@@ -202,7 +203,8 @@ int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
 int gine_linear_wgrad_num_chunks(int64_t rows, int32_t out_features, int32_t in_features,
                                  int32_t* num_chunks);
 int gine_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out_features,
-                      int32_t in_features, float* slab, float* dw, float* db, void* stream);
+                      int32_t in_features, float* slab, float* dw, float* db, float bias_scale,
+                      void* stream);
 
 #ifdef __cplusplus
 }

@@ -131,7 +131,8 @@ __global__ __launch_bounds__(256) void k_linear_slab_reduce(const float* __restr
                                                             int chunks, int64_t per,
                                                             int64_t wsize,
                                                             float* __restrict__ dw,
-                                                            float* __restrict__ db) {
+                                                            float* __restrict__ db,
+                                                            float bias_scale) {
   __shared__ double s_part[4][64];
   const int64_t e = blockIdx.x * (int64_t)64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
@@ -144,11 +145,11 @@ __global__ __launch_bounds__(256) void k_linear_slab_reduce(const float* __restr
   __syncthreads();
   if (g != 0 || e >= per) return;
   const int j = threadIdx.x & 63;
-  const float v = (float)((s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]));
+  const double v = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
   if (e < wsize) {
-    dw[e] = v;
+    dw[e] = (float)v;
   } else if (db != nullptr) {
-    db[e - wsize] = v;
+    db[e - wsize] = (float)(v * (double)bias_scale);
   }
 }
 
@@ -167,7 +168,7 @@ extern "C" int gine_linear_wgrad_num_chunks(int64_t rows, int32_t out_features,
 
 extern "C" int gine_linear_wgrad(const float* dy, const float* x, int64_t rows,
                                  int32_t out_features, int32_t in_features, float* slab,
-                                 float* dw, float* db, void* stream) {
+                                 float* dw, float* db, float bias_scale, void* stream) {
   if (rows < 0 || out_features <= 0 || in_features <= 0 || !dw || !slab)
     return GINE_ERR_INVALID;
   if (rows > 0 && (!dy || !x)) return GINE_ERR_INVALID;
@@ -183,7 +184,7 @@ extern "C" int gine_linear_wgrad(const float* dy, const float* x, int64_t rows,
     GINE_LAUNCH_STATUS();
   }
   hipLaunchKernelGGL(k_linear_slab_reduce, dim3((unsigned)ceil_div(per, 64)), dim3(256), 0, s,
-                     slab, rows == 0 ? 1 : p.chunks, per, (int64_t)O * I, dw, db);
+                     slab, rows == 0 ? 1 : p.chunks, per, (int64_t)O * I, dw, db, bias_scale);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

@@ -54,7 +54,7 @@ _SIGNATURES = {
     "gine_crps_bwd": [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
     "gine_linear_wgrad_num_chunks": [_i64, _i32, _i32, ctypes.POINTER(_i32)],
     "gine_linear_wgrad": [_c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p,
-                          _c_void_p, _c_void_p],
+                          _c_void_p, _f32, _c_void_p],
 }
 
 EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)

@@ -19,12 +19,19 @@ from .gradbuf import grad_out
 
 
 class _RowLinearFn(torch.autograd.Function):
+    """y = x W^T + bias_scale * b."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, bias_scale=1.0):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.params = (weight, bias)
-        return F.linear(x, weight, bias)
+        ctx.bias_scale = float(bias_scale)
+        if bias is None or bias_scale == 1.0:
+            return F.linear(x, weight, bias)
+        x2 = x.reshape(-1, x.size(-1))
+        y = torch.addmm(bias, x2, weight.t(), beta=bias_scale)
+        return y.reshape(*x.shape[:-1], weight.size(0))
 
     @staticmethod
     def backward(ctx, dy):
@@ -42,13 +49,16 @@ class _RowLinearFn(torch.autograd.Function):
             dw = grad_out(ctx.params[0], (O, I), dy.device)
             db = grad_out(ctx.params[1], (O,), dy.device) if ctx.has_bias else None
             _lib.call("gine_linear_wgrad", _lib.ptr(dy2), _lib.ptr(x2), R, O, I, _lib.ptr(slab),
-                      _lib.ptr(dw), _lib.ptr(db), _lib.stream_handle(dy.device))
-        return dx, dw, db
+                      _lib.ptr(dw), _lib.ptr(db), ctx.bias_scale, _lib.stream_handle(dy.device))
+        return dx, dw, db, None
 
 
 class Linear(torch.nn.Linear):
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, bias_scale: float = 1.0) -> torch.Tensor:
+        """``x W^T + bias_scale * b`` (bias_scale=1: torch.nn.Linear)."""
         if (x.is_cuda and x.dtype == torch.float32 and self.weight.dtype == torch.float32
                 and torch.is_grad_enabled()):
-            return _RowLinearFn.apply(x, self.weight, self.bias)
-        return F.linear(x, self.weight, self.bias)
+            return _RowLinearFn.apply(x, self.weight, self.bias, bias_scale)
+        if bias_scale == 1.0 or self.bias is None:
+            return F.linear(x, self.weight, self.bias)
+        return F.linear(x, self.weight) + bias_scale * self.bias

@@ -66,7 +66,7 @@ class DeepSetEncoder(nn.Module):
     def forward(self, ensemble_feats):
         lin1, act, lin2 = self.phi
         r = act(lin1(ensemble_feats)).sum(dim=1)                       # [N, H]
-        phi_sum = lin2(r) + (ensemble_feats.size(1) - 1) * lin2.bias   # = sum_m lin2(r_m)
+        phi_sum = lin2(r, bias_scale=ensemble_feats.size(1))           # = sum_m lin2(r_m)
         return self.rho(phi_sum)
 
 

@@ -26,7 +26,7 @@ def test_flat_adamw_matches_torch_adamw():
         # identical gradients on both sides: only the optimizer arithmetic is compared
         opt_ref.zero_grad()
         ref(x).square().mean().backward()
-        opt.zero_grad()
+        opt.zero_grad(set_to_none=False)
         for p, q in zip(net.parameters(), ref.parameters()):
             p.grad.copy_(q.grad)
         opt.step()
