@@ -34,6 +34,9 @@ for s in $STEPS; do
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ;;
+    counters) run list_counters 300 rocprofv3 -L ;;
+    sq)    run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d "$OUT/pmc_sq" -o run -- \
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ;;
   esac
 done
 echo "session done" | tee -a "$OUT/session.log"
