@@ -22,6 +22,8 @@
 #include "gine_common.hpp"
 #include "gine_reduce.hpp"
 
+#include <algorithm>
+
 namespace gine {
 namespace {
 
@@ -35,7 +37,6 @@ __device__ __forceinline__ floatx16 zero16() {
 }
 
 constexpr int kRowTile = 32;
-constexpr int kMaxRowBlocks = 1024;
 constexpr int kChunkTarget = 64;
 
 enum Pro { PRO_PLAIN = 0, PRO_BNRELU = 1, PRO_DO = 2, PRO_DA1 = 3 };
@@ -136,6 +137,94 @@ __device__ __forceinline__ TileRange xcd_tile_range(int num_tiles) {
 //   BT = true : B[k][j] = W[j][k]   (Y = X W^T, forward Linear)
 //   BT = false: B[k][j] = W[k][j]   (dX = dY W, backward Linear)
 // ----------------------------------------------------------------------------------------
+// Raw (pre-prologue) values of one staged float4 item, loaded a tile ahead.
+struct RawItem {
+  float4 v;    // primary input
+  float4 aux;  // y (PRO_DO, ReLU epilogue) | a1 (PRO_DA1)
+  uchar4 m;    // ReLU mask (PRO_DO, residual epilogue)
+};
+
+// Per-thread column constants of the prologue (a thread always stages the same column
+// group q = tid % (D/4), so these are loaded once per workgroup).
+struct ColConst {
+  float4 a, b, c, d, e;
+};
+
+template <int PRO>
+__device__ __forceinline__ ColConst col_const(const ProArgs& p, int D, int q) {
+  ColConst k;
+  k.a = k.b = k.c = k.d = k.e = f4_zero();
+  if constexpr (PRO == PRO_BNRELU) {
+    const BnView b = bn_view(p.bn, D);
+    k.a = *reinterpret_cast<const float4*>(b.alpha + 4 * q);
+    k.b = *reinterpret_cast<const float4*>(b.shift + 4 * q);
+  } else if constexpr (PRO == PRO_DA1) {
+    const BnView b = bn_view(p.bn, D);
+    k.a = *reinterpret_cast<const float4*>(p.coef + 4 * q);
+    k.b = *reinterpret_cast<const float4*>(p.coef + D + 4 * q);
+    k.c = *reinterpret_cast<const float4*>(p.coef + 2 * D + 4 * q);
+    k.d = *reinterpret_cast<const float4*>(b.mean + 4 * q);
+    k.e = *reinterpret_cast<const float4*>(b.invstd + 4 * q);
+  }
+  return k;
+}
+
+template <int PRO>
+__device__ __forceinline__ RawItem raw_load(const ProArgs& p, int D, int64_t n, int q) {
+  RawItem r;
+  const int64_t off = n * D + 4 * q;
+  r.v = *reinterpret_cast<const float4*>(p.x + off);
+  r.aux = f4_zero();
+  r.m = make_uchar4(1, 1, 1, 1);
+  if constexpr (PRO == PRO_DO) {
+    if (p.epi == GINE_EPI_RELU) r.aux = *reinterpret_cast<const float4*>(p.aux + off);
+    if (p.epi == GINE_EPI_RESIDUAL_RELU) r.m = *reinterpret_cast<const uchar4*>(p.mask + off);
+  } else if constexpr (PRO == PRO_DA1) {
+    r.aux = *reinterpret_cast<const float4*>(p.aux + off);
+  }
+  return r;
+}
+
+// Same arithmetic as prologue<PRO>() (the weight-gradient kernel recomputes through that).
+template <int PRO>
+__device__ __forceinline__ float4 transform(const ProArgs& p, const RawItem& r,
+                                            const ColConst& k) {
+  const float4 v = r.v;
+  if constexpr (PRO == PRO_PLAIN) {
+    return v;
+  } else if constexpr (PRO == PRO_BNRELU) {
+    return make_float4(relu_nan(bn_apply(v.x, k.a.x, k.b.x)), relu_nan(bn_apply(v.y, k.a.y, k.b.y)),
+                       relu_nan(bn_apply(v.z, k.a.z, k.b.z)), relu_nan(bn_apply(v.w, k.a.w, k.b.w)));
+  } else if constexpr (PRO == PRO_DO) {
+    if (p.epi == GINE_EPI_RELU) {
+      const float4 y = r.aux;
+      return make_float4(y.x > 0.f ? v.x : 0.f, y.y > 0.f ? v.y : 0.f, y.z > 0.f ? v.z : 0.f,
+                         y.w > 0.f ? v.w : 0.f);
+    } else if (p.epi == GINE_EPI_RESIDUAL_RELU) {
+      const uchar4 m = r.m;
+      return make_float4(m.x ? v.x : 0.f, m.y ? v.y : 0.f, m.z ? v.z : 0.f, m.w ? v.w : 0.f);
+    }
+    return v;
+  } else {  // PRO_DA1
+    const float4 a1 = r.aux;
+    float4 o;
+    o.x = k.a.x * v.x + k.b.x * ((a1.x - k.d.x) * k.e.x) + k.c.x;
+    o.y = k.a.y * v.y + k.b.y * ((a1.y - k.d.y) * k.e.y) + k.c.y;
+    o.z = k.a.z * v.z + k.b.z * ((a1.z - k.d.z) * k.e.z) + k.c.z;
+    o.w = k.a.w * v.w + k.b.w * ((a1.w - k.d.w) * k.e.w) + k.c.w;
+    return o;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Row-tile GEMM: out[n][j] = epi( sum_k pro(X)[n][k] * B[k][j] )
+//   BT = true : B[k][j] = W[j][k]   (Y = X W^T, forward Linear)
+//   BT = false: B[k][j] = W[k][j]   (dX = dY W, backward Linear)
+// Persistent: about one workgroup per CU walks a contiguous (XCD-local) range of 32-row
+// tiles.  Per tile: the raw inputs of the NEXT tile and the epilogue operands of THIS tile
+// are loaded into registers before this tile's 64-long MFMA chain, so HBM latency hides
+// under the matrix pipe instead of serialising with it.
+// ----------------------------------------------------------------------------------------
 template <int D, int PRO, int EPI, bool BT>
 __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, ProArgs pa,
                                                    EpiArgs ea, int64_t N, int num_tiles) {
@@ -144,11 +233,14 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
   constexpr int LD = D + 4;      // padded LDS row (floats)
   constexpr int D4 = D / 4;
   constexpr int ITEMS = kRowTile * D4 / NT;  // float4 staged per thread (= 4)
+  constexpr int RSTEP = NT / D4;             // row step between a thread's items (= 8)
+  constexpr bool EPI_LOAD = (EPI == EPI_DBN) || (EPI == EPI_OUT);
   __shared__ __attribute__((aligned(16))) float s_x[kRowTile * LD];
 
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
+  const int q_me = threadIdx.x % D4, r_me = threadIdx.x / D4;
 
   float bf[KS];
   if constexpr (BT) {
@@ -165,6 +257,7 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
 #pragma unroll
     for (int s = 0; s < KS; ++s) bf[s] = W[(size_t)(h * KS + s) * D + col];
   }
+  const ColConst kc = col_const<PRO>(pa, D, q_me);
 
   float bias = 0.f;
   if constexpr (EPI == EPI_A1STATS || EPI == EPI_OUT) bias = ea.bias[col];
@@ -176,21 +269,43 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
     mean = b.mean[col];
     invstd = b.invstd[col];
   }
+  const bool resid = (EPI == EPI_OUT) && ea.mode == GINE_EPI_RESIDUAL_RELU;
   double st1 = 0.0, st2 = 0.0;
 
-  const TileRange tr = xcd_tile_range(num_tiles);
-  for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+  auto load_tile = [&](int tile, RawItem (&raw)[ITEMS]) {
     const int64_t n0 = (int64_t)tile * kRowTile;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-      const int idx = threadIdx.x + i * NT;
-      const int r = idx / D4, q = idx % D4;
-      const int64_t n = n0 + r;
-      float4 v = prologue<PRO>(pa, D, n < N ? n : N - 1, q);  // clamped: load always issued
-      if (n >= N) v = f4_zero();
-      *reinterpret_cast<float4*>(&s_x[r * LD + 4 * q]) = v;
+      const int64_t n = n0 + r_me + i * RSTEP;
+      raw[i] = raw_load<PRO>(pa, D, n < N ? n : N - 1, q_me);  // clamped: always issued
+    }
+  };
+
+  const TileRange tr = xcd_tile_range(num_tiles);
+  RawItem raw[ITEMS];
+  if (tr.first < tr.end) load_tile(tr.first, raw);
+  for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+    const int64_t n0 = (int64_t)tile * kRowTile;
+    __syncthreads();  // previous tile's fragment reads of s_x are done
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int r = r_me + i * RSTEP;
+      float4 v = transform<PRO>(pa, raw[i], kc);
+      if (n0 + r >= N) v = f4_zero();
+      *reinterpret_cast<float4*>(&s_x[r * LD + 4 * q_me]) = v;
     }
     __syncthreads();
+    if (tile + tr.step < tr.end) load_tile(tile + tr.step, raw);  // next tile, in flight
+    float ep[16];
+    if constexpr (EPI_LOAD) {  // epilogue operands of this tile, in flight too
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        n = n < N ? n : N - 1;
+        if constexpr (EPI == EPI_DBN) ep[r] = ea.a1[n * D + col];
+        else ep[r] = resid ? ea.resid[n * D + col] : 0.f;
+      }
+    }
     floatx16 acc = zero16();
     const float* arow = &s_x[c32 * LD + h * KS];
 #pragma unroll
@@ -201,7 +316,6 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
     }
-    __syncthreads();  // s_x is restaged by the next tile
 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -222,12 +336,12 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
         } else if (ea.mode == GINE_EPI_RELU) {
           y = relu_nan(o);
         } else {
-          y = ea.resid[off] + relu_nan(o);
+          y = ep[r] + relu_nan(o);
           ea.mask_out[off] = (o > 0.f) ? 1 : 0;
         }
         ea.out[off] = y;
       } else if constexpr (EPI == EPI_DBN) {
-        const float a1 = ea.a1[off];
+        const float a1 = ep[r];
         const float bn = bn_apply(a1, alpha, shift);
         const float dbn = (bn > 0.f) ? v : 0.f;
         ea.out[off] = dbn;
@@ -251,16 +365,18 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
   }
 }
 
-inline int rowgemm_grid(int64_t N) {
+// Persistent grid: ~4 waves per CU (one wave per SIMD) on the 256 CUs of an MI355X.
+inline int rowgemm_grid(int64_t N, int D) {
   const int64_t tiles = ceil_div(N, kRowTile);
-  const int64_t g = tiles < kMaxRowBlocks ? tiles : kMaxRowBlocks;
+  const int64_t cap = std::max(256, 1024 / (D / 32));
+  const int64_t g = tiles < cap ? tiles : cap;
   return (int)(g > 0 ? g : 1);
 }
 
 template <int PRO, int EPI, bool BT>
 int launch_rowgemm(int D, const float* W, const ProArgs& pa, const EpiArgs& ea, int64_t N,
                    hipStream_t s) {
-  const int grid = rowgemm_grid(N);
+  const int grid = rowgemm_grid(N, D);
   const int tiles = (int)ceil_div(N, kRowTile);
   switch (D) {
     case 32:
@@ -502,7 +618,7 @@ extern "C" int gine_mlp_num_partials(int64_t num_nodes, int32_t channels,
                                      int32_t* num_partials) {
   if (!num_partials || num_nodes < 0) return GINE_ERR_INVALID;
   if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
-  *num_partials = rowgemm_grid(num_nodes);
+  *num_partials = rowgemm_grid(num_nodes, channels);
   return GINE_OK;
 }
 
