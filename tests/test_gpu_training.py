@@ -165,8 +165,12 @@ def test_grads_land_in_flat_buffer_without_copies():
         for p, off in zip(opt1.params, opt1._offsets):
             assert p.grad.data_ptr() == base_ptr + 4 * off   # adopted, not copied
         opt1.step()
-        opt2.zero_grad()
-        m2.loss_fn.crps(m2(batch), batch.y).backward()
-        opt2.step()
-    for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
-        assert rel_err(p.detach(), q.detach()) <= 1e-5, n
+        if step == 0:
+            # one step from identical weights: same gradients, same AdamW arithmetic.  (Later
+            # steps are not comparable elementwise: Adam turns ulp-level gradient differences
+            # on near-zero components into +-lr steps.)
+            opt2.zero_grad()
+            m2.loss_fn.crps(m2(batch), batch.y).backward()
+            opt2.step()
+            for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+                assert rel_err(p.detach(), q.detach()) <= 1e-6, n
