@@ -206,6 +206,27 @@ int gine_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out
                       int32_t in_features, float* slab, float* dw, float* db, float bias_scale,
                       void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * DeepSetEncoder phi first layer + ReLU + member sum, fused (models/gnn.py:48-68,
+ * replaces phi[0](x) -> phi[1] ReLU -> .sum(dim=1) of the reference's Sequential; the
+ * member-sum moves before phi[2] because a Linear commutes with the sum):
+ *   r [N, H] = sum_m relu(ens[n, m, :] w1^T + b1)
+ * ens [N, M, F] (row-major, contiguous), w1 [H, F], b1 [H], fp32.
+ * H in {32, 64, 128, 256}; 1 <= F <= 64; M >= 1.  The [N, M, H] activation is never
+ * written to memory.
+ * gine_deepset_bwd: weight gradients for dr = d loss / d r, recomputing the activation:
+ *   dw1 [H, F] = sum_{n,m} (dr[n] * 1[pre > 0])^T ens[n, m],  db1 [H] likewise summed
+ * slab: gine_deepset_bwd_num_partials(N) * (H*F + H) floats of per-workgroup partials,
+ * reduced in fixed order (deterministic).  db1 may be NULL.
+ * ---------------------------------------------------------------------------------- */
+int gine_deepset_fwd(const float* ens, const float* w1, const float* b1, float* r,
+                     int64_t num_nodes, int32_t members, int32_t in_features, int32_t hidden,
+                     void* stream);
+int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t* num_partials);
+int gine_deepset_bwd(const float* ens, const float* w1, const float* b1, const float* dr,
+                     float* slab, float* dw1, float* db1, int64_t num_nodes, int32_t members,
+                     int32_t in_features, int32_t hidden, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,7 +19,8 @@ constexpr int kRows = 32;         // rows per staged sub-tile
 constexpr int kTile = 64;         // output tile edge
 constexpr int kLds = kTile + 1;   // padded LDS row
 constexpr int kPer = kRows * kTile / 256;  // elements per thread per array per sub-tile
-constexpr int kTargetBlocks = 768;
+constexpr int kTargetBlocks = 256;
+constexpr int kMinSubtiles = 8;  // per chunk: keeps the partial slab small next to the GEMM
 
 struct Plan {
   int tiles_o, tiles_i, chunks, rows_per_chunk;
@@ -31,7 +32,7 @@ inline Plan plan(int64_t R, int O, int I) {
   p.tiles_i = (int)ceil_div(I, kTile);
   const int64_t subtiles = ceil_div(R > 0 ? R : 1, kRows);
   int64_t chunks = ceil_div(kTargetBlocks, (int64_t)p.tiles_o * p.tiles_i);
-  if (chunks > subtiles) chunks = subtiles;
+  if (chunks > ceil_div(subtiles, kMinSubtiles)) chunks = ceil_div(subtiles, kMinSubtiles);
   if (chunks < 1) chunks = 1;
   const int64_t per = ceil_div(subtiles, chunks);  // sub-tiles per chunk
   p.rows_per_chunk = (int)(per * kRows);

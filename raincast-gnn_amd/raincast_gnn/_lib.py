@@ -17,6 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GINE_HIP_LIB", os.path.join(_HERE, "_native", "libgine_hip.so"))
 
 GINE_OK = 0
+GINE_ERR_INVALID, GINE_ERR_DIM = 1, 2
 GINE_ERR_HIP_BASE = 1000
 GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
@@ -55,6 +56,11 @@ _SIGNATURES = {
     "gine_linear_wgrad_num_chunks": [_i64, _i32, _i32, ctypes.POINTER(_i32)],
     "gine_linear_wgrad": [_c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p,
                           _c_void_p, _f32, _c_void_p],
+    "gine_deepset_fwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32, _i32,
+                         _c_void_p],
+    "gine_deepset_bwd_num_partials": [_i64, ctypes.POINTER(_i32)],
+    "gine_deepset_bwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                         _c_void_p, _i64, _i32, _i32, _i32, _c_void_p],
 }
 
 EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)

@@ -1,0 +1,67 @@
+"""Fused DeepSet phi head: ``sum_m relu(phi[0](ens[:, m]))`` on one HIP kernel pair.
+
+models/gnn.py:48-68 evaluates ``phi = Sequential(Linear(F, H), ReLU(), Linear(H, H))`` on
+every (station, member) row and sums over members.  :class:`~raincast_gnn.models.
+DeepSetEncoder` moves the member sum before ``phi[2]`` (a Linear commutes with a sum); what
+remains, ``r = sum_m relu(ens W1^T + b1)``, is the ``[N, M, H]`` activation the reference
+materialises three times per training step (90 MB each at the 24h_mixed benchmark shape).
+``gine_deepset_fwd`` keeps it in MFMA accumulators and writes only ``r [N, H]``;
+``gine_deepset_bwd`` recomputes it for the ReLU mask and produces dW1/db1 directly
+(csrc/gine_deepset.hip).  The ensemble tensor is data (never requires grad in the
+reference); a caller that needs d/d(ens) gets the unfused torch path.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .gradbuf import grad_out
+
+HIDDEN = (32, 64, 128, 256)
+MAX_FEATURES = 64
+
+
+def fusable(ens: torch.Tensor, weight: torch.Tensor, bias) -> bool:
+    return (ens.is_cuda and ens.dim() == 3 and ens.dtype == torch.float32
+            and weight.dtype == torch.float32 and bias is not None
+            and weight.size(0) in HIDDEN and 0 < weight.size(1) <= MAX_FEATURES
+            and ens.size(2) == weight.size(1) and ens.size(1) > 0
+            and not ens.requires_grad)
+
+
+class _PhiSumFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ens, weight, bias):
+        ens = ens.contiguous()
+        weight, bias = weight.contiguous(), bias.contiguous()
+        N, M, Fdim = ens.shape
+        H = weight.size(0)
+        r = torch.empty(N, H, dtype=torch.float32, device=ens.device)
+        _lib.call("gine_deepset_fwd", _lib.ptr(ens), _lib.ptr(weight), _lib.ptr(bias),
+                  _lib.ptr(r), N, M, Fdim, H, _lib.stream_handle(ens.device))
+        ctx.save_for_backward(ens, weight, bias)
+        ctx.params = (weight, bias)
+        return r
+
+    @staticmethod
+    def backward(ctx, dr):
+        ens, weight, bias = ctx.saved_tensors
+        N, M, Fdim = ens.shape
+        H = weight.size(0)
+        dr = dr.contiguous()
+        parts = ctypes.c_int32(0)
+        _lib.call("gine_deepset_bwd_num_partials", N, ctypes.byref(parts))
+        slab = torch.empty(parts.value * (H * Fdim + H), dtype=torch.float32, device=dr.device)
+        dw = grad_out(ctx.params[0], (H, Fdim), dr.device)
+        db = grad_out(ctx.params[1], (H,), dr.device)
+        _lib.call("gine_deepset_bwd", _lib.ptr(ens), _lib.ptr(weight), _lib.ptr(bias),
+                  _lib.ptr(dr), _lib.ptr(slab), _lib.ptr(dw), _lib.ptr(db), N, M, Fdim, H,
+                  _lib.stream_handle(dr.device))
+        return None, dw, db
+
+
+def phi_sum(ens: torch.Tensor, lin1: torch.nn.Linear) -> torch.Tensor:
+    """``relu(lin1(ens)).sum(dim=1)`` for ens [N, M, F] on the fused kernels."""
+    return _PhiSumFn.apply(ens, lin1.weight, lin1.bias)

@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 from torch.nn import Linear, ModuleList, ReLU
 
+from . import deepset
 from .linear import Linear as RowLinear
 from .loss import MixedLoss, MixedNormalCRPS, NormalCRPS
 from .nn import GINEConv
@@ -53,7 +54,8 @@ class DeepSetEncoder(nn.Module):
     phi's last layer is affine, so ``sum_m (W2 r_m + b2) = W2 (sum_m r_m) + M b2``: the
     member sum is taken before that Linear (same function, same parameters and state_dict
     keys), which shrinks its GEMM -- and its weight-gradient GEMM -- from N*M rows to N rows
-    (176,000 -> 16,000 at the 24h_mixed benchmark shape).
+    (176,000 -> 16,000 at the 24h_mixed benchmark shape).  On the GPU the remaining
+    ``sum_m relu(phi[0](ens_m))`` runs on the fused kernel pair of :mod:`.deepset`.
     """
 
     def __init__(self, ensemble_in_dim, hidden_channels, out_channels):
@@ -65,7 +67,10 @@ class DeepSetEncoder(nn.Module):
 
     def forward(self, ensemble_feats):
         lin1, act, lin2 = self.phi
-        r = act(lin1(ensemble_feats)).sum(dim=1)                       # [N, H]
+        if isinstance(act, nn.ReLU) and deepset.fusable(ensemble_feats, lin1.weight, lin1.bias):
+            r = deepset.phi_sum(ensemble_feats, lin1)                  # fused HIP kernels
+        else:
+            r = act(lin1(ensemble_feats)).sum(dim=1)                   # [N, H]
         phi_sum = lin2(r, bias_scale=ensemble_feats.size(1))           # = sum_m lin2(r_m)
         return self.rho(phi_sum)
 
