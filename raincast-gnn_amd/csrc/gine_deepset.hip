@@ -5,15 +5,18 @@
 //   dW1 = sum_{n,m} dh[n, m, :]^T ens[n, m, :],   db1 = sum_{n,m} dh[n, m, :]
 // The reference materialises the [N, M, H] pre-activation (90 MB at the 24h_mixed
 // benchmark shape) three times per step (Linear output, ReLU output, ReLU gradient).  Here
-// it never leaves the MFMA accumulators: rows are (node, member) pairs, a workgroup walks
-// groups of 32 nodes = M tiles of 32 rows; per tile the v_mfma_f32_32x32x2_f32 chain over
-// the (padded) features yields the pre-activations of 32 rows x 32 hidden units per wave.
-//  * forward: bias + ReLU in registers, member sums accumulated per node in LDS (fixed
-//    order, deterministic);
-//  * backward: the same chain is recomputed, masked with dr of the row's node, and the
-//    masked accumulator registers are fed straight back as the A operand of the dW1 MFMA
-//    (lane (c, h) holds rows (r&3)+8(r>>2)+4h of hidden unit c -- exactly a 32x32x2 A
-//    fragment under a k-permutation that B, read from the staged ens tile, follows too).
+// it never leaves the MFMA accumulators.  Rows are (node, member) pairs; a workgroup walks
+// groups of 32 nodes = 32*M rows as M tiles of 32 rows, and each wave owns 32 hidden units.
+// Row placement: the accumulator register q of lane half h (v_mfma_f32_32x32x2_f32 output
+// row (q&3)+8(q>>2)+4h) holds group row 16*M*h + 16*t + q in tile t, i.e. half 0 walks the
+// rows of nodes 0-15 and half 1 those of nodes 16-31, both in member order.  So
+//  * forward: bias + ReLU in registers and a running per-node sum per lane, written once
+//    when the node changes (wave-uniform: both halves are at the same local row) -- no
+//    LDS read-modify-write, deterministic member order;
+//  * backward: the chain is recomputed, masked with dr of the row's node, and the masked
+//    accumulator registers are fed straight back as the A operand of the dW1 MFMA (a lane
+//    half's 16 registers are 16 distinct k of a 32x32x2 A fragment under a k-permutation
+//    that B -- read from the staged ens rows 16h+q -- follows too).
 #include "gine_common.hpp"
 
 #include <algorithm>
@@ -32,33 +35,49 @@ __device__ __forceinline__ floatx16 zero16() {
   return v;
 }
 
-__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+// LDS row holding MFMA output row i (see the row placement above): 16*h + q.
+__device__ __forceinline__ int staged_row(int i) {
+  return 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+}
 
-// Stage rows [row0, row0+32) of ens (contiguous: 32*F floats) into s_e[32][KP+4], zero
-// padded beyond F and beyond the valid rows.  `vals` is the register copy (prefetch).
+// Tile t of a group stages, into s_e[32][KP+4], LDS rows 16c+j <- group row 16*M*c + 16*t + j
+// (c = lane half, j < 16): two contiguous runs of 16*F floats.  Offsets depend only on the
+// thread, so they are computed once; `vals` is the register prefetch of the next tile.
 template <int NT, int KP>
 struct Stager {
   static constexpr int PER = (32 * 64 + NT - 1) / NT;  // >= 32*F / NT for F <= 64
+  static constexpr int LD = KP + 4;
   float vals[PER];
-  __device__ __forceinline__ void load(const float* __restrict__ ens, int64_t row0,
-                                       int64_t row_end, int F) {
-    const int64_t base = row0 * F;
-    const int64_t lim = (row_end > row0 ? (row_end - row0) : 0) * F;
+  int src[PER];  // float offset from the tile's first row; -1: thread has no element
+  int row[PER];  // group-row offset from the tile's first row
+  int dst[PER];  // LDS offset
+  __device__ __forceinline__ void init(int F, int M) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = threadIdx.x + i * NT;
-      const bool ok = e < 32 * F && e < lim;
-      const float v = ens[base + (ok ? e : 0)];
+      const int c = e >= 16 * F ? 1 : 0;
+      const int off = e - c * 16 * F;
+      const int j = off / F, f = off - j * F;
+      const bool has = e < 32 * F;
+      src[i] = has ? c * 16 * M * F + off : -1;
+      row[i] = c * 16 * M + j;
+      dst[i] = has ? (16 * c + j) * LD + f : -1;
+    }
+  }
+  // row0: first group row of the tile (group base + 16 t)
+  __device__ __forceinline__ void load(const float* __restrict__ ens, int64_t row0,
+                                       int64_t rows_total, int F) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const bool ok = src[i] >= 0 && row0 + row[i] < rows_total;
+      const float v = ens[ok ? row0 * F + src[i] : 0];  // clamped: every lane loads
       vals[i] = ok ? v : 0.f;
     }
   }
-  __device__ __forceinline__ void store(float* s_e, int F) const {
-    constexpr int LD = KP + 4;
+  __device__ __forceinline__ void store(float* s_e) const {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = threadIdx.x + i * NT;
-      if (e < 32 * F) s_e[(e / F) * LD + e % F] = vals[i];
-    }
+    for (int i = 0; i < PER; ++i)
+      if (dst[i] >= 0) s_e[dst[i]] = vals[i];
   }
 };
 
@@ -78,7 +97,7 @@ __device__ __forceinline__ floatx16 pre_tile(const float* s_e, const float (&bf)
   constexpr int LD = KP + 4;
   constexpr int KS = KP / 2;
   floatx16 acc = zero16();
-  const float* arow = s_e + c32 * LD + h * KS;
+  const float* arow = s_e + staged_row(c32) * LD + h * KS;
 #pragma unroll
   for (int q = 0; q < KS / 4; ++q) {
     const float4 a4 = *reinterpret_cast<const float4*>(arow + 4 * q);
@@ -99,6 +118,12 @@ __device__ __forceinline__ void load_b(const float* __restrict__ w1, int col, in
     const int k = h * KS + s;
     bf[s] = k < F ? w1[(size_t)col * F + k] : 0.f;
   }
+}
+
+// node (within a lane half's 16) of half-local row l < 16*M: exact for M < 2^16 (the
+// fractional part of (l + 0.5)/M is at least 0.5/M from an integer)
+__device__ __forceinline__ int node_of(int l, float inv_m) {
+  return (int)(((float)l + 0.5f) * inv_m);
 }
 
 // groups of one XCD form a contiguous range walked by that XCD's workgroups
@@ -122,10 +147,10 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
                                                        int M, int F, int num_groups) {
   constexpr int NT = 2 * H;
   __shared__ __attribute__((aligned(16))) float s_e[32 * (KP + 4)];
-  __shared__ float s_sum[kNodes * H];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
+  const float inv_m = 1.f / (float)M;
   float bf[KP / 2];
   load_b<KP>(w1, col, h, F, bf);
   const float bias = b1[col];
@@ -133,47 +158,36 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
 
   const int64_t rows_total = N * M;
   Stager<NT, KP> st;
+  st.init(F, M);
   const Range rg = xcd_range(num_groups);
   if (rg.first < rg.end) st.load(ens, (int64_t)rg.first * kNodes * M, rows_total, F);
   for (int g = rg.first; g < rg.end; g += rg.step) {
-    const int64_t node0 = (int64_t)g * kNodes;
-    const int64_t row_base = node0 * M;
-    for (int i = lane; i < kNodes * 32; i += kWave)  // this wave's 32 columns
-      s_sum[(i >> 5) * H + wave * 32 + (i & 31)] = 0.f;
+    const int64_t row_base = (int64_t)g * kNodes * M;
+    const int64_t my_node0 = (int64_t)g * kNodes + 16 * h;  // this half's first node
+    int cur = 0;
+    float run = 0.f;
     for (int t = 0; t < M; ++t) {
-      const int64_t row0 = row_base + 32 * t;
+      const int64_t row0 = row_base + 16 * t;
       __syncthreads();
-      st.store(s_e, F);
+      st.store(s_e);
       __syncthreads();
       // prefetch the next tile (of this group, or the first of the next group)
-      if (t + 1 < M) st.load(ens, row0 + 32, rows_total, F);
+      if (t + 1 < M) st.load(ens, row0 + 16, rows_total, F);
       else if (g + rg.step < rg.end)
         st.load(ens, (int64_t)(g + rg.step) * kNodes * M, rows_total, F);
       const floatx16 acc = pre_tile<KP>(s_e, bf, c32, h);
-      // member sums: the two lane halves in turn (they can share a node), rows in order
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        if (h == hh) {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int64_t row = row0 + acc_row(q, h);
-            if (row < rows_total) {
-              const int slot = (int)(row / M - node0);
-              const float v = relu_nan(acc[q] + bias);
-              s_sum[slot * H + col] += v;
-            }
-          }
+      for (int q = 0; q < 16; ++q) {
+        const int node = node_of(16 * t + q, inv_m);  // wave-uniform
+        if (node != cur) {
+          if (my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
+          cur = node;
+          run = 0.f;
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        run += relu_nan(acc[q] + bias);
       }
     }
-    __syncthreads();
-    for (int i = lane; i < kNodes * 32; i += kWave) {
-      const int64_t n = node0 + (i >> 5);
-      const int c = wave * 32 + (i & 31);
-      if (n < N) r[n * H + c] = s_sum[(i >> 5) * H + c];
-    }
+    if (my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
   }
 }
 
@@ -193,6 +207,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
+  const float inv_m = 1.f / (float)M;
   float bf[KP / 2];
   load_b<KP>(w1, col, h, F, bf);
   const float bias = b1[col];
@@ -205,6 +220,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
 
   const int64_t rows_total = N * M;
   Stager<NT, KP> st;
+  st.init(F, M);
   const Range rg = xcd_range(num_groups);
   if (rg.first < rg.end) st.load(ens, (int64_t)rg.first * kNodes * M, rows_total, F);
   for (int g = rg.first; g < rg.end; g += rg.step) {
@@ -216,29 +232,31 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
       s_dr[(i >> 5) * H + c] = n < N ? dr[n * H + c] : 0.f;
     }
     for (int t = 0; t < M; ++t) {
-      const int64_t row0 = row_base + 32 * t;
+      const int64_t row0 = row_base + 16 * t;
       __syncthreads();
-      st.store(s_e, F);
+      st.store(s_e);
       __syncthreads();
-      if (t + 1 < M) st.load(ens, row0 + 32, rows_total, F);
+      if (t + 1 < M) st.load(ens, row0 + 16, rows_total, F);
       else if (g + rg.step < rg.end)
         st.load(ens, (int64_t)(g + rg.step) * kNodes * M, rows_total, F);
       floatx16 dh = pre_tile<KP>(s_e, bf, c32, h);
+      int cur = -1;
+      float dcur = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int64_t row = row0 + acc_row(q, h);
-        float v = 0.f;
-        if (row < rows_total) {
-          const int slot = (int)(row / M - node0);
-          v = (dh[q] + bias > 0.f) ? s_dr[slot * H + col] : 0.f;  // ReLU backward
+        const int node = node_of(16 * t + q, inv_m);  // wave-uniform
+        if (node != cur) {
+          cur = node;
+          dcur = s_dr[(16 * h + node) * H + col];  // 0 for nodes >= N
         }
+        const float v = (dh[q] + bias > 0.f) ? dcur : 0.f;  // ReLU backward
         dh[q] = v;
         gb += (double)v;
       }
-      // dW1[o][i] += sum_rows dh[row][o] ens[row][i]: A = dh (registers), B = staged ens
+      // dW1[o][i] += sum_rows dh[row][o] ens[row][i]: A = dh (registers), B = staged rows
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const float* erow = s_e + acc_row(q, h) * LD;
+        const float* erow = s_e + (16 * h + q) * LD;
 #pragma unroll
         for (int it = 0; it < NI; ++it) {
           const int i = 32 * it + c32;
@@ -254,7 +272,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   for (int it = 0; it < NI; ++it) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int o = wave * 32 + acc_row(q, h);
+      const int o = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
       const int i = 32 * it + c32;
       if (i < F) out[(size_t)o * F + i] = gw[it][q];
     }
