@@ -40,14 +40,13 @@ __device__ __forceinline__ int staged_row(int i) {
   return 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
 }
 
-// Tile t of a group stages, into s_e[32][KP+4], LDS rows 16c+j <- group row 16*M*c + 16*t + j
-// (c = lane half, j < 16): two contiguous runs of 16*F floats.  Offsets depend only on the
-// thread, so they are computed once; `vals` is the register prefetch of the next tile.
+// Tile t of a group stages, into an LDS tile [32][KP+4], rows 16c+j <- group row
+// 16*M*c + 16*t + j (c = lane half, j < 16): two contiguous runs of 16*F floats.  Offsets
+// depend only on the thread, so they are computed once.
 template <int NT, int KP>
 struct Stager {
-  static constexpr int PER = (32 * 64 + NT - 1) / NT;  // >= 32*F / NT for F <= 64
+  static constexpr int PER = (32 * KP + NT - 1) / NT;  // >= 32*F / NT
   static constexpr int LD = KP + 4;
-  float vals[PER];
   int src[PER];  // float offset from the tile's first row; -1: thread has no element
   int row[PER];  // group-row offset from the tile's first row
   int dst[PER];  // LDS offset
@@ -65,19 +64,19 @@ struct Stager {
     }
   }
   // row0: first group row of the tile (group base + 16 t)
-  __device__ __forceinline__ void load(const float* __restrict__ ens, int64_t row0,
-                                       int64_t rows_total, int F) {
+  __device__ __forceinline__ void load(float (&v)[PER], const float* __restrict__ ens,
+                                       int64_t row0, int64_t rows_total, int F) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const bool ok = src[i] >= 0 && row0 + row[i] < rows_total;
-      const float v = ens[ok ? row0 * F + src[i] : 0];  // clamped: every lane loads
-      vals[i] = ok ? v : 0.f;
+      const float x = ens[ok ? row0 * F + src[i] : 0];  // clamped: every lane loads
+      v[i] = ok ? x : 0.f;
     }
   }
-  __device__ __forceinline__ void store(float* s_e) const {
+  __device__ __forceinline__ void store(float* s_e, const float (&v)[PER]) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-      if (dst[i] >= 0) s_e[dst[i]] = vals[i];
+      if (dst[i] >= 0) s_e[dst[i]] = v[i];
   }
 };
 
@@ -126,16 +125,53 @@ __device__ __forceinline__ int node_of(int l, float inv_m) {
   return (int)(((float)l + 0.5f) * inv_m);
 }
 
-// groups of one XCD form a contiguous range walked by that XCD's workgroups
-struct Range {
-  int first, end, step;
+// The tiles of this workgroup: groups first, first+step, ... < end (one XCD's groups form a
+// contiguous range walked by that XCD's workgroups), M tiles each, as one flat sequence so
+// that loads run two tiles ahead across group boundaries.
+struct Tiles {
+  int first, step, M, count;
+  __device__ __forceinline__ Tiles(int num_groups, int M_) : M(M_) {
+    const int nb = gridDim.x;
+    const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
+    const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
+    const int span = (num_groups + kNumXcd - 1) / kNumXcd;
+    const int end = min(num_groups, xcd * span + span);
+    first = xcd * span + pos;
+    step = here;
+    count = first < end ? ((end - first + step - 1) / step) * M : 0;
+  }
+  __device__ __forceinline__ int group(int k) const { return first + (k / M) * step; }
+  __device__ __forceinline__ int64_t row0(int k) const {  // first group row of tile k
+    const int gi = k / M;
+    return (int64_t)(first + gi * step) * kNodes * M + 16 * (k - gi * M);
+  }
 };
-__device__ __forceinline__ Range xcd_range(int n) {
-  const int nb = gridDim.x;
-  const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
-  const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
-  const int span = (n + kNumXcd - 1) / kNumXcd;
-  return Range{xcd * span + pos, min(n, xcd * span + span), here};
+
+// Drive `tile(k, buf)` over the workgroup's tiles with a two-deep register ring and a
+// double-buffered LDS tile: tile k+2 is loaded while tile k computes, tile k+1 is stored
+// after it, one barrier per tile.
+template <int NT, int KP, class Body>
+__device__ __forceinline__ void walk_tiles(const Tiles& tl, const Stager<NT, KP>& st,
+                                           const float* __restrict__ ens, int64_t rows_total,
+                                           int F, float* buf0, float* buf1, Body&& tile) {
+  constexpr int PER = Stager<NT, KP>::PER;
+  float va[PER], vb[PER];
+  if (tl.count > 0) {
+    st.load(va, ens, tl.row0(0), rows_total, F);
+    st.store(buf0, va);
+  }
+  if (tl.count > 1) st.load(vb, ens, tl.row0(1), rows_total, F);
+  __syncthreads();
+  auto step = [&](int k, float (&cur)[PER], float (&nxt)[PER], float* bcur, float* bnxt) {
+    if (k + 2 < tl.count) st.load(cur, ens, tl.row0(k + 2), rows_total, F);
+    tile(k, bcur);
+    if (k + 1 < tl.count) st.store(bnxt, nxt);
+    __syncthreads();
+  };
+  for (int k = 0; k < tl.count; k += 2) {
+    step(k, va, vb, buf0, buf1);
+    if (k + 1 < tl.count) step(k + 1, vb, va, buf1, buf0);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -146,7 +182,8 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
                                                        float* __restrict__ r, int64_t N,
                                                        int M, int F, int num_groups) {
   constexpr int NT = 2 * H;
-  __shared__ __attribute__((aligned(16))) float s_e[32 * (KP + 4)];
+  constexpr int LD = KP + 4;
+  __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
@@ -154,41 +191,34 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
   float bf[KP / 2];
   load_b<KP>(w1, col, h, F, bf);
   const float bias = b1[col];
-  zero_pad<KP>(s_e, F);
+  zero_pad<KP>(s_e[0], F);
+  zero_pad<KP>(s_e[1], F);
 
-  const int64_t rows_total = N * M;
   Stager<NT, KP> st;
   st.init(F, M);
-  const Range rg = xcd_range(num_groups);
-  if (rg.first < rg.end) st.load(ens, (int64_t)rg.first * kNodes * M, rows_total, F);
-  for (int g = rg.first; g < rg.end; g += rg.step) {
-    const int64_t row_base = (int64_t)g * kNodes * M;
-    const int64_t my_node0 = (int64_t)g * kNodes + 16 * h;  // this half's first node
-    int cur = 0;
-    float run = 0.f;
-    for (int t = 0; t < M; ++t) {
-      const int64_t row0 = row_base + 16 * t;
-      __syncthreads();
-      st.store(s_e);
-      __syncthreads();
-      // prefetch the next tile (of this group, or the first of the next group)
-      if (t + 1 < M) st.load(ens, row0 + 16, rows_total, F);
-      else if (g + rg.step < rg.end)
-        st.load(ens, (int64_t)(g + rg.step) * kNodes * M, rows_total, F);
-      const floatx16 acc = pre_tile<KP>(s_e, bf, c32, h);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int node = node_of(16 * t + q, inv_m);  // wave-uniform
-        if (node != cur) {
-          if (my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
-          cur = node;
-          run = 0.f;
-        }
-        run += relu_nan(acc[q] + bias);
-      }
+  const Tiles tl(num_groups, M);
+  int cur = 0;
+  float run = 0.f;
+  walk_tiles(tl, st, ens, N * M, F, s_e[0], s_e[1], [&](int k, const float* buf) {
+    const int gi = k / M, t = k - gi * M;
+    const int64_t my_node0 = (int64_t)(tl.first + gi * tl.step) * kNodes + 16 * h;
+    const floatx16 acc = pre_tile<KP>(buf, bf, c32, h);
+    if (t == 0) {
+      cur = 0;
+      run = 0.f;
     }
-    if (my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
-  }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int node = node_of(16 * t + q, inv_m);  // wave-uniform
+      if (node != cur) {
+        if (my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
+        cur = node;
+        run = 0.f;
+      }
+      run += relu_nan(acc[q] + bias);
+    }
+    if (t == M - 1 && my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
+  });
 }
 
 // ---------------------------------------------------------------------------------------
@@ -202,7 +232,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   constexpr int NT = 2 * H;
   constexpr int LD = KP + 4;
   constexpr int NI = (KP + 31) / 32;  // 32-wide feature tiles of dW1
-  __shared__ __attribute__((aligned(16))) float s_e[32 * LD];
+  __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
   __shared__ float s_dr[kNodes * H];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
@@ -211,61 +241,47 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   float bf[KP / 2];
   load_b<KP>(w1, col, h, F, bf);
   const float bias = b1[col];
-  zero_pad<KP>(s_e, F);
+  zero_pad<KP>(s_e[0], F);
+  zero_pad<KP>(s_e[1], F);
 
   floatx16 gw[NI];
 #pragma unroll
   for (int it = 0; it < NI; ++it) gw[it] = zero16();
   double gb = 0.0;
 
-  const int64_t rows_total = N * M;
   Stager<NT, KP> st;
   st.init(F, M);
-  const Range rg = xcd_range(num_groups);
-  if (rg.first < rg.end) st.load(ens, (int64_t)rg.first * kNodes * M, rows_total, F);
-  for (int g = rg.first; g < rg.end; g += rg.step) {
-    const int64_t node0 = (int64_t)g * kNodes;
-    const int64_t row_base = node0 * M;
-    for (int i = lane; i < kNodes * 32; i += kWave) {  // dr of this group, own columns
-      const int64_t n = node0 + (i >> 5);
-      const int c = wave * 32 + (i & 31);
-      s_dr[(i >> 5) * H + c] = n < N ? dr[n * H + c] : 0.f;
-    }
-    for (int t = 0; t < M; ++t) {
-      const int64_t row0 = row_base + 16 * t;
-      __syncthreads();
-      st.store(s_e);
-      __syncthreads();
-      if (t + 1 < M) st.load(ens, row0 + 16, rows_total, F);
-      else if (g + rg.step < rg.end)
-        st.load(ens, (int64_t)(g + rg.step) * kNodes * M, rows_total, F);
-      floatx16 dh = pre_tile<KP>(s_e, bf, c32, h);
-      int cur = -1;
-      float dcur = 0.f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int node = node_of(16 * t + q, inv_m);  // wave-uniform
-        if (node != cur) {
-          cur = node;
-          dcur = s_dr[(16 * h + node) * H + col];  // 0 for nodes >= N
-        }
-        const float v = (dh[q] + bias > 0.f) ? dcur : 0.f;  // ReLU backward
-        dh[q] = v;
-        gb += (double)v;
-      }
-      // dW1[o][i] += sum_rows dh[row][o] ens[row][i]: A = dh (registers), B = staged rows
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float* erow = s_e + (16 * h + q) * LD;
-#pragma unroll
-        for (int it = 0; it < NI; ++it) {
-          const int i = 32 * it + c32;
-          const float b = i < KP ? erow[i] : 0.f;
-          gw[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(dh[q], b, gw[it], 0, 0, 0);
-        }
+  const Tiles tl(num_groups, M);
+  walk_tiles(tl, st, ens, N * M, F, s_e[0], s_e[1], [&](int k, const float* buf) {
+    const int gi = k / M, t = k - gi * M;
+    if (t == 0) {  // dr of this group, this wave's columns (read by this wave only)
+      const int64_t node0 = (int64_t)(tl.first + gi * tl.step) * kNodes;
+      for (int i = lane; i < kNodes * 32; i += kWave) {
+        const int64_t n = node0 + (i >> 5);
+        const int c = wave * 32 + (i & 31);
+        s_dr[(i >> 5) * H + c] = n < N ? dr[n * H + c] : 0.f;
       }
     }
-  }
+    floatx16 dh = pre_tile<KP>(buf, bf, c32, h);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {  // independent LDS reads: no branch on the node change
+      const float d = s_dr[(16 * h + node_of(16 * t + q, inv_m)) * H + col];  // 0 if >= N
+      const float v = (dh[q] + bias > 0.f) ? d : 0.f;  // ReLU backward
+      dh[q] = v;
+      gb += (double)v;
+    }
+    // dW1[o][i] += sum_rows dh[row][o] ens[row][i]: A = dh (registers), B = staged rows
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float* erow = buf + (16 * h + q) * LD;
+#pragma unroll
+      for (int it = 0; it < NI; ++it) {
+        const int i = 32 * it + c32;
+        const float b = (32 * it + 32 <= KP || i < KP) ? erow[i] : 0.f;
+        gw[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(dh[q], b, gw[it], 0, 0, 0);
+      }
+    }
+  });
   // slab row of this workgroup: [H*F weights | H bias]
   float* out = slab + (size_t)blockIdx.x * ((size_t)H * F + H);
 #pragma unroll
@@ -281,25 +297,29 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   if (h == 0) out[(size_t)H * F + col] = (float)gb;
 }
 
+// 16 consecutive slab elements x 16 chunk groups per workgroup (many workgroups for the
+// few thousand elements of dW1), fixed summation order, fp64.
 __global__ __launch_bounds__(256) void k_deepset_slab_reduce(const float* __restrict__ slab,
                                                              int chunks, int64_t per,
                                                              int64_t wsize,
                                                              float* __restrict__ dw,
                                                              float* __restrict__ db) {
-  __shared__ double s_part[4][64];
-  const int64_t e = blockIdx.x * (int64_t)64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
+  __shared__ double s_part[16][17];
+  const int j = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t e = blockIdx.x * (int64_t)16 + j;
   double acc = 0.0;
   if (e < per) {
-    for (int c = g; c < chunks; c += 4) acc += (double)slab[(size_t)c * per + e];
+#pragma unroll 4
+    for (int c = g; c < chunks; c += 16) acc += (double)slab[(size_t)c * per + e];
   }
-  s_part[g][threadIdx.x & 63] = acc;
+  s_part[g][j] = acc;
   __syncthreads();
   if (g != 0 || e >= per) return;
-  const int j = threadIdx.x & 63;
-  const float v = (float)((s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]));
-  if (e < wsize) dw[e] = v;
-  else if (db) db[e - wsize] = v;
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v += s_part[k][j];
+  if (e < wsize) dw[e] = (float)v;
+  else if (db) db[e - wsize] = (float)v;
 }
 
 inline int pad_features(int F) {
@@ -315,7 +335,7 @@ inline bool hidden_ok(int H) { return H == 32 || H == 64 || H == 128 || H == 256
 
 inline int bwd_grid(int64_t N) {
   const int64_t groups = ceil_div(N > 0 ? N : 1, kNodes);
-  return (int)std::min<int64_t>(groups, 256);
+  return (int)std::min<int64_t>(groups, 512);
 }
 
 #define DS_DISPATCH(H_, KP_, MACRO)                       \
@@ -390,7 +410,7 @@ extern "C" int gine_deepset_bwd(const float* ens, const float* w1, const float* 
 #undef LAUNCH_BWD
     GINE_LAUNCH_STATUS();
   }
-  hipLaunchKernelGGL(k_deepset_slab_reduce, dim3((unsigned)ceil_div(per, 64)), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_deepset_slab_reduce, dim3((unsigned)ceil_div(per, 16)), dim3(256), 0, s,
                      slab, grid, per, (int64_t)hidden * in_features, dw1, db1);
   GINE_LAUNCH_STATUS();
   return GINE_OK;

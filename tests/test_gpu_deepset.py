@@ -117,4 +117,4 @@ def test_abi_rejects_unsupported_shapes():
                                 96, s) == _lib.GINE_ERR_DIM
     assert not deepset.fusable(x, w, b)
     n = ctypes.c_int32(0)
-    assert lib.gine_deepset_bwd_num_partials(16000, ctypes.byref(n)) == 0 and n.value == 256
+    assert lib.gine_deepset_bwd_num_partials(16000, ctypes.byref(n)) == 0 and n.value == 500
