@@ -213,18 +213,20 @@ int gine_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out
  *   r [N, H] = sum_m relu(ens[n, m, :] w1^T + b1)
  * ens [N, M, F] (row-major, contiguous), w1 [H, F], b1 [H], fp32.
  * H in {32, 64, 128, 256}; 1 <= F <= 64; M >= 1.  The [N, M, H] activation is never
- * written to memory.
- * gine_deepset_bwd: weight gradients for dr = d loss / d r, recomputing the activation:
+ * written to memory; mask (optional, gine_deepset_mask_bytes bytes) receives its ReLU
+ * pattern as bits, for the backward.
+ * gine_deepset_bwd: weight gradients for dr = d loss / d r from the forward's mask:
  *   dw1 [H, F] = sum_{n,m} (dr[n] * 1[pre > 0])^T ens[n, m],  db1 [H] likewise summed
  * slab: gine_deepset_bwd_num_partials(N) * (H*F + H) floats of per-workgroup partials,
  * reduced in fixed order (deterministic).  db1 may be NULL.
  * ---------------------------------------------------------------------------------- */
+int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32_t hidden, size_t* bytes);
 int gine_deepset_fwd(const float* ens, const float* w1, const float* b1, float* r,
-                     int64_t num_nodes, int32_t members, int32_t in_features, int32_t hidden,
-                     void* stream);
+                     uint16_t* mask, int64_t num_nodes, int32_t members, int32_t in_features,
+                     int32_t hidden, void* stream);
 int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t* num_partials);
-int gine_deepset_bwd(const float* ens, const float* w1, const float* b1, const float* dr,
-                     float* slab, float* dw1, float* db1, int64_t num_nodes, int32_t members,
+int gine_deepset_bwd(const float* ens, const uint16_t* mask, const float* dr, float* slab,
+                     float* dw1, float* db1, int64_t num_nodes, int32_t members,
                      int32_t in_features, int32_t hidden, void* stream);
 
 #ifdef __cplusplus

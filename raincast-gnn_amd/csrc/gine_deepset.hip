@@ -42,14 +42,15 @@ __device__ __forceinline__ int staged_row(int i) {
 
 // Tile t of a group stages, into an LDS tile [32][KP+4], rows 16c+j <- group row
 // 16*M*c + 16*t + j (c = lane half, j < 16): two contiguous runs of 16*F floats.  Offsets
-// depend only on the thread, so they are computed once.
+// depend only on the thread, so they are computed once; the loads address a uniform
+// (scalar) tile base plus a 32-bit lane offset.
 template <int NT, int KP>
 struct Stager {
   static constexpr int PER = (32 * KP + NT - 1) / NT;  // >= 32*F / NT
   static constexpr int LD = KP + 4;
-  int src[PER];  // float offset from the tile's first row; -1: thread has no element
-  int row[PER];  // group-row offset from the tile's first row
-  int dst[PER];  // LDS offset
+  int src[PER];  // float offset from the tile's first row (0 if the thread has no element)
+  int row[PER];  // group-row offset from the tile's first row (INT_MAX: no element)
+  int dst[PER];  // LDS offset (-1: no element)
   __device__ __forceinline__ void init(int F, int M) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -58,18 +59,18 @@ struct Stager {
       const int off = e - c * 16 * F;
       const int j = off / F, f = off - j * F;
       const bool has = e < 32 * F;
-      src[i] = has ? c * 16 * M * F + off : -1;
-      row[i] = c * 16 * M + j;
+      src[i] = has ? c * 16 * M * F + off : 0;
+      row[i] = has ? c * 16 * M + j : 0x7fffffff;
       dst[i] = has ? (16 * c + j) * LD + f : -1;
     }
   }
-  // row0: first group row of the tile (group base + 16 t)
-  __device__ __forceinline__ void load(float (&v)[PER], const float* __restrict__ ens,
-                                       int64_t row0, int64_t rows_total, int F) const {
+  // base: ens + (first group row of the tile) * F;  lim: rows left from that row (clamped)
+  __device__ __forceinline__ void load(float (&v)[PER], const float* __restrict__ base,
+                                       int lim) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const bool ok = src[i] >= 0 && row0 + row[i] < rows_total;
-      const float x = ens[ok ? row0 * F + src[i] : 0];  // clamped: every lane loads
+      const bool ok = row[i] < lim;
+      const float x = base[ok ? src[i] : 0];
       v[i] = ok ? x : 0.f;
     }
   }
@@ -119,75 +120,115 @@ __device__ __forceinline__ void load_b(const float* __restrict__ w1, int col, in
   }
 }
 
-// node (within a lane half's 16) of half-local row l < 16*M: exact for M < 2^16 (the
-// fractional part of (l + 0.5)/M is at least 0.5/M from an integer)
-__device__ __forceinline__ int node_of(int l, float inv_m) {
-  return (int)(((float)l + 0.5f) * inv_m);
-}
-
-// The tiles of this workgroup: groups first, first+step, ... < end (one XCD's groups form a
-// contiguous range walked by that XCD's workgroups), M tiles each, as one flat sequence so
-// that loads run two tiles ahead across group boundaries.
-struct Tiles {
-  int first, step, M, count;
-  __device__ __forceinline__ Tiles(int num_groups, int M_) : M(M_) {
+// The groups of this workgroup: each XCD owns a contiguous range of groups proportional to
+// the number of workgroups it holds (blocks are dealt round-robin over the XCDs), walked by
+// its workgroups with stride = that number.
+struct Groups {
+  int first, step, end;
+  __device__ __forceinline__ explicit Groups(int num_groups) {
     const int nb = gridDim.x;
     const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
-    const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
-    const int span = (num_groups + kNumXcd - 1) / kNumXcd;
-    const int end = min(num_groups, xcd * span + span);
-    first = xcd * span + pos;
+    const int q = nb / kNumXcd, rm = nb % kNumXcd;
+    const int here = q + (xcd < rm ? 1 : 0);
+    const int before = xcd * q + min(xcd, rm);  // workgroups on lower XCDs
+    const int lo = (int)((int64_t)num_groups * before / nb);
+    end = (int)((int64_t)num_groups * (before + here) / nb);
+    first = lo + pos;
     step = here;
-    count = first < end ? ((end - first + step - 1) / step) * M : 0;
-  }
-  __device__ __forceinline__ int group(int k) const { return first + (k / M) * step; }
-  __device__ __forceinline__ int64_t row0(int k) const {  // first group row of tile k
-    const int gi = k / M;
-    return (int64_t)(first + gi * step) * kNodes * M + 16 * (k - gi * M);
   }
 };
 
-// Drive `tile(k, buf)` over the workgroup's tiles with a two-deep register ring and a
-// double-buffered LDS tile: tile k+2 is loaded while tile k computes, tile k+1 is stored
-// after it, one barrier per tile.
-template <int NT, int KP, class Body>
-__device__ __forceinline__ void walk_tiles(const Tiles& tl, const Stager<NT, KP>& st,
-                                           const float* __restrict__ ens, int64_t rows_total,
-                                           int F, float* buf0, float* buf1, Body&& tile) {
-  constexpr int PER = Stager<NT, KP>::PER;
-  float va[PER], vb[PER];
-  if (tl.count > 0) {
-    st.load(va, ens, tl.row0(0), rows_total, F);
-    st.store(buf0, va);
+// Position of a tile in the flat walk over (group, tile-in-group), advanced incrementally.
+struct Cursor {
+  int g, t;     // group index, tile within the group
+  int64_t row;  // first group row of the tile: g*32*M + 16*t
+  __device__ __forceinline__ void start(int g0, int M) {
+    g = g0;
+    t = 0;
+    row = (int64_t)g0 * kNodes * M;
   }
-  if (tl.count > 1) st.load(vb, ens, tl.row0(1), rows_total, F);
-  __syncthreads();
-  auto step = [&](int k, float (&cur)[PER], float (&nxt)[PER], float* bcur, float* bnxt) {
-    if (k + 2 < tl.count) st.load(cur, ens, tl.row0(k + 2), rows_total, F);
-    tile(k, bcur);
-    if (k + 1 < tl.count) st.store(bnxt, nxt);
-    __syncthreads();
+  __device__ __forceinline__ void advance(int M, int step) {
+    if (++t == M) {
+      t = 0;
+      g += step;
+      row = (int64_t)g * kNodes * M;
+    } else {
+      row += 16;
+    }
+  }
+};
+
+__device__ __forceinline__ int rows_left(int64_t rows_total, int64_t row) {
+  const int64_t d = rows_total - row;
+  return d > 0x7fffffff ? 0x7fffffff : (int)d;
+}
+
+// Drive `tile(cursor, buf, mbits)` over the workgroup's tiles with a two-deep register ring
+// and a double-buffered LDS tile: tile k+2 is loaded while tile k computes, tile k+1 is
+// stored after it, one barrier per tile.  With `mask_in`, each thread's 16-bit ReLU mask
+// word of the tile rides in the same ring (registers only: a thread reads its own word).
+template <int NT, int KP, class Body>
+__device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager<NT, KP>& st,
+                                           const float* __restrict__ ens, int64_t rows_total,
+                                           int F, float* buf0, float* buf1,
+                                           const uint16_t* __restrict__ mask_in, Body&& tile) {
+  constexpr int PER = Stager<NT, KP>::PER;
+  if (gr.first >= gr.end) return;
+  const int count = ((gr.end - gr.first + gr.step - 1) / gr.step) * M;
+  Cursor cur, pf;  // tile being computed, tile being loaded
+  cur.start(gr.first, M);
+  pf = cur;
+  auto mload = [&](const Cursor& c) -> uint32_t {
+    return mask_in ? (uint32_t)mask_in[((int64_t)c.g * M + c.t) * NT + threadIdx.x] : 0u;
   };
-  for (int k = 0; k < tl.count; k += 2) {
-    step(k, va, vb, buf0, buf1);
-    if (k + 1 < tl.count) step(k + 1, vb, va, buf1, buf0);
+  float va[PER], vb[PER];
+  uint32_t ma = 0, mb = 0;
+  st.load(va, ens + pf.row * F, rows_left(rows_total, pf.row));
+  ma = mload(pf);
+  st.store(buf0, va);
+  if (count > 1) {
+    pf.advance(M, gr.step);
+    st.load(vb, ens + pf.row * F, rows_left(rows_total, pf.row));
+    mb = mload(pf);
+  }
+  pf.advance(M, gr.step);  // pf: tile k+2
+  __syncthreads();
+  auto step = [&](int k, float (&vcur)[PER], uint32_t& mcur, float (&vnxt)[PER], float* bcur,
+                  float* bnxt) {
+    const uint32_t bits = mcur;
+    if (k + 2 < count) {
+      st.load(vcur, ens + pf.row * F, rows_left(rows_total, pf.row));
+      mcur = mload(pf);
+    }
+    tile(cur, bcur, bits);
+    if (k + 1 < count) st.store(bnxt, vnxt);
+    __syncthreads();
+    cur.advance(M, gr.step);
+    pf.advance(M, gr.step);
+  };
+  for (int k = 0; k < count; k += 2) {
+    step(k, va, ma, vb, buf0, buf1);
+    if (k + 1 < count) step(k + 1, vb, mb, va, buf1, buf0);
   }
 }
 
 // ---------------------------------------------------------------------------------------
+// Forward.  mask_out (optional): bit q of word [(g*M + t)*NT + thread] = ReLU active for the
+// row in accumulator register q -- what the backward needs instead of the activation.
 template <int H, int KP>
 __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__ ens,
                                                        const float* __restrict__ w1,
                                                        const float* __restrict__ b1,
-                                                       float* __restrict__ r, int64_t N,
-                                                       int M, int F, int num_groups) {
+                                                       float* __restrict__ r,
+                                                       uint16_t* __restrict__ mask_out,
+                                                       int64_t N, int M, int F,
+                                                       int num_groups) {
   constexpr int NT = 2 * H;
   constexpr int LD = KP + 4;
   __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
-  const float inv_m = 1.f / (float)M;
   float bf[KP / 2];
   load_b<KP>(w1, col, h, F, bf);
   const float bias = b1[col];
@@ -196,102 +237,132 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
 
   Stager<NT, KP> st;
   st.init(F, M);
-  const Tiles tl(num_groups, M);
-  int cur = 0;
+  const Groups gr(num_groups);
+  // uniform walk state: node (0..15 within each half's 16) and rows left in it
+  int node = 0, rem = M;
   float run = 0.f;
-  walk_tiles(tl, st, ens, N * M, F, s_e[0], s_e[1], [&](int k, const float* buf) {
-    const int gi = k / M, t = k - gi * M;
-    const int64_t my_node0 = (int64_t)(tl.first + gi * tl.step) * kNodes + 16 * h;
-    const floatx16 acc = pre_tile<KP>(buf, bf, c32, h);
-    if (t == 0) {
-      cur = 0;
+  float* rout = r;        // this lane's column of the current half's first node
+  int64_t nvalid = 0;     // nodes of this half that exist
+  walk_tiles(gr, M, st, ens, N * M, F, s_e[0], s_e[1], nullptr,
+             [&](const Cursor& c, const float* buf, uint32_t) {
+    if (c.t == 0) {
+      const int64_t n0 = (int64_t)c.g * kNodes + 16 * h;
+      rout = r + n0 * H + col;
+      nvalid = N - n0;
+      node = 0;
+      rem = M;
       run = 0.f;
     }
+    const floatx16 acc = pre_tile<KP>(buf, bf, c32, h);
+    uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int node = node_of(16 * t + q, inv_m);  // wave-uniform
-      if (node != cur) {
-        if (my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
-        cur = node;
+      const float v = acc[q] + bias;
+      bits |= (v > 0.f ? 1u : 0u) << q;
+      run += relu_nan(v);
+      if (--rem == 0) {  // last member of this node: write its sum
+        if (node < nvalid) rout[(int64_t)node * H] = run;
         run = 0.f;
+        ++node;
+        rem = M;
       }
-      run += relu_nan(acc[q] + bias);
     }
-    if (t == M - 1 && my_node0 + cur < N) r[(my_node0 + cur) * H + col] = run;
+    if (mask_out) mask_out[((int64_t)c.g * M + c.t) * NT + threadIdx.x] = (uint16_t)bits;
   });
 }
 
 // ---------------------------------------------------------------------------------------
+// Backward for the weights from the forward's ReLU mask:
+//   dh = dr[node] * mask;  dW1 += dh^T ens (MFMA over 32-feature tiles, A = dh straight from
+//   registers, B = staged rows; the last F % 32 features as fp32 FMAs);  db1 += sum dh.
 template <int H, int KP>
 __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__ ens,
-                                                       const float* __restrict__ w1,
-                                                       const float* __restrict__ b1,
+                                                       const uint16_t* __restrict__ mask,
                                                        const float* __restrict__ dr,
                                                        float* __restrict__ slab, int64_t N,
                                                        int M, int F, int num_groups) {
   constexpr int NT = 2 * H;
   constexpr int LD = KP + 4;
-  constexpr int NI = (KP + 31) / 32;  // 32-wide feature tiles of dW1
+  constexpr int NIF = KP / 32;         // full 32-wide feature tiles (MFMA)
+  constexpr int TAIL = KP - 32 * NIF;  // remaining features, multiple of 4 (VALU)
   __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
   __shared__ float s_dr[kNodes * H];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
-  const float inv_m = 1.f / (float)M;
-  float bf[KP / 2];
-  load_b<KP>(w1, col, h, F, bf);
-  const float bias = b1[col];
   zero_pad<KP>(s_e[0], F);
   zero_pad<KP>(s_e[1], F);
 
-  floatx16 gw[NI];
+  floatx16 gw[NIF > 0 ? NIF : 1];
 #pragma unroll
-  for (int it = 0; it < NI; ++it) gw[it] = zero16();
+  for (int it = 0; it < NIF; ++it) gw[it] = zero16();
+  float tw[TAIL > 0 ? TAIL : 1];
+#pragma unroll
+  for (int j = 0; j < TAIL; ++j) tw[j] = 0.f;
   double gb = 0.0;
 
   Stager<NT, KP> st;
   st.init(F, M);
-  const Tiles tl(num_groups, M);
-  walk_tiles(tl, st, ens, N * M, F, s_e[0], s_e[1], [&](int k, const float* buf) {
-    const int gi = k / M, t = k - gi * M;
-    if (t == 0) {  // dr of this group, this wave's columns (read by this wave only)
-      const int64_t node0 = (int64_t)(tl.first + gi * tl.step) * kNodes;
+  const Groups gr(num_groups);
+  const float* my_dr = s_dr + 16 * h * H + col;  // this lane: node j of its half at j*H
+  int node = 0, rem = M;
+  walk_tiles(gr, M, st, ens, N * M, F, s_e[0], s_e[1], mask,
+             [&](const Cursor& c, const float* buf, uint32_t bits) {
+    if (c.t == 0) {  // dr of this group, this wave's columns (read by this wave only)
+      const int64_t node0 = (int64_t)c.g * kNodes;
       for (int i = lane; i < kNodes * 32; i += kWave) {
         const int64_t n = node0 + (i >> 5);
-        const int c = wave * 32 + (i & 31);
-        s_dr[(i >> 5) * H + c] = n < N ? dr[n * H + c] : 0.f;
+        const int cc = wave * 32 + (i & 31);
+        s_dr[(i >> 5) * H + cc] = n < N ? dr[n * H + cc] : 0.f;
+      }
+      node = 0;
+      rem = M;
+    }
+    float dh[16];
+    float gsum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {  // independent LDS reads, uniform node walk
+      const float d = my_dr[node * H];  // 0 for nodes >= N
+      const float v = ((bits >> q) & 1u) ? d : 0.f;
+      dh[q] = v;
+      gsum += v;
+      if (--rem == 0) {
+        ++node;
+        rem = M;
       }
     }
-    floatx16 dh = pre_tile<KP>(buf, bf, c32, h);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {  // independent LDS reads: no branch on the node change
-      const float d = s_dr[(16 * h + node_of(16 * t + q, inv_m)) * H + col];  // 0 if >= N
-      const float v = (dh[q] + bias > 0.f) ? d : 0.f;  // ReLU backward
-      dh[q] = v;
-      gb += (double)v;
-    }
-    // dW1[o][i] += sum_rows dh[row][o] ens[row][i]: A = dh (registers), B = staged rows
+    gb += (double)gsum;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float* erow = buf + (16 * h + q) * LD;
 #pragma unroll
-      for (int it = 0; it < NI; ++it) {
-        const int i = 32 * it + c32;
-        const float b = (32 * it + 32 <= KP || i < KP) ? erow[i] : 0.f;
-        gw[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(dh[q], b, gw[it], 0, 0, 0);
+      for (int it = 0; it < NIF; ++it)
+        gw[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(dh[q], erow[32 * it + c32], gw[it], 0,
+                                                      0, 0);
+#pragma unroll
+      for (int j = 0; j < TAIL; j += 4) {
+        const float4 e4 = *reinterpret_cast<const float4*>(erow + 32 * NIF + j);
+        tw[j] = __builtin_fmaf(dh[q], e4.x, tw[j]);
+        tw[j + 1] = __builtin_fmaf(dh[q], e4.y, tw[j + 1]);
+        tw[j + 2] = __builtin_fmaf(dh[q], e4.z, tw[j + 2]);
+        tw[j + 3] = __builtin_fmaf(dh[q], e4.w, tw[j + 3]);
       }
     }
   });
   // slab row of this workgroup: [H*F weights | H bias]
   float* out = slab + (size_t)blockIdx.x * ((size_t)H * F + H);
 #pragma unroll
-  for (int it = 0; it < NI; ++it) {
+  for (int it = 0; it < NIF; ++it) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int o = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      const int i = 32 * it + c32;
-      if (i < F) out[(size_t)o * F + i] = gw[it][q];
+      out[(size_t)o * F + 32 * it + c32] = gw[it][q];
     }
+  }
+#pragma unroll
+  for (int j = 0; j < TAIL; ++j) {
+    const float v = tw[j] + __shfl_xor(tw[j], 32, kWave);
+    if (h == 0 && 32 * NIF + j < F) out[(size_t)col * F + 32 * NIF + j] = v;
   }
   gb += shfl_xor_d(gb, 32);
   if (h == 0) out[(size_t)H * F + col] = (float)gb;
@@ -322,9 +393,19 @@ __global__ __launch_bounds__(256) void k_deepset_slab_reduce(const float* __rest
   else if (db) db[e - wsize] = (float)v;
 }
 
-inline int pad_features(int F) {
+// forward: the MFMA k-split needs KP % 8 == 0; backward: rows stage as float4, KP % 4 == 0
+inline int pad_fwd(int F) {
   if (F <= 16) return 16;
   if (F <= 32) return 32;
+  if (F <= 40) return 40;
+  if (F <= 48) return 48;
+  if (F <= 64) return 64;
+  return -1;
+}
+inline int pad_bwd(int F) {
+  if (F <= 16) return 16;
+  if (F <= 32) return 32;
+  if (F <= 36) return 36;
   if (F <= 40) return 40;
   if (F <= 48) return 48;
   if (F <= 64) return 64;
@@ -338,7 +419,7 @@ inline int bwd_grid(int64_t N) {
   return (int)std::min<int64_t>(groups, 512);
 }
 
-#define DS_DISPATCH(H_, KP_, MACRO)                       \
+#define DS_FWD_KP(H_, KP_, MACRO)                         \
   switch (KP_) {                                          \
     case 16: MACRO(H_, 16); break;                        \
     case 32: MACRO(H_, 32); break;                        \
@@ -347,12 +428,22 @@ inline int bwd_grid(int64_t N) {
     default: MACRO(H_, 64); break;                        \
   }
 
-#define DS_DISPATCH_H(H, KP, MACRO)                       \
+#define DS_BWD_KP(H_, KP_, MACRO)                         \
+  switch (KP_) {                                          \
+    case 16: MACRO(H_, 16); break;                        \
+    case 32: MACRO(H_, 32); break;                        \
+    case 36: MACRO(H_, 36); break;                        \
+    case 40: MACRO(H_, 40); break;                        \
+    case 48: MACRO(H_, 48); break;                        \
+    default: MACRO(H_, 64); break;                        \
+  }
+
+#define DS_DISPATCH_H(H, KP, KPSWITCH, MACRO)             \
   switch (H) {                                            \
-    case 32: DS_DISPATCH(32, KP, MACRO); break;           \
-    case 64: DS_DISPATCH(64, KP, MACRO); break;           \
-    case 128: DS_DISPATCH(128, KP, MACRO); break;         \
-    default: DS_DISPATCH(256, KP, MACRO); break;          \
+    case 32: KPSWITCH(32, KP, MACRO); break;              \
+    case 64: KPSWITCH(64, KP, MACRO); break;              \
+    case 128: KPSWITCH(128, KP, MACRO); break;            \
+    default: KPSWITCH(256, KP, MACRO); break;             \
   }
 
 }  // namespace
@@ -360,10 +451,17 @@ inline int bwd_grid(int64_t N) {
 
 using namespace gine;
 
+extern "C" int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32_t hidden,
+                                       size_t* bytes) {
+  if (!bytes || num_nodes < 0 || members <= 0 || !hidden_ok(hidden)) return GINE_ERR_INVALID;
+  *bytes = (size_t)ceil_div(num_nodes, kNodes) * members * 2 * hidden * sizeof(uint16_t);
+  return GINE_OK;
+}
+
 extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* b1, float* r,
-                                int64_t num_nodes, int32_t members, int32_t in_features,
-                                int32_t hidden, void* stream) {
-  const int KP = pad_features(in_features);
+                                uint16_t* mask, int64_t num_nodes, int32_t members,
+                                int32_t in_features, int32_t hidden, void* stream) {
+  const int KP = pad_fwd(in_features);
   if (!hidden_ok(hidden) || KP < 0 || in_features <= 0) return GINE_ERR_DIM;
   if (num_nodes < 0 || members <= 0) return GINE_ERR_INVALID;
   if (num_nodes == 0) return GINE_OK;
@@ -374,8 +472,8 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD(H_, KP_)                                                                 \
   hipLaunchKernelGGL((k_deepset_fwd<H_, KP_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, b1, \
-                     r, num_nodes, members, in_features, groups)
-  DS_DISPATCH_H(hidden, KP, LAUNCH_FWD);
+                     r, mask, num_nodes, members, in_features, groups)
+  DS_DISPATCH_H(hidden, KP, DS_FWD_KP, LAUNCH_FWD);
 #undef LAUNCH_FWD
   GINE_LAUNCH_STATUS();
   return GINE_OK;
@@ -387,14 +485,14 @@ extern "C" int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t* num_par
   return GINE_OK;
 }
 
-extern "C" int gine_deepset_bwd(const float* ens, const float* w1, const float* b1,
-                                const float* dr, float* slab, float* dw1, float* db1,
-                                int64_t num_nodes, int32_t members, int32_t in_features,
-                                int32_t hidden, void* stream) {
-  const int KP = pad_features(in_features);
+extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const float* dr,
+                                float* slab, float* dw1, float* db1, int64_t num_nodes,
+                                int32_t members, int32_t in_features, int32_t hidden,
+                                void* stream) {
+  const int KP = pad_bwd(in_features);
   if (!hidden_ok(hidden) || KP < 0 || in_features <= 0) return GINE_ERR_DIM;
   if (num_nodes < 0 || members <= 0 || !slab || !dw1) return GINE_ERR_INVALID;
-  if (num_nodes > 0 && (!ens || !w1 || !b1 || !dr)) return GINE_ERR_INVALID;
+  if (num_nodes > 0 && (!ens || !mask || !dr)) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   const int groups = (int)ceil_div(num_nodes > 0 ? num_nodes : 1, kNodes);
   const int grid = bwd_grid(num_nodes);
@@ -403,10 +501,10 @@ extern "C" int gine_deepset_bwd(const float* ens, const float* w1, const float* 
   if (num_nodes == 0) {
     GINE_RETURN_IF_HIP(hipMemsetAsync(slab, 0, sizeof(float) * per * grid, s));
   } else {
-#define LAUNCH_BWD(H_, KP_)                                                                 \
-  hipLaunchKernelGGL((k_deepset_bwd<H_, KP_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, b1, \
-                     dr, slab, num_nodes, members, in_features, groups)
-    DS_DISPATCH_H(hidden, KP, LAUNCH_BWD);
+#define LAUNCH_BWD(H_, KP_)                                                                   \
+  hipLaunchKernelGGL((k_deepset_bwd<H_, KP_>), dim3(grid), dim3(2 * H_), 0, s, ens, mask, dr, \
+                     slab, num_nodes, members, in_features, groups)
+    DS_DISPATCH_H(hidden, KP, DS_BWD_KP, LAUNCH_BWD);
 #undef LAUNCH_BWD
     GINE_LAUNCH_STATUS();
   }

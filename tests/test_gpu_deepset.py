@@ -41,7 +41,7 @@ def _run(N, M, F, H, seed=0, scale=1.0):
 @pytest.mark.parametrize("N,M,F,H", [
     (1, 1, 1, 32), (31, 11, 35, 128), (33, 11, 35, 128), (1000, 11, 35, 128),
     (16000, 11, 35, 128), (257, 1, 16, 64), (100, 33, 64, 256), (77, 5, 20, 32),
-    (500, 51, 35, 128), (64, 2, 40, 128), (65, 3, 48, 64)])
+    (500, 51, 35, 128), (64, 2, 40, 128), (65, 3, 48, 64), (90, 7, 33, 128), (40, 4, 61, 32)])
 def test_phi_sum_forward_and_weight_grads(N, M, F, H):
     ens, lin = _run(N, M, F, H, seed=N + M + F + H)
     r = deepset.phi_sum(ens, lin)
@@ -75,6 +75,15 @@ def test_phi_sum_deterministic():
         outs.append((r.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_phi_sum_eval_has_no_mask():
+    """Without grad the forward runs alone (no mask buffer) and gives the same r."""
+    ens, lin = _run(1000, 11, 35, 128, seed=7)
+    r_train = deepset.phi_sum(ens, lin)
+    with torch.no_grad():
+        r_eval = deepset.phi_sum(ens, lin)
+    assert torch.equal(r_train, r_eval)
 
 
 def test_phi_sum_empty():
@@ -111,10 +120,10 @@ def test_abi_rejects_unsupported_shapes():
     r = torch.zeros(4, 128, device=DEV)
     s = _lib.stream_handle(DEV)
     lib = _lib.load()
-    assert lib.gine_deepset_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(r), 4, 2, 65,
-                                128, s) == _lib.GINE_ERR_DIM
-    assert lib.gine_deepset_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(r), 4, 2, 35,
-                                96, s) == _lib.GINE_ERR_DIM
+    assert lib.gine_deepset_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(r), None, 4, 2,
+                                65, 128, s) == _lib.GINE_ERR_DIM
+    assert lib.gine_deepset_fwd(_lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(r), None, 4, 2,
+                                35, 96, s) == _lib.GINE_ERR_DIM
     assert not deepset.fusable(x, w, b)
     n = ctypes.c_int32(0)
     assert lib.gine_deepset_bwd_num_partials(16000, ctypes.byref(n)) == 0 and n.value == 500

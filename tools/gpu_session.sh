@@ -35,6 +35,11 @@ for s in $STEPS; do
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ;;
     counters) run list_counters 300 rocprofv3 -L ;;
+    dsmicro) run ds_micro 300 python tools/ds_micro.py ;;
+    dssq)  run ds_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d "$OUT/ds_sq1" -o run -- \
+               python3 tools/ds_micro.py --reps 5 --nodes 16000
+           run ds_sq2 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/ds_sq2" -o run -- \
+               python3 tools/ds_micro.py --reps 5 --nodes 16000 ;;
     sq)    run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d "$OUT/pmc_sq" -o run -- \
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ;;
   esac
