@@ -28,6 +28,22 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kNodes = 32;  // nodes per group; a group is exactly M tiles of 32 rows
 
+#ifdef GINE_DS_PROFILE
+// Debug build only: block 0 / thread 0 records s_memtime at phase boundaries of its tiles.
+__device__ long long g_ds_prof[4096];
+__device__ int g_ds_prof_n;
+#define DS_MARK(tag)                                                          \
+  do {                                                                        \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && g_ds_prof_n < 2040) {          \
+      g_ds_prof[2 * g_ds_prof_n] = (tag);                                     \
+      g_ds_prof[2 * g_ds_prof_n + 1] = (long long)__builtin_amdgcn_s_memtime(); \
+      ++g_ds_prof_n;                                                          \
+    }                                                                         \
+  } while (0)
+#else
+#define DS_MARK(tag) do {} while (0)
+#endif
+
 __device__ __forceinline__ floatx16 zero16() {
   floatx16 v;
 #pragma unroll
@@ -196,13 +212,18 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
   auto step = [&](int k, float (&vcur)[PER], uint32_t& mcur, float (&vnxt)[PER], float* bcur,
                   float* bnxt) {
     const uint32_t bits = mcur;
+    DS_MARK(0);
     if (k + 2 < count) {
       st.load(vcur, ens + pf.row * F, rows_left(rows_total, pf.row));
       mcur = mload(pf);
     }
+    DS_MARK(1);
     tile(cur, bcur, bits);
+    DS_MARK(4);
     if (k + 1 < count) st.store(bnxt, vnxt);
+    DS_MARK(5);
     __syncthreads();
+    DS_MARK(6);
     cur.advance(M, gr.step);
     pf.advance(M, gr.step);
   };
@@ -254,6 +275,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
       run = 0.f;
     }
     const floatx16 acc = pre_tile<KP>(buf, bf, c32, h);
+    DS_MARK(2 + 0 * (int)acc[15]);
     uint32_t bits = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -267,6 +289,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
         rem = M;
       }
     }
+    DS_MARK(3 + 0 * (int)run);
     if (mask_out) mask_out[((int64_t)c.g * M + c.t) * NT + threadIdx.x] = (uint16_t)bits;
   });
 }
@@ -356,7 +379,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int o = wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      out[(size_t)o * F + 32 * it + c32] = gw[it][q];
+      if (32 * it + c32 < F) out[(size_t)o * F + 32 * it + c32] = gw[it][q];
     }
   }
 #pragma unroll
@@ -513,3 +536,14 @@ extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const fl
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
+
+#ifdef GINE_DS_PROFILE
+extern "C" int gine_debug_ds_prof(long long* out, int* n) {
+  GINE_RETURN_IF_HIP(hipDeviceSynchronize());
+  GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(n, HIP_SYMBOL(g_ds_prof_n), sizeof(int)));
+  GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ds_prof), sizeof(long long) * 4096));
+  const int zero = 0;
+  GINE_RETURN_IF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ds_prof_n), &zero, sizeof(int)));
+  return GINE_OK;
+}
+#endif

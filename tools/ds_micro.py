@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--M", type=int, default=11)
     ap.add_argument("--F", type=int, default=35)
     ap.add_argument("--H", type=int, default=128)
+    ap.add_argument("--prof", action="store_true",
+                    help="phase profile of the forward (needs GINE_HIP_LIB = the dsprof build)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     out = {}
@@ -41,6 +43,28 @@ def main():
                                 _lib.ptr(r), _lib.ptr(mask), N, a.M, a.F, a.H, s)
         bwd = lambda: _lib.call("gine_deepset_bwd", _lib.ptr(ens), _lib.ptr(mask), _lib.ptr(dr),
                                 _lib.ptr(slab), _lib.ptr(dw), _lib.ptr(db), N, a.M, a.F, a.H, s)
+        if a.prof:
+            lib = _lib.load()
+            buf = (ctypes.c_longlong * 4096)()
+            n = ctypes.c_int(0)
+            fwd()
+            lib.gine_debug_ds_prof(buf, ctypes.byref(n))   # reset
+            fwd()
+            lib.gine_debug_ds_prof(buf, ctypes.byref(n))
+            ev = [(buf[2 * i], buf[2 * i + 1]) for i in range(n.value)]
+            names = {0: "top", 1: "loads issued", 2: "mfma chain", 3: "epilogue",
+                     4: "mask store", 5: "lds store", 6: "barrier"}
+            acc, cnt = {}, {}
+            for (t0, c0), (t1, c1) in zip(ev, ev[1:]):
+                if t1 == 0:
+                    continue
+                acc[t1] = acc.get(t1, 0) + (c1 - c0)
+                cnt[t1] = cnt.get(t1, 0) + 1
+            tot = sum(acc[k] / cnt[k] for k in acc)
+            print(N, "phase cycles/tile (s_memtime):",
+                  {names[k]: round(acc[k] / cnt[k]) for k in sorted(acc)}, "total", round(tot),
+                  flush=True)
+            continue
         res = {}
         for name, fn in (("fwd", fwd), ("bwd", bwd)):
             for _ in range(3):
