@@ -17,10 +17,12 @@
 // product is unchanged, and each lane's A fragments become contiguous in LDS, so four
 // k-steps are fetched with one ds_read_b128 (row stride D+4 floats: conflict-free).
 //
-// Weight gradients (K = N rows) use k_wgrad: 64x64 output blocks x row chunks, fp32
-// partial slabs, reduced in fixed chunk order in fp64 by k_slab_reduce -> deterministic.
+// Weight gradients (K = N rows) run on the shared engine of gine_wgrad.hpp (64x128 output
+// tiles x row chunks, fp32 partial slabs) and are reduced in fixed chunk order in fp64 by
+// k_slab_reduce -> deterministic.
 #include "gine_common.hpp"
 #include "gine_reduce.hpp"
+#include "gine_wgrad.hpp"
 
 #include <algorithm>
 
@@ -37,7 +39,6 @@ __device__ __forceinline__ floatx16 zero16() {
 }
 
 constexpr int kRowTile = 32;
-constexpr int kChunkTarget = 64;
 
 enum Pro { PRO_PLAIN = 0, PRO_BNRELU = 1, PRO_DO = 2, PRO_DA1 = 3 };
 enum Epi { EPI_A1STATS = 0, EPI_OUT = 1, EPI_DBN = 2, EPI_PLAIN = 3 };
@@ -474,98 +475,32 @@ __global__ __launch_bounds__(kColsumThreads) void k_bn_bwd_finalize(
 // Weight gradients: dW[o][i] = sum_n P[n][o] * Q[n][i], db[o] = sum_n P[n][o]
 //   z = 0: P = do (PRO_DO of dy), Q = r = relu(bn(a1))  -> dW2, db2
 //   z = 1: P = da1 (PRO_DA1 of dbn), Q = z               -> dW1, db1
-// grid = (chunks, 64x64 output blocks, 2); 4 waves per block, one 32x32 tile per wave.
+// on the shared engine (gine_wgrad.hpp); this is its operand source.
 // ----------------------------------------------------------------------------------------
-struct WgradArgs {
+struct MlpWgradSrc {
   ProArgs p_do, q_r, p_da1, q_z;
-  float* slab;  // [2][chunks][D*D + D]
-  int chunks, rows_per_chunk;
+  int D;
+  using Raw = RawItem;
+  using Col = ColConst;
+  __device__ Col p_col(int z, int q) const {
+    return z == 0 ? col_const<PRO_DO>(p_do, D, q) : col_const<PRO_DA1>(p_da1, D, q);
+  }
+  __device__ Col q_col(int z, int q) const {
+    return z == 0 ? col_const<PRO_BNRELU>(q_r, D, q) : col_const<PRO_PLAIN>(q_z, D, q);
+  }
+  __device__ Raw p_load(int z, int64_t n, int q) const {
+    return z == 0 ? raw_load<PRO_DO>(p_do, D, n, q) : raw_load<PRO_DA1>(p_da1, D, n, q);
+  }
+  __device__ Raw q_load(int z, int64_t n, int q) const {
+    return z == 0 ? raw_load<PRO_BNRELU>(q_r, D, n, q) : raw_load<PRO_PLAIN>(q_z, D, n, q);
+  }
+  __device__ float4 p_xform(int z, const Raw& r, const Col& c) const {
+    return z == 0 ? transform<PRO_DO>(p_do, r, c) : transform<PRO_DA1>(p_da1, r, c);
+  }
+  __device__ float4 q_xform(int z, const Raw& r, const Col& c) const {
+    return z == 0 ? transform<PRO_BNRELU>(q_r, r, c) : transform<PRO_PLAIN>(q_z, r, c);
+  }
 };
-
-template <int D>
-__global__ __launch_bounds__(256) void k_wgrad(WgradArgs wa, int64_t N) {
-  constexpr int BW = D < 64 ? D : 64;    // block tile width (o and i)
-  constexpr int NBI = D / BW;            // block tiles along i
-  constexpr int LDW = BW + 1;
-  constexpr int BW4 = BW / 4;
-  __shared__ float sP[kRowTile * LDW];
-  __shared__ float sQ[kRowTile * LDW];
-
-  const int chunk = blockIdx.x, bt = blockIdx.y, zsel = blockIdx.z;
-  const int o0 = (bt / NBI) * BW, i0 = (bt % NBI) * BW;
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int h = lane >> 5, c32 = lane & 31;
-  const int wr = wave >> 1, wc = wave & 1;
-  const bool active = (32 * wr < BW) && (32 * wc < BW);
-  const bool do_bias = active && wc == 0 && i0 == 0;
-  const ProArgs& P = zsel == 0 ? wa.p_do : wa.p_da1;
-  const ProArgs& Q = zsel == 0 ? wa.q_r : wa.q_z;
-
-  const int64_t r_begin = (int64_t)chunk * wa.rows_per_chunk;
-  const int64_t r_end = min<int64_t>(N, r_begin + wa.rows_per_chunk);
-  floatx16 acc = zero16();
-  double bsum = 0.0;
-
-  // Software pipeline: the next 32-row sub-tile's prologue values are loaded into
-  // registers while the current sub-tile's MFMAs run.
-  constexpr int ITEMS = (kRowTile * BW4 + 255) / 256;
-  float4 vp[ITEMS], vq[ITEMS];
-  auto load = [&](int64_t n0) {
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int idx = threadIdx.x + k * 256;
-      const int r = idx / BW4, q = idx % BW4;
-      const int64_t n = n0 + r;
-      const int64_t nc = n < r_end ? n : r_end - 1;
-      float4 a = zsel == 0 ? prologue<PRO_DO>(P, D, nc, o0 / 4 + q)
-                           : prologue<PRO_DA1>(P, D, nc, o0 / 4 + q);
-      float4 b = zsel == 0 ? prologue<PRO_BNRELU>(Q, D, nc, i0 / 4 + q)
-                           : prologue<PRO_PLAIN>(Q, D, nc, i0 / 4 + q);
-      if (n >= r_end || idx >= kRowTile * BW4) a = b = f4_zero();
-      vp[k] = a;
-      vq[k] = b;
-    }
-  };
-  load(r_begin);
-  for (int64_t n0 = r_begin; n0 < r_end; n0 += kRowTile) {
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-      const int idx = threadIdx.x + k * 256;
-      if (idx < kRowTile * BW4) {
-        const int r = idx / BW4, q = idx % BW4;
-        float* dp = &sP[r * LDW + 4 * q];
-        float* dq = &sQ[r * LDW + 4 * q];
-        dp[0] = vp[k].x; dp[1] = vp[k].y; dp[2] = vp[k].z; dp[3] = vp[k].w;
-        dq[0] = vq[k].x; dq[1] = vq[k].y; dq[2] = vq[k].z; dq[3] = vq[k].w;
-      }
-    }
-    __syncthreads();
-    if (n0 + kRowTile < r_end) load(n0 + kRowTile);
-    if (active) {
-#pragma unroll
-      for (int s = 0; s < kRowTile / 2; ++s) {
-        const int rr = h * (kRowTile / 2) + s;
-        const float a = sP[rr * LDW + 32 * wr + c32];
-        const float b = sQ[rr * LDW + 32 * wc + c32];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-        if (do_bias) bsum += (double)a;
-      }
-    }
-    __syncthreads();
-  }
-
-  float* slab = wa.slab + ((size_t)zsel * wa.chunks + chunk) * (size_t)(D * D + D);
-  if (active) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = o0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int i = i0 + 32 * wc + c32;
-      slab[(size_t)o * D + i] = acc[r];
-    }
-  }
-  bsum += shfl_xor_d(bsum, 32);
-  if (do_bias && h == 0) slab[(size_t)D * D + o0 + 32 * wr + c32] = (float)bsum;
-}
 
 // Sum the chunk slabs: workgroup = 64 consecutive elements x 4 chunk groups (chunk c goes
 // to group c % 4, summed in chunk order), groups combined in fixed order through LDS.
@@ -601,13 +536,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
 
 inline bool mlp_dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
-inline void wgrad_plan(int64_t N, int* chunks, int* rows) {
-  int64_t tiles = ceil_div(N, kRowTile);
-  if (tiles < 1) tiles = 1;
-  const int64_t per = ceil_div(tiles, kChunkTarget);  // tiles per chunk
-  *rows = (int)(per * kRowTile);
-  *chunks = (int)ceil_div(N > 0 ? N : 1, *rows);
-}
+inline WgPlan mlp_wgrad_plan(int64_t N, int D) { return wg_plan(N, D, D, 2); }
 
 }  // namespace
 }  // namespace gine
@@ -722,9 +651,7 @@ extern "C" int gine_mlp_wgrad_num_chunks(int64_t num_nodes, int32_t channels,
                                          int32_t* num_chunks) {
   if (!num_chunks || num_nodes < 0) return GINE_ERR_INVALID;
   if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
-  int chunks, rows;
-  wgrad_plan(num_nodes, &chunks, &rows);
-  *num_chunks = chunks;
+  *num_chunks = mlp_wgrad_plan(num_nodes, channels).chunks;
   return GINE_OK;
 }
 
@@ -739,27 +666,20 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
   const int D = channels;
-  WgradArgs wa;
-  wa.p_do = ProArgs{dy, y, mask, nullptr, nullptr, epilogue};
-  wa.q_r = ProArgs{a1, nullptr, nullptr, bn_save, nullptr, 0};
-  wa.p_da1 = ProArgs{dbn, a1, nullptr, bn_save, coef, 0};
-  wa.q_z = ProArgs{z, nullptr, nullptr, nullptr, nullptr, 0};
-  wa.slab = slab;
-  wgrad_plan(num_nodes, &wa.chunks, &wa.rows_per_chunk);
-  const int bw = D < 64 ? D : 64;
-  const int nbt = (D / bw) * (D / bw);
+  MlpWgradSrc src;
+  src.p_do = ProArgs{dy, y, mask, nullptr, nullptr, epilogue};
+  src.q_r = ProArgs{a1, nullptr, nullptr, bn_save, nullptr, 0};
+  src.p_da1 = ProArgs{dbn, a1, nullptr, bn_save, coef, 0};
+  src.q_z = ProArgs{z, nullptr, nullptr, nullptr, nullptr, 0};
+  src.D = D;
+  const WgPlan p = mlp_wgrad_plan(num_nodes, D);
+  const size_t per = (size_t)D * D + D;
   hipStream_t s = as_stream(stream);
-  const dim3 grid(wa.chunks, nbt, 2);
-  switch (D) {
-    case 32: hipLaunchKernelGGL(k_wgrad<32>, grid, dim3(256), 0, s, wa, num_nodes); break;
-    case 64: hipLaunchKernelGGL(k_wgrad<64>, grid, dim3(256), 0, s, wa, num_nodes); break;
-    case 128: hipLaunchKernelGGL(k_wgrad<128>, grid, dim3(256), 0, s, wa, num_nodes); break;
-    default: hipLaunchKernelGGL(k_wgrad<256>, grid, dim3(256), 0, s, wa, num_nodes); break;
-  }
-  GINE_LAUNCH_STATUS();
+  const int st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+  if (st != GINE_OK) return st;
   const int total = 2 * (D * D + D);
   hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)ceil_div(total, 64)), dim3(256), 0, s, slab,
-                     wa.chunks, D, dw2, db2, dw1, db1);
+                     p.chunks, D, dw2, db2, dw1, db1);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

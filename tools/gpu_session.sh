@@ -28,12 +28,19 @@ for s in $STEPS; do
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    bench1) run bench_cfg1 600 python bench.py --config 1 ;;
+    bench3) run bench_cfg3 600 python bench.py --config 3 --steps 20 ;;
+    bench5) run bench_cfg5 600 python bench.py --config 5 --steps 20 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ;;
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
+           python tools/pmc_summary.py "$OUT"/pmc_fetch/run_counter_collection.csv \
+               "$OUT"/pmc_write/run_counter_collection.csv --traffic-json "$OUT/pmc_traffic.json" \
+               > "$OUT/pmc_summary.txt" 2>&1 ;;
+    floor) run launch_floor 300 python tools/launch_floor.py ;;
     counters) run list_counters 300 rocprofv3 -L ;;
     dsmicro) run ds_micro 300 python tools/ds_micro.py ;;
     dssq)  run ds_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d "$OUT/ds_sq1" -o run -- \
