@@ -138,6 +138,7 @@ def time_kernels(tr: Trainer, reps: int):
     l1, bn, _, l2 = conv.nn
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    S = [sh]  # launch stream of the timed lambdas (switched to the capture stream below)
     from raincast_gnn._lib import call, ptr
     lin = Fn.edge_linear_flag()
     P = Fn._count("gine_mlp_num_partials", N, D)
@@ -156,6 +157,7 @@ def time_kernels(tr: Trainer, reps: int):
     Pm = Fn._count("gine_mp_bwd_num_partials", N, D)
     mp_part = torch.empty(Pm, 3, D, dtype=torch.float64, device=dev)
     dx = torch.empty_like(x)
+    lw_g, lb_g, eps_g = torch.empty(D, device=dev), torch.empty(D, device=dev), torch.empty(1, device=dev)
     z = Fn.mp_forward(x, g, lw, lb, ep)
     rm = torch.zeros(D, device=dev)
     rv = torch.ones(D, device=dev)
@@ -172,29 +174,37 @@ def time_kernels(tr: Trainer, reps: int):
     kernels = {
         "gine_mp_fwd": (lambda: call("gine_mp_fwd", ptr(x), ptr(g.in_rowptr), ptr(g.in_src),
                                      ptr(g.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(z), N, D,
-                                     lin, sh),
+                                     lin, S[0]),
                         {"bytes": 4 * (2 * N * D + 2 * E + N + 1)}),
         "gine_mp_bwd": (lambda: call("gine_mp_bwd", ptr(dz), ptr(x), ptr(g.out_rowptr),
                                      ptr(g.out_dst), ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep),
-                                     ptr(dz), ptr(dx), ptr(mp_part), N, D, 1 | lin, sh),
+                                     ptr(dz), ptr(dx), ptr(mp_part), N, D, 1 | lin, S[0]),
                         {"bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D}),
         "gine_mlp_fwd1": (lambda: call("gine_mlp_fwd1", ptr(z), ptr(w1), ptr(b1), ptr(a1),
-                                       ptr(partials), N, D, sh),
+                                       ptr(partials), N, D, S[0]),
                           {"flops": 2 * N * D * D, "bytes": 8 * N * D}),
         "gine_mlp_fwd2": (lambda: call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2), ptr(b2),
-                                       ptr(x), ptr(y), ptr(mask), N, D, 2, sh),
+                                       ptr(x), ptr(y), ptr(mask), N, D, 2, S[0]),
                           {"flops": 2 * N * D * D, "bytes": 13 * N * D}),
         "gine_mlp_bwd2": (lambda: call("gine_mlp_bwd2", ptr(dz), None, ptr(mask), ptr(a1),
                                        ptr(bn_save), ptr(w2), ptr(dbn), ptr(partials), N, D, 2,
-                                       sh),
+                                       S[0]),
                           {"flops": 2 * N * D * D, "bytes": 13 * N * D}),
         "gine_mlp_bwd1": (lambda: call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save),
-                                       ptr(coef), ptr(w1), ptr(dx), N, D, sh),
+                                       ptr(coef), ptr(w1), ptr(dx), N, D, S[0]),
                           {"flops": 2 * N * D * D, "bytes": 12 * N * D}),
         "gine_mlp_wgrad": (lambda: call("gine_mlp_wgrad", ptr(dz), None, ptr(mask), ptr(a1),
                                         ptr(bn_save), ptr(dbn), ptr(coef), ptr(z), ptr(slab),
-                                        ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), N, D, 2, sh),
+                                        ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), N, D, 2, S[0]),
                            {"flops": 4 * N * D * D, "bytes": 4 * 4 * N * D + 5 * N * D}),
+        # the reduction launches between the GEMMs (partials reduced in place; re-running them
+        # on their own output only re-sums, shapes unchanged)
+        "gine_bn_fwd_finalize": (lambda: call("gine_bn_fwd_finalize", ptr(partials), P,
+                                              ptr(bn.weight), ptr(bn.bias), ptr(rm), ptr(rv),
+                                              None, ptr(bn_save), N, D, 0.1, 1e-5, 1, 0, S[0]),
+                                 {}),
+        "gine_mp_bwd_finalize": (lambda: call("gine_mp_bwd_finalize", ptr(mp_part), Pm, D,
+                                              ptr(lw_g), ptr(lb_g), ptr(eps_g), S[0]), {}),
     }
     out = {}
     for name, (fn, work) in kernels.items():
@@ -207,7 +217,24 @@ def time_kernels(tr: Trainer, reps: int):
         ev1.record(stream)
         ev1.synchronize()
         us = ev0.elapsed_time(ev1) * 1e3 / reps
-        rec = {"us": round(us, 3)}
+        # the same launches captured in one HIP graph: no host launch gaps, the way the
+        # training step runs them
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(stream)
+        graph = torch.cuda.CUDAGraph()
+        S[0] = side.cuda_stream
+        with torch.cuda.graph(graph, stream=side):
+            for _ in range(reps):
+                fn()
+        S[0] = sh
+        stream.wait_stream(side)
+        graph.replay()
+        ev0.record(stream)
+        graph.replay()
+        ev1.record(stream)
+        ev1.synchronize()
+        us_graph = ev0.elapsed_time(ev1) * 1e3 / reps
+        rec = {"us": round(us, 3), "us_graph": round(us_graph, 3)}
         if "bytes" in work:
             rec["alg_bytes"] = work["bytes"]
             rec["GBps"] = round(work["bytes"] / us * 1e-3, 1)
@@ -220,7 +247,8 @@ def time_kernels(tr: Trainer, reps: int):
 
 def roofline_for(kernels: dict, layers: int):
     # launches per step: every kernel once per layer
-    dominant = max(kernels, key=lambda k: kernels[k]["us"])
+    timed = [k for k in kernels if "alg_bytes" in kernels[k] or "alg_flops" in kernels[k]]
+    dominant = max(timed, key=lambda k: kernels[k]["us"])
     rec = kernels[dominant]
     if "flops" in rec or "alg_flops" in rec:
         achieved = rec["TFLOPps"]
@@ -233,21 +261,43 @@ def roofline_for(kernels: dict, layers: int):
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4)}
     roof["avg_us"] = rec["us"]
     roof["launches_per_step"] = layers
-    roof["traffic"] = pmc_traffic(dominant)
+    t = pmc_traffic(dominant)
+    roof["traffic"] = t["bytes"] if t else None
+    roof["traffic_source"] = t["source"] if t else None
     return roof
 
 
+# entry point -> the kernels one call launches (names as in the rocprofv3 PMC summary; D=128,
+# the residual epilogue of layers >= 1)
+PMC_KERNELS = {
+    "gine_mp_fwd": ["gine::k_mp_fwd<32, 1, "],
+    "gine_mp_bwd": ["gine::k_mp_bwd<32, 1, "],
+    "gine_mlp_fwd1": ["gine::k_rowgemm<128, 0, 0, true>"],
+    "gine_mlp_fwd2": ["gine::k_rowgemm<128, 1, 5, true>"],
+    "gine_mlp_bwd2": ["gine::k_rowgemm<128, 5, 2, false>"],
+    "gine_mlp_bwd1": ["gine::k_rowgemm<128, 3, 3, false>"],
+    "gine_mlp_wgrad": ["gine::k_wgrad_engine<gine::MlpWgradSrc<5> >", "gine::k_slab_reduce"],
+}
+
+
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (FETCH_SIZE x2 on
-    gfx950 + WRITE_SIZE, KB units) for this kernel, if one was collected; else None."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))):
+    """HBM bytes per call of entry point ``kernel`` from the committed rocprofv3 PMC summary
+    (profiles/*pmc_traffic.json: per-kernel (2 x FETCH_SIZE + WRITE_SIZE) bytes per launch,
+    the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md), summed over the kernels the
+    call launches; None when no summary covers them."""
+    names = PMC_KERNELS.get(kernel)
+    if not names:
+        return None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")),
+                       reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            if kernel in d:
-                return d[kernel]
         except (OSError, ValueError):
             continue
+        hits = [next((v for k, v in d.items() if k.startswith(n)), None) for n in names]
+        if all(h is not None for h in hits):
+            return {"bytes": int(sum(hits)), "source": os.path.basename(path)}
     return None
 
 

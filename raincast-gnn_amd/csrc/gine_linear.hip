@@ -13,32 +13,37 @@ namespace gine {
 namespace {
 
 // Operand source of the engine: P = dy [R, O], Q = x [R, I], plain row-major fp32.
-// Rows whose length is not a multiple of 4 floats (dim_red's input: 35 + 128 = 163) or
-// unaligned bases are read element-wise.
+// VEC: rows are whole float4s (ld % 4 == 0, 16-B aligned base); otherwise (dim_red's input
+// row is 35 + 128 = 163 floats) four scalar loads at clamped addresses, zeroed past ld.
+template <bool VEC>
 __device__ __forceinline__ float4 row_quad(const float* __restrict__ a, int64_t n, int ld,
-                                           int q, bool vec) {
+                                           int q) {
   const float* row = a + n * ld;
   const int c = 4 * q;
-  if (vec) return *reinterpret_cast<const float4*>(row + c);
-  return make_float4(c < ld ? row[c] : 0.f, c + 1 < ld ? row[c + 1] : 0.f,
-                     c + 2 < ld ? row[c + 2] : 0.f, c + 3 < ld ? row[c + 3] : 0.f);
+  if constexpr (VEC) {
+    return *reinterpret_cast<const float4*>(row + c);
+  } else {
+    const float v0 = row[min(c, ld - 1)], v1 = row[min(c + 1, ld - 1)];
+    const float v2 = row[min(c + 2, ld - 1)], v3 = row[min(c + 3, ld - 1)];
+    return make_float4(v0, c + 1 < ld ? v1 : 0.f, c + 2 < ld ? v2 : 0.f, c + 3 < ld ? v3 : 0.f);
+  }
 }
 
+template <bool VP, bool VQ>
 struct LinWgradSrc {
   const float* dy;
   const float* x;
   int O, I;
-  bool vec_p, vec_q;
   struct Raw {
     float4 v;
   };
   struct Col {};
-  __device__ Col p_col(int, int) const { return Col{}; }
-  __device__ Col q_col(int, int) const { return Col{}; }
-  __device__ Raw p_load(int, int64_t n, int q) const { return Raw{row_quad(dy, n, O, q, vec_p)}; }
-  __device__ Raw q_load(int, int64_t n, int q) const { return Raw{row_quad(x, n, I, q, vec_q)}; }
-  __device__ float4 p_xform(int, const Raw& r, const Col&) const { return r.v; }
-  __device__ float4 q_xform(int, const Raw& r, const Col&) const { return r.v; }
+  template <int Z> __device__ Col p_col(int) const { return Col{}; }
+  template <int Z> __device__ Col q_col(int) const { return Col{}; }
+  template <int Z> __device__ Raw p_load(int64_t n, int q) const { return Raw{row_quad<VP>(dy, n, O, q)}; }
+  template <int Z> __device__ Raw q_load(int64_t n, int q) const { return Raw{row_quad<VQ>(x, n, I, q)}; }
+  template <int Z> __device__ float4 p_xform(const Raw& r, const Col&) const { return r.v; }
+  template <int Z> __device__ float4 q_xform(const Raw& r, const Col&) const { return r.v; }
 };
 
 inline bool vec_ok(const float* p, int ld) {
@@ -98,8 +103,21 @@ extern "C" int gine_linear_wgrad(const float* dy, const float* x, int64_t rows,
   if (rows == 0) {
     GINE_RETURN_IF_HIP(hipMemsetAsync(slab, 0, sizeof(float) * per, s));
   } else {
-    const LinWgradSrc src{dy, x, O, I, vec_ok(dy, O), vec_ok(x, I)};
-    const int st = launch_wgrad_engine(src, rows, O, I, 1, p, 0, (size_t)per, slab, s);
+    const bool vp = vec_ok(dy, O), vq = vec_ok(x, I);
+    int st;
+    if (vp && vq) {
+      st = launch_wgrad_engine(LinWgradSrc<true, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
+                               (size_t)per, slab, s);
+    } else if (vp) {
+      st = launch_wgrad_engine(LinWgradSrc<true, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
+                               (size_t)per, slab, s);
+    } else if (vq) {
+      st = launch_wgrad_engine(LinWgradSrc<false, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
+                               (size_t)per, slab, s);
+    } else {
+      st = launch_wgrad_engine(LinWgradSrc<false, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
+                               (size_t)per, slab, s);
+    }
     if (st != GINE_OK) return st;
   }
   hipLaunchKernelGGL(k_linear_slab_reduce, dim3((unsigned)ceil_div(per, 64)), dim3(256), 0, s,

@@ -40,8 +40,15 @@ __device__ __forceinline__ floatx16 zero16() {
 
 constexpr int kRowTile = 32;
 
-enum Pro { PRO_PLAIN = 0, PRO_BNRELU = 1, PRO_DO = 2, PRO_DA1 = 3 };
-enum Epi { EPI_A1STATS = 0, EPI_OUT = 1, EPI_DBN = 2, EPI_PLAIN = 3 };
+// Compile-time variants only: a runtime branch between loads makes the compiler drain the
+// memory queue (s_waitcnt vmcnt(0)) at the merge, serialising what should be in flight.
+//   PRO_DOR: do = dy * 1[y > 0]  (ReLU epilogue)     PRO_DOM: do = dy * mask (residual)
+//   (no epilogue: do = dy, PRO_PLAIN)
+enum Pro { PRO_PLAIN = 0, PRO_BNRELU = 1, PRO_DA1 = 3, PRO_DOR = 4, PRO_DOM = 5 };
+//   EPI_OUT / EPI_OUT_RELU / EPI_OUT_RES: y = o | relu(o) | x + relu(o) (+ mask)
+enum Epi { EPI_A1STATS = 0, EPI_OUT = 1, EPI_DBN = 2, EPI_PLAIN = 3, EPI_OUT_RELU = 4,
+           EPI_OUT_RES = 5 };
+
 
 // bn_save layout: [mean | invstd | alpha | shift], each [D]
 struct BnView {
@@ -56,11 +63,10 @@ __device__ __forceinline__ BnView bn_view(const float* s, int D) {
 
 struct ProArgs {
   const float* x;        // primary [N][D]: z | a1 | dy | dbn
-  const float* aux;      // a1 for PRO_DA1; y for PRO_DO with the ReLU epilogue
-  const uint8_t* mask;   // PRO_DO, residual epilogue
+  const float* aux;      // a1 for PRO_DA1; y for PRO_DOR
+  const uint8_t* mask;   // PRO_DOM
   const float* bn;       // bn_save
   const float* coef;     // [c1 | c2 | c3] (PRO_DA1)
-  int epi;               // GINE_EPI_* of the forward output (PRO_DO)
 };
 
 // Same rounding sequence wherever bn is recomputed (forward GEMM2 prologue, backward
@@ -82,16 +88,13 @@ __device__ __forceinline__ float4 prologue(const ProArgs& p, int D, int64_t n, i
     const float4 sh = *reinterpret_cast<const float4*>(b.shift + 4 * q);
     return make_float4(relu_nan(bn_apply(v.x, al.x, sh.x)), relu_nan(bn_apply(v.y, al.y, sh.y)),
                        relu_nan(bn_apply(v.z, al.z, sh.z)), relu_nan(bn_apply(v.w, al.w, sh.w)));
-  } else if constexpr (PRO == PRO_DO) {
-    if (p.epi == GINE_EPI_RELU) {
-      const float4 y = *reinterpret_cast<const float4*>(p.aux + off);
-      return make_float4(y.x > 0.f ? v.x : 0.f, y.y > 0.f ? v.y : 0.f, y.z > 0.f ? v.z : 0.f,
-                         y.w > 0.f ? v.w : 0.f);
-    } else if (p.epi == GINE_EPI_RESIDUAL_RELU) {
-      const uchar4 m = *reinterpret_cast<const uchar4*>(p.mask + off);
-      return make_float4(m.x ? v.x : 0.f, m.y ? v.y : 0.f, m.z ? v.z : 0.f, m.w ? v.w : 0.f);
-    }
-    return v;
+  } else if constexpr (PRO == PRO_DOR) {
+    const float4 y = *reinterpret_cast<const float4*>(p.aux + off);
+    return make_float4(y.x > 0.f ? v.x : 0.f, y.y > 0.f ? v.y : 0.f, y.z > 0.f ? v.z : 0.f,
+                       y.w > 0.f ? v.w : 0.f);
+  } else if constexpr (PRO == PRO_DOM) {
+    const uchar4 m = *reinterpret_cast<const uchar4*>(p.mask + off);
+    return make_float4(m.x ? v.x : 0.f, m.y ? v.y : 0.f, m.z ? v.z : 0.f, m.w ? v.w : 0.f);
   } else {  // PRO_DA1: da1 = c1*dbn + c2*xhat + c3, xhat = (a1 - mean)*invstd
     const BnView b = bn_view(p.bn, D);
     const float4 a1 = *reinterpret_cast<const float4*>(p.aux + off);
@@ -141,8 +144,8 @@ __device__ __forceinline__ TileRange xcd_tile_range(int num_tiles) {
 // Raw (pre-prologue) values of one staged float4 item, loaded a tile ahead.
 struct RawItem {
   float4 v;    // primary input
-  float4 aux;  // y (PRO_DO, ReLU epilogue) | a1 (PRO_DA1)
-  uchar4 m;    // ReLU mask (PRO_DO, residual epilogue)
+  float4 aux;  // y (PRO_DOR) | a1 (PRO_DA1)
+  uchar4 m;    // ReLU mask (PRO_DOM)
 };
 
 // Per-thread column constants of the prologue (a thread always stages the same column
@@ -177,9 +180,10 @@ __device__ __forceinline__ RawItem raw_load(const ProArgs& p, int D, int64_t n, 
   r.v = *reinterpret_cast<const float4*>(p.x + off);
   r.aux = f4_zero();
   r.m = make_uchar4(1, 1, 1, 1);
-  if constexpr (PRO == PRO_DO) {
-    if (p.epi == GINE_EPI_RELU) r.aux = *reinterpret_cast<const float4*>(p.aux + off);
-    if (p.epi == GINE_EPI_RESIDUAL_RELU) r.m = *reinterpret_cast<const uchar4*>(p.mask + off);
+  if constexpr (PRO == PRO_DOR) {
+    r.aux = *reinterpret_cast<const float4*>(p.aux + off);
+  } else if constexpr (PRO == PRO_DOM) {
+    r.m = *reinterpret_cast<const uchar4*>(p.mask + off);
   } else if constexpr (PRO == PRO_DA1) {
     r.aux = *reinterpret_cast<const float4*>(p.aux + off);
   }
@@ -196,16 +200,13 @@ __device__ __forceinline__ float4 transform(const ProArgs& p, const RawItem& r,
   } else if constexpr (PRO == PRO_BNRELU) {
     return make_float4(relu_nan(bn_apply(v.x, k.a.x, k.b.x)), relu_nan(bn_apply(v.y, k.a.y, k.b.y)),
                        relu_nan(bn_apply(v.z, k.a.z, k.b.z)), relu_nan(bn_apply(v.w, k.a.w, k.b.w)));
-  } else if constexpr (PRO == PRO_DO) {
-    if (p.epi == GINE_EPI_RELU) {
-      const float4 y = r.aux;
-      return make_float4(y.x > 0.f ? v.x : 0.f, y.y > 0.f ? v.y : 0.f, y.z > 0.f ? v.z : 0.f,
-                         y.w > 0.f ? v.w : 0.f);
-    } else if (p.epi == GINE_EPI_RESIDUAL_RELU) {
-      const uchar4 m = r.m;
-      return make_float4(m.x ? v.x : 0.f, m.y ? v.y : 0.f, m.z ? v.z : 0.f, m.w ? v.w : 0.f);
-    }
-    return v;
+  } else if constexpr (PRO == PRO_DOR) {
+    const float4 y = r.aux;
+    return make_float4(y.x > 0.f ? v.x : 0.f, y.y > 0.f ? v.y : 0.f, y.z > 0.f ? v.z : 0.f,
+                       y.w > 0.f ? v.w : 0.f);
+  } else if constexpr (PRO == PRO_DOM) {
+    const uchar4 m = r.m;
+    return make_float4(m.x ? v.x : 0.f, m.y ? v.y : 0.f, m.z ? v.z : 0.f, m.w ? v.w : 0.f);
   } else {  // PRO_DA1
     const float4 a1 = r.aux;
     float4 o;
@@ -235,7 +236,8 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
   constexpr int D4 = D / 4;
   constexpr int ITEMS = kRowTile * D4 / NT;  // float4 staged per thread (= 4)
   constexpr int RSTEP = NT / D4;             // row step between a thread's items (= 8)
-  constexpr bool EPI_LOAD = (EPI == EPI_DBN) || (EPI == EPI_OUT);
+  constexpr bool IS_OUT = (EPI == EPI_OUT) || (EPI == EPI_OUT_RELU) || (EPI == EPI_OUT_RES);
+  constexpr bool EPI_LOAD = (EPI == EPI_DBN) || (EPI == EPI_OUT_RES);
   __shared__ __attribute__((aligned(16))) float s_x[kRowTile * LD];
 
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
   const ColConst kc = col_const<PRO>(pa, D, q_me);
 
   float bias = 0.f;
-  if constexpr (EPI == EPI_A1STATS || EPI == EPI_OUT) bias = ea.bias[col];
+  if constexpr (EPI == EPI_A1STATS || IS_OUT) bias = ea.bias[col];
   float alpha = 0.f, shift = 0.f, mean = 0.f, invstd = 0.f;
   if constexpr (EPI == EPI_DBN) {
     const BnView b = bn_view(ea.bn, D);
@@ -270,7 +272,6 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
     mean = b.mean[col];
     invstd = b.invstd[col];
   }
-  const bool resid = (EPI == EPI_OUT) && ea.mode == GINE_EPI_RESIDUAL_RELU;
   double st1 = 0.0, st2 = 0.0;
 
   auto load_tile = [&](int tile, RawItem (&raw)[ITEMS]) {
@@ -304,7 +305,7 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
         int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         n = n < N ? n : N - 1;
         if constexpr (EPI == EPI_DBN) ep[r] = ea.a1[n * D + col];
-        else ep[r] = resid ? ea.resid[n * D + col] : 0.f;
+        else ep[r] = ea.resid[n * D + col];
       }
     }
     floatx16 acc = zero16();
@@ -329,12 +330,12 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
         ea.out[off] = a1;
         st1 += (double)a1;
         st2 += (double)a1 * (double)a1;
-      } else if constexpr (EPI == EPI_OUT) {
+      } else if constexpr (IS_OUT) {
         const float o = v + bias;
         float y;
-        if (ea.mode == GINE_EPI_NONE) {
+        if constexpr (EPI == EPI_OUT) {
           y = o;
-        } else if (ea.mode == GINE_EPI_RELU) {
+        } else if constexpr (EPI == EPI_OUT_RELU) {
           y = relu_nan(o);
         } else {
           y = ep[r] + relu_nan(o);
@@ -477,28 +478,35 @@ __global__ __launch_bounds__(kColsumThreads) void k_bn_bwd_finalize(
 //   z = 1: P = da1 (PRO_DA1 of dbn), Q = z               -> dW1, db1
 // on the shared engine (gine_wgrad.hpp); this is its operand source.
 // ----------------------------------------------------------------------------------------
+template <int PDO>  // PRO_PLAIN | PRO_DOR | PRO_DOM: how do is formed from dy
 struct MlpWgradSrc {
   ProArgs p_do, q_r, p_da1, q_z;
   int D;
   using Raw = RawItem;
   using Col = ColConst;
-  __device__ Col p_col(int z, int q) const {
-    return z == 0 ? col_const<PRO_DO>(p_do, D, q) : col_const<PRO_DA1>(p_da1, D, q);
+  template <int Z> __device__ Col p_col(int q) const {
+    if constexpr (Z == 0) return col_const<PDO>(p_do, D, q);
+    else return col_const<PRO_DA1>(p_da1, D, q);
   }
-  __device__ Col q_col(int z, int q) const {
-    return z == 0 ? col_const<PRO_BNRELU>(q_r, D, q) : col_const<PRO_PLAIN>(q_z, D, q);
+  template <int Z> __device__ Col q_col(int q) const {
+    if constexpr (Z == 0) return col_const<PRO_BNRELU>(q_r, D, q);
+    else return col_const<PRO_PLAIN>(q_z, D, q);
   }
-  __device__ Raw p_load(int z, int64_t n, int q) const {
-    return z == 0 ? raw_load<PRO_DO>(p_do, D, n, q) : raw_load<PRO_DA1>(p_da1, D, n, q);
+  template <int Z> __device__ Raw p_load(int64_t n, int q) const {
+    if constexpr (Z == 0) return raw_load<PDO>(p_do, D, n, q);
+    else return raw_load<PRO_DA1>(p_da1, D, n, q);
   }
-  __device__ Raw q_load(int z, int64_t n, int q) const {
-    return z == 0 ? raw_load<PRO_BNRELU>(q_r, D, n, q) : raw_load<PRO_PLAIN>(q_z, D, n, q);
+  template <int Z> __device__ Raw q_load(int64_t n, int q) const {
+    if constexpr (Z == 0) return raw_load<PRO_BNRELU>(q_r, D, n, q);
+    else return raw_load<PRO_PLAIN>(q_z, D, n, q);
   }
-  __device__ float4 p_xform(int z, const Raw& r, const Col& c) const {
-    return z == 0 ? transform<PRO_DO>(p_do, r, c) : transform<PRO_DA1>(p_da1, r, c);
+  template <int Z> __device__ float4 p_xform(const Raw& r, const Col& c) const {
+    if constexpr (Z == 0) return transform<PDO>(p_do, r, c);
+    else return transform<PRO_DA1>(p_da1, r, c);
   }
-  __device__ float4 q_xform(int z, const Raw& r, const Col& c) const {
-    return z == 0 ? transform<PRO_BNRELU>(q_r, r, c) : transform<PRO_PLAIN>(q_z, r, c);
+  template <int Z> __device__ float4 q_xform(const Raw& r, const Col& c) const {
+    if constexpr (Z == 0) return transform<PRO_BNRELU>(q_r, r, c);
+    else return transform<PRO_PLAIN>(q_z, r, c);
   }
 };
 
@@ -557,7 +565,7 @@ extern "C" int gine_mlp_fwd1(const float* z, const float* w1, const float* b1, f
   if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
   if (num_nodes <= 0 || !z || !w1 || !b1 || !a1 || !partials) return GINE_ERR_INVALID;
   if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
-  ProArgs pa{z, nullptr, nullptr, nullptr, nullptr, 0};
+  ProArgs pa{z, nullptr, nullptr, nullptr, nullptr};
   EpiArgs ea{b1, a1, nullptr, nullptr, nullptr, nullptr, partials, 0};
   return launch_rowgemm<PRO_PLAIN, EPI_A1STATS, true>(channels, w1, pa, ea, num_nodes,
                                                       as_stream(stream));
@@ -596,10 +604,17 @@ extern "C" int gine_mlp_fwd2(const float* a1, const float* bn_save, const float*
   if (num_nodes <= 0 || !a1 || !bn_save || !w2 || !b2 || !y) return GINE_ERR_INVALID;
   if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RESIDUAL_RELU && (!x || !mask)) return GINE_ERR_INVALID;
-  ProArgs pa{a1, nullptr, nullptr, bn_save, nullptr, 0};
+  ProArgs pa{a1, nullptr, nullptr, bn_save, nullptr};
   EpiArgs ea{b2, y, mask, x, nullptr, nullptr, nullptr, epilogue};
-  return launch_rowgemm<PRO_BNRELU, EPI_OUT, true>(channels, w2, pa, ea, num_nodes,
-                                                   as_stream(stream));
+  hipStream_t s = as_stream(stream);
+  switch (epilogue) {
+    case GINE_EPI_NONE:
+      return launch_rowgemm<PRO_BNRELU, EPI_OUT, true>(channels, w2, pa, ea, num_nodes, s);
+    case GINE_EPI_RELU:
+      return launch_rowgemm<PRO_BNRELU, EPI_OUT_RELU, true>(channels, w2, pa, ea, num_nodes, s);
+    default:
+      return launch_rowgemm<PRO_BNRELU, EPI_OUT_RES, true>(channels, w2, pa, ea, num_nodes, s);
+  }
 }
 
 extern "C" int gine_mlp_bwd2(const float* dy, const float* y, const uint8_t* mask,
@@ -611,10 +626,17 @@ extern "C" int gine_mlp_bwd2(const float* dy, const float* y, const uint8_t* mas
     return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
-  ProArgs pa{dy, y, mask, nullptr, nullptr, epilogue};
+  ProArgs pa{dy, y, mask, nullptr, nullptr};
   EpiArgs ea{nullptr, dbn, nullptr, nullptr, a1, bn_save, partials, 0};
-  return launch_rowgemm<PRO_DO, EPI_DBN, false>(channels, w2, pa, ea, num_nodes,
-                                                as_stream(stream));
+  hipStream_t s = as_stream(stream);
+  switch (epilogue) {
+    case GINE_EPI_NONE:
+      return launch_rowgemm<PRO_PLAIN, EPI_DBN, false>(channels, w2, pa, ea, num_nodes, s);
+    case GINE_EPI_RELU:
+      return launch_rowgemm<PRO_DOR, EPI_DBN, false>(channels, w2, pa, ea, num_nodes, s);
+    default:
+      return launch_rowgemm<PRO_DOM, EPI_DBN, false>(channels, w2, pa, ea, num_nodes, s);
+  }
 }
 
 extern "C" int gine_bn_bwd_finalize(const double* partials, int32_t num_partials,
@@ -641,7 +663,7 @@ extern "C" int gine_mlp_bwd1(const float* dbn, const float* a1, const float* bn_
   if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
   if (num_nodes <= 0 || !dbn || !a1 || !bn_save || !coef || !w1 || !dz)
     return GINE_ERR_INVALID;
-  ProArgs pa{dbn, a1, nullptr, bn_save, coef, 0};
+  ProArgs pa{dbn, a1, nullptr, bn_save, coef};
   EpiArgs ea{nullptr, dz, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   return launch_rowgemm<PRO_DA1, EPI_PLAIN, false>(channels, w1, pa, ea, num_nodes,
                                                    as_stream(stream));
@@ -666,16 +688,24 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
   const int D = channels;
-  MlpWgradSrc src;
-  src.p_do = ProArgs{dy, y, mask, nullptr, nullptr, epilogue};
-  src.q_r = ProArgs{a1, nullptr, nullptr, bn_save, nullptr, 0};
-  src.p_da1 = ProArgs{dbn, a1, nullptr, bn_save, coef, 0};
-  src.q_z = ProArgs{z, nullptr, nullptr, nullptr, nullptr, 0};
-  src.D = D;
+  const ProArgs p_do{dy, y, mask, nullptr, nullptr};
+  const ProArgs q_r{a1, nullptr, nullptr, bn_save, nullptr};
+  const ProArgs p_da1{dbn, a1, nullptr, bn_save, coef};
+  const ProArgs q_z{z, nullptr, nullptr, nullptr, nullptr};
   const WgPlan p = mlp_wgrad_plan(num_nodes, D);
   const size_t per = (size_t)D * D + D;
   hipStream_t s = as_stream(stream);
-  const int st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+  int st;
+  if (epilogue == GINE_EPI_NONE) {
+    const MlpWgradSrc<PRO_PLAIN> src{p_do, q_r, p_da1, q_z, D};
+    st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+  } else if (epilogue == GINE_EPI_RELU) {
+    const MlpWgradSrc<PRO_DOR> src{p_do, q_r, p_da1, q_z, D};
+    st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+  } else {
+    const MlpWgradSrc<PRO_DOM> src{p_do, q_r, p_da1, q_z, D};
+    st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+  }
   if (st != GINE_OK) return st;
   const int total = 2 * (D * D + D);
   hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)ceil_div(total, 64)), dim3(256), 0, s, slab,

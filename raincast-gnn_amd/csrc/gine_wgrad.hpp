@@ -53,34 +53,35 @@ inline WgPlan wg_plan(int64_t R, int O, int I, int Z) {
   return p;
 }
 
-// Src policy (see the users in gine_mlp.hip / gine_linear.hip):
+// Src policy (see the users in gine_mlp.hip / gine_linear.hip); every member is a
+// template on the product index Z, so each body is free of runtime branches between loads
+// (a branch merge makes the compiler drain the memory queue, serialising the prefetch):
 //   typename Src::Raw, Src::Col
-//   Col p_col(z, q4) / q_col(z, q4)          per-column constants (q4 = float4 column)
-//   Raw p_load(z, n, q4) / q_load(z, n, q4)  raw operands of row n (n always in range)
-//   float4 p_xform(z, raw, col) / q_xform    the staged value
-template <class Src>
-__global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O, int I,
-                                                      int rows_per_chunk, int tiles_i,
-                                                      size_t zstride, size_t cstride,
-                                                      float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float sP[kWgRows * kWgLdP];
-  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
+//   Col p_col<Z>(q4) / q_col<Z>(q4)          per-column constants (q4 = float4 column)
+//   Raw p_load<Z>(n, q4) / q_load<Z>(n, q4)  raw operands of row n (n always in range)
+//   float4 p_xform<Z>(raw, col) / q_xform<Z> the staged value
+template <class Src, int Z>
+__device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int I,
+                                           int rows_per_chunk, int tiles_i, size_t zstride,
+                                           size_t cstride, float* __restrict__ slab,
+                                           float* __restrict__ sP, float* __restrict__ sQ) {
   using Raw = typename Src::Raw;
   using Col = typename Src::Col;
 
-  const int chunk = blockIdx.x, z = blockIdx.z;
+  const int chunk = blockIdx.x;
   const int o0 = (blockIdx.y / tiles_i) * kWgTO, i0 = (blockIdx.y % tiles_i) * kWgTI;
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
-  const bool bias_wave = (i0 == 0) && (wave == 0);
+  const bool bias_block = (i0 == 0);
 
   // staging coordinates: a thread always stages the same float4 column of P and of Q
   const int pq = threadIdx.x % (kWgTO / 4), pr = threadIdx.x / (kWgTO / 4);  // rows pr+16k
   const int qq = threadIdx.x % (kWgTI / 4), qr = threadIdx.x / (kWgTI / 4);  // rows qr+8k
   const bool p_ok = o0 + 4 * pq < O, q_ok = i0 + 4 * qq < I;
   const int pqa = p_ok ? o0 / 4 + pq : 0, qqa = q_ok ? i0 / 4 + qq : 0;
-  const Col pc = src.p_col(z, pqa);
-  const Col qc = src.q_col(z, qqa);
+  const Col pc = src.template p_col<Z>(pqa);
+  const Col qc = src.template q_col<Z>(qqa);
 
   const int64_t r_begin = (int64_t)chunk * rows_per_chunk;
   const int64_t r_end = min<int64_t>(R, r_begin + rows_per_chunk);
@@ -88,19 +89,19 @@ __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O,
   wg_floatx16 acc0, acc1;
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc0[k] = acc1[k] = 0.f;
-  double bs0 = 0.0, bs1 = 0.0;
+  double bsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias partials of this thread's P column quad
 
   Raw rp[kWgPItems], rq[kWgQItems];
   auto load = [&](int64_t n0) {
 #pragma unroll
     for (int k = 0; k < kWgPItems; ++k) {
       const int64_t n = n0 + pr + 16 * k;
-      rp[k] = src.p_load(z, n < r_end ? n : r_end - 1, pqa);
+      rp[k] = src.template p_load<Z>(n < r_end ? n : r_end - 1, pqa);
     }
 #pragma unroll
     for (int k = 0; k < kWgQItems; ++k) {
       const int64_t n = n0 + qr + 8 * k;
-      rq[k] = src.q_load(z, n < r_end ? n : r_end - 1, qqa);
+      rq[k] = src.template q_load<Z>(n < r_end ? n : r_end - 1, qqa);
     }
   };
 
@@ -109,14 +110,18 @@ __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O,
 #pragma unroll
     for (int k = 0; k < kWgPItems; ++k) {
       const int r = pr + 16 * k;
-      float4 v = src.p_xform(z, rp[k], pc);
+      float4 v = src.template p_xform<Z>(rp[k], pc);
       if (n0 + r >= r_end || !p_ok) v = f4_zero();
       *reinterpret_cast<float4*>(&sP[r * kWgLdP + 4 * pq]) = v;
+      bsum[0] += (double)v.x;
+      bsum[1] += (double)v.y;
+      bsum[2] += (double)v.z;
+      bsum[3] += (double)v.w;
     }
 #pragma unroll
     for (int k = 0; k < kWgQItems; ++k) {
       const int r = qr + 8 * k;
-      float4 v = src.q_xform(z, rq[k], qc);
+      float4 v = src.template q_xform<Z>(rq[k], qc);
       if (n0 + r >= r_end || !q_ok) v = f4_zero();
       *reinterpret_cast<float4*>(&sQ[r * kWgLdQ + 4 * qq]) = v;
     }
@@ -132,15 +137,11 @@ __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O,
       const float b = qb[s * kWgLdQ];
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc1, 0, 0, 0);
-      if (bias_wave) {
-        bs0 += (double)a0;
-        bs1 += (double)a1;
-      }
     }
     __syncthreads();
   }
 
-  float* out = slab + (size_t)z * zstride + (size_t)chunk * cstride;
+  float* out = slab + (size_t)Z * zstride + (size_t)chunk * cstride;
   const int i = i0 + 32 * wave + c32;
   if (i < I) {
 #pragma unroll
@@ -150,15 +151,30 @@ __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O,
       if (o + 32 < O) out[(size_t)(o + 32) * I + i] = acc1[r];
     }
   }
-  if (bias_wave) {
-    bs0 += shfl_xor_d(bs0, 32);
-    bs1 += shfl_xor_d(bs1, 32);
-    if (h == 0) {
-      float* ob = out + (size_t)O * I;
-      if (o0 + c32 < O) ob[o0 + c32] = (float)bs0;
-      if (o0 + 32 + c32 < O) ob[o0 + 32 + c32] = (float)bs1;
+  if (bias_block) {  // fixed-order sum of the 16 row groups' partials through LDS
+    double* sb = reinterpret_cast<double*>(sQ);  // [16][64], sQ is free after the loop
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sb[pr * kWgTO + 4 * pq + j] = bsum[j];
+    __syncthreads();
+    if (threadIdx.x < kWgTO && o0 + (int)threadIdx.x < O) {
+      double t = 0.0;
+      for (int g = 0; g < 256 / (kWgTO / 4); ++g) t += sb[g * kWgTO + threadIdx.x];
+      out[(size_t)O * I + o0 + threadIdx.x] = (float)t;
     }
   }
+}
+
+template <class Src>
+__global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O, int I,
+                                                      int rows_per_chunk, int tiles_i,
+                                                      size_t zstride, size_t cstride,
+                                                      float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float sP[kWgRows * kWgLdP];
+  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
+  if (blockIdx.z == 0)
+    wgrad_body<Src, 0>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP, sQ);
+  else
+    wgrad_body<Src, 1>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP, sQ);
 }
 
 template <class Src>
