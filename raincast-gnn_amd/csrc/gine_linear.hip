@@ -7,6 +7,7 @@
 // gine_wgrad.hpp splits the ROWS (the contraction) instead, with fp32 partial slabs reduced
 // over chunks in fixed order in fp64 (deterministic).
 #include "gine_common.hpp"
+#include "gine_slab.hpp"
 #include "gine_wgrad.hpp"
 
 namespace gine {
@@ -50,32 +51,16 @@ inline bool vec_ok(const float* p, int ld) {
   return ld % 4 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
 }
 
-// 64 consecutive slab elements x 4 chunk groups per workgroup (fixed order, see gine_mlp).
-__global__ __launch_bounds__(256) void k_linear_slab_reduce(const float* __restrict__ slab,
-                                                            int chunks, int64_t per,
-                                                            int64_t wsize,
-                                                            float* __restrict__ dw,
-                                                            float* __restrict__ db,
-                                                            float bias_scale) {
-  __shared__ double s_part[4][64];
-  const int64_t e = blockIdx.x * (int64_t)64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
-  double acc = 0.0;
-  if (e < per) {
-    const float* base = slab + e;
-    for (int c = g; c < chunks; c += 4) acc += (double)base[(size_t)c * per];
+struct LinWgradOut {
+  float* dw;
+  float* db;
+  int64_t wsize;
+  float bias_scale;
+  __device__ void operator()(int, int64_t e, double v) const {
+    if (e < wsize) dw[e] = (float)v;
+    else if (db) db[e - wsize] = (float)(v * (double)bias_scale);
   }
-  s_part[g][threadIdx.x & 63] = acc;
-  __syncthreads();
-  if (g != 0 || e >= per) return;
-  const int j = threadIdx.x & 63;
-  const double v = (s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]);
-  if (e < wsize) {
-    dw[e] = (float)v;
-  } else if (db != nullptr) {
-    db[e - wsize] = (float)(v * (double)bias_scale);
-  }
-}
+};
 
 }  // namespace
 }  // namespace gine
@@ -86,7 +71,7 @@ extern "C" int gine_linear_wgrad_num_chunks(int64_t rows, int32_t out_features,
                                             int32_t in_features, int32_t* num_chunks) {
   if (!num_chunks || rows < 0 || out_features <= 0 || in_features <= 0)
     return GINE_ERR_INVALID;
-  *num_chunks = wg_plan(rows, out_features, in_features, 1).chunks;
+  *num_chunks = wg_plan(rows, out_features, in_features, 1, 64).chunks;
   return GINE_OK;
 }
 
@@ -97,7 +82,7 @@ extern "C" int gine_linear_wgrad(const float* dy, const float* x, int64_t rows,
     return GINE_ERR_INVALID;
   if (rows > 0 && (!dy || !x)) return GINE_ERR_INVALID;
   const int O = out_features, I = in_features;
-  const WgPlan p = wg_plan(rows, O, I, 1);
+  const WgPlan p = wg_plan(rows, O, I, 1, 64);
   hipStream_t s = as_stream(stream);
   const int64_t per = (int64_t)O * I + O;
   if (rows == 0) {
@@ -106,22 +91,20 @@ extern "C" int gine_linear_wgrad(const float* dy, const float* x, int64_t rows,
     const bool vp = vec_ok(dy, O), vq = vec_ok(x, I);
     int st;
     if (vp && vq) {
-      st = launch_wgrad_engine(LinWgradSrc<true, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<true, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
                                (size_t)per, slab, s);
     } else if (vp) {
-      st = launch_wgrad_engine(LinWgradSrc<true, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<true, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
                                (size_t)per, slab, s);
     } else if (vq) {
-      st = launch_wgrad_engine(LinWgradSrc<false, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<false, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
                                (size_t)per, slab, s);
     } else {
-      st = launch_wgrad_engine(LinWgradSrc<false, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<false, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
                                (size_t)per, slab, s);
     }
     if (st != GINE_OK) return st;
   }
-  hipLaunchKernelGGL(k_linear_slab_reduce, dim3((unsigned)ceil_div(per, 64)), dim3(256), 0, s,
-                     slab, rows == 0 ? 1 : p.chunks, per, (int64_t)O * I, dw, db, bias_scale);
-  GINE_LAUNCH_STATUS();
-  return GINE_OK;
+  return launch_slab_sum(slab, rows == 0 ? 1 : p.chunks, per, (size_t)per, 0, 1,
+                         LinWgradOut{dw, db, (int64_t)O * I, bias_scale}, s);
 }

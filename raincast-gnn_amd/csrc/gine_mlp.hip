@@ -19,9 +19,10 @@
 //
 // Weight gradients (K = N rows) run on the shared engine of gine_wgrad.hpp (64x128 output
 // tiles x row chunks, fp32 partial slabs) and are reduced in fixed chunk order in fp64 by
-// k_slab_reduce -> deterministic.
+// k_slab_sum (gine_slab.hpp) -> deterministic.
 #include "gine_common.hpp"
 #include "gine_reduce.hpp"
+#include "gine_slab.hpp"
 #include "gine_wgrad.hpp"
 
 #include <algorithm>
@@ -510,41 +511,24 @@ struct MlpWgradSrc {
   }
 };
 
-// Sum the chunk slabs: workgroup = 64 consecutive elements x 4 chunk groups (chunk c goes
-// to group c % 4, summed in chunk order), groups combined in fixed order through LDS.
-__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int chunks,
-                                                     int D, float* __restrict__ dw2,
-                                                     float* __restrict__ db2,
-                                                     float* __restrict__ dw1,
-                                                     float* __restrict__ db1) {
-  __shared__ double s_part[4][64];
-  const int per = D * D + D;
-  const int e = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
-  double acc = 0.0;
-  if (e < 2 * per) {
-    const int zsel = e / per, r = e % per;
-    const float* base = slab + (size_t)zsel * chunks * per + r;
-    for (int c = g; c < chunks; c += 4) acc += (double)base[(size_t)c * per];
+// Destination of the reduced slabs: z = 0 -> dW2 | db2, z = 1 -> dW1 | db1.
+struct MlpWgradOut {
+  float *dw2, *db2, *dw1, *db1;
+  int D;
+  __device__ void operator()(int z, int64_t e, double v) const {
+    float* w = z == 0 ? dw2 : dw1;
+    float* b = z == 0 ? db2 : db1;
+    if (e < (int64_t)D * D) {
+      if (w) w[e] = (float)v;
+    } else if (b) {
+      b[e - (int64_t)D * D] = (float)v;
+    }
   }
-  s_part[g][threadIdx.x & 63] = acc;
-  __syncthreads();
-  if (g != 0 || e >= 2 * per) return;
-  const int j = threadIdx.x & 63;
-  const float v = (float)((s_part[0][j] + s_part[1][j]) + (s_part[2][j] + s_part[3][j]));
-  const int zsel = e / per, r = e % per;
-  float* w = zsel == 0 ? dw2 : dw1;
-  float* b = zsel == 0 ? db2 : db1;
-  if (r < D * D) {
-    if (w) w[r] = v;
-  } else {
-    if (b) b[r - D * D] = v;
-  }
-}
+};
 
 inline bool mlp_dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
-inline WgPlan mlp_wgrad_plan(int64_t N, int D) { return wg_plan(N, D, D, 2); }
+inline WgPlan mlp_wgrad_plan(int64_t N, int D) { return wg_plan(N, D, D, 2, 64); }
 
 }  // namespace
 }  // namespace gine
@@ -698,18 +682,16 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   int st;
   if (epilogue == GINE_EPI_NONE) {
     const MlpWgradSrc<PRO_PLAIN> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
   } else if (epilogue == GINE_EPI_RELU) {
     const MlpWgradSrc<PRO_DOR> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
   } else {
     const MlpWgradSrc<PRO_DOM> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
   }
   if (st != GINE_OK) return st;
-  const int total = 2 * (D * D + D);
-  hipLaunchKernelGGL(k_slab_reduce, dim3((unsigned)ceil_div(total, 64)), dim3(256), 0, s, slab,
-                     p.chunks, D, dw2, db2, dw1, db1);
-  GINE_LAUNCH_STATUS();
-  return GINE_OK;
+  if (st != GINE_OK) return st;
+  return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 2,
+                         MlpWgradOut{dw2, db2, dw1, db1, D}, s);
 }

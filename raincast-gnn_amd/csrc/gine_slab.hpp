@@ -1,0 +1,82 @@
+// Fixed-order reduction of split-K partial slabs (deterministic, no float atomics).
+//
+// Split-row weight-gradient kernels (gine_wgrad.hpp, gine_deepset.hip) leave Z products x
+// C chunks of fp32 partials: slab[z * zstride + c * cstride + e], e < per.  out(z, e, v)
+// receives sum_c partial in fp64, summed in chunk order within each of kSlabGroups
+// interleaved chunk groups and then over the groups in group order -- a function of the
+// shapes only, so a rerun is bit-identical.  A workgroup covers 32 float4 quads (128
+// elements) x 8 chunk groups; loads are 16-byte and independent (four per loop trip).
+#pragma once
+
+#include "gine_common.hpp"
+
+namespace gine {
+
+constexpr int kSlabQuads = 32;   // float4 quads per workgroup
+constexpr int kSlabGroups = 8;   // interleaved chunk groups per workgroup
+
+template <bool VEC, class Out>
+__global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab, int chunks,
+                                                  int64_t per, size_t cstride, size_t zstride,
+                                                  Out out) {
+  __shared__ double s_part[kSlabGroups][kSlabQuads * 4 + 1];
+  const int q = threadIdx.x % kSlabQuads, g = threadIdx.x / kSlabQuads;
+  const int z = blockIdx.y;
+  const int64_t e0 = ((int64_t)blockIdx.x * kSlabQuads + q) * 4;
+  const float* base = slab + (size_t)z * zstride;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (e0 < per) {
+    if constexpr (VEC) {
+#pragma unroll 4
+      for (int c = g; c < chunks; c += kSlabGroups) {
+        const float4 v = *reinterpret_cast<const float4*>(base + (size_t)c * cstride + e0);
+        a0 += (double)v.x;
+        a1 += (double)v.y;
+        a2 += (double)v.z;
+        a3 += (double)v.w;
+      }
+    } else {
+      const int64_t last = per - 1;
+#pragma unroll 4
+      for (int c = g; c < chunks; c += kSlabGroups) {
+        const float* r = base + (size_t)c * cstride;
+        a0 += (double)r[e0];
+        a1 += (double)r[min(e0 + 1, last)];
+        a2 += (double)r[min(e0 + 2, last)];
+        a3 += (double)r[min(e0 + 3, last)];
+      }
+    }
+  }
+  double* sp = &s_part[g][4 * q];
+  sp[0] = a0;
+  sp[1] = a1;
+  sp[2] = a2;
+  sp[3] = a3;
+  __syncthreads();
+  if (threadIdx.x >= kSlabQuads * 4) return;
+  const int j = threadIdx.x;
+  const int64_t e = (int64_t)blockIdx.x * kSlabQuads * 4 + j;
+  if (e >= per) return;
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < kSlabGroups; ++k) v += s_part[k][j];
+  out(z, e, v);
+}
+
+template <class Out>
+inline int launch_slab_sum(const float* slab, int chunks, int64_t per, size_t cstride,
+                           size_t zstride, int Z, const Out& out, hipStream_t s) {
+  const dim3 grid((unsigned)ceil_div(per, kSlabQuads * 4), Z);
+  const bool vec = per % 4 == 0 && cstride % 4 == 0 && zstride % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(slab) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL((k_slab_sum<true, Out>), grid, dim3(256), 0, s, slab, chunks, per,
+                       cstride, zstride, out);
+  else
+    hipLaunchKernelGGL((k_slab_sum<false, Out>), grid, dim3(256), 0, s, slab, chunks, per,
+                       cstride, zstride, out);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+}  // namespace gine

@@ -7,10 +7,10 @@
 // operands and apply the elementwise prologue (ReLU masks, BatchNorm backward, ...) when
 // the tile is staged, so the [N x D] operands are never materialised.
 //
-// Decomposition: grid = (row chunks, 64x128 output tiles, Z independent products).  A
-// 256-thread workgroup owns one 64(o) x 128(i) output tile of one row chunk; wave w holds
-// i-columns [32w, 32w+32) for all 64 o-rows as two v_mfma_f32_32x32x2_f32 accumulators
-// (one B fragment feeds two MFMAs).  64-row sub-tiles of P and Q are staged through LDS;
+// Decomposition: grid = (row chunks, TO x 128 output tiles, Z independent products).  A
+// 256-thread workgroup owns one TO(o) x 128(i) output tile of one row chunk, as
+// v_mfma_f32_32x32x2_f32 accumulators spread over its 4 waves (see wgrad_body for TO = 64
+// and 128).  64-row sub-tiles of P and Q are staged through LDS;
 // the RAW operands of the next sub-tile are loaded into registers before this sub-tile's
 // 64-long MFMA chain and transformed only when staged, so their HBM latency hides under
 // the matrix pipe.  Each (chunk, tile) writes an fp32 partial slab; slabs are reduced over
@@ -23,24 +23,22 @@ namespace gine {
 
 typedef float wg_floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int kWgRows = 64;                           // rows per staged sub-tile
-constexpr int kWgTO = 64;                             // o-rows per workgroup tile
-constexpr int kWgTI = 128;                            // i-columns per workgroup tile
-constexpr int kWgLdP = kWgTO + 4;                     // padded LDS rows (floats)
-constexpr int kWgLdQ = kWgTI + 4;
-constexpr int kWgPItems = kWgRows * kWgTO / 4 / 256;  // float4 per thread per sub-tile: 4
-constexpr int kWgQItems = kWgRows * kWgTI / 4 / 256;  // 8
-constexpr int kWgTargetBlocks = 256;                  // one workgroup per CU
-constexpr int kWgMinSubtiles = 2;                     // per chunk
+constexpr int kWgRows = 64;                   // rows per staged sub-tile
+constexpr int kWgTI = 128;                    // i-columns per workgroup tile
+constexpr int kWgLdQ = kWgTI + 4;             // padded LDS rows (floats)
+constexpr int kWgQItems = kWgRows * kWgTI / 4 / 256;  // Q float4 per thread per sub-tile: 8
+constexpr int kWgTargetBlocks = 256;          // one workgroup per CU
+constexpr int kWgMinSubtiles = 2;             // per chunk
 
 struct WgPlan {
   int tiles_o, tiles_i, chunks, rows_per_chunk;
 };
 
-// Z products of [O x I] over R rows: about one workgroup per CU, >= 2 sub-tiles per chunk.
-inline WgPlan wg_plan(int64_t R, int O, int I, int Z) {
+// Z products of [O x I] over R rows in TO x 128 output tiles: about one workgroup per CU,
+// >= 2 sub-tiles per chunk.
+inline WgPlan wg_plan(int64_t R, int O, int I, int Z, int TO) {
   WgPlan p;
-  p.tiles_o = (int)ceil_div(O, kWgTO);
+  p.tiles_o = (int)ceil_div(O, TO);
   p.tiles_i = (int)ceil_div(I, kWgTI);
   const int64_t subtiles = ceil_div(R > 0 ? R : 1, kWgRows);
   int64_t chunks = ceil_div(kWgTargetBlocks, (int64_t)Z * p.tiles_o * p.tiles_i);
@@ -60,24 +58,37 @@ inline WgPlan wg_plan(int64_t R, int O, int I, int Z) {
 //   Col p_col<Z>(q4) / q_col<Z>(q4)          per-column constants (q4 = float4 column)
 //   Raw p_load<Z>(n, q4) / q_load<Z>(n, q4)  raw operands of row n (n always in range)
 //   float4 p_xform<Z>(raw, col) / q_xform<Z> the staged value
-template <class Src, int Z>
+//
+// TO = 128: wave w holds the 64x64 quadrant (o-half w>>1, i-half w&1) as 2x2 32x32
+//           accumulators (P and Q each read once per chunk; for the Z=2 node-MLP products).
+// TO = 64:  wave w holds i-columns [32w, 32w+32) x all 64 o-rows (2x1 accumulators; twice
+//           the workgroups for a single product).
+template <class Src, int Z, int TO>
 __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int I,
                                            int rows_per_chunk, int tiles_i, size_t zstride,
                                            size_t cstride, float* __restrict__ slab,
                                            float* __restrict__ sP, float* __restrict__ sQ) {
   using Raw = typename Src::Raw;
   using Col = typename Src::Col;
+  constexpr int LDP = TO + 4;
+  constexpr int PQ = TO / 4;                 // float4 columns of the P tile
+  constexpr int PG = 256 / PQ;               // P row groups (rows pr + PG*k)
+  constexpr int PITEMS = kWgRows / PG;
+  constexpr int QQ = kWgTI / 4, QG = 256 / QQ;
+  constexpr int NI = TO == 128 ? 2 : 1;      // 32-wide i-tiles per wave
 
   const int chunk = blockIdx.x;
-  const int o0 = (blockIdx.y / tiles_i) * kWgTO, i0 = (blockIdx.y % tiles_i) * kWgTI;
+  const int o0 = (blockIdx.y / tiles_i) * TO, i0 = (blockIdx.y % tiles_i) * kWgTI;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
+  const int ob = TO == 128 ? 64 * (wave >> 1) : 0;      // wave's o origin in the tile
+  const int ib = TO == 128 ? 64 * (wave & 1) : 32 * wave;
   const bool bias_block = (i0 == 0);
 
   // staging coordinates: a thread always stages the same float4 column of P and of Q
-  const int pq = threadIdx.x % (kWgTO / 4), pr = threadIdx.x / (kWgTO / 4);  // rows pr+16k
-  const int qq = threadIdx.x % (kWgTI / 4), qr = threadIdx.x / (kWgTI / 4);  // rows qr+8k
+  const int pq = threadIdx.x % PQ, pr = threadIdx.x / PQ;
+  const int qq = threadIdx.x % QQ, qr = threadIdx.x / QQ;
   const bool p_ok = o0 + 4 * pq < O, q_ok = i0 + 4 * qq < I;
   const int pqa = p_ok ? o0 / 4 + pq : 0, qqa = q_ok ? i0 / 4 + qq : 0;
   const Col pc = src.template p_col<Z>(pqa);
@@ -86,21 +97,25 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   const int64_t r_begin = (int64_t)chunk * rows_per_chunk;
   const int64_t r_end = min<int64_t>(R, r_begin + rows_per_chunk);
 
-  wg_floatx16 acc0, acc1;
+  wg_floatx16 acc[2][NI];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) acc0[k] = acc1[k] = 0.f;
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][k][e] = 0.f;
   double bsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias partials of this thread's P column quad
 
-  Raw rp[kWgPItems], rq[kWgQItems];
+  Raw rp[PITEMS], rq[kWgQItems];
   auto load = [&](int64_t n0) {
 #pragma unroll
-    for (int k = 0; k < kWgPItems; ++k) {
-      const int64_t n = n0 + pr + 16 * k;
+    for (int k = 0; k < PITEMS; ++k) {
+      const int64_t n = n0 + pr + PG * k;
       rp[k] = src.template p_load<Z>(n < r_end ? n : r_end - 1, pqa);
     }
 #pragma unroll
     for (int k = 0; k < kWgQItems; ++k) {
-      const int64_t n = n0 + qr + 8 * k;
+      const int64_t n = n0 + qr + QG * k;
       rq[k] = src.template q_load<Z>(n < r_end ? n : r_end - 1, qqa);
     }
   };
@@ -108,11 +123,11 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   if (r_begin < r_end) load(r_begin);
   for (int64_t n0 = r_begin; n0 < r_end; n0 += kWgRows) {
 #pragma unroll
-    for (int k = 0; k < kWgPItems; ++k) {
-      const int r = pr + 16 * k;
+    for (int k = 0; k < PITEMS; ++k) {
+      const int r = pr + PG * k;
       float4 v = src.template p_xform<Z>(rp[k], pc);
       if (n0 + r >= r_end || !p_ok) v = f4_zero();
-      *reinterpret_cast<float4*>(&sP[r * kWgLdP + 4 * pq]) = v;
+      *reinterpret_cast<float4*>(&sP[r * LDP + 4 * pq]) = v;
       bsum[0] += (double)v.x;
       bsum[1] += (double)v.y;
       bsum[2] += (double)v.z;
@@ -120,7 +135,7 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
     }
 #pragma unroll
     for (int k = 0; k < kWgQItems; ++k) {
-      const int r = qr + 8 * k;
+      const int r = qr + QG * k;
       float4 v = src.template q_xform<Z>(rq[k], qc);
       if (n0 + r >= r_end || !q_ok) v = f4_zero();
       *reinterpret_cast<float4*>(&sQ[r * kWgLdQ + 4 * qq]) = v;
@@ -128,60 +143,71 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
     __syncthreads();
     if (n0 + kWgRows < r_end) load(n0 + kWgRows);  // raw operands of the next sub-tile
     // lane half h contracts rows [32h, 32h+32): the same permutation for A and B
-    const float* pa = &sP[(32 * h) * kWgLdP + c32];
-    const float* qb = &sQ[(32 * h) * kWgLdQ + 32 * wave + c32];
+    const float* pa = &sP[(32 * h) * LDP + ob + c32];
+    const float* qb = &sQ[(32 * h) * kWgLdQ + ib + c32];
 #pragma unroll
     for (int s = 0; s < kWgRows / 2; ++s) {
-      const float a0 = pa[s * kWgLdP];
-      const float a1 = pa[s * kWgLdP + 32];
-      const float b = qb[s * kWgLdQ];
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc1, 0, 0, 0);
+      float a[2], b[NI];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) a[j] = pa[s * LDP + 32 * j];
+#pragma unroll
+      for (int k = 0; k < NI; ++k) b[k] = qb[s * kWgLdQ + 32 * k];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int k = 0; k < NI; ++k)
+          acc[j][k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[k], acc[j][k], 0, 0, 0);
     }
     __syncthreads();
   }
 
   float* out = slab + (size_t)Z * zstride + (size_t)chunk * cstride;
-  const int i = i0 + 32 * wave + c32;
-  if (i < I) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = o0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (o < O) out[(size_t)o * I + i] = acc0[r];
-      if (o + 32 < O) out[(size_t)(o + 32) * I + i] = acc1[r];
+  for (int k = 0; k < NI; ++k) {
+    const int i = i0 + ib + 32 * k + c32;
+    if (i >= I) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + ob + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o < O) out[(size_t)o * I + i] = acc[j][k][r];
+      }
     }
   }
-  if (bias_block) {  // fixed-order sum of the 16 row groups' partials through LDS
-    double* sb = reinterpret_cast<double*>(sQ);  // [16][64], sQ is free after the loop
+  if (bias_block) {  // fixed-order sum of the row groups' partials through LDS
+    double* sb = reinterpret_cast<double*>(sQ);  // [PG][TO], sQ is free after the loop
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sb[pr * kWgTO + 4 * pq + j] = bsum[j];
+    for (int j = 0; j < 4; ++j) sb[pr * TO + 4 * pq + j] = bsum[j];
     __syncthreads();
-    if (threadIdx.x < kWgTO && o0 + (int)threadIdx.x < O) {
+    if ((int)threadIdx.x < TO && o0 + (int)threadIdx.x < O) {
       double t = 0.0;
-      for (int g = 0; g < 256 / (kWgTO / 4); ++g) t += sb[g * kWgTO + threadIdx.x];
+      for (int g = 0; g < PG; ++g) t += sb[g * TO + threadIdx.x];
       out[(size_t)O * I + o0 + threadIdx.x] = (float)t;
     }
   }
 }
 
-template <class Src>
+template <class Src, int TO>
 __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O, int I,
                                                       int rows_per_chunk, int tiles_i,
                                                       size_t zstride, size_t cstride,
                                                       float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float sP[kWgRows * kWgLdP];
+  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (TO + 4)];
   __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
   if (blockIdx.z == 0)
-    wgrad_body<Src, 0>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP, sQ);
+    wgrad_body<Src, 0, TO>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP,
+                           sQ);
   else
-    wgrad_body<Src, 1>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP, sQ);
+    wgrad_body<Src, 1, TO>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP,
+                           sQ);
 }
 
-template <class Src>
+template <int TO, class Src>
 inline int launch_wgrad_engine(const Src& src, int64_t R, int O, int I, int Z,
                                const WgPlan& p, size_t zstride, size_t cstride, float* slab,
                                hipStream_t s) {
-  hipLaunchKernelGGL((k_wgrad_engine<Src>), dim3(p.chunks, p.tiles_o * p.tiles_i, Z),
+  hipLaunchKernelGGL((k_wgrad_engine<Src, TO>), dim3(p.chunks, p.tiles_o * p.tiles_i, Z),
                      dim3(256), 0, s, src, R, O, I, p.rows_per_chunk, p.tiles_i, zstride,
                      cstride, slab);
   GINE_LAUNCH_STATUS();
