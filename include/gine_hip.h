@@ -229,6 +229,26 @@ int gine_deepset_bwd(const float* ens, const uint16_t* mask, const float* dr, fl
                      float* dw1, float* db1, int64_t num_nodes, int32_t members,
                      int32_t in_features, int32_t hidden, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Output head: aggr = Linear(D, K) + PostProcess (models/gnn.py:123,125,140-141;
+ * models/model_utils.py:42-113), K and the column transforms given by the loss `kind`
+ * (GINE_LOSS_*, K = 2, 3, 4, 5):  pred[:, 0] = raw (mu); sigma, sigma_u -> softplus + 1e-6;
+ * p -> sigmoid; u (GINE_LOSS_MIXED_U) -> 2.12 * sigmoid.
+ *   gine_head_fwd: raw [N, K] = h [N, D] W^T + b;  pred [N, K] = PostProcess(raw)
+ *   gine_head_bwd: d raw = PostProcess'(raw) * grad_pred;  dh [N, D] = d raw W;
+ *                  dw [K, D] = d raw^T h, db [K] = sum d raw (db may be NULL), through
+ *                  gine_head_bwd_slab_floats() floats of per-workgroup partials, reduced
+ *                  in fixed order (deterministic).
+ * D multiple of 4, D <= 256.
+ * ---------------------------------------------------------------------------------- */
+int gine_head_fwd(const float* h, const float* w, const float* b, float* raw, float* pred,
+                  int64_t num_nodes, int32_t channels, int32_t kind, void* stream);
+int gine_head_bwd_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind,
+                              size_t* floats);
+int gine_head_bwd(const float* grad_pred, const float* raw, const float* h, const float* w,
+                  float* dh, float* slab, float* dw, float* db, int64_t num_nodes,
+                  int32_t channels, int32_t kind, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,297 @@
+// Output head of the station-graph GNN on gfx950: aggr = Linear(D, K) followed by
+// PostProcess, forward and backward, one kernel each.
+//
+// Replaces (models/gnn.py:123,125,140-141 and models/model_utils.py:42-113):
+//   raw  = h W^T + b                      GNN.aggr (Linear(hidden, out_channels))
+//   pred = PostProcess(raw):  column 0 (mu) as is; sigma, sigma_u -> softplus(.) + 1e-6;
+//          p -> sigmoid(.); u -> sigmoid(.) * 2.12  (per loss, see gine_hip.h)
+// and their autograd, which the reference runs as one library GEMV, ~5 elementwise kernels
+// and a concatenation each way.  K <= 5 outputs per node, so the head is a row-streaming
+// kernel bound by reading h [N, D] once: one 32-lane half-wave per node, lane t holding
+// float4 columns t, t+32, ... of the row; the K dot products are reduced across the
+// half-wave in a fixed butterfly order.  softplus / sigmoid and their derivatives follow
+// ATen's formulas (threshold 20 for softplus, sigmoid backward from the saved output).
+//
+// Backward: d raw = PostProcess'(raw) * d pred; dh = d raw W (written once); dW = d raw^T h
+// and db = sum d raw as fp32 per-workgroup partials in a slab, reduced in fixed order by
+// k_slab_sum (deterministic).
+#include "gine_common.hpp"
+#include "gine_slab.hpp"
+
+#include <algorithm>
+
+namespace gine {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kRowsPerBlock = kThreads / 32;  // one node per half-wave
+constexpr int kMaxK = 5;
+constexpr int kMaxChunks = 2;                  // D <= 256: two float4 per lane
+constexpr int kHeadBlocks = 256;               // backward grid (partials = one slab row each)
+
+// Column roles of the K outputs for each loss (models/model_utils.py:80-111).
+enum Role { R_ID = 0, R_SOFTPLUS = 1, R_SIGMOID = 2, R_SIGMOID_U = 3 };
+
+__device__ __forceinline__ int role_of(int kind, int k) {
+  if (k == 0) return R_ID;                              // mu
+  if (k == 1 || k == 3) return R_SOFTPLUS;              // sigma, sigma_u
+  if (k == 2) return R_SIGMOID;                         // p
+  return kind == GINE_LOSS_MIXED_U ? R_SIGMOID_U : R_ID;  // u (learned threshold)
+}
+
+// torch.nn.functional.softplus(beta=1, threshold=20)
+__device__ __forceinline__ float softplus_f(float x) {
+  return x > 20.f ? x : log1pf(expf(x));
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
+
+__device__ __forceinline__ float post(int role, float x) {
+  switch (role) {
+    case R_SOFTPLUS: return softplus_f(x) + 1e-6f;
+    case R_SIGMOID: return sigmoid_f(x);
+    case R_SIGMOID_U: return sigmoid_f(x) * 2.12f;
+    default: return x;
+  }
+}
+
+// d post / d x applied to g (ATen: softplus_backward z = exp(x), g*z/(z+1) below the
+// threshold; sigmoid_backward g*(1-s)*s from the output s)
+__device__ __forceinline__ float post_bwd(int role, float x, float g) {
+  switch (role) {
+    case R_SOFTPLUS: {
+      if (x > 20.f) return g;
+      const float z = expf(x);
+      return g * z / (z + 1.f);
+    }
+    case R_SIGMOID: {
+      const float s = sigmoid_f(x);
+      return g * (1.f - s) * s;
+    }
+    case R_SIGMOID_U: {
+      const float s = sigmoid_f(x);
+      return (g * 2.12f) * (1.f - s) * s;
+    }
+    default: return g;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kThreads) void k_head_fwd(const float* __restrict__ h,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ b,
+                                                       float* __restrict__ raw,
+                                                       float* __restrict__ pred, int64_t N,
+                                                       int D, int kind) {
+  const int t = threadIdx.x & 31;
+  const int D4 = D / 4;
+  for (int64_t n = (int64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / 32; n < N;
+       n += (int64_t)gridDim.x * kRowsPerBlock) {
+    float acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int c = 0; c < kMaxChunks; ++c) {
+      const int q = t + 32 * c;
+      if (q < D4) {
+        const float4 x = reinterpret_cast<const float4*>(h + n * D)[q];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float4 wk = reinterpret_cast<const float4*>(w + (size_t)k * D)[q];
+          acc[k] = __builtin_fmaf(x.x, wk.x, acc[k]);
+          acc[k] = __builtin_fmaf(x.y, wk.y, acc[k]);
+          acc[k] = __builtin_fmaf(x.z, wk.z, acc[k]);
+          acc[k] = __builtin_fmaf(x.w, wk.w, acc[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int m = 16; m >= 1; m >>= 1) acc[k] += __shfl_xor(acc[k], m, 32);
+    }
+    if (t < K) {  // lane k finalises output k
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) v = (t == k) ? acc[k] : v;
+      v = v + b[t];
+      raw[n * K + t] = v;
+      pred[n * K + t] = post(role_of(kind, t), v);
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kThreads) void k_head_bwd(const float* __restrict__ gpred,
+                                                       const float* __restrict__ raw,
+                                                       const float* __restrict__ h,
+                                                       const float* __restrict__ w,
+                                                       float* __restrict__ dh,
+                                                       float* __restrict__ slab, int64_t N,
+                                                       int D, int kind) {
+  __shared__ float s_part[kRowsPerBlock][kMaxK * 256 + kMaxK];
+  const int t = threadIdx.x & 31, hw = threadIdx.x / 32;
+  const int D4 = D / 4;
+  float4 aw[kMaxChunks][K];  // sum over this half-wave's nodes of d raw[k] * h[n, cols]
+  float ab[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    ab[k] = 0.f;
+#pragma unroll
+    for (int c = 0; c < kMaxChunks; ++c) aw[c][k] = f4_zero();
+  }
+  float4 wk[kMaxChunks][K];
+#pragma unroll
+  for (int c = 0; c < kMaxChunks; ++c) {
+    const int q = min(t + 32 * c, D4 - 1);
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[c][k] = reinterpret_cast<const float4*>(w + (size_t)k * D)[q];
+  }
+  for (int64_t n = (int64_t)blockIdx.x * kRowsPerBlock + hw; n < N;
+       n += (int64_t)gridDim.x * kRowsPerBlock) {
+    float g[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      g[k] = post_bwd(role_of(kind, k), raw[n * K + k], gpred[n * K + k]);
+      ab[k] += g[k];
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxChunks; ++c) {
+      const int q = t + 32 * c;
+      if (q < D4) {
+        const float4 x = reinterpret_cast<const float4*>(h + n * D)[q];
+        float4 o = f4_zero();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          o.x = __builtin_fmaf(g[k], wk[c][k].x, o.x);
+          o.y = __builtin_fmaf(g[k], wk[c][k].y, o.y);
+          o.z = __builtin_fmaf(g[k], wk[c][k].z, o.z);
+          o.w = __builtin_fmaf(g[k], wk[c][k].w, o.w);
+          aw[c][k].x = __builtin_fmaf(g[k], x.x, aw[c][k].x);
+          aw[c][k].y = __builtin_fmaf(g[k], x.y, aw[c][k].y);
+          aw[c][k].z = __builtin_fmaf(g[k], x.z, aw[c][k].z);
+          aw[c][k].w = __builtin_fmaf(g[k], x.w, aw[c][k].w);
+        }
+        reinterpret_cast<float4*>(dh + n * D)[q] = o;
+      }
+    }
+  }
+  // workgroup partial: the 8 half-waves summed in fixed order (fp64) -> one slab row
+#pragma unroll
+  for (int c = 0; c < kMaxChunks; ++c) {
+    const int q = t + 32 * c;
+    if (q < D4) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        *reinterpret_cast<float4*>(&s_part[hw][k * D + 4 * q]) = aw[c][k];
+    }
+  }
+  if (t < K) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) v = (t == k) ? ab[k] : v;
+    s_part[hw][K * D + t] = v;
+  }
+  __syncthreads();
+  const int per = K * D + K;
+  float* out = slab + (size_t)blockIdx.x * per;
+  for (int e = threadIdx.x; e < per; e += kThreads) {
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < kRowsPerBlock; ++r) s += (double)s_part[r][e];
+    out[e] = (float)s;
+  }
+}
+
+struct HeadOut {
+  float* dw;
+  float* db;
+  int64_t wsize;
+  __device__ void operator()(int, int64_t e, double v) const {
+    if (e < wsize) dw[e] = (float)v;
+    else if (db) db[e - wsize] = (float)v;
+  }
+};
+
+inline int k_of(int kind) {
+  switch (kind) {
+    case GINE_LOSS_NORMAL: return 2;
+    case GINE_LOSS_MIXED_NORMAL: return 3;
+    case GINE_LOSS_MIXED: return 4;
+    case GINE_LOSS_MIXED_U: return 5;
+    default: return -1;
+  }
+}
+
+inline bool head_dim_ok(int D) { return D > 0 && D % 4 == 0 && D <= 32 * 4 * kMaxChunks; }
+
+inline int head_bwd_grid(int64_t N) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kHeadBlocks, ceil_div(N, kRowsPerBlock)));
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_head_fwd(const float* h, const float* w, const float* b, float* raw,
+                             float* pred, int64_t num_nodes, int32_t channels, int32_t kind,
+                             void* stream) {
+  const int K = k_of(kind);
+  if (K < 0 || num_nodes < 0) return GINE_ERR_INVALID;
+  if (!head_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes == 0) return GINE_OK;
+  if (!h || !w || !b || !raw || !pred) return GINE_ERR_INVALID;
+  const int grid = (int)std::min<int64_t>(2048, ceil_div(num_nodes, kRowsPerBlock));
+  hipStream_t s = as_stream(stream);
+#define HEAD_FWD(KK)                                                                      \
+  hipLaunchKernelGGL(k_head_fwd<KK>, dim3(grid), dim3(kThreads), 0, s, h, w, b, raw, pred, \
+                     num_nodes, channels, kind)
+  switch (K) {
+    case 2: HEAD_FWD(2); break;
+    case 3: HEAD_FWD(3); break;
+    case 4: HEAD_FWD(4); break;
+    default: HEAD_FWD(5); break;
+  }
+#undef HEAD_FWD
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_head_bwd_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind,
+                                         size_t* floats) {
+  const int K = k_of(kind);
+  if (K < 0 || num_nodes < 0 || !floats) return GINE_ERR_INVALID;
+  if (!head_dim_ok(channels)) return GINE_ERR_DIM;
+  *floats = (size_t)head_bwd_grid(num_nodes) * (size_t)(K * channels + K);
+  return GINE_OK;
+}
+
+extern "C" int gine_head_bwd(const float* grad_pred, const float* raw, const float* h,
+                             const float* w, float* dh, float* slab, float* dw, float* db,
+                             int64_t num_nodes, int32_t channels, int32_t kind, void* stream) {
+  const int K = k_of(kind);
+  if (K < 0 || num_nodes < 0) return GINE_ERR_INVALID;
+  if (!head_dim_ok(channels)) return GINE_ERR_DIM;
+  if (!w || !dw || !slab) return GINE_ERR_INVALID;
+  if (num_nodes > 0 && (!grad_pred || !raw || !h || !dh)) return GINE_ERR_INVALID;
+  const int grid = head_bwd_grid(num_nodes);
+  const int64_t per = (int64_t)K * channels + K;
+  hipStream_t s = as_stream(stream);
+  if (num_nodes == 0) {
+    GINE_RETURN_IF_HIP(hipMemsetAsync(slab, 0, sizeof(float) * per, s));
+  } else {
+#define HEAD_BWD(KK)                                                                          \
+  hipLaunchKernelGGL(k_head_bwd<KK>, dim3(grid), dim3(kThreads), 0, s, grad_pred, raw, h, w, \
+                     dh, slab, num_nodes, channels, kind)
+    switch (K) {
+      case 2: HEAD_BWD(2); break;
+      case 3: HEAD_BWD(3); break;
+      case 4: HEAD_BWD(4); break;
+      default: HEAD_BWD(5); break;
+    }
+#undef HEAD_BWD
+    GINE_LAUNCH_STATUS();
+  }
+  return launch_slab_sum(slab, num_nodes == 0 ? 1 : grid, per, (size_t)per, 0, 1,
+                         HeadOut{dw, db, (int64_t)K * channels}, s);
+}

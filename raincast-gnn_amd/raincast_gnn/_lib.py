@@ -62,6 +62,9 @@ _SIGNATURES = {
     "gine_deepset_bwd_num_partials": [_i64, ctypes.POINTER(_i32)],
     "gine_deepset_bwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                          _i64, _i32, _i32, _i32, _c_void_p],
+    "gine_head_fwd": [_c_void_p] * 5 + [_i64, _i32, _i32, _c_void_p],
+    "gine_head_bwd_slab_floats": [_i64, _i32, _i32, ctypes.POINTER(_size)],
+    "gine_head_bwd": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
 }
 
 EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)

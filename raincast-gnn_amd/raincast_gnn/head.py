@@ -1,0 +1,80 @@
+"""Fused output head: ``PostProcess(aggr(h))`` on one HIP kernel each way.
+
+models/gnn.py:140-141 evaluates ``self.postprocess(self.aggr(h))`` -- a Linear(D, K) and
+the per-column transforms of models/model_utils.py:70-113 (softplus + 1e-6 on the scales,
+sigmoid on the point mass, 2.12 * sigmoid on a learned threshold).  ``gine_head_fwd`` /
+``gine_head_bwd`` (csrc/gine_head.hip) run both, forward and backward, in one row-streaming
+kernel each; the module structure and parameters (``GNN.aggr``, ``GNN.postprocess``) are
+unchanged.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .gradbuf import grad_out
+
+MAX_CHANNELS = 256
+
+
+def loss_kind(loss: str, grad_u) -> int | None:
+    """GINE_LOSS_* of PostProcess(loss, grad_u) (its ``== "True"`` string test, gnn.py:98)."""
+    if loss == "NormalCRPS":
+        return _lib.LOSS_NORMAL
+    if loss == "MixedNormalCRPS":
+        return _lib.LOSS_MIXED_NORMAL
+    if loss == "MixedLoss":
+        return _lib.LOSS_MIXED_U if grad_u == "True" else _lib.LOSS_MIXED
+    return None
+
+
+K_OF = {_lib.LOSS_NORMAL: 2, _lib.LOSS_MIXED_NORMAL: 3, _lib.LOSS_MIXED: 4, _lib.LOSS_MIXED_U: 5}
+
+
+def fusable(h: torch.Tensor, lin: torch.nn.Linear, kind) -> bool:
+    return (kind is not None and h.is_cuda and h.dim() == 2 and h.dtype == torch.float32
+            and lin.weight.dtype == torch.float32 and lin.bias is not None
+            and lin.out_features == K_OF[kind] and lin.in_features == h.size(1)
+            and h.size(1) % 4 == 0 and h.size(1) <= MAX_CHANNELS)
+
+
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, weight, bias, kind):
+        h = h.contiguous()
+        w, b = weight.detach().contiguous(), bias.detach().contiguous()
+        N, D = h.shape
+        K = w.size(0)
+        raw = torch.empty(N, K, dtype=torch.float32, device=h.device)
+        pred = torch.empty(N, K, dtype=torch.float32, device=h.device)
+        _lib.call("gine_head_fwd", _lib.ptr(h), _lib.ptr(w), _lib.ptr(b), _lib.ptr(raw),
+                  _lib.ptr(pred), N, D, kind, _lib.stream_handle(h.device))
+        ctx.save_for_backward(h, w, raw)
+        ctx.kind = kind
+        ctx.params = (weight, bias)
+        return pred
+
+    @staticmethod
+    def backward(ctx, gpred):
+        h, w, raw = ctx.saved_tensors
+        N, D = h.shape
+        K = w.size(0)
+        dev = h.device
+        gpred = gpred.float().contiguous()
+        floats = ctypes.c_size_t(0)
+        _lib.call("gine_head_bwd_slab_floats", N, D, ctx.kind, ctypes.byref(floats))
+        slab = torch.empty(floats.value, dtype=torch.float32, device=dev)
+        dh = torch.empty_like(h)
+        dw = grad_out(ctx.params[0], (K, D), dev)
+        db = grad_out(ctx.params[1], (K,), dev)
+        _lib.call("gine_head_bwd", _lib.ptr(gpred), _lib.ptr(raw), _lib.ptr(h), _lib.ptr(w),
+                  _lib.ptr(dh), _lib.ptr(slab), _lib.ptr(dw), _lib.ptr(db), N, D, ctx.kind,
+                  _lib.stream_handle(dev))
+        return dh, dw, db, None
+
+
+def head(h: torch.Tensor, lin: torch.nn.Linear, kind: int) -> torch.Tensor:
+    """``PostProcess(lin(h))`` for the loss ``kind`` on the fused kernels."""
+    return _HeadFn.apply(h, lin.weight, lin.bias, kind)

@@ -12,6 +12,7 @@ import torch.nn as nn
 from torch.nn import Linear, ModuleList, ReLU
 
 from . import deepset
+from . import head as fused_head
 from .linear import Linear as RowLinear
 from .loss import MixedLoss, MixedNormalCRPS, NormalCRPS
 from .nn import GINEConv
@@ -113,6 +114,9 @@ class GNN(nn.Module):
         emb = self.deepset(data.ensemble)
         h = self.dim_red(torch.cat([data.x, emb], dim=1))
         h = self.conv(h, data.edge_index, data.edge_attr)
+        kind = fused_head.loss_kind(self.postprocess.loss, self.postprocess.grad_u)
+        if type(self.aggr) in (RowLinear, Linear) and fused_head.fusable(h, self.aggr, kind):
+            return fused_head.head(h, self.aggr, kind)   # aggr + PostProcess, one kernel
         return self.postprocess(self.aggr(h))
 
     def configure_optimizers(self):
