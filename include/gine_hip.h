@@ -249,6 +249,33 @@ int gine_head_bwd(const float* grad_pred, const float* raw, const float* h, cons
                   float* dh, float* slab, float* dw, float* db, int64_t num_nodes,
                   int32_t channels, int32_t kind, void* stream);
 
+/* ------------------------------------------------------------------------------------
+ * Dense layers between the DeepSet member sum and the GINE stack (models/gnn.py:48-68,
+ * 112-113, 132-135), phi's last Linear applied after the member sum:
+ *   s = r Wp2^T + bias_scale * bp2;  u = relu(s Wr0^T + br0);  e = u Wr1^T + br1;
+ *   h0 = [x | e] Wdr^T + bdr
+ * r [N, D] = gine_deepset_fwd output, x [N, F] node features, D in {64, 128}, F <= 64.
+ * gine_chain_fwd writes s, u, e (saved for the backward) and h0.
+ * gine_chain_bwd, from dh0 = d loss / d h0: de = dh0 Wdr[:, F:], dt = (de Wr1) * 1[u > 0],
+ *   ds = dt Wr0, dr = ds Wp2 (dr feeds gine_deepset_bwd), and all eight parameter
+ *   gradients (dbp2 scaled by bias_scale; bias pointers may be NULL) through
+ *   gine_chain_bwd_slab_floats() floats of partials reduced in fixed order.
+ * ---------------------------------------------------------------------------------- */
+int gine_chain_fwd(const float* r, const float* x, const float* wp2, const float* bp2,
+                   float bias_scale, const float* wr0, const float* br0, const float* wr1,
+                   const float* br1, const float* wdr, const float* bdr, float* s, float* u,
+                   float* e, float* h0, int64_t num_nodes, int32_t hidden,
+                   int32_t in_features, void* stream);
+int gine_chain_bwd_slab_floats(int64_t num_nodes, int32_t hidden, int32_t in_features,
+                               size_t* floats);
+int gine_chain_bwd(const float* dh0, const float* x, const float* r, const float* s,
+                   const float* u, const float* e, const float* wp2, const float* wr0,
+                   const float* wr1, const float* wdr, float* de, float* dt, float* ds,
+                   float* dr, float* slab, float* dwp2, float* dbp2, float bias_scale,
+                   float* dwr0, float* dbr0, float* dwr1, float* dbr1, float* dwdr,
+                   float* dbdr, int64_t num_nodes, int32_t hidden, int32_t in_features,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,6 +52,6 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   return __shfl_xor(v, m, kWave);
 }
 
-inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace gine

@@ -32,6 +32,7 @@ __device__ __forceinline__ float4 row_quad(const float* __restrict__ a, int64_t 
 
 template <bool VP, bool VQ>
 struct LinWgradSrc {
+  static constexpr int kZ = 1;
   const float* dy;
   const float* x;
   int O, I;
@@ -39,6 +40,7 @@ struct LinWgradSrc {
     float4 v;
   };
   struct Col {};
+  template <int Z> __device__ int i_dim(int I) const { return I; }
   template <int Z> __device__ Col p_col(int) const { return Col{}; }
   template <int Z> __device__ Col q_col(int) const { return Col{}; }
   template <int Z> __device__ Raw p_load(int64_t n, int q) const { return Raw{row_quad<VP>(dy, n, O, q)}; }
@@ -91,16 +93,16 @@ extern "C" int gine_linear_wgrad(const float* dy, const float* x, int64_t rows,
     const bool vp = vec_ok(dy, O), vq = vec_ok(x, I);
     int st;
     if (vp && vq) {
-      st = launch_wgrad_engine<64>(LinWgradSrc<true, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<true, true>{dy, x, O, I}, rows, O, I, p.tiles_o * p.tiles_i, p, 0,
                                (size_t)per, slab, s);
     } else if (vp) {
-      st = launch_wgrad_engine<64>(LinWgradSrc<true, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<true, false>{dy, x, O, I}, rows, O, I, p.tiles_o * p.tiles_i, p, 0,
                                (size_t)per, slab, s);
     } else if (vq) {
-      st = launch_wgrad_engine<64>(LinWgradSrc<false, true>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<false, true>{dy, x, O, I}, rows, O, I, p.tiles_o * p.tiles_i, p, 0,
                                (size_t)per, slab, s);
     } else {
-      st = launch_wgrad_engine<64>(LinWgradSrc<false, false>{dy, x, O, I}, rows, O, I, 1, p, 0,
+      st = launch_wgrad_engine<64>(LinWgradSrc<false, false>{dy, x, O, I}, rows, O, I, p.tiles_o * p.tiles_i, p, 0,
                                (size_t)per, slab, s);
     }
     if (st != GINE_OK) return st;

@@ -481,10 +481,12 @@ __global__ __launch_bounds__(kColsumThreads) void k_bn_bwd_finalize(
 // ----------------------------------------------------------------------------------------
 template <int PDO>  // PRO_PLAIN | PRO_DOR | PRO_DOM: how do is formed from dy
 struct MlpWgradSrc {
+  static constexpr int kZ = 2;
   ProArgs p_do, q_r, p_da1, q_z;
   int D;
   using Raw = RawItem;
   using Col = ColConst;
+  template <int Z> __device__ int i_dim(int I) const { return I; }
   template <int Z> __device__ Col p_col(int q) const {
     if constexpr (Z == 0) return col_const<PDO>(p_do, D, q);
     else return col_const<PRO_DA1>(p_da1, D, q);
@@ -682,13 +684,13 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   int st;
   if (epilogue == GINE_EPI_NONE) {
     const MlpWgradSrc<PRO_PLAIN> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p, per * p.chunks, per, slab, s);
   } else if (epilogue == GINE_EPI_RELU) {
     const MlpWgradSrc<PRO_DOR> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p, per * p.chunks, per, slab, s);
   } else {
     const MlpWgradSrc<PRO_DOM> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p, per * p.chunks, per, slab, s);
   }
   if (st != GINE_OK) return st;
   if (st != GINE_OK) return st;

@@ -35,13 +35,15 @@ struct WgPlan {
 };
 
 // Z products of [O x I] over R rows in TO x 128 output tiles: about one workgroup per CU,
-// >= 2 sub-tiles per chunk.
-inline WgPlan wg_plan(int64_t R, int O, int I, int Z, int TO) {
+// >= 2 sub-tiles per chunk.  total_tiles: output tiles of all Z products together
+// (default Z * tiles_o * tiles_i; less when a policy gives some products a narrower I).
+inline WgPlan wg_plan(int64_t R, int O, int I, int Z, int TO, int total_tiles = 0) {
   WgPlan p;
   p.tiles_o = (int)ceil_div(O, TO);
   p.tiles_i = (int)ceil_div(I, kWgTI);
   const int64_t subtiles = ceil_div(R > 0 ? R : 1, kWgRows);
-  int64_t chunks = ceil_div(kWgTargetBlocks, (int64_t)Z * p.tiles_o * p.tiles_i);
+  if (total_tiles <= 0) total_tiles = Z * p.tiles_o * p.tiles_i;
+  int64_t chunks = ceil_div(kWgTargetBlocks, (int64_t)total_tiles);
   const int64_t cap = ceil_div(subtiles, kWgMinSubtiles);
   if (chunks > cap) chunks = cap;
   if (chunks < 1) chunks = 1;
@@ -58,14 +60,16 @@ inline WgPlan wg_plan(int64_t R, int O, int I, int Z, int TO) {
 //   Col p_col<Z>(q4) / q_col<Z>(q4)          per-column constants (q4 = float4 column)
 //   Raw p_load<Z>(n, q4) / q_load<Z>(n, q4)  raw operands of row n (n always in range)
 //   float4 p_xform<Z>(raw, col) / q_xform<Z> the staged value
+//   int i_dim<Z>(I)                          I of product Z (<= the launch's I)
+//   static constexpr int kZ                  number of products (<= 4)
 //
 // TO = 128: wave w holds the 64x64 quadrant (o-half w>>1, i-half w&1) as 2x2 32x32
 //           accumulators (P and Q each read once per chunk; for the Z=2 node-MLP products).
 // TO = 64:  wave w holds i-columns [32w, 32w+32) x all 64 o-rows (2x1 accumulators; twice
 //           the workgroups for a single product).
 template <class Src, int Z, int TO>
-__device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int I,
-                                           int rows_per_chunk, int tiles_i, size_t zstride,
+__device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int I, int tile,
+                                           int rows_per_chunk, size_t zstride,
                                            size_t cstride, float* __restrict__ slab,
                                            float* __restrict__ sP, float* __restrict__ sQ) {
   using Raw = typename Src::Raw;
@@ -78,7 +82,8 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   constexpr int NI = TO == 128 ? 2 : 1;      // 32-wide i-tiles per wave
 
   const int chunk = blockIdx.x;
-  const int o0 = (blockIdx.y / tiles_i) * TO, i0 = (blockIdx.y % tiles_i) * kWgTI;
+  const int tiles_i = (int)ceil_div(I, kWgTI);
+  const int o0 = (tile / tiles_i) * TO, i0 = (tile % tiles_i) * kWgTI;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
@@ -188,28 +193,59 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   }
 }
 
+// Output tiles of product z: tiles_o * ceil(I_z / 128).
+template <class Src, int Z>
+__device__ __forceinline__ int wg_tiles(const Src& src, int O, int I, int TO) {
+  return (int)(ceil_div(O, TO) * ceil_div(src.template i_dim<Z>(I), kWgTI));
+}
+
+// grid = (chunks, sum over z of the product's output tiles); blockIdx.y -> (z, tile).
 template <class Src, int TO>
 __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O, int I,
-                                                      int rows_per_chunk, int tiles_i,
-                                                      size_t zstride, size_t cstride,
+                                                      int rows_per_chunk, size_t zstride,
+                                                      size_t cstride,
                                                       float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) float sP[kWgRows * (TO + 4)];
   __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
-  if (blockIdx.z == 0)
-    wgrad_body<Src, 0, TO>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP,
-                           sQ);
-  else
-    wgrad_body<Src, 1, TO>(src, R, O, I, rows_per_chunk, tiles_i, zstride, cstride, slab, sP,
-                           sQ);
+  int y = blockIdx.y;
+  const int t0 = wg_tiles<Src, 0>(src, O, I, TO);
+  if (y < t0) {
+    wgrad_body<Src, 0, TO>(src, R, O, src.template i_dim<0>(I), y, rows_per_chunk, zstride,
+                           cstride, slab, sP, sQ);
+    return;
+  }
+  y -= t0;
+  if constexpr (Src::kZ > 1) {
+    const int t1 = wg_tiles<Src, 1>(src, O, I, TO);
+    if (y < t1) {
+      wgrad_body<Src, 1, TO>(src, R, O, src.template i_dim<1>(I), y, rows_per_chunk, zstride,
+                             cstride, slab, sP, sQ);
+      return;
+    }
+    y -= t1;
+  }
+  if constexpr (Src::kZ > 2) {
+    const int t2 = wg_tiles<Src, 2>(src, O, I, TO);
+    if (y < t2) {
+      wgrad_body<Src, 2, TO>(src, R, O, src.template i_dim<2>(I), y, rows_per_chunk, zstride,
+                             cstride, slab, sP, sQ);
+      return;
+    }
+    y -= t2;
+  }
+  if constexpr (Src::kZ > 3) {
+    wgrad_body<Src, 3, TO>(src, R, O, src.template i_dim<3>(I), y, rows_per_chunk, zstride,
+                           cstride, slab, sP, sQ);
+  }
 }
 
+// Z must equal Src::kZ; total_tiles = sum of the products' output tiles (the plan's).
 template <int TO, class Src>
-inline int launch_wgrad_engine(const Src& src, int64_t R, int O, int I, int Z,
+inline int launch_wgrad_engine(const Src& src, int64_t R, int O, int I, int total_tiles,
                                const WgPlan& p, size_t zstride, size_t cstride, float* slab,
                                hipStream_t s) {
-  hipLaunchKernelGGL((k_wgrad_engine<Src, TO>), dim3(p.chunks, p.tiles_o * p.tiles_i, Z),
-                     dim3(256), 0, s, src, R, O, I, p.rows_per_chunk, p.tiles_i, zstride,
-                     cstride, slab);
+  hipLaunchKernelGGL((k_wgrad_engine<Src, TO>), dim3(p.chunks, total_tiles), dim3(256), 0, s,
+                     src, R, O, I, p.rows_per_chunk, zstride, cstride, slab);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

@@ -1,0 +1,86 @@
+"""Fused dense layers between the DeepSet member sum and the GINE stack.
+
+models/gnn.py:132-135 computes ``dim_red(cat([x, DeepSetEncoder(ensemble)], 1))``; after the
+fused member sum ``r = sum_m relu(phi[0](ens_m))`` (:mod:`.deepset`) what remains is four
+dense Linears and a ReLU on [N, D] rows::
+
+    s = phi[2](r) (bias x M)  ->  u = relu(rho[0](s))  ->  e = rho[2](u)  ->  h0 = dim_red([x | e])
+
+``gine_chain_fwd`` runs them as two 2-stage row-chain kernels and ``gine_chain_bwd`` the
+backward (two chain kernels, one weight-gradient launch for all four Linears, one
+reduction) -- csrc/gine_chain.hip.  Modules, parameters and state_dict keys are the
+reference's; this is only the execution of ``GNN.forward``'s first half.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .gradbuf import grad_out
+
+HIDDEN = (64, 128)
+MAX_FEATURES = 64
+
+
+def fusable(r: torch.Tensor, x: torch.Tensor, lins) -> bool:
+    p2, r0, r1, dr = lins
+    D = r.size(1)
+    F = x.size(1)
+    shapes = ((p2, D, D), (r0, D, D), (r1, D, D), (dr, F + D, D))
+    return (r.is_cuda and x.is_cuda and r.dtype == torch.float32 and x.dtype == torch.float32
+            and D in HIDDEN and 0 < F <= MAX_FEATURES and not x.requires_grad
+            and all(isinstance(m, torch.nn.Linear) and m.bias is not None
+                    and m.weight.dtype == torch.float32 and m.in_features == i
+                    and m.out_features == o for m, i, o in shapes))
+
+
+class _ChainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, r, x, wp2, bp2, wr0, br0, wr1, br1, wdr, bdr, members):
+        r = r.contiguous()
+        x = x.contiguous()
+        N, D = r.shape
+        F = x.size(1)
+        dev = r.device
+        ws = [t.detach().contiguous() for t in (wp2, bp2, wr0, br0, wr1, br1, wdr, bdr)]
+        s, u, e, h0 = (torch.empty(N, D, dtype=torch.float32, device=dev) for _ in range(4))
+        P = _lib.ptr
+        _lib.call("gine_chain_fwd", P(r), P(x), P(ws[0]), P(ws[1]), float(members), P(ws[2]),
+                  P(ws[3]), P(ws[4]), P(ws[5]), P(ws[6]), P(ws[7]), P(s), P(u), P(e), P(h0),
+                  N, D, F, _lib.stream_handle(dev))
+        ctx.save_for_backward(r, x, s, u, e, ws[0], ws[2], ws[4], ws[6])
+        ctx.params = (wp2, bp2, wr0, br0, wr1, br1, wdr, bdr)
+        ctx.members = float(members)
+        return h0
+
+    @staticmethod
+    def backward(ctx, dh0):
+        r, x, s, u, e, wp2, wr0, wr1, wdr = ctx.saved_tensors
+        N, D = r.shape
+        F = x.size(1)
+        dev = r.device
+        dh0 = dh0.contiguous()
+        de, dt, ds, dr = (torch.empty(N, D, dtype=torch.float32, device=dev) for _ in range(4))
+        floats = ctypes.c_size_t(0)
+        _lib.call("gine_chain_bwd_slab_floats", N, D, F, ctypes.byref(floats))
+        slab = torch.empty(floats.value, dtype=torch.float32, device=dev)
+        p = ctx.params
+        g = [grad_out(p[0], (D, D), dev), grad_out(p[1], (D,), dev),
+             grad_out(p[2], (D, D), dev), grad_out(p[3], (D,), dev),
+             grad_out(p[4], (D, D), dev), grad_out(p[5], (D,), dev),
+             grad_out(p[6], (D, F + D), dev), grad_out(p[7], (D,), dev)]
+        P = _lib.ptr
+        _lib.call("gine_chain_bwd", P(dh0), P(x), P(r), P(s), P(u), P(e), P(wp2), P(wr0),
+                  P(wr1), P(wdr), P(de), P(dt), P(ds), P(dr), P(slab), P(g[0]), P(g[1]),
+                  ctx.members, P(g[2]), P(g[3]), P(g[4]), P(g[5]), P(g[6]), P(g[7]), N, D, F,
+                  _lib.stream_handle(dev))
+        return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
+
+
+def chain(r: torch.Tensor, x: torch.Tensor, lins, members: int) -> torch.Tensor:
+    """``dim_red(cat([x, rho(phi[2](r) summed over members)]))`` on the fused kernels."""
+    p2, r0, r1, dr = lins
+    return _ChainFn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight, r1.bias,
+                          dr.weight, dr.bias, members)

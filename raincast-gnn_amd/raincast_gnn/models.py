@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 from torch.nn import Linear, ModuleList, ReLU
 
+from . import chain as fused_chain
 from . import deepset
 from . import head as fused_head
 from .linear import Linear as RowLinear
@@ -110,9 +111,27 @@ class GNN(nn.Module):
         self.optimizer_class = optimizer_class
         self.optimizer_params = optimizer_params
 
+    def _front(self, data):
+        """``dim_red(cat([x, deepset(ensemble)]))`` (gnn.py:132-135); on a HIP device with
+        the reference's layer types, the fused member-sum kernels plus the fused dense
+        chain (raincast_gnn/chain.py)."""
+        ds = self.deepset
+        ens, x = data.ensemble, data.x
+        lin1, act, lin2 = ds.phi
+        rho0, rho_act, rho1 = ds.rho
+        lins = (lin2, rho0, rho1, self.dim_red)
+        if (isinstance(act, nn.ReLU) and isinstance(rho_act, nn.ReLU)
+                and deepset.fusable(ens, lin1.weight, lin1.bias)):
+            r = deepset.phi_sum(ens, lin1)
+            if fused_chain.fusable(r, x, lins):
+                return fused_chain.chain(r, x, lins, ens.size(1))
+            emb = ds.rho(lin2(r, bias_scale=ens.size(1)))
+            return self.dim_red(torch.cat([x, emb], dim=1))
+        emb = ds(ens)
+        return self.dim_red(torch.cat([x, emb], dim=1))
+
     def forward(self, data):
-        emb = self.deepset(data.ensemble)
-        h = self.dim_red(torch.cat([data.x, emb], dim=1))
+        h = self._front(data)
         h = self.conv(h, data.edge_index, data.edge_attr)
         kind = fused_head.loss_kind(self.postprocess.loss, self.postprocess.grad_u)
         if type(self.aggr) in (RowLinear, Linear) and fused_head.fusable(h, self.aggr, kind):
