@@ -19,16 +19,30 @@
 
 #include "gine_common.hpp"
 
+// Diagnostic switches (tools/wg_micro.hip only; 0 in the library): bit 0 skips the MFMA
+// chain, bit 1 replaces the operand loads by zeros, bit 2 skips the slab stores, bit 3
+// stamps s_memtime / s_memrealtime at body entry and exit into gine_wg_clock[block][4].
+#ifndef GINE_WG_VARIANT
+#define GINE_WG_VARIANT 0
+#endif
+
 namespace gine {
+
+#if (GINE_WG_VARIANT & 8) != 0
+__device__ unsigned long long gine_wg_clock[4096][4];
+#endif
 
 typedef float wg_floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kWgRows = 64;                   // rows per staged sub-tile
 constexpr int kWgTI = 128;                    // i-columns per workgroup tile
 constexpr int kWgLdQ = kWgTI + 4;             // padded LDS rows (floats)
-constexpr int kWgQItems = kWgRows * kWgTI / 4 / 256;  // Q float4 per thread per sub-tile: 8
 constexpr int kWgTargetBlocks = 256;          // one workgroup per CU
 constexpr int kWgMinSubtiles = 2;             // per chunk
+#ifndef GINE_WG_WAVES64
+#define GINE_WG_WAVES64 8
+#endif
+constexpr int kWgWaves64 = GINE_WG_WAVES64;   // waves per workgroup of the 64-row tiles
 
 struct WgPlan {
   int tiles_o, tiles_i, chunks, rows_per_chunk;
@@ -67,19 +81,31 @@ inline WgPlan wg_plan(int64_t R, int O, int I, int Z, int TO, int total_tiles = 
 //           accumulators (P and Q each read once per chunk; for the Z=2 node-MLP products).
 // TO = 64:  wave w holds i-columns [32w, 32w+32) x all 64 o-rows (2x1 accumulators; twice
 //           the workgroups for a single product).
-template <class Src, int Z, int TO>
+template <class Src, int Z, int TO, int NW>
 __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int I, int tile,
                                            int rows_per_chunk, size_t zstride,
                                            size_t cstride, float* __restrict__ slab,
                                            float* __restrict__ sP, float* __restrict__ sQ) {
   using Raw = typename Src::Raw;
   using Col = typename Src::Col;
+#if (GINE_WG_VARIANT & 8) != 0
+  const int blin = blockIdx.x + gridDim.x * blockIdx.y;
+  if (threadIdx.x == 0 && blin < 4096) {
+    gine_wg_clock[blin][0] = __builtin_amdgcn_s_memtime();
+    gine_wg_clock[blin][1] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
+  constexpr int NT = 64 * NW;                // threads
   constexpr int LDP = TO + 4;
   constexpr int PQ = TO / 4;                 // float4 columns of the P tile
-  constexpr int PG = 256 / PQ;               // P row groups (rows pr + PG*k)
+  constexpr int PG = NT / PQ;                // P row groups (rows pr + PG*k)
   constexpr int PITEMS = kWgRows / PG;
-  constexpr int QQ = kWgTI / 4, QG = 256 / QQ;
-  constexpr int NI = TO == 128 ? 2 : 1;      // 32-wide i-tiles per wave
+  constexpr int QQ = kWgTI / 4, QG = NT / QQ;
+  constexpr int QITEMS = kWgRows / QG;
+  // accumulators per wave: NJ 32-row o-tiles x NI 32-col i-tiles
+  constexpr int NJ = NW == 8 ? 1 : 2;
+  constexpr int NI = (NW == 4 && TO == 128) ? 2 : 1;
+  static_assert(NW == 4 || (NW == 8 && TO == 64), "engine shapes");
 
   const int chunk = blockIdx.x;
   const int tiles_i = (int)ceil_div(I, kWgTI);
@@ -87,8 +113,9 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
-  const int ob = TO == 128 ? 64 * (wave >> 1) : 0;      // wave's o origin in the tile
-  const int ib = TO == 128 ? 64 * (wave & 1) : 32 * wave;
+  // wave's o / i origin in the tile
+  const int ob = NW == 8 ? 32 * (wave >> 2) : (TO == 128 ? 64 * (wave >> 1) : 0);
+  const int ib = NW == 8 ? 32 * (wave & 3) : (TO == 128 ? 64 * (wave & 1) : 32 * wave);
   const bool bias_block = (i0 == 0);
 
   // staging coordinates: a thread always stages the same float4 column of P and of Q
@@ -102,30 +129,37 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   const int64_t r_begin = (int64_t)chunk * rows_per_chunk;
   const int64_t r_end = min<int64_t>(R, r_begin + rows_per_chunk);
 
-  wg_floatx16 acc[2][NI];
+  wg_floatx16 acc[NJ][NI];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int k = 0; k < NI; ++k)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][k][e] = 0.f;
   double bsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias partials of this thread's P column quad
 
-  Raw rp[PITEMS], rq[kWgQItems];
-  auto load = [&](int64_t n0) {
-#pragma unroll
-    for (int k = 0; k < PITEMS; ++k) {
-      const int64_t n = n0 + pr + PG * k;
-      rp[k] = src.template p_load<Z>(n < r_end ? n : r_end - 1, pqa);
-    }
-#pragma unroll
-    for (int k = 0; k < kWgQItems; ++k) {
+  Raw rp[PITEMS]{}, rq[QITEMS]{};
+  // raw operands of staged item j (P items first, then Q) for the sub-tile at row n0;
+  // rows past the chunk clamp to its last row (always issued: no branch around a load)
+  auto load_item = [&](int j, int64_t n0) {
+    if constexpr ((GINE_WG_VARIANT & 2) != 0) return;
+    if (j < PITEMS) {
+      const int64_t n = n0 + pr + PG * j;
+      rp[j] = src.template p_load<Z>(n < r_end ? n : r_end - 1, pqa);
+    } else {
+      const int k = j - PITEMS;
       const int64_t n = n0 + qr + QG * k;
       rq[k] = src.template q_load<Z>(n < r_end ? n : r_end - 1, qqa);
     }
   };
+  constexpr int NITEMS = PITEMS + QITEMS;     // <= 16: one per SP k-steps below
+  constexpr int SP = (kWgRows / 2) / NITEMS;
+  static_assert(SP >= 2, "at most one raw load per two k-steps");
 
-  if (r_begin < r_end) load(r_begin);
+  if (r_begin < r_end) {
+#pragma unroll
+    for (int j = 0; j < NITEMS; ++j) load_item(j, r_begin);
+  }
   for (int64_t n0 = r_begin; n0 < r_end; n0 += kWgRows) {
 #pragma unroll
     for (int k = 0; k < PITEMS; ++k) {
@@ -139,40 +173,61 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
       bsum[3] += (double)v.w;
     }
 #pragma unroll
-    for (int k = 0; k < kWgQItems; ++k) {
+    for (int k = 0; k < QITEMS; ++k) {
       const int r = qr + QG * k;
       float4 v = src.template q_xform<Z>(rq[k], qc);
       if (n0 + r >= r_end || !q_ok) v = f4_zero();
       *reinterpret_cast<float4*>(&sQ[r * kWgLdQ + 4 * qq]) = v;
     }
     __syncthreads();
-    if (n0 + kWgRows < r_end) load(n0 + kWgRows);  // raw operands of the next sub-tile
-    // lane half h contracts rows [32h, 32h+32): the same permutation for A and B
+    // MFMA chain over the 64 staged rows (lane half h contracts rows [32h, 32h+32): the
+    // same permutation for A and B).  The next sub-tile's raw loads are spread over the
+    // chain, one every other k-step: a wave that issued them all at once would stall on
+    // the memory queue before its first MFMA (no second wave on the SIMD to cover it).
+    // Each k-step's LDS operands are read one step ahead; sched_barrier keeps the order.
+    const int64_t n1 = n0 + kWgRows;
     const float* pa = &sP[(32 * h) * LDP + ob + c32];
     const float* qb = &sQ[(32 * h) * kWgLdQ + ib + c32];
+    float a[NJ], b[NI], an[NJ], bn[NI];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) a[j] = pa[32 * j];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) b[k] = qb[32 * k];
 #pragma unroll
     for (int s = 0; s < kWgRows / 2; ++s) {
-      float a[2], b[NI];
+      if (s + 1 < kWgRows / 2) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) a[j] = pa[s * LDP + 32 * j];
+        for (int j = 0; j < NJ; ++j) an[j] = pa[(s + 1) * LDP + 32 * j];
 #pragma unroll
-      for (int k = 0; k < NI; ++k) b[k] = qb[s * kWgLdQ + 32 * k];
+        for (int k = 0; k < NI; ++k) bn[k] = qb[(s + 1) * kWgLdQ + 32 * k];
+      }
+      if (s % SP == 0 && s / SP < NITEMS) load_item(s / SP, n1);
+      if constexpr ((GINE_WG_VARIANT & 1) == 0) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int k = 0; k < NI; ++k)
-          acc[j][k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[k], acc[j][k], 0, 0, 0);
+          for (int k = 0; k < NI; ++k)
+            acc[j][k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[k], acc[j][k], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) a[j] = an[j];
+#pragma unroll
+      for (int k = 0; k < NI; ++k) b[k] = bn[k];
     }
     __syncthreads();
   }
 
   float* out = slab + (size_t)Z * zstride + (size_t)chunk * cstride;
+  if constexpr ((GINE_WG_VARIANT & 4) != 0) {
+    if (acc[0][0][0] != 12345.f) return;  // keeps the accumulators live
+  }
 #pragma unroll
   for (int k = 0; k < NI; ++k) {
     const int i = i0 + ib + 32 * k + c32;
     if (i >= I) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int o = o0 + ob + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -180,6 +235,12 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
       }
     }
   }
+#if (GINE_WG_VARIANT & 8) != 0
+  if (threadIdx.x == 0 && blin < 4096) {
+    gine_wg_clock[blin][2] = __builtin_amdgcn_s_memtime();
+    gine_wg_clock[blin][3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   if (bias_block) {  // fixed-order sum of the row groups' partials through LDS
     double* sb = reinterpret_cast<double*>(sQ);  // [PG][TO], sQ is free after the loop
 #pragma unroll
@@ -187,6 +248,7 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
     __syncthreads();
     if ((int)threadIdx.x < TO && o0 + (int)threadIdx.x < O) {
       double t = 0.0;
+#pragma unroll 8
       for (int g = 0; g < PG; ++g) t += sb[g * TO + threadIdx.x];
       out[(size_t)O * I + o0 + threadIdx.x] = (float)t;
     }
@@ -200,8 +262,8 @@ __device__ __forceinline__ int wg_tiles(const Src& src, int O, int I, int TO) {
 }
 
 // grid = (chunks, sum over z of the product's output tiles); blockIdx.y -> (z, tile).
-template <class Src, int TO>
-__global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O, int I,
+template <class Src, int TO, int NW>
+__global__ __launch_bounds__(64 * NW) void k_wgrad_engine(Src src, int64_t R, int O, int I,
                                                       int rows_per_chunk, size_t zstride,
                                                       size_t cstride,
                                                       float* __restrict__ slab) {
@@ -210,7 +272,7 @@ __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O,
   int y = blockIdx.y;
   const int t0 = wg_tiles<Src, 0>(src, O, I, TO);
   if (y < t0) {
-    wgrad_body<Src, 0, TO>(src, R, O, src.template i_dim<0>(I), y, rows_per_chunk, zstride,
+    wgrad_body<Src, 0, TO, NW>(src, R, O, src.template i_dim<0>(I), y, rows_per_chunk, zstride,
                            cstride, slab, sP, sQ);
     return;
   }
@@ -218,7 +280,7 @@ __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O,
   if constexpr (Src::kZ > 1) {
     const int t1 = wg_tiles<Src, 1>(src, O, I, TO);
     if (y < t1) {
-      wgrad_body<Src, 1, TO>(src, R, O, src.template i_dim<1>(I), y, rows_per_chunk, zstride,
+      wgrad_body<Src, 1, TO, NW>(src, R, O, src.template i_dim<1>(I), y, rows_per_chunk, zstride,
                              cstride, slab, sP, sQ);
       return;
     }
@@ -227,14 +289,14 @@ __global__ __launch_bounds__(256) void k_wgrad_engine(Src src, int64_t R, int O,
   if constexpr (Src::kZ > 2) {
     const int t2 = wg_tiles<Src, 2>(src, O, I, TO);
     if (y < t2) {
-      wgrad_body<Src, 2, TO>(src, R, O, src.template i_dim<2>(I), y, rows_per_chunk, zstride,
+      wgrad_body<Src, 2, TO, NW>(src, R, O, src.template i_dim<2>(I), y, rows_per_chunk, zstride,
                              cstride, slab, sP, sQ);
       return;
     }
     y -= t2;
   }
   if constexpr (Src::kZ > 3) {
-    wgrad_body<Src, 3, TO>(src, R, O, src.template i_dim<3>(I), y, rows_per_chunk, zstride,
+    wgrad_body<Src, 3, TO, NW>(src, R, O, src.template i_dim<3>(I), y, rows_per_chunk, zstride,
                            cstride, slab, sP, sQ);
   }
 }
@@ -244,7 +306,9 @@ template <int TO, class Src>
 inline int launch_wgrad_engine(const Src& src, int64_t R, int O, int I, int total_tiles,
                                const WgPlan& p, size_t zstride, size_t cstride, float* slab,
                                hipStream_t s) {
-  hipLaunchKernelGGL((k_wgrad_engine<Src, TO>), dim3(p.chunks, total_tiles), dim3(256), 0, s,
+  constexpr int NW = TO == 64 ? kWgWaves64 : 4;
+  hipLaunchKernelGGL((k_wgrad_engine<Src, TO, NW>), dim3(p.chunks, total_tiles), dim3(64 * NW),
+                     0, s,
                      src, R, O, I, p.rows_per_chunk, zstride, cstride, slab);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
