@@ -86,11 +86,12 @@ int gine_mp_fwd(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
  *   dx_j   = sum over out-edges of j in original order of dm_e   (index_add_, bit-exact)
  *            [+ (1 + eps) * dz_j  if flags & GINE_MP_BWD_SELF]
  *            [+ dres_j            if dres != NULL]
- *   partials[b] (fp64, [3][D] per block b): sum dm*a, sum dm, sum dz*x for the block
+ *   partials[b] (fp64, a [3][D] row per block b): sum dm*a [D], sum dm [D], then the
+ *            block's sum over channels of dz*x (one value; the rest of the row unused)
  *   flags may also carry GINE_MP_LIN_MULADD (must match the forward).
  * gine_mp_bwd_finalize reduces the partials in fixed block order into
- *   dlin_w [D], dlin_b [D], deps [1].  Finalize calls reduce IN PLACE: the partials
- *   buffer is consumed (overwritten) -- true of every *_finalize below too.
+ *   dlin_w [D], dlin_b [D], deps [1] (one launch).  Finalize calls may reduce IN PLACE:
+ *   treat the partials buffer as consumed -- true of every *_finalize below too.
  * ---------------------------------------------------------------------------------- */
 #define GINE_MP_BWD_SELF 1
 int gine_mp_bwd_num_partials(int64_t num_nodes, int32_t channels, int32_t* num_partials);

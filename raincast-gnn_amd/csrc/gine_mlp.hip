@@ -26,6 +26,7 @@
 #include "gine_wgrad.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace gine {
 namespace {
@@ -369,9 +370,18 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
 }
 
 // Persistent grid: ~4 waves per CU (one wave per SIMD) on the 256 CUs of an MI355X.
+// Persistent grid.  GINE_ROWGEMM_BLOCKS (tuning experiments only) overrides the cap.
+inline int rowgemm_cap(int D) {
+  static const int env = [] {
+    const char* e = getenv("GINE_ROWGEMM_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  return env > 0 ? env : std::max(256, 1024 / (D / 32));
+}
+
 inline int rowgemm_grid(int64_t N, int D) {
   const int64_t tiles = ceil_div(N, kRowTile);
-  const int64_t cap = std::max(256, 1024 / (D / 32));
+  const int64_t cap = rowgemm_cap(D);
   const int64_t g = tiles < cap ? tiles : cap;
   return (int)(g > 0 ? g : 1);
 }
@@ -454,25 +464,6 @@ __global__ __launch_bounds__(kColsumThreads) void k_bn_fwd_finalize(
   }
 }
 
-__global__ __launch_bounds__(kColsumThreads) void k_bn_bwd_finalize(
-    const double* __restrict__ partials, int P, const float* __restrict__ gamma,
-    const float* __restrict__ bn_save, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ coef, int64_t N, int D, int training) {
-  __shared__ double s_tmp[kColsumThreads];
-  __shared__ double s_sum[2 * 256];  // [sum dbn | sum dbn*xhat]
-  block_colsum(partials, P, 2 * D, 2 * D * kSliceRows, s_tmp, s_sum);
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    const double sd = s_sum[c], sx = s_sum[D + c];
-    if (dgamma) dgamma[c] = (float)sx;
-    if (dbeta) dbeta[c] = (float)sd;
-    const double g = gamma ? (double)gamma[c] : 1.0;
-    const double c1 = g * (double)bn_save[D + c];
-    coef[c] = (float)c1;
-    coef[D + c] = training ? (float)(-c1 * sx / (double)N) : 0.f;
-    coef[2 * D + c] = training ? (float)(-c1 * sd / (double)N) : 0.f;
-  }
-}
-
 // ----------------------------------------------------------------------------------------
 // Weight gradients: dW[o][i] = sum_n P[n][o] * Q[n][i], db[o] = sum_n P[n][o]
 //   z = 0: P = do (PRO_DO of dy), Q = r = relu(bn(a1))  -> dW2, db2
@@ -528,6 +519,77 @@ struct MlpWgradOut {
   }
 };
 
+// Finish of the BatchNorm statistics (k_colsum_fin<4>): workgroup b owns channels 2b, 2b+1;
+// column j < 2 is the sum of a1 of channel 2b+j, j >= 2 its sum of squares.
+constexpr int kBnFinCh = 2;  // channels per finish workgroup
+struct BnFwdFin {
+  const float *gamma, *beta;
+  float *rmean, *rvar;
+  int64_t* nbt;
+  float* bn_save;
+  int64_t N;
+  int D;
+  float momentum, bn_eps;
+  int update_running;
+  __device__ int col(int b, int j) const {
+    const int c = kBnFinCh * b + (j % kBnFinCh);
+    if (c >= D) return -1;
+    return j < kBnFinCh ? c : D + c;
+  }
+  __device__ void finish(int b, const double* tot) const {
+    const int t = threadIdx.x;
+    if (b == 0 && t == 0 && update_running && nbt != nullptr) nbt[0] = nbt[0] + 1;
+    const int c = kBnFinCh * b + t;
+    if (t >= kBnFinCh || c >= D) return;
+    const double mean = tot[t] / (double)N;
+    double var = tot[kBnFinCh + t] / (double)N - mean * mean;
+    if (var < 0.0) var = 0.0;
+    if (update_running && rmean != nullptr) {  // momentum >= 0 here (None: other path)
+      const double f = (double)momentum;
+      const double unbiased = N > 1 ? var * (double)N / (double)(N - 1) : var;
+      rmean[c] = (float)(f * mean + (1.0 - f) * (double)rmean[c]);
+      rvar[c] = (float)(f * unbiased + (1.0 - f) * (double)rvar[c]);
+    }
+    const double invstd = 1.0 / sqrt(var + (double)bn_eps);
+    const double g = gamma ? (double)gamma[c] : 1.0;
+    const double bt = beta ? (double)beta[c] : 0.0;
+    const double alpha = g * invstd;
+    bn_save[c] = (float)mean;
+    bn_save[D + c] = (float)invstd;
+    bn_save[2 * D + c] = (float)alpha;
+    bn_save[3 * D + c] = (float)(bt - mean * alpha);
+  }
+};
+
+// Finish of the BatchNorm backward sums (k_colsum_fin<4>): column j < 2 = sum dbn of
+// channel 2b+j, j >= 2 = sum dbn * xhat.
+struct BnBwdFin {
+  const float* gamma;
+  const float* bn_save;
+  float *dgamma, *dbeta, *coef;
+  int64_t N;
+  int D;
+  int training;
+  __device__ int col(int b, int j) const {
+    const int c = kBnFinCh * b + (j % kBnFinCh);
+    if (c >= D) return -1;
+    return j < kBnFinCh ? c : D + c;
+  }
+  __device__ void finish(int b, const double* tot) const {
+    const int t = threadIdx.x;
+    const int c = kBnFinCh * b + t;
+    if (t >= kBnFinCh || c >= D) return;
+    const double sd = tot[t], sx = tot[kBnFinCh + t];
+    if (dgamma) dgamma[c] = (float)sx;
+    if (dbeta) dbeta[c] = (float)sd;
+    const double g = gamma ? (double)gamma[c] : 1.0;
+    const double c1 = g * (double)bn_save[D + c];
+    coef[c] = (float)c1;
+    coef[D + c] = training ? (float)(-c1 * sx / (double)N) : 0.f;
+    coef[2 * D + c] = training ? (float)(-c1 * sd / (double)N) : 0.f;
+  }
+};
+
 inline bool mlp_dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
 inline WgPlan mlp_wgrad_plan(int64_t N, int D) { return wg_plan(N, D, D, 2, 64); }
@@ -568,16 +630,26 @@ extern "C" int gine_bn_fwd_finalize(const double* partials, int32_t num_partials
   if (!training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
   if (update_running && training && (!running_mean || !running_var)) return GINE_ERR_INVALID;
   if (channels > 256) return GINE_ERR_DIM;
-  int S = 0;
-  if (training) {  // stage 1 of the partial reduction; stage 2 inside the finalize
-    S = launch_colsum_slices(const_cast<double*>(partials), num_partials, 2 * channels,
-                             as_stream(stream));
+  hipStream_t s = as_stream(stream);
+  const bool cumulative = training && update_running && momentum < 0.f;
+  if (training && !cumulative) {
+    // one launch: workgroup b owns two channels (their sums and sums of squares)
+    const BnFwdFin fin{gamma, beta, running_mean, running_var, num_batches_tracked, bn_save,
+                       num_nodes, channels, momentum, bn_eps, update_running};
+    hipLaunchKernelGGL((k_colsum_fin<2 * kBnFinCh, BnFwdFin>),
+                       dim3((unsigned)ceil_div(channels, kBnFinCh)),
+                       dim3(256), 0, s, partials, num_partials, 2 * channels, fin);
+    GINE_LAUNCH_STATUS();
+    return GINE_OK;
+  }
+  int S = num_partials;
+  if (training) {  // momentum=None: every channel needs the one num_batches_tracked bump
+    S = launch_colsum_slices(const_cast<double*>(partials), num_partials, 2 * channels, s);
     GINE_LAUNCH_STATUS();
   }
-  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3(1), dim3(kColsumThreads), 0, as_stream(stream),
-                     partials,
-                     S, gamma, beta, running_mean, running_var, num_batches_tracked,
-                     bn_save, num_nodes, channels, momentum, bn_eps, training, update_running);
+  hipLaunchKernelGGL(k_bn_fwd_finalize, dim3(1), dim3(kColsumThreads), 0, s, partials, S,
+                     gamma, beta, running_mean, running_var, num_batches_tracked, bn_save,
+                     num_nodes, channels, momentum, bn_eps, training, update_running);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
@@ -632,13 +704,10 @@ extern "C" int gine_bn_bwd_finalize(const double* partials, int32_t num_partials
   if (channels <= 0 || !partials || num_partials <= 0 || !bn_save || !coef || num_nodes <= 0)
     return GINE_ERR_INVALID;
   if (channels > 256) return GINE_ERR_DIM;
-  const int S = launch_colsum_slices(const_cast<double*>(partials), num_partials, 2 * channels,
-                                     as_stream(stream));
-  GINE_LAUNCH_STATUS();
-  hipLaunchKernelGGL(k_bn_bwd_finalize, dim3(1), dim3(kColsumThreads), 0, as_stream(stream),
-                     partials,
-                     S, gamma, bn_save, dgamma, dbeta, coef, num_nodes, channels,
-                     training);
+  const BnBwdFin fin{gamma, bn_save, dgamma, dbeta, coef, num_nodes, channels, training};
+  hipLaunchKernelGGL((k_colsum_fin<2 * kBnFinCh, BnBwdFin>),
+                     dim3((unsigned)ceil_div(channels, kBnFinCh)), dim3(256), 0,
+                     as_stream(stream), partials, num_partials, 2 * channels, fin);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

@@ -290,24 +290,35 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
     }
     __syncthreads();
   }
+  // row layout [dW_e (D) | db_e (D) | sum over channels of dz*x (1) | unused]
+  block_tree_sum(s_red + 2 * D, D);
   double* out = partials + (size_t)blockIdx.x * 3 * D;
-  for (int i = threadIdx.x; i < 3 * D; i += kThreads) out[i] = s_red[i];
+  for (int i = threadIdx.x; i <= 2 * D; i += kThreads) out[i] = s_red[i];
 }
 
-__global__ __launch_bounds__(kColsumThreads) void k_mp_bwd_finalize(
-    const double* __restrict__ partials, int S, int D, float* __restrict__ dlin_w,
-    float* __restrict__ dlin_b, float* __restrict__ deps) {
-  __shared__ double s_tmp[kColsumThreads];
-  extern __shared__ __attribute__((aligned(16))) double s_out[];  // [3D]
-  // stage 2: the S slice heads left by k_colsum_slices (row stride kSliceRows rows)
-  block_colsum(partials, S, 3 * D, 3 * D * kSliceRows, s_tmp, s_out);
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    dlin_w[c] = (float)s_out[c];
-    dlin_b[c] = (float)s_out[D + c];
+// Finish of the parameter-gradient partials (k_colsum_fin<4>): workgroups b < nb-1 own 4
+// of the 2D columns [dW_e | db_e]; the last one reduces the per-block eps column (2D).
+constexpr int kMpFinCols = 4;
+struct MpBwdFin {
+  float *dlin_w, *dlin_b, *deps;
+  int D, nb;
+  __device__ int col(int b, int j) const {
+    if (b == nb - 1) return j == 0 ? 2 * D : -1;
+    const int c = kMpFinCols * b + j;
+    return c < 2 * D ? c : -1;
   }
-  block_tree_sum(s_out + 2 * D, D);  // sum over channels of sum dz*x
-  if (threadIdx.x == 0) deps[0] = (float)s_out[2 * D];
-}
+  __device__ void finish(int b, const double* tot) const {
+    const int t = threadIdx.x;
+    if (b == nb - 1) {
+      if (t == 0) deps[0] = (float)tot[0];
+      return;
+    }
+    const int c = kMpFinCols * b + t;
+    if (t >= kMpFinCols || c >= 2 * D) return;
+    if (c < D) dlin_w[c] = (float)tot[t];
+    else dlin_b[c - D] = (float)tot[t];
+  }
+};
 
 // ----------------------------------------------------------------------------------------
 // Host dispatch
@@ -420,7 +431,9 @@ extern "C" int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_r
   const int D4 = channels / 4;
   const int grid = bwd_grid(num_nodes, sh);
   const int tiles = (int)ceil_div(num_nodes, nodes_per_block(sh));
-  const size_t smem = sizeof(double) * 3 * (size_t)channels;
+  int m = 1;
+  while (m < channels) m <<= 1;  // tree-sum scratch of the eps column
+  const size_t smem = sizeof(double) * (2 * (size_t)channels + (size_t)m);
   hipStream_t s = as_stream(stream);
   const bool fma = (flags & GINE_MP_LIN_MULADD) == 0;
 #define LAUNCH_BWD(L_, C_, F_)                                                               \
@@ -439,14 +452,10 @@ extern "C" int gine_mp_bwd_finalize(const double* partials, int32_t num_partials
                                     float* deps, void* stream) {
   if (num_partials < 0 || channels <= 0) return GINE_ERR_INVALID;
   if (!partials || !dlin_w || !dlin_b || !deps) return GINE_ERR_INVALID;
-  int m = 1;
-  while (m < channels) m <<= 1;  // tree-sum scratch beyond 3D
-  const size_t smem = sizeof(double) * (size_t)(2 * channels + m);
-  hipStream_t s = as_stream(stream);
-  const int S = launch_colsum_slices(const_cast<double*>(partials), num_partials, 3 * channels, s);
-  GINE_LAUNCH_STATUS();
-  hipLaunchKernelGGL(k_mp_bwd_finalize, dim3(1), dim3(kColsumThreads), smem, s, partials, S,
-                     channels, dlin_w, dlin_b, deps);
+  const int nb = (int)ceil_div(2 * channels, kMpFinCols) + 1;
+  const MpBwdFin fin{dlin_w, dlin_b, deps, channels, nb};
+  hipLaunchKernelGGL((k_colsum_fin<kMpFinCols, MpBwdFin>), dim3(nb), dim3(256), 0,
+                     as_stream(stream), partials, num_partials, 3 * channels, fin);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

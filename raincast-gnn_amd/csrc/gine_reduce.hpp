@@ -97,4 +97,45 @@ __device__ inline void block_tree_sum(double* v, int n) {
   }
 }
 
+// Single-launch fixed-order column reduction + finish.  Workgroup b reduces the COLS
+// columns fin.col(b, j) (j < COLS; -1 = none) of a row-major [P][ld] fp64 matrix: 256
+// threads = COLS columns x (256 / COLS) interleaved row groups, 4 independent accumulators
+// per thread, the group sums added in group order through LDS; then fin.finish(b, tot)
+// runs with tot[j] = total of column j (LDS, all threads of the workgroup).  Narrow
+// workgroups (few columns, many row groups) keep each thread's dependent chain short, so
+// one launch of many small workgroups replaces the slice + single-block two-launch form.
+template <int COLS, class Fin>
+__global__ __launch_bounds__(256) void k_colsum_fin(const double* __restrict__ a, int P, int ld,
+                                                    Fin fin) {
+  constexpr int G = 256 / COLS;
+  __shared__ double s_part[G][COLS];
+  __shared__ double s_tot[COLS];
+  const int j = threadIdx.x % COLS, g = threadIdx.x / COLS;
+  const int c = fin.col(blockIdx.x, j);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (c >= 0) {
+    const double* colp = a + c;
+    const size_t step = (size_t)G * ld;
+    int p = g;
+    for (; p + 3 * G < P; p += 4 * G) {
+      const double* r = colp + (size_t)p * ld;
+      a0 += r[0];
+      a1 += r[step];
+      a2 += r[2 * step];
+      a3 += r[3 * step];
+    }
+    for (; p < P; p += G) a0 += colp[(size_t)p * ld];
+  }
+  s_part[g][j] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (threadIdx.x < COLS) {
+    double t = 0.0;
+#pragma unroll 8
+    for (int k = 0; k < G; ++k) t += s_part[k][threadIdx.x];
+    s_tot[threadIdx.x] = t;
+  }
+  __syncthreads();
+  fin.finish(blockIdx.x, s_tot);
+}
+
 }  // namespace gine

@@ -40,6 +40,7 @@ for s in $STEPS; do
            python tools/pmc_summary.py "$OUT"/pmc_fetch/run_counter_collection.csv \
                "$OUT"/pmc_write/run_counter_collection.csv --traffic-json "$OUT/pmc_traffic.json" \
                > "$OUT/pmc_summary.txt" 2>&1 ;;
+    rgsweep) for g in 256 512 1024; do export GINE_ROWGEMM_BLOCKS=$g; run bench_rg$g 300 python bench.py --no-cpu --steps 30; done; unset GINE_ROWGEMM_BLOCKS ;;
     floor) run launch_floor 300 python tools/launch_floor.py ;;
     counters) run list_counters 300 rocprofv3 -L ;;
     dsmicro) run ds_micro 300 python tools/ds_micro.py ;;
