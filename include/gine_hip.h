@@ -102,6 +102,16 @@ int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_rowptr,
                 void* stream);
 int gine_mp_bwd_finalize(const double* partials, int32_t num_partials, int32_t channels,
                          float* dlin_w, float* dlin_b, float* deps, void* stream);
+/* gine_mp_bwd plus, in the same launch, the fixed-order reduction of the node-MLP
+ * weight-gradient slab that gine_mlp_bwd1_wgrad left when called with NULL dw1/db1/dw2/db2
+ * (wg_chunks = gine_mlp_wgrad_num_chunks(num_nodes, mlp_channels)); writes dw1, db1, dw2,
+ * db2 exactly as gine_mlp_wgrad would. */
+int gine_mp_bwd_side(const float* dz, const float* x, const int32_t* out_rowptr,
+                     const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                     const float* lin_b, const float* eps, const float* dres, float* dx,
+                     double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                     const float* wg_slab, int32_t wg_chunks, int32_t mlp_channels, float* dw1,
+                     float* db1, float* dw2, float* db2, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Node MLP  nn = Sequential(Linear(D,D), BatchNorm1d(D), ReLU(), Linear(D,D))
@@ -158,11 +168,20 @@ int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* mask, const f
                    float* slab, float* dw1, float* db1, float* dw2, float* db2,
                    int64_t num_nodes, int32_t channels, int32_t epilogue, void* stream);
 
+/* gine_mlp_bwd1 + gine_mlp_wgrad in one launch (same arguments as the two; the weight
+ * gradients and dz are computed side by side on the CUs).  Same results bit for bit. */
+int gine_mlp_bwd1_wgrad(const float* dy, const float* y, const uint8_t* mask, const float* a1,
+                        const float* bn_save, const float* dbn, const float* coef,
+                        const float* z, const float* w1, float* dz, float* slab, float* dw1,
+                        float* db1, float* dw2, float* db2, int64_t num_nodes,
+                        int32_t channels, int32_t epilogue, void* stream);
+
 /* ------------------------------------------------------------------------------------
  * AdamW over one flat fp32 parameter buffer (the optimizer of the benchmarked training
  * step, train.py:67-69 with torch.optim.AdamW, lr from params.json).  Bumps the device
- * step counter `step` (fp32 [1]) and updates param / exp_avg / exp_avg_sq in place with
- * torch.optim.AdamW's default (amsgrad=False) formulation.  Two launches, graph-safe.
+ * step counter `step` (fp32 [2]: the count, then a ticket word that must start at 0 and is
+ * left at 0) and updates param / exp_avg / exp_avg_sq in place with torch.optim.AdamW's
+ * default (amsgrad=False) formulation.  One launch, graph-safe.
  * ---------------------------------------------------------------------------------- */
 int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                     float* step, int64_t n, float lr, float beta1, float beta2, float eps,

@@ -129,9 +129,8 @@ struct EpiArgs {
 struct TileRange {
   int first, end, step;
 };
-__device__ __forceinline__ TileRange xcd_tile_range(int num_tiles) {
-  const int nb = gridDim.x;
-  const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
+__device__ __forceinline__ TileRange xcd_tile_range(int num_tiles, int vb, int nb) {
+  const int xcd = vb % kNumXcd, pos = vb / kNumXcd;
   const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
   const int span = (num_tiles + kNumXcd - 1) / kNumXcd;
   const int b = xcd * span;
@@ -229,9 +228,12 @@ __device__ __forceinline__ float4 transform(const ProArgs& p, const RawItem& r,
 // are loaded into registers before this tile's 64-long MFMA chain, so HBM latency hides
 // under the matrix pipe instead of serialising with it.
 // ----------------------------------------------------------------------------------------
+// One persistent workgroup (virtual index vb of vgrid) of the row-tile GEMM; s_x: LDS of
+// kRowTile * (D + 4) floats.
 template <int D, int PRO, int EPI, bool BT>
-__global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, ProArgs pa,
-                                                   EpiArgs ea, int64_t N, int num_tiles) {
+__device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const ProArgs& pa,
+                                             const EpiArgs& ea, int64_t N, int num_tiles,
+                                             float* __restrict__ s_x, int vb, int vgrid) {
   constexpr int NT = 2 * D;      // threads: D/32 waves
   constexpr int KS = D / 2;      // k-steps per lane half
   constexpr int LD = D + 4;      // padded LDS row (floats)
@@ -240,7 +242,6 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
   constexpr int RSTEP = NT / D4;             // row step between a thread's items (= 8)
   constexpr bool IS_OUT = (EPI == EPI_OUT) || (EPI == EPI_OUT_RELU) || (EPI == EPI_OUT_RES);
   constexpr bool EPI_LOAD = (EPI == EPI_DBN) || (EPI == EPI_OUT_RES);
-  __shared__ __attribute__((aligned(16))) float s_x[kRowTile * LD];
 
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
     }
   };
 
-  const TileRange tr = xcd_tile_range(num_tiles);
+  const TileRange tr = xcd_tile_range(num_tiles, vb, vgrid);
   RawItem raw[ITEMS];
   if (tr.first < tr.end) load_tile(tr.first, raw);
   for (int tile = tr.first; tile < tr.end; tile += tr.step) {
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
     st1 += shfl_xor_d(st1, 32);
     st2 += shfl_xor_d(st2, 32);
     if (h == 0) {
-      double* p = ea.partials + (size_t)blockIdx.x * 2 * D;
+      double* p = ea.partials + (size_t)vb * 2 * D;
       p[col] = st1;
       p[D + col] = st2;
     }
@@ -370,6 +371,13 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
 }
 
 // Persistent grid: ~4 waves per CU (one wave per SIMD) on the 256 CUs of an MI355X.
+template <int D, int PRO, int EPI, bool BT>
+__global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, ProArgs pa,
+                                                   EpiArgs ea, int64_t N, int num_tiles) {
+  __shared__ __attribute__((aligned(16))) float s_x[kRowTile * (D + 4)];
+  rowgemm_body<D, PRO, EPI, BT>(W, pa, ea, N, num_tiles, s_x, blockIdx.x, gridDim.x);
+}
+
 // Persistent grid.  GINE_ROWGEMM_BLOCKS (tuning experiments only) overrides the cap.
 inline int rowgemm_cap(int D) {
   static const int env = [] {
@@ -504,20 +512,6 @@ struct MlpWgradSrc {
   }
 };
 
-// Destination of the reduced slabs: z = 0 -> dW2 | db2, z = 1 -> dW1 | db1.
-struct MlpWgradOut {
-  float *dw2, *db2, *dw1, *db1;
-  int D;
-  __device__ void operator()(int z, int64_t e, double v) const {
-    float* w = z == 0 ? dw2 : dw1;
-    float* b = z == 0 ? db2 : db1;
-    if (e < (int64_t)D * D) {
-      if (w) w[e] = (float)v;
-    } else if (b) {
-      b[e - (int64_t)D * D] = (float)v;
-    }
-  }
-};
 
 // Finish of the BatchNorm statistics (k_colsum_fin<4>): workgroup b owns channels 2b, 2b+1;
 // column j < 2 is the sum of a1 of channel 2b+j, j >= 2 its sum of squares.
@@ -589,6 +583,31 @@ struct BnBwdFin {
     coef[2 * D + c] = training ? (float)(-c1 * sd / (double)N) : 0.f;
   }
 };
+
+// Backward GEMM dz = da1 W1 and the weight gradients (dW1, dW2, biases) in ONE launch: they
+// read the same inputs (dy, the ReLU mask, a1, dbn, z) and are independent, so the first
+// eng_blocks workgroups run the weight-gradient engine (the longer job starts first) and
+// the rest run the row-tile GEMM, sharing the CUs instead of taking two launches.  D = 128
+// (both parts then use 256-thread workgroups).
+template <int PDO>
+__global__ __launch_bounds__(256) void k_bwd1_wgrad(const float* __restrict__ w1, ProArgs pa,
+                                                    EpiArgs ea, int64_t N, int num_tiles,
+                                                    int rg_grid, MlpWgradSrc<PDO> src,
+                                                    int chunks, int rows_per_chunk,
+                                                    size_t zstride, size_t cstride,
+                                                    float* __restrict__ slab, int eng_blocks) {
+  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (64 + 4)];
+  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
+  const int b = blockIdx.x;
+  if (b < eng_blocks) {
+    wgrad_block<MlpWgradSrc<PDO>, 64, 4>(src, N, 128, 128, b % chunks, b / chunks,
+                                         rows_per_chunk, zstride, cstride, slab, sP, sQ);
+  } else {
+    static_assert(kRowTile * (128 + 4) <= kWgRows * kWgLdQ, "row tile fits in sQ");
+    rowgemm_body<128, PRO_DA1, EPI_PLAIN, false>(w1, pa, ea, N, num_tiles, sQ,
+                                                 b - eng_blocks, rg_grid);
+  }
+}
 
 inline bool mlp_dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
@@ -763,6 +782,50 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   }
   if (st != GINE_OK) return st;
   if (st != GINE_OK) return st;
+  return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 2,
+                         MlpWgradOut{dw2, db2, dw1, db1, D}, s);
+}
+
+extern "C" int gine_mlp_bwd1_wgrad(const float* dy, const float* y, const uint8_t* mask,
+                                   const float* a1, const float* bn_save, const float* dbn,
+                                   const float* coef, const float* z, const float* w1, float* dz,
+                                   float* slab, float* dw1, float* db1, float* dw2, float* db2,
+                                   int64_t num_nodes, int32_t channels, int32_t epilogue,
+                                   void* stream) {
+  if (channels != 128) {  // fused launch for the 256-thread shapes; two launches otherwise
+    int rc = gine_mlp_bwd1(dbn, a1, bn_save, coef, w1, dz, num_nodes, channels, stream);
+    if (rc != GINE_OK) return rc;
+    return gine_mlp_wgrad(dy, y, mask, a1, bn_save, dbn, coef, z, slab, dw1, db1, dw2, db2,
+                          num_nodes, channels, epilogue, stream);
+  }
+  if (num_nodes <= 0 || !dy || !a1 || !bn_save || !dbn || !coef || !z || !w1 || !dz || !slab)
+    return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
+  const int D = channels;
+  const ProArgs pa{dbn, a1, nullptr, bn_save, coef};
+  const EpiArgs ea{nullptr, dz, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  const ProArgs p_do{dy, y, mask, nullptr, nullptr};
+  const ProArgs q_r{a1, nullptr, nullptr, bn_save, nullptr};
+  const ProArgs p_da1{dbn, a1, nullptr, bn_save, coef};
+  const ProArgs q_z{z, nullptr, nullptr, nullptr, nullptr};
+  const WgPlan p = mlp_wgrad_plan(num_nodes, D);
+  const size_t per = (size_t)D * D + D;
+  const int eng = p.chunks * 2 * p.tiles_o * p.tiles_i;
+  const int rg = rowgemm_grid(num_nodes, D);
+  const int tiles = (int)ceil_div(num_nodes, kRowTile);
+  hipStream_t s = as_stream(stream);
+#define BWD1_WGRAD(PD)                                                                        \
+  hipLaunchKernelGGL(k_bwd1_wgrad<PD>, dim3(eng + rg), dim3(256), 0, s, w1, pa, ea, num_nodes, \
+                     tiles, rg, MlpWgradSrc<PD>{p_do, q_r, p_da1, q_z, D}, p.chunks,           \
+                     p.rows_per_chunk, per * p.chunks, per, slab, eng)
+  if (epilogue == GINE_EPI_NONE) BWD1_WGRAD(PRO_PLAIN);
+  else if (epilogue == GINE_EPI_RELU) BWD1_WGRAD(PRO_DOR);
+  else BWD1_WGRAD(PRO_DOM);
+#undef BWD1_WGRAD
+  GINE_LAUNCH_STATUS();
+  if (!dw1 && !dw2 && !db1 && !db2) return GINE_OK;  // slab left for gine_mp_bwd_side
   return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 2,
                          MlpWgradOut{dw2, db2, dw1, db1, D}, s);
 }

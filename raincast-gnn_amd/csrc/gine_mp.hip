@@ -17,6 +17,7 @@
 // bit-identical to CPU scatter_add_ / index_add_.
 #include "gine_common.hpp"
 #include "gine_reduce.hpp"
+#include "gine_slab.hpp"
 
 namespace gine {
 namespace {
@@ -133,12 +134,19 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
     const float* __restrict__ attr, const float4* __restrict__ lw4,
     const float4* __restrict__ lb4, const float* __restrict__ eps,
     const float4* __restrict__ dres4, float4* __restrict__ dx4, double* __restrict__ partials,
-    int64_t N, int D4, int num_tiles, int flags) {
+    int64_t N, int D4, int num_tiles, int flags, MlpSlabJob job) {
   constexpr int GPW = kWave / L;
   constexpr int U = MpUnroll<C>::value;
   __shared__ int32_t s_nbr[kWaves][kWave];
   __shared__ float s_attr[kWaves][kWave];
   extern __shared__ __attribute__((aligned(16))) double s_red[];  // [3][D]
+  // side job: the first job.nblocks workgroups reduce the preceding weight-gradient slabs
+  if ((int)blockIdx.x < job.nblocks) {
+    __shared__ double s_job[kSlabGroups][kSlabQuads * 4 + 1];
+    job.run(blockIdx.x, s_job);
+    return;
+  }
+  const int vb = blockIdx.x - job.nblocks, nb = gridDim.x - job.nblocks;
 
   const int D = D4 * 4;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
@@ -161,8 +169,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
   float* my_attr = &s_attr[wave][g * L];
 
   // Tiles are split into 8 contiguous XCD ranges; the blocks of one XCD stride its range.
-  const int nb = gridDim.x;
-  const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
+  const int xcd = vb % kNumXcd, pos = vb / kNumXcd;
   const int blocks_here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
   const int span = (num_tiles + kNumXcd - 1) / kNumXcd;
   const int t_begin = xcd * span, t_end = min(num_tiles, t_begin + span);
@@ -292,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
   }
   // row layout [dW_e (D) | db_e (D) | sum over channels of dz*x (1) | unused]
   block_tree_sum(s_red + 2 * D, D);
-  double* out = partials + (size_t)blockIdx.x * 3 * D;
+  double* out = partials + (size_t)vb * 3 * D;
   for (int i = threadIdx.x; i <= 2 * D; i += kThreads) out[i] = s_red[i];
 }
 
@@ -416,11 +423,11 @@ extern "C" int gine_mp_bwd_num_partials(int64_t num_nodes, int32_t channels,
   return GINE_OK;
 }
 
-extern "C" int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_rowptr,
-                           const int32_t* out_dst, const float* out_attr, const float* lin_w,
-                           const float* lin_b, const float* eps, const float* dres, float* dx,
-                           double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
-                           void* stream) {
+static int mp_bwd_launch(const float* dz, const float* x, const int32_t* out_rowptr,
+                         const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                         const float* lin_b, const float* eps, const float* dres, float* dx,
+                         double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                         const MlpSlabJob& job, void* stream) {
   Shape sh;
   if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
   if (num_nodes < 0 || (flags & ~(GINE_MP_BWD_SELF | GINE_MP_LIN_MULADD)) != 0)
@@ -437,14 +444,42 @@ extern "C" int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_r
   hipStream_t s = as_stream(stream);
   const bool fma = (flags & GINE_MP_LIN_MULADD) == 0;
 #define LAUNCH_BWD(L_, C_, F_)                                                               \
-  hipLaunchKernelGGL((k_mp_bwd<L_, C_, F_>), dim3((unsigned)grid), dim3(kThreads), smem, s,     \
-                     (const float4*)dz, (const float4*)x, out_rowptr, out_dst, out_attr,     \
-                     (const float4*)lin_w, (const float4*)lin_b, eps, (const float4*)dres,   \
-                     (float4*)dx, partials, num_nodes, D4, tiles, flags)
+  hipLaunchKernelGGL((k_mp_bwd<L_, C_, F_>), dim3((unsigned)(grid + job.nblocks)),            \
+                     dim3(kThreads), smem, s, (const float4*)dz, (const float4*)x, out_rowptr,  \
+                     out_dst, out_attr, (const float4*)lin_w, (const float4*)lin_b, eps,       \
+                     (const float4*)dres, (float4*)dx, partials, num_nodes, D4, tiles, flags,  \
+                     job)
   GINE_MP_DISPATCH(sh, fma, LAUNCH_BWD);
 #undef LAUNCH_BWD
   GINE_LAUNCH_STATUS();
   return GINE_OK;
+}
+
+extern "C" int gine_mp_bwd(const float* dz, const float* x, const int32_t* out_rowptr,
+                           const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                           const float* lin_b, const float* eps, const float* dres, float* dx,
+                           double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                           void* stream) {
+  const MlpSlabJob none{nullptr, 0, 0, 0, MlpWgradOut{nullptr, nullptr, nullptr, nullptr, 0}};
+  return mp_bwd_launch(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps, dres, dx,
+                       partials, num_nodes, channels, flags, none, stream);
+}
+
+extern "C" int gine_mp_bwd_side(const float* dz, const float* x, const int32_t* out_rowptr,
+                                const int32_t* out_dst, const float* out_attr,
+                                const float* lin_w, const float* lin_b, const float* eps,
+                                const float* dres, float* dx, double* partials,
+                                int64_t num_nodes, int32_t channels, int32_t flags,
+                                const float* wg_slab, int32_t wg_chunks, int32_t mlp_channels,
+                                float* dw1, float* db1, float* dw2, float* db2, void* stream) {
+  if (!wg_slab || wg_chunks <= 0 || mlp_channels <= 0) return GINE_ERR_INVALID;
+  const int64_t per = (int64_t)mlp_channels * mlp_channels + mlp_channels;
+  if (per % 4 != 0 || (reinterpret_cast<uintptr_t>(wg_slab) & 15) != 0) return GINE_ERR_INVALID;
+  const int cols = (int)ceil_div(per, kSlabQuads * 4);
+  const MlpSlabJob job{wg_slab, wg_chunks, cols, 2 * cols,
+                       MlpWgradOut{dw2, db2, dw1, db1, mlp_channels}};
+  return mp_bwd_launch(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps, dres, dx,
+                       partials, num_nodes, channels, flags, job, stream);
 }
 
 extern "C" int gine_mp_bwd_finalize(const double* partials, int32_t num_partials,

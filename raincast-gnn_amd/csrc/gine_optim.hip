@@ -9,21 +9,22 @@
 //   m   = m + (1-b1)*(g - m)                 (lerp, weight < 0.5 branch)
 //   v   = v*b2 + (1-b2)*g*g
 //   p  += -(lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
-// The step counter lives on the device (a separate 1-thread launch bumps it first), so the
-// update is legal inside a captured HIP graph and replays correctly.
+// The step counter lives on the device, so the update is legal inside a captured HIP graph
+// and replays correctly: every workgroup uses step[0] + 1, and the workgroup that finishes
+// last (ticket in step[1]; by then every workgroup has read step[0]) stores the bump and
+// re-arms the ticket -- one launch per optimizer step.
 #include "gine_common.hpp"
 
 namespace gine {
 namespace {
 
-__global__ void k_adamw_tick(float* __restrict__ step) { step[0] = step[0] + 1.0f; }
-
 __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                float* __restrict__ m, float* __restrict__ v,
-                                               const float* __restrict__ step, int64_t n,
+                                               float* __restrict__ step, int64_t n,
                                                float lr, float beta1, float beta2, float eps,
                                                float weight_decay) {
-  const double t = (double)step[0];
+  const float t_new = step[0] + 1.0f;
+  const double t = (double)t_new;
   const float decay = (float)(1.0 - (double)lr * (double)weight_decay);
   const float neg_step_size = (float)(-((double)lr / (1.0 - pow((double)beta1, t))));
   const float bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, t));
@@ -43,6 +44,14 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
     m[i] = mi;
     v[i] = vi;
   }
+  __syncthreads();  // every thread of this workgroup has read step[0]
+  if (threadIdx.x == 0) {
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(&step[1]);  // 0.0f == 0u
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      step[0] = t_new;
+      *ticket = 0u;
+    }
+  }
 }
 
 }  // namespace
@@ -57,11 +66,9 @@ extern "C" int gine_adamw_step(float* param, const float* grad, float* exp_avg,
   if (n < 0 || !step) return GINE_ERR_INVALID;
   if (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)) return GINE_ERR_INVALID;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(k_adamw_tick, dim3(1), dim3(1), 0, s, step);
-  GINE_LAUNCH_STATUS();
-  if (n == 0) return GINE_OK;
-  int64_t blocks = ceil_div(n, 256);
-  if (blocks > 2048) blocks = 2048;
+  // grid-stride over at most 256 workgroups: few tickets to serialise on one word
+  int64_t blocks = ceil_div(n > 0 ? n : 1, 256);
+  if (blocks > 256) blocks = 256;
   hipLaunchKernelGGL(k_adamw, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg,
                      exp_avg_sq, step, n, lr, beta1, beta2, eps, weight_decay);
   GINE_LAUNCH_STATUS();

@@ -15,14 +15,15 @@ namespace gine {
 constexpr int kSlabQuads = 32;   // float4 quads per workgroup
 constexpr int kSlabGroups = 8;   // interleaved chunk groups per workgroup
 
+// One workgroup (column block bx of product z); s_part: kSlabGroups x (4*kSlabQuads+1)
+// doubles of LDS.
 template <bool VEC, class Out>
-__global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab, int chunks,
-                                                  int64_t per, size_t cstride, size_t zstride,
-                                                  Out out) {
-  __shared__ double s_part[kSlabGroups][kSlabQuads * 4 + 1];
+__device__ __forceinline__ void slab_sum_block(const float* __restrict__ slab, int chunks,
+                                               int64_t per, size_t cstride, size_t zstride,
+                                               const Out& out, int bx, int z,
+                                               double (*s_part)[kSlabQuads * 4 + 1]) {
   const int q = threadIdx.x % kSlabQuads, g = threadIdx.x / kSlabQuads;
-  const int z = blockIdx.y;
-  const int64_t e0 = ((int64_t)blockIdx.x * kSlabQuads + q) * 4;
+  const int64_t e0 = ((int64_t)bx * kSlabQuads + q) * 4;
   const float* base = slab + (size_t)z * zstride;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (e0 < per) {
@@ -55,13 +56,52 @@ __global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab
   __syncthreads();
   if (threadIdx.x >= kSlabQuads * 4) return;
   const int j = threadIdx.x;
-  const int64_t e = (int64_t)blockIdx.x * kSlabQuads * 4 + j;
+  const int64_t e = (int64_t)bx * kSlabQuads * 4 + j;
   if (e >= per) return;
   double v = 0.0;
 #pragma unroll
   for (int k = 0; k < kSlabGroups; ++k) v += s_part[k][j];
   out(z, e, v);
 }
+
+template <bool VEC, class Out>
+__global__ __launch_bounds__(256) void k_slab_sum(const float* __restrict__ slab, int chunks,
+                                                  int64_t per, size_t cstride, size_t zstride,
+                                                  Out out) {
+  __shared__ double s_part[kSlabGroups][kSlabQuads * 4 + 1];
+  slab_sum_block<VEC, Out>(slab, chunks, per, cstride, zstride, out, blockIdx.x, blockIdx.y,
+                           s_part);
+}
+
+// Destination of the node-MLP weight-gradient slabs: z = 0 -> dW2 | db2, z = 1 -> dW1 | db1.
+struct MlpWgradOut {
+  float *dw2, *db2, *dw1, *db1;
+  int D;
+  __device__ void operator()(int z, int64_t e, double v) const {
+    float* w = z == 0 ? dw2 : dw1;
+    float* b = z == 0 ? db2 : db1;
+    if (e < (int64_t)D * D) {
+      if (w) w[e] = (float)v;
+    } else if (b) {
+      b[e - (int64_t)D * D] = (float)v;
+    }
+  }
+};
+
+// The node-MLP slab reduction run as extra workgroups of another launch (gine_mp_bwd_side):
+// block b < nblocks reduces column block b % cols of product b / cols.
+struct MlpSlabJob {
+  const float* slab;
+  int chunks;
+  int cols;     // column blocks per product
+  int nblocks;  // 2 * cols, or 0 = no job
+  MlpWgradOut out;
+  __device__ void run(int b, double (*s_part)[kSlabQuads * 4 + 1]) const {
+    const int64_t per = (int64_t)out.D * out.D + out.D;
+    slab_sum_block<true, MlpWgradOut>(slab, chunks, per, (size_t)per, (size_t)per * chunks, out,
+                                      b % cols, b / cols, s_part);
+  }
+};
 
 template <class Out>
 inline int launch_slab_sum(const float* slab, int chunks, int64_t per, size_t cstride,

@@ -82,14 +82,14 @@ inline WgPlan wg_plan(int64_t R, int O, int I, int Z, int TO, int total_tiles = 
 // TO = 64:  wave w holds i-columns [32w, 32w+32) x all 64 o-rows (2x1 accumulators; twice
 //           the workgroups for a single product).
 template <class Src, int Z, int TO, int NW>
-__device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int I, int tile,
-                                           int rows_per_chunk, size_t zstride,
+__device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int I, int chunk,
+                                           int tile, int rows_per_chunk, size_t zstride,
                                            size_t cstride, float* __restrict__ slab,
                                            float* __restrict__ sP, float* __restrict__ sQ) {
   using Raw = typename Src::Raw;
   using Col = typename Src::Col;
 #if (GINE_WG_VARIANT & 8) != 0
-  const int blin = blockIdx.x + gridDim.x * blockIdx.y;
+  const int blin = blockIdx.x + gridDim.x * blockIdx.y + gridDim.x * gridDim.y * blockIdx.z;
   if (threadIdx.x == 0 && blin < 4096) {
     gine_wg_clock[blin][0] = __builtin_amdgcn_s_memtime();
     gine_wg_clock[blin][1] = __builtin_amdgcn_s_memrealtime();
@@ -107,7 +107,6 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   constexpr int NI = (NW == 4 && TO == 128) ? 2 : 1;
   static_assert(NW == 4 || (NW == 8 && TO == 64), "engine shapes");
 
-  const int chunk = blockIdx.x;
   const int tiles_i = (int)ceil_div(I, kWgTI);
   const int o0 = (tile / tiles_i) * TO, i0 = (tile % tiles_i) * kWgTI;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -261,27 +260,25 @@ __device__ __forceinline__ int wg_tiles(const Src& src, int O, int I, int TO) {
   return (int)(ceil_div(O, TO) * ceil_div(src.template i_dim<Z>(I), kWgTI));
 }
 
-// grid = (chunks, sum over z of the product's output tiles); blockIdx.y -> (z, tile).
+// One engine workgroup: output tile y of the concatenated per-product tile lists, rows of
+// chunk `chunk`.  sP / sQ: kWgRows * (TO + 4) and kWgRows * kWgLdQ floats of LDS.
 template <class Src, int TO, int NW>
-__global__ __launch_bounds__(64 * NW) void k_wgrad_engine(Src src, int64_t R, int O, int I,
-                                                      int rows_per_chunk, size_t zstride,
-                                                      size_t cstride,
-                                                      float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (TO + 4)];
-  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
-  int y = blockIdx.y;
+__device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, int I, int chunk,
+                                            int y, int rows_per_chunk, size_t zstride,
+                                            size_t cstride, float* __restrict__ slab,
+                                            float* sP, float* sQ) {
   const int t0 = wg_tiles<Src, 0>(src, O, I, TO);
   if (y < t0) {
-    wgrad_body<Src, 0, TO, NW>(src, R, O, src.template i_dim<0>(I), y, rows_per_chunk, zstride,
-                           cstride, slab, sP, sQ);
+    wgrad_body<Src, 0, TO, NW>(src, R, O, src.template i_dim<0>(I), chunk, y, rows_per_chunk,
+                               zstride, cstride, slab, sP, sQ);
     return;
   }
   y -= t0;
   if constexpr (Src::kZ > 1) {
     const int t1 = wg_tiles<Src, 1>(src, O, I, TO);
     if (y < t1) {
-      wgrad_body<Src, 1, TO, NW>(src, R, O, src.template i_dim<1>(I), y, rows_per_chunk, zstride,
-                             cstride, slab, sP, sQ);
+      wgrad_body<Src, 1, TO, NW>(src, R, O, src.template i_dim<1>(I), chunk, y,
+                                 rows_per_chunk, zstride, cstride, slab, sP, sQ);
       return;
     }
     y -= t1;
@@ -289,16 +286,28 @@ __global__ __launch_bounds__(64 * NW) void k_wgrad_engine(Src src, int64_t R, in
   if constexpr (Src::kZ > 2) {
     const int t2 = wg_tiles<Src, 2>(src, O, I, TO);
     if (y < t2) {
-      wgrad_body<Src, 2, TO, NW>(src, R, O, src.template i_dim<2>(I), y, rows_per_chunk, zstride,
-                             cstride, slab, sP, sQ);
+      wgrad_body<Src, 2, TO, NW>(src, R, O, src.template i_dim<2>(I), chunk, y,
+                                 rows_per_chunk, zstride, cstride, slab, sP, sQ);
       return;
     }
     y -= t2;
   }
   if constexpr (Src::kZ > 3) {
-    wgrad_body<Src, 3, TO, NW>(src, R, O, src.template i_dim<3>(I), y, rows_per_chunk, zstride,
-                           cstride, slab, sP, sQ);
+    wgrad_body<Src, 3, TO, NW>(src, R, O, src.template i_dim<3>(I), chunk, y, rows_per_chunk,
+                               zstride, cstride, slab, sP, sQ);
   }
+}
+
+// grid = (chunks, sum over z of the product's output tiles); blockIdx.y -> (z, tile).
+template <class Src, int TO, int NW>
+__global__ __launch_bounds__(64 * NW) void k_wgrad_engine(Src src, int64_t R, int O, int I,
+                                                          int rows_per_chunk, size_t zstride,
+                                                          size_t cstride,
+                                                          float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (TO + 4)];
+  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
+  wgrad_block<Src, TO, NW>(src, R, O, I, blockIdx.x, blockIdx.y, rows_per_chunk, zstride,
+                           cstride, slab, sP, sQ);
 }
 
 // Z must equal Src::kZ; total_tiles = sum of the products' output tiles (the plan's).

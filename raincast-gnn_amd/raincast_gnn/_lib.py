@@ -37,6 +37,8 @@ _SIGNATURES = {
     "gine_mp_fwd": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
     "gine_mp_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mp_bwd": [_c_void_p] * 11 + [_i64, _i32, _i32, _c_void_p],
+    "gine_mp_bwd_side": [_c_void_p] * 11 + [_i64, _i32, _i32, _c_void_p, _i32, _i32]
+                        + [_c_void_p] * 5,
     "gine_mp_bwd_finalize": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "gine_mlp_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_fwd1": [_c_void_p] * 5 + [_i64, _i32, _c_void_p],
@@ -48,6 +50,7 @@ _SIGNATURES = {
     "gine_mlp_bwd1": [_c_void_p] * 6 + [_i64, _i32, _c_void_p],
     "gine_mlp_wgrad_num_chunks": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_wgrad": [_c_void_p] * 13 + [_i64, _i32, _i32, _c_void_p],
+    "gine_mlp_bwd1_wgrad": [_c_void_p] * 15 + [_i64, _i32, _i32, _c_void_p],
     "gine_adamw_step": [_c_void_p] * 5 + [_i64, _f32, _f32, _f32, _f32, _f32, _c_void_p],
     "gine_crps_num_partials": [_i64, ctypes.POINTER(_i32)],
     "gine_crps_fwd": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64, _c_void_p,

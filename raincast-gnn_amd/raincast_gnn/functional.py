@@ -90,9 +90,11 @@ def mp_forward(x, graph, lin_w, lin_b, eps, lin_flag=None):
 
 
 def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_flag=None,
-                params=(None, None, None)):
+                params=(None, None, None), side=None):
     """Returns (dx, dlin_w, dlin_b, deps); ``params`` = the (lin.weight, lin.bias, eps)
-    Parameters, whose gradients then go straight to their flat-buffer slices if any."""
+    Parameters, whose gradients then go straight to their flat-buffer slices if any.
+    ``side`` = (slab, chunks, D, dw1, db1, dw2, db2): a node-MLP weight-gradient slab left
+    by gine_mlp_bwd1_wgrad, reduced by extra workgroups of the same launch."""
     N, D = x.shape
     dev = x.device
     dx = torch.empty_like(x)
@@ -107,9 +109,16 @@ def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_
     stream = _lib.stream_handle(dev)
     flags = (_lib.GINE_MP_BWD_SELF if self_term else 0) | (
         edge_linear_flag() if lin_flag is None else lin_flag)
-    call("gine_mp_bwd", ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst),
-         ptr(graph.out_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx),
-         ptr(partials), N, D, flags, stream)
+    if side is None:
+        call("gine_mp_bwd", ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst),
+             ptr(graph.out_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx),
+             ptr(partials), N, D, flags, stream)
+    else:
+        slab, chunks, Dm, dw1, db1, dw2, db2 = side
+        call("gine_mp_bwd_side", ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst),
+             ptr(graph.out_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx),
+             ptr(partials), N, D, flags, ptr(slab), chunks, Dm, ptr(dw1), ptr(db1), ptr(dw2),
+             ptr(db2), stream)
     call("gine_mp_bwd_finalize", ptr(partials), P, D, ptr(dlw), ptr(dlb), ptr(deps), stream)
     return dx, dlw, dlb, deps
 
@@ -219,18 +228,19 @@ class GineLayer(torch.autograd.Function):
         call("gine_bn_bwd_finalize", ptr(partials), P, ptr(g), ptr(bn_save), ptr(dgamma),
              ptr(dbeta), ptr(coef), N, D, int(ctx.use_batch_stats), stream)
         dz = torch.empty_like(x)
-        call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save), ptr(coef), ptr(w1c), ptr(dz), N,
-             D, stream)
         C = _count("gine_mlp_wgrad_num_chunks", N, D)
         slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
         dw1, db1 = grad_out(p_w1, (D, D), dev), grad_out(p_b1, (D,), dev)
         dw2, db2 = grad_out(p_w2, (D, D), dev), grad_out(p_b2, (D,), dev)
-        call("gine_mlp_wgrad", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save), ptr(dbn),
-             ptr(coef), ptr(z), ptr(slab), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), N, D, epi,
-             stream)
+        # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch; the slabs
+        # are reduced by extra workgroups of the message-passing backward launch
+        call("gine_mlp_bwd1_wgrad", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save),
+             ptr(dbn), ptr(coef), ptr(z), ptr(w1c), ptr(dz), ptr(slab), None, None, None,
+             None, N, D, epi, stream)
         dres = dy if epi == EPI_RESIDUAL_RELU else None
         dx, dlw, dlb, deps = mp_backward(dz, x, ctx.graph, lw, lb, ep, dres=dres,
-                                         params=(p_lw, p_lb, p_eps))
+                                         params=(p_lw, p_lb, p_eps),
+                                         side=(slab, C, D, dw1, db1, dw2, db2))
         lin_w_shape, affine = ctx.shapes
         return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1, dgamma, dbeta,
                 dw2, db2, None, None, None)

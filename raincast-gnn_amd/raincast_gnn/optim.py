@@ -41,7 +41,9 @@ class FlatAdamW:
                 off += k
         self.exp_avg = torch.zeros_like(self.flat_param)
         self.exp_avg_sq = torch.zeros_like(self.flat_param)
-        self.step_count = torch.zeros(1, dtype=torch.float32, device=dev)
+        # [count, ticket]: gine_adamw_step bumps the count in its last workgroup
+        self._step_state = torch.zeros(2, dtype=torch.float32, device=dev)
+        self.step_count = self._step_state[:1]
 
     @property
     def numel(self) -> int:
@@ -84,7 +86,7 @@ class FlatAdamW:
         self.gather_grads()
         b1, b2 = self.betas
         _lib.call("gine_adamw_step", _lib.ptr(self.flat_param), _lib.ptr(self.flat_grad),
-                  _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), _lib.ptr(self.step_count),
+                  _lib.ptr(self.exp_avg), _lib.ptr(self.exp_avg_sq), _lib.ptr(self._step_state),
                   self.numel, self.lr, float(b1), float(b2), self.eps, self.weight_decay,
                   _lib.stream_handle(self.flat_param.device))
 
