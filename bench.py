@@ -276,7 +276,8 @@ PMC_KERNELS = {
     "gine_mlp_fwd2": ["gine::k_rowgemm<128, 1, 5, true>"],
     "gine_mlp_bwd2": ["gine::k_rowgemm<128, 5, 2, false>"],
     "gine_mlp_bwd1": ["gine::k_rowgemm<128, 3, 3, false>"],
-    "gine_mlp_wgrad": ["gine::k_wgrad_engine<gine::MlpWgradSrc<5> >", "gine::k_slab_reduce"],
+    "gine_mlp_wgrad": ["gine::k_wgrad_engine<gine::MlpWgradSrc<5>, 64, 8>",
+                       "gine::k_slab_sum<true, gine::MlpWgradOut>"],
 }
 
 
