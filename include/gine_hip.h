@@ -268,6 +268,9 @@ int gine_head_bwd_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind,
 int gine_head_bwd(const float* grad_pred, const float* raw, const float* h, const float* w,
                   float* dh, float* slab, float* dw, float* db, int64_t num_nodes,
                   int32_t channels, int32_t kind, void* stream);
+/* dw = NULL in gine_head_bwd leaves the partial slab; this reduces it (another stream). */
+int gine_head_bwd_reduce(const float* slab, float* dw, float* db, int64_t num_nodes,
+                         int32_t channels, int32_t kind, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Dense layers between the DeepSet member sum and the GINE stack (models/gnn.py:48-68,
@@ -295,6 +298,15 @@ int gine_chain_bwd(const float* dh0, const float* x, const float* r, const float
                    float* dwr0, float* dbr0, float* dwr1, float* dbr1, float* dwdr,
                    float* dbdr, int64_t num_nodes, int32_t hidden, int32_t in_features,
                    void* stream);
+/* The parameter-gradient half of gine_chain_bwd on its own (call gine_chain_bwd with
+ * slab = NULL for the input-gradient half): lets it run on another stream, beside the
+ * DeepSet backward that consumes dr. */
+int gine_chain_wgrad(const float* dh0, const float* x, const float* r, const float* s,
+                     const float* u, const float* e, const float* de, const float* dt,
+                     const float* ds, float* slab, float* dwp2, float* dbp2, float bias_scale,
+                     float* dwr0, float* dbr0, float* dwr1, float* dbr1, float* dwdr,
+                     float* dbdr, int64_t num_nodes, int32_t hidden, int32_t in_features,
+                     void* stream);
 
 #ifdef __cplusplus
 }

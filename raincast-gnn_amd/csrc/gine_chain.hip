@@ -381,8 +381,9 @@ extern "C" int gine_chain_bwd(const float* dh0, const float* x, const float* r, 
   if (num_nodes <= 0) return GINE_ERR_INVALID;
   if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   if (!dh0 || !x || !r || !s || !u || !e || !wp2 || !wr0 || !wr1 || !wdr || !de || !dt ||
-      !ds || !dr || !slab || !dwp2 || !dwr0 || !dwr1 || !dwdr)
+      !ds || !dr)
     return GINE_ERR_INVALID;
+  if (slab && (!dwp2 || !dwr0 || !dwr1 || !dwdr)) return GINE_ERR_INVALID;
   hipStream_t st = as_stream(stream);
   const int D = hidden, F = in_features;
   const ChainArgs b1{dh0, nullptr, u, wdr, nullptr, wr1, nullptr, de, dt, 1.f, F};
@@ -393,7 +394,26 @@ extern "C" int gine_chain_bwd(const float* dh0, const float* x, const float* r, 
   if (rc == GINE_OK) rc = launch_chain<DD, FF, CH_B2>(b2, num_nodes, st)
   GINE_CHAIN_DISPATCH(D, F, CALL_B);
 #undef CALL_B
-  if (rc != GINE_OK) return rc;
+  if (rc != GINE_OK || !slab) return rc;  // no slab: weight gradients via gine_chain_wgrad
+  return gine_chain_wgrad(dh0, x, r, s, u, e, de, dt, ds, slab, dwp2, dbp2, bias_scale, dwr0,
+                          dbr0, dwr1, dbr1, dwdr, dbdr, num_nodes, hidden, in_features, stream);
+}
+
+extern "C" int gine_chain_wgrad(const float* dh0, const float* x, const float* r,
+                                const float* s, const float* u, const float* e,
+                                const float* de, const float* dt, const float* ds, float* slab,
+                                float* dwp2, float* dbp2, float bias_scale, float* dwr0,
+                                float* dbr0, float* dwr1, float* dbr1, float* dwdr, float* dbdr,
+                                int64_t num_nodes, int32_t hidden, int32_t in_features,
+                                void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0) return GINE_ERR_INVALID;
+  if (!dh0 || !x || !r || !s || !u || !e || !de || !dt || !ds || !slab || !dwp2 || !dwr0 ||
+      !dwr1 || !dwdr)
+    return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  const int D = hidden, F = in_features;
+  int rc;
   const WgPlan p = chain_wgrad_plan(num_nodes, D, F);
   const size_t per = (size_t)D * (D + F) + D;
   const ChainWgradSrc src{dh0, de, dt, ds, x, e, u, s, r, D, F};

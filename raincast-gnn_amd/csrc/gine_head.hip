@@ -272,7 +272,7 @@ extern "C" int gine_head_bwd(const float* grad_pred, const float* raw, const flo
   const int K = k_of(kind);
   if (K < 0 || num_nodes < 0) return GINE_ERR_INVALID;
   if (!head_dim_ok(channels)) return GINE_ERR_DIM;
-  if (!w || !dw || !slab) return GINE_ERR_INVALID;
+  if (!w || !slab) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!grad_pred || !raw || !h || !dh)) return GINE_ERR_INVALID;
   const int grid = head_bwd_grid(num_nodes);
   const int64_t per = (int64_t)K * channels + K;
@@ -292,6 +292,17 @@ extern "C" int gine_head_bwd(const float* grad_pred, const float* raw, const flo
 #undef HEAD_BWD
     GINE_LAUNCH_STATUS();
   }
+  if (!dw) return GINE_OK;  // slab left for gine_head_bwd_reduce
   return launch_slab_sum(slab, num_nodes == 0 ? 1 : grid, per, (size_t)per, 0, 1,
                          HeadOut{dw, db, (int64_t)K * channels}, s);
+}
+
+extern "C" int gine_head_bwd_reduce(const float* slab, float* dw, float* db, int64_t num_nodes,
+                                    int32_t channels, int32_t kind, void* stream) {
+  const int K = k_of(kind);
+  if (K < 0 || num_nodes < 0 || !slab || !dw) return GINE_ERR_INVALID;
+  if (!head_dim_ok(channels)) return GINE_ERR_DIM;
+  const int64_t per = (int64_t)K * channels + K;
+  return launch_slab_sum(slab, num_nodes == 0 ? 1 : head_bwd_grid(num_nodes), per, (size_t)per,
+                         0, 1, HeadOut{dw, db, (int64_t)K * channels}, as_stream(stream));
 }

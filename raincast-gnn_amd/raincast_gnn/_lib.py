@@ -51,6 +51,9 @@ _SIGNATURES = {
     "gine_mlp_wgrad_num_chunks": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_wgrad": [_c_void_p] * 13 + [_i64, _i32, _i32, _c_void_p],
     "gine_mlp_bwd1_wgrad": [_c_void_p] * 15 + [_i64, _i32, _i32, _c_void_p],
+    "gine_chain_wgrad": [_c_void_p] * 12 + [_f32] + [_c_void_p] * 6 + [_i64, _i32, _i32,
+                                                                        _c_void_p],
+    "gine_head_bwd_reduce": [_c_void_p] * 3 + [_i64, _i32, _i32, _c_void_p],
     "gine_adamw_step": [_c_void_p] * 5 + [_i64, _f32, _f32, _f32, _f32, _f32, _c_void_p],
     "gine_crps_num_partials": [_i64, ctypes.POINTER(_i32)],
     "gine_crps_fwd": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64, _c_void_p,

@@ -17,7 +17,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, sidework
 from .gradbuf import grad_out
 
 HIDDEN = (64, 128)
@@ -72,10 +72,18 @@ class _ChainFn(torch.autograd.Function):
              grad_out(p[4], (D, D), dev), grad_out(p[5], (D,), dev),
              grad_out(p[6], (D, F + D), dev), grad_out(p[7], (D,), dev)]
         P = _lib.ptr
+        # input gradients (de, dt, ds -> dr) on the current stream: the DeepSet backward
+        # needs dr next ...
         _lib.call("gine_chain_bwd", P(dh0), P(x), P(r), P(s), P(u), P(e), P(wp2), P(wr0),
-                  P(wr1), P(wdr), P(de), P(dt), P(ds), P(dr), P(slab), P(g[0]), P(g[1]),
-                  ctx.members, P(g[2]), P(g[3]), P(g[4]), P(g[5]), P(g[6]), P(g[7]), N, D, F,
-                  _lib.stream_handle(dev))
+                  P(wr1), P(wdr), P(de), P(dt), P(ds), P(dr), None, None, None, ctx.members,
+                  None, None, None, None, None, None, N, D, F, _lib.stream_handle(dev))
+        # ... while the four weight gradients run beside it on the side stream
+        members = ctx.members
+        sidework.launch(dev, lambda sh: _lib.call(
+            "gine_chain_wgrad", P(dh0), P(x), P(r), P(s), P(u), P(e), P(de), P(dt), P(ds),
+            P(slab), P(g[0]), P(g[1]), members, P(g[2]), P(g[3]), P(g[4]), P(g[5]), P(g[6]),
+            P(g[7]), N, D, F, sh), keep_alive=(dh0, x, r, s, u, e, de, dt, ds, slab),
+            params=p)
         return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
 
 
