@@ -265,17 +265,22 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
   }
   const ColConst kc = col_const<PRO>(pa, D, q_me);
 
-  float bias = 0.f;
-  if constexpr (EPI == EPI_A1STATS || IS_OUT) bias = ea.bias[col];
-  float alpha = 0.f, shift = 0.f, mean = 0.f, invstd = 0.f;
+  // Epilogue in the row-major domain: after the MFMA chain the accumulator tile goes
+  // through LDS (s_x, free by then), and each thread finishes the float4 column group q_me
+  // of rows r_me + RSTEP*i -- 16-byte loads of the epilogue operands and 16-byte stores
+  // (4-byte stores of the ReLU mask) instead of 16 scalar accesses per lane.
+  float4 bias4 = f4_zero();
+  if constexpr (EPI == EPI_A1STATS || IS_OUT)
+    bias4 = *reinterpret_cast<const float4*>(ea.bias + 4 * q_me);
+  float4 al4 = f4_zero(), sh4 = f4_zero(), mu4 = f4_zero(), is4 = f4_zero();
   if constexpr (EPI == EPI_DBN) {
     const BnView b = bn_view(ea.bn, D);
-    alpha = b.alpha[col];
-    shift = b.shift[col];
-    mean = b.mean[col];
-    invstd = b.invstd[col];
+    al4 = *reinterpret_cast<const float4*>(b.alpha + 4 * q_me);
+    sh4 = *reinterpret_cast<const float4*>(b.shift + 4 * q_me);
+    mu4 = *reinterpret_cast<const float4*>(b.mean + 4 * q_me);
+    is4 = *reinterpret_cast<const float4*>(b.invstd + 4 * q_me);
   }
-  double st1 = 0.0, st2 = 0.0;
+  double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
 
   auto load_tile = [&](int tile, RawItem (&raw)[ITEMS]) {
     const int64_t n0 = (int64_t)tile * kRowTile;
@@ -291,7 +296,7 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
   if (tr.first < tr.end) load_tile(tr.first, raw);
   for (int tile = tr.first; tile < tr.end; tile += tr.step) {
     const int64_t n0 = (int64_t)tile * kRowTile;
-    __syncthreads();  // previous tile's fragment reads of s_x are done
+    __syncthreads();  // previous tile's epilogue reads of s_x are done
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
       const int r = r_me + i * RSTEP;
@@ -301,14 +306,14 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
     }
     __syncthreads();
     if (tile + tr.step < tr.end) load_tile(tile + tr.step, raw);  // next tile, in flight
-    float ep[16];
+    float4 ep[ITEMS];
     if constexpr (EPI_LOAD) {  // epilogue operands of this tile, in flight too
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      for (int i = 0; i < ITEMS; ++i) {
+        int64_t n = n0 + r_me + i * RSTEP;
         n = n < N ? n : N - 1;
-        if constexpr (EPI == EPI_DBN) ep[r] = ea.a1[n * D + col];
-        else ep[r] = ea.resid[n * D + col];
+        const float* src = EPI == EPI_DBN ? ea.a1 : ea.resid;
+        ep[i] = *reinterpret_cast<const float4*>(src + n * D + 4 * q_me);
       }
     }
     floatx16 acc = zero16();
@@ -321,56 +326,93 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
     }
+    __syncthreads();  // every wave's A-fragment reads of s_x are done
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s_x[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + col] = acc[r];
+    __syncthreads();
 
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    for (int i = 0; i < ITEMS; ++i) {
+      const int r = r_me + i * RSTEP;
+      const int64_t n = n0 + r;
+      const float4 v = *reinterpret_cast<const float4*>(&s_x[r * LD + 4 * q_me]);
+      const float vv[4] = {v.x, v.y, v.z, v.w};
       if (n >= N) continue;
-      const int64_t off = n * D + col;
-      const float v = acc[r];
+      const int64_t off = n * D + 4 * q_me;
+      float o4[4];
       if constexpr (EPI == EPI_A1STATS) {
-        const float a1 = v + bias;
-        ea.out[off] = a1;
-        st1 += (double)a1;
-        st2 += (double)a1 * (double)a1;
-      } else if constexpr (IS_OUT) {
-        const float o = v + bias;
-        float y;
-        if constexpr (EPI == EPI_OUT) {
-          y = o;
-        } else if constexpr (EPI == EPI_OUT_RELU) {
-          y = relu_nan(o);
-        } else {
-          y = ep[r] + relu_nan(o);
-          ea.mask_out[off] = (o > 0.f) ? 1 : 0;
+        const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          o4[k] = vv[k] + bb[k];
+          st1[k] += (double)o4[k];
+          st2[k] += (double)o4[k] * (double)o4[k];
         }
-        ea.out[off] = y;
+      } else if constexpr (IS_OUT) {
+        const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
+        if constexpr (EPI == EPI_OUT_RES) {
+          const float xr[4] = {ep[i].x, ep[i].y, ep[i].z, ep[i].w};
+          uchar4 m;
+          unsigned char mk[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float o = vv[k] + bb[k];
+            o4[k] = xr[k] + relu_nan(o);
+            mk[k] = (o > 0.f) ? 1 : 0;
+          }
+          m.x = mk[0];
+          m.y = mk[1];
+          m.z = mk[2];
+          m.w = mk[3];
+          *reinterpret_cast<uchar4*>(ea.mask_out + off) = m;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float o = vv[k] + bb[k];
+            o4[k] = (EPI == EPI_OUT_RELU) ? relu_nan(o) : o;
+          }
+        }
       } else if constexpr (EPI == EPI_DBN) {
-        const float a1 = ep[r];
-        const float bn = bn_apply(a1, alpha, shift);
-        const float dbn = (bn > 0.f) ? v : 0.f;
-        ea.out[off] = dbn;
-        const double xhat = (double)((a1 - mean) * invstd);
-        st1 += (double)dbn;
-        st2 += (double)dbn * xhat;
+        const float a1[4] = {ep[i].x, ep[i].y, ep[i].z, ep[i].w};
+        const float al[4] = {al4.x, al4.y, al4.z, al4.w}, sh[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+        const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float bn = bn_apply(a1[k], al[k], sh[k]);
+          o4[k] = (bn > 0.f) ? vv[k] : 0.f;
+          const double xhat = (double)((a1[k] - mu[k]) * is[k]);
+          st1[k] += (double)o4[k];
+          st2[k] += (double)o4[k] * xhat;
+        }
       } else {
-        ea.out[off] = v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o4[k] = vv[k];
       }
+      *reinterpret_cast<float4*>(ea.out + off) = make_float4(o4[0], o4[1], o4[2], o4[3]);
     }
   }
 
   if constexpr (EPI == EPI_A1STATS || EPI == EPI_DBN) {
-    st1 += shfl_xor_d(st1, 32);
-    st2 += shfl_xor_d(st2, 32);
-    if (h == 0) {
-      double* p = ea.partials + (size_t)vb * 2 * D;
-      p[col] = st1;
-      p[D + col] = st2;
+    // per-column partials of the workgroup: the RSTEP row groups added in fixed order
+    __syncthreads();
+    double* sr = reinterpret_cast<double*>(s_x);  // [2][RSTEP][D] (fits: 16*D*8 <= 32*LD*4)
+    static_assert(2 * RSTEP * D * 8 <= kRowTile * LD * 4, "partials fit in the tile");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sr[(0 * RSTEP + r_me) * D + 4 * q_me + k] = st1[k];
+      sr[(1 * RSTEP + r_me) * D + 4 * q_me + k] = st2[k];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * D; c += NT) {
+      const int which = c / D, cc = c % D;
+      double t = 0.0;
+#pragma unroll
+      for (int g = 0; g < RSTEP; ++g) t += sr[(which * RSTEP + g) * D + cc];
+      ea.partials[(size_t)vb * 2 * D + c] = t;
     }
   }
 }
 
-// Persistent grid: ~4 waves per CU (one wave per SIMD) on the 256 CUs of an MI355X.
 template <int D, int PRO, int EPI, bool BT>
 __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, ProArgs pa,
                                                    EpiArgs ea, int64_t N, int num_tiles) {
