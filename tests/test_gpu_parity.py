@@ -367,3 +367,47 @@ def test_graph_capture_replay_matches_eager():
     got = warm + replayed
     for a, b in zip(got, eager):
         assert abs(a - b) <= 1e-6 * abs(b), (got, eager)
+
+
+def test_eval_mode_prediction_and_ensemble_match_oracle(tmp_path):
+    """eval.py's path: after training steps (non-trivial BatchNorm running statistics) the
+    eval-mode forward under no_grad matches the oracle's eval forward, and the
+    checkpoint-ensemble average matches averaging the oracle's predictions."""
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.evaluate import ensemble_crps, predict_ensemble
+    from raincast_gnn.optim import FlatAdamW
+    torch.manual_seed(5)
+    batches = [synthetic_batch(300, 2, k=8, seed=s) for s in (11, 12)]
+    states = []
+    for seed in (1, 2):
+        torch.manual_seed(seed)
+        model = GNN(35, 128, 128, 4, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5).to(DEV)
+        opt = FlatAdamW(model.parameters(), lr=1e-3)
+        model.train()
+        for b in batches:
+            opt.zero_grad()
+            bb = b.to(DEV)
+            model.loss_fn.crps(model(bb), bb.y).backward()
+            opt.step()
+        path = str(tmp_path / f"ck{seed}.pth")
+        torch.save(model.state_dict(), path)
+        states.append(path)
+
+    def make():
+        return GNN(35, 128, 128, 4, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5)
+
+    preds = predict_ensemble(make, states, batches, DEV)
+    refs = []
+    for path in states:
+        ref = O.OracleGNN(35, 128, 4, "MixedLoss", "False", 1.71, 0.5)
+        ref.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+        ref.eval()
+        with torch.no_grad():
+            refs.append(torch.cat([ref(b) for b in batches], 0))
+    ref_mean = torch.stack(refs, 0).mean(0)
+    assert preds.shape == ref_mean.shape
+    assert rel_err(preds, ref_mean) <= 1e-5, rel_err(preds, ref_mean)
+    y = torch.cat([b.y for b in batches])
+    c = ensemble_crps(make(), preds, y)
+    c_ref = ensemble_crps(make(), ref_mean, y)
+    assert abs(c.item() - c_ref.item()) <= 1e-5 * abs(c_ref.item())
