@@ -1,0 +1,99 @@
+"""Device-resident dataset and batching for a static station graph.
+
+The reference builds ONE edge list per station set and shares it by every sample
+(utils/data.py:300, 330-335); PyG's DataLoader then collates each batch on the host
+(train.py:155-156: ``Batch.from_data_list``) and ``batch.to(device)`` copies it, edge_index
+included, every step (train.py:62).  Here the samples live in HBM as stacked tensors
+([T, N, F] features, [T, N, M, F] ensemble, [T, N] targets) and a batch is a device gather
+by sample index.  The block-diagonal edge list of a batch of B graphs depends only on B,
+so it is built once per B and the SAME tensor object is returned for every batch of that
+size: the engine's graph cache (raincast_gnn/graph.py, keyed on tensor identity) then
+sorts it into its two CSRs once for the whole run instead of once per step.
+
+Node order, edge order and attributes are exactly PyG collation's (tests/test_batching.py
+compares with :func:`raincast_gnn.data.collate`).
+"""
+from __future__ import annotations
+
+import torch
+
+from .data import GraphBatch
+
+
+class DeviceDataset:
+    """Samples of one station graph, stacked on ``device``."""
+
+    def __init__(self, samples: list[GraphBatch], device):
+        if not samples:
+            raise ValueError("empty dataset")
+        base = samples[0]
+        for s in samples:
+            if s.edge_index is not base.edge_index and not torch.equal(s.edge_index,
+                                                                      base.edge_index):
+                raise ValueError("all samples must share one station graph (utils/data.py:300)")
+        self.device = torch.device(device)
+        self.num_stations = base.num_nodes
+        self.x = torch.stack([s.x for s in samples]).to(self.device)
+        self.ensemble = torch.stack([s.ensemble for s in samples]).to(self.device)
+        self.y = torch.stack([s.y for s in samples]).to(self.device)
+        self.edge_index = base.edge_index.to(self.device)
+        self.edge_attr = base.edge_attr.to(self.device)
+        self._blocks: dict[int, tuple] = {}
+
+    def __len__(self) -> int:
+        return self.x.size(0)
+
+    def block_graph(self, num_graphs: int):
+        """(edge_index, edge_attr, batch, ptr) of ``num_graphs`` copies of the station graph,
+        built once per size and returned as the same tensors afterwards."""
+        hit = self._blocks.get(num_graphs)
+        if hit is None:
+            n, E = self.num_stations, self.edge_index.size(1)
+            offs = (torch.arange(num_graphs, device=self.device, dtype=torch.long) * n)
+            ei = (self.edge_index.unsqueeze(1) + offs.view(1, -1, 1)).reshape(2, num_graphs * E)
+            ea = self.edge_attr.repeat(num_graphs, 1)
+            batch = torch.arange(num_graphs, device=self.device).repeat_interleave(n)
+            ptr = torch.arange(num_graphs + 1, device=self.device, dtype=torch.long) * n
+            hit = (ei.contiguous(), ea.contiguous(), batch, ptr)
+            self._blocks[num_graphs] = hit
+        return hit
+
+    def batch(self, indices: torch.Tensor) -> GraphBatch:
+        """The collated batch of samples ``indices`` (a device or host LongTensor)."""
+        idx = indices.to(self.device, dtype=torch.long)
+        B, n = idx.numel(), self.num_stations
+        ei, ea, batch, ptr = self.block_graph(B)
+        F = self.x.size(-1)
+        return GraphBatch(
+            x=self.x.index_select(0, idx).reshape(B * n, F),
+            ensemble=self.ensemble.index_select(0, idx).reshape(B * n, *self.ensemble.shape[2:]),
+            edge_index=ei, edge_attr=ea,
+            y=self.y.index_select(0, idx).reshape(B * n),
+            batch=batch, ptr=ptr, num_graphs=B)
+
+
+class DeviceLoader:
+    """Epoch iterator over a :class:`DeviceDataset` (train.py:155: shuffle=True,
+    batch_size from params.json); the permutation is drawn on the device."""
+
+    def __init__(self, dataset: DeviceDataset, batch_size: int, shuffle: bool = True,
+                 seed: int = 0, drop_last: bool = False):
+        self.dataset, self.batch_size = dataset, int(batch_size)
+        self.shuffle, self.drop_last = shuffle, drop_last
+        self._gen = torch.Generator(device=dataset.device)
+        self._gen.manual_seed(seed)
+
+    def __len__(self) -> int:
+        T = len(self.dataset)
+        return T // self.batch_size if self.drop_last else -(-T // self.batch_size)
+
+    def __iter__(self):
+        T = len(self.dataset)
+        dev = self.dataset.device
+        order = (torch.randperm(T, generator=self._gen, device=dev) if self.shuffle
+                 else torch.arange(T, device=dev))
+        for i in range(0, T, self.batch_size):
+            idx = order[i:i + self.batch_size]
+            if self.drop_last and idx.numel() < self.batch_size:
+                return
+            yield self.dataset.batch(idx)

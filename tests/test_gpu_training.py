@@ -174,3 +174,27 @@ def test_grads_land_in_flat_buffer_without_copies():
             opt2.step()
             for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
                 assert rel_err(p.detach(), q.detach()) <= 1e-6, n
+
+
+def test_device_loader_training_builds_graph_once():
+    """With the device-resident batcher every batch of one size shares one edge list, so
+    the engine's CSR build runs once for the whole epoch."""
+    from raincast_gnn.batching import DeviceDataset, DeviceLoader
+    from raincast_gnn.data import synthetic_samples
+    from raincast_gnn.graph import graph_cache
+    from raincast_gnn.models import GNN
+    from raincast_gnn.optim import FlatAdamW
+    graph_cache.clear()
+    ds = DeviceDataset(synthetic_samples(80, 12, k=6, seed=2), DEV)
+    torch.manual_seed(0)
+    model = GNN(35, 128, 128, 2, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5).to(DEV)
+    opt = FlatAdamW(model.parameters(), lr=1e-3)
+    losses = []
+    for batch in DeviceLoader(ds, batch_size=4, shuffle=True, seed=1):
+        opt.zero_grad()
+        loss = model.loss_fn.crps(model(batch), batch.y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert len(losses) == 3 and all(l == l for l in losses)
+    assert len(graph_cache._entries) == 1
