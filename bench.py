@@ -59,6 +59,9 @@ def parse():
                     help="target duration of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm, the benchmark) | gloo (multi-rank rehearsal on "
+                         "one GPU: ranks share the device)")
     return ap.parse_args()
 
 
@@ -341,8 +344,8 @@ def main():
     args = parse()
     rank, local_rank, world = env_rank()
     if world > 1:
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local_rank)
+        dist.init_process_group(args.dist_backend)
+    device = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
     cfg = BENCH_CONFIGS[args.config]
     if args.config == 4:  # global batch fixed -> strong scaling

@@ -19,6 +19,8 @@
 #include "gine_reduce.hpp"
 #include "gine_slab.hpp"
 
+#include <cstdlib>
+
 namespace gine {
 namespace {
 
@@ -32,9 +34,18 @@ __device__ __forceinline__ float edge_lin(float a, float w, float b) {
   return a * w + b;  // -ffp-contract=off: two roundings
 }
 
+// Neighbour rows in flight per lane.  (16 -- one round for k <= 15 -- was measured slower
+// at cfg2: the extra VGPRs halve the waves per SIMD, and those hide more latency.)
 template <int C>
 struct MpUnroll {
   static constexpr int value = C == 1 ? 8 : (C == 2 ? 4 : 2);
+};
+#ifndef GINE_MPBWD_U
+#define GINE_MPBWD_U 8
+#endif
+template <int C>
+struct MpUnrollBwd {
+  static constexpr int value = C == 1 ? GINE_MPBWD_U : (C == 2 ? 4 : 2);
 };
 
 // ----------------------------------------------------------------------------------------
@@ -136,7 +147,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
     const float4* __restrict__ dres4, float4* __restrict__ dx4, double* __restrict__ partials,
     int64_t N, int D4, int num_tiles, int flags, MlpSlabJob job) {
   constexpr int GPW = kWave / L;
-  constexpr int U = MpUnroll<C>::value;
+  constexpr int U = MpUnrollBwd<C>::value;
   __shared__ int32_t s_nbr[kWaves][kWave];
   __shared__ float s_attr[kWaves][kWave];
   extern __shared__ __attribute__((aligned(16))) double s_red[];  // [3][D]
@@ -178,12 +189,16 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
     const int64_t node = (int64_t)tile * (kWaves * GPW) + wave * GPW + g;
     if (node >= N) continue;
     const int64_t row = node * D4;
-    float4 h[C], g_self[C], acc[C];
+    float4 h[C], g_self[C], acc[C], r_self[C];
+    // the residual gradient row is loaded with the node's own rows (unconditionally, from
+    // dz when there is none): a load behind the gather would add a round trip per tile
+    const float4* rsrc = dres4 != nullptr ? dres4 : dz4;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       acc[c] = f4_zero();
       h[c] = x4[row + qc[c]];
       g_self[c] = dz4[row + qc[c]];
+      r_self[c] = rsrc[row + qc[c]];
     }
     // pre-activation of this node's outgoing messages: h + (a*W + b) depends on the edge
     // only through a, so h is loaded once per source node.
@@ -244,7 +259,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
           o.w = o.w + ope * g_self[c].w;
         }
         if (dres4 != nullptr) {
-          const float4 d = dres4[row + q];
+          const float4 d = r_self[c];
           o.x = o.x + d.x;
           o.y = o.y + d.y;
           o.z = o.z + d.z;
@@ -351,11 +366,19 @@ inline bool pick_shape(int D, Shape* s) {
 
 inline int nodes_per_block(const Shape& s) { return kWaves * (kWave / s.L); }
 
-constexpr int kMaxBwdBlocks = 1024;
+// Persistent grid cap (GINE_MPBWD_BLOCKS overrides it, for tuning experiments only).
+inline int64_t max_bwd_blocks() {
+  static const int env = [] {
+    const char* e = getenv("GINE_MPBWD_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  return env > 0 ? env : 1024;
+}
 
 inline int bwd_grid(int64_t N, const Shape& s) {
   const int64_t tiles = ceil_div(N, nodes_per_block(s));
-  int64_t g = tiles < kMaxBwdBlocks ? tiles : kMaxBwdBlocks;
+  const int64_t cap = max_bwd_blocks();
+  int64_t g = tiles < cap ? tiles : cap;
   return (int)(g > 0 ? g : 1);
 }
 
