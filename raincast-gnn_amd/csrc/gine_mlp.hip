@@ -31,6 +31,43 @@
 namespace gine {
 namespace {
 
+#ifdef GINE_RG_PROFILE
+// Debug build only (make rgprof): workgroup 0 / thread 0 stamps s_memtime at the phase
+// boundaries of the row-tile GEMM into LDS (no global access between the stamps, so no
+// vmcnt wait is introduced) and flushes them at the end; tools/rg_prof.py reads them.
+__device__ long long g_rg_prof[4096];
+__device__ int g_rg_prof_n;
+#define RG_DECL                    \
+  __shared__ long long s_rgp[64];  \
+  int rg_n = 0
+#define RG_MARK(tag)                                                                  \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    if (vb == 0 && threadIdx.x == 0 && rg_n < 32) {                                   \
+      long long t_;                                                                   \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));              \
+      s_rgp[2 * rg_n] = (tag);                                                        \
+      s_rgp[2 * rg_n + 1] = t_;                                                       \
+      ++rg_n;                                                                         \
+    }                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  } while (0)
+#define RG_FLUSH()                                                                    \
+  do {                                                                                \
+    if (vb == 0 && threadIdx.x == 0) {                                                \
+      const int b_ = atomicAdd(&g_rg_prof_n, rg_n);                                   \
+      for (int i_ = 0; i_ < rg_n && b_ + i_ < 2040; ++i_) {                           \
+        g_rg_prof[2 * (b_ + i_)] = s_rgp[2 * i_];                                     \
+        g_rg_prof[2 * (b_ + i_) + 1] = s_rgp[2 * i_ + 1];                             \
+      }                                                                               \
+    }                                                                                 \
+  } while (0)
+#else
+#define RG_DECL do {} while (0)
+#define RG_MARK(tag) do {} while (0)
+#define RG_FLUSH() do {} while (0)
+#endif
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ floatx16 zero16() {
@@ -230,7 +267,7 @@ __device__ __forceinline__ float4 transform(const ProArgs& p, const RawItem& r,
 // ----------------------------------------------------------------------------------------
 // One persistent workgroup (virtual index vb of vgrid) of the row-tile GEMM; s_x: LDS of
 // kRowTile * (D + 4) floats.
-template <int D, int PRO, int EPI, bool BT>
+template <int D, int PRO, int EPI, bool BT, bool WL = false>
 __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const ProArgs& pa,
                                              const EpiArgs& ea, int64_t N, int num_tiles,
                                              float* __restrict__ s_x, int vb, int vgrid) {
@@ -247,9 +284,22 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
   const int q_me = threadIdx.x % D4, r_me = threadIdx.x / D4;
+  RG_DECL;
+  RG_MARK(0);
 
   float bf[KS];
-  if constexpr (BT) {
+  // WL: W^T fragments via LDS.  A lane's fragment is 64 consecutive floats of ONE row of W,
+  // so direct loads touch 64 cache lines per instruction (16 B used of each): ~4K line
+  // lookups per workgroup, the bulk of the kernel's start-up.  Instead the workgroup reads
+  // W with unit-stride 16-byte loads (8 lines per instruction), writes it to the padded
+  // LDS tile (s_x holds D*(D+4) floats in this variant) and reads the fragments from there.
+  constexpr int WCH = D * D4 / NT;  // float4 chunks of W per thread
+  float4 wtmp[WL ? WCH : 1];
+  if constexpr (WL) {
+    const float4* w4 = reinterpret_cast<const float4*>(W);
+#pragma unroll
+    for (int j = 0; j < WCH; ++j) wtmp[j] = w4[threadIdx.x + NT * j];
+  } else if constexpr (BT) {
     const float4* wr = reinterpret_cast<const float4*>(W + (size_t)col * D + h * KS);
 #pragma unroll
     for (int q = 0; q < KS / 4; ++q) {
@@ -294,8 +344,27 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
   const TileRange tr = xcd_tile_range(num_tiles, vb, vgrid);
   RawItem raw[ITEMS];
   if (tr.first < tr.end) load_tile(tr.first, raw);
+  if constexpr (WL) {
+#pragma unroll
+    for (int j = 0; j < WCH; ++j) {
+      const int idx = threadIdx.x + NT * j;
+      *reinterpret_cast<float4*>(&s_x[(idx / D4) * LD + 4 * (idx % D4)]) = wtmp[j];
+    }
+    __syncthreads();
+    const float* wr = &s_x[col * LD + h * KS];
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(&wr[4 * q]);
+      bf[4 * q] = v.x;
+      bf[4 * q + 1] = v.y;
+      bf[4 * q + 2] = v.z;
+      bf[4 * q + 3] = v.w;
+    }
+    // the first tile's __syncthreads() below orders these reads before the staging writes
+  }
   for (int tile = tr.first; tile < tr.end; tile += tr.step) {
     const int64_t n0 = (int64_t)tile * kRowTile;
+    RG_MARK(1);
     __syncthreads();  // previous tile's epilogue reads of s_x are done
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -316,6 +385,7 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
         ep[i] = *reinterpret_cast<const float4*>(src + n * D + 4 * q_me);
       }
     }
+    RG_MARK(2);
     floatx16 acc = zero16();
     const float* arow = &s_x[c32 * LD + h * KS];
 #pragma unroll
@@ -326,6 +396,10 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
     }
+#ifdef GINE_RG_PROFILE
+    if (acc[0] == 1.2345e-30f) s_x[0] = 0.f;  // the stamp below waits for the chain
+#endif
+    RG_MARK(3);
     __syncthreads();  // every wave's A-fragment reads of s_x are done
 #pragma unroll
     for (int r = 0; r < 16; ++r) s_x[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + col] = acc[r];
@@ -390,6 +464,7 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
       }
       *reinterpret_cast<float4*>(ea.out + off) = make_float4(o4[0], o4[1], o4[2], o4[3]);
     }
+    RG_MARK(4);
   }
 
   if constexpr (EPI == EPI_A1STATS || EPI == EPI_DBN) {
@@ -411,13 +486,16 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
       ea.partials[(size_t)vb * 2 * D + c] = t;
     }
   }
+  RG_MARK(5);
+  RG_FLUSH();
 }
 
 template <int D, int PRO, int EPI, bool BT>
 __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, ProArgs pa,
                                                    EpiArgs ea, int64_t N, int num_tiles) {
-  __shared__ __attribute__((aligned(16))) float s_x[kRowTile * (D + 4)];
-  rowgemm_body<D, PRO, EPI, BT>(W, pa, ea, N, num_tiles, s_x, blockIdx.x, gridDim.x);
+  constexpr bool WL = BT && D <= 128;  // W^T staged through LDS (fits: 128*132*4 B)
+  __shared__ __attribute__((aligned(16))) float s_x[(WL ? D : kRowTile) * (D + 4)];
+  rowgemm_body<D, PRO, EPI, BT, WL>(W, pa, ea, N, num_tiles, s_x, blockIdx.x, gridDim.x);
 }
 
 // Persistent grid.  GINE_ROWGEMM_BLOCKS (tuning experiments only) overrides the cap.
@@ -871,3 +949,14 @@ extern "C" int gine_mlp_bwd1_wgrad(const float* dy, const float* y, const uint8_
   return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 2,
                          MlpWgradOut{dw2, db2, dw1, db1, D}, s);
 }
+
+#ifdef GINE_RG_PROFILE
+extern "C" int gine_debug_rg_prof(long long* out, int* n) {
+  GINE_RETURN_IF_HIP(hipDeviceSynchronize());
+  GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(n, HIP_SYMBOL(g_rg_prof_n), sizeof(int)));
+  GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rg_prof), sizeof(long long) * 4096));
+  const int zero = 0;
+  GINE_RETURN_IF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rg_prof_n), &zero, sizeof(int)));
+  return GINE_OK;
+}
+#endif

@@ -45,6 +45,7 @@ for s in $STEPS; do
     dist2) run bench_dist2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --dist-backend gloo \
                --steps 10 --warmup 3 ;;
+    rgprof) GINE_HIP_LIB=raincast-gnn_amd/csrc/build/dbg/libgine_hip_rgprof.so run rg_prof 300 python tools/rg_prof.py ;;
     floor) run launch_floor 300 python tools/launch_floor.py ;;
     counters) run list_counters 300 rocprofv3 -L ;;
     dsmicro) run ds_micro 300 python tools/ds_micro.py ;;
