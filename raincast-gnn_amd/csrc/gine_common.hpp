@@ -26,6 +26,7 @@ namespace gine {
 
 constexpr int kWave = 64;   // CDNA wavefront width
 constexpr int kNumXcd = 8;  // MI355X: 8 XCDs, each with a private 4 MiB L2
+constexpr int kNumCu = 256;  // 32 CUs per XCD
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

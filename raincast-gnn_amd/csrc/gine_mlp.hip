@@ -498,18 +498,24 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
   rowgemm_body<D, PRO, EPI, BT, WL>(W, pa, ea, N, num_tiles, s_x, blockIdx.x, gridDim.x);
 }
 
-// Persistent grid.  GINE_ROWGEMM_BLOCKS (tuning experiments only) overrides the cap.
-inline int rowgemm_cap(int D) {
+// Persistent grid.  One workgroup per CU while each has at most 4 tiles; past that two
+// per CU, so one workgroup's epilogue and staging run beside the other's MFMA chain (cfg3,
+// 4,000 tiles: 48 -> 44 us fwd1, 65 -> 54 us bwd2; at cfg2, 500 tiles, the second
+// workgroup's weight staging costs more than the overlap gains).  GINE_ROWGEMM_BLOCKS
+// (tuning experiments only) overrides the cap.
+inline int rowgemm_cap(int D, int64_t tiles) {
   static const int env = [] {
     const char* e = getenv("GINE_ROWGEMM_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  return env > 0 ? env : std::max(256, 1024 / (D / 32));
+  if (env > 0) return env;
+  const int per_cu = (D == 128 && tiles > 4 * kNumCu) ? 2 : 1;
+  return std::max(kNumCu * per_cu, 1024 / (D / 32));
 }
 
 inline int rowgemm_grid(int64_t N, int D) {
   const int64_t tiles = ceil_div(N, kRowTile);
-  const int64_t cap = rowgemm_cap(D);
+  const int64_t cap = rowgemm_cap(D, tiles);
   const int64_t g = tiles < cap ? tiles : cap;
   return (int)(g > 0 ? g : 1);
 }

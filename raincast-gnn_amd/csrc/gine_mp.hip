@@ -36,12 +36,15 @@ __device__ __forceinline__ float edge_lin(float a, float w, float b) {
 
 // Neighbour rows in flight per lane.  (16 -- one round for k <= 15 -- was measured slower
 // at cfg2: the extra VGPRs halve the waves per SIMD, and those hide more latency.)
+#ifndef GINE_MPFWD_U
+#define GINE_MPFWD_U 6
+#endif
 template <int C>
 struct MpUnroll {
-  static constexpr int value = C == 1 ? 8 : (C == 2 ? 4 : 2);
+  static constexpr int value = C == 1 ? GINE_MPFWD_U : (C == 2 ? 4 : 2);
 };
 #ifndef GINE_MPBWD_U
-#define GINE_MPBWD_U 8
+#define GINE_MPBWD_U 6
 #endif
 template <int C>
 struct MpUnrollBwd {

@@ -40,12 +40,16 @@ for s in $STEPS; do
            python tools/pmc_summary.py "$OUT"/pmc_fetch/run_counter_collection.csv \
                "$OUT"/pmc_write/run_counter_collection.csv --traffic-json "$OUT/pmc_traffic.json" \
                > "$OUT/pmc_summary.txt" 2>&1 ;;
-    rgsweep) for g in 256 512 1024; do export GINE_ROWGEMM_BLOCKS=$g; run bench_rg$g 300 python bench.py --no-cpu --steps 30; done; unset GINE_ROWGEMM_BLOCKS ;;
+    rgsweep) for g in 256 512 1024; do export GINE_ROWGEMM_BLOCKS=$g; run bench_rg$g 300 python bench.py --no-cpu --steps 30 ${VARARGS:-}; done; unset GINE_ROWGEMM_BLOCKS ;;
     mbsweep) for g in 512 1024 2048 4096; do export GINE_MPBWD_BLOCKS=$g; run bench_mb$g 300 python bench.py --no-cpu --steps 30; done; unset GINE_MPBWD_BLOCKS ;;
     dist2) run bench_dist2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --dist-backend gloo \
                --steps 10 --warmup 3 ;;
     rgprof) GINE_HIP_LIB=raincast-gnn_amd/csrc/build/dbg/libgine_hip_rgprof.so run rg_prof 300 python tools/rg_prof.py ;;
+    var)   for v in raincast-gnn_amd/csrc/build/var/*/; do n=$(basename "$v")
+             GINE_HIP_LIB=${v}libgine_hip.so run var_${n}_base 300 python bench.py --no-cpu --steps 30 ${VARARGS:-}
+           done ;;
+    varbase) run var_base 300 python bench.py --no-cpu --steps 30 ${VARARGS:-} ;;
     floor) run launch_floor 300 python tools/launch_floor.py ;;
     counters) run list_counters 300 rocprofv3 -L ;;
     dsmicro) run ds_micro 300 python tools/ds_micro.py ;;
