@@ -44,9 +44,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
 
 __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
-// relu with ATen's NaN propagation (clamp_min keeps NaN); the sign of a zero result never
-// changes a sum that starts from +0, so 0 vs -0 is immaterial.
-__device__ __forceinline__ float relu_nan(float v) { return (v <= 0.f) ? 0.f : v; }
+// relu with ATen's NaN propagation (clamp_min keeps NaN): IEEE-754-2019 maximum(v, +0)
+// propagates NaN and orders -0 < +0 -- one v_maximum3_f32 on gfx950 instead of a compare
+// and a select.  A NaN comes out quieted (its payload may differ from the CPU's).
+__device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.0f); }
 
 // Double-precision block reduction helper over the 32 lanes of one MFMA column half.
 __device__ __forceinline__ double shfl_xor_d(double v, int m) {

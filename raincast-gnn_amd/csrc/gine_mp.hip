@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
 
   float4 w[C], b[C];
   int qc[C];
-  double pw[C][4], pb[C][4], pe[C][4];  // sum dm*a, sum dm, sum dz*x
+  double pw[C][4], pb[C][4], pe[C][4];  // sum dm*a, sum dm, sum dz*x (per-node terms)
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     qc[c] = min(t + c * L, D4 - 1);
@@ -192,13 +192,14 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
     const int64_t node = (int64_t)tile * (kWaves * GPW) + wave * GPW + g;
     if (node >= N) continue;
     const int64_t row = node * D4;
-    float4 h[C], g_self[C], acc[C], r_self[C];
+    float4 h[C], g_self[C], acc[C], accw[C], r_self[C];
     // the residual gradient row is loaded with the node's own rows (unconditionally, from
     // dz when there is none): a load behind the gather would add a round trip per tile
     const float4* rsrc = dres4 != nullptr ? dres4 : dz4;
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       acc[c] = f4_zero();
+      accw[c] = f4_zero();
       h[c] = x4[row + qc[c]];
       g_self[c] = dz4[row + qc[c]];
       r_self[c] = rsrc[row + qc[c]];
@@ -227,23 +228,22 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (j + u < cnt) {
-            const double ad = (double)a[u];
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-              float dm[4];
-              dm[0] = (h[c].x + edge_lin<FMA>(a[u], w[c].x, b[c].x) > 0.f) ? r[u][c].x : 0.f;
-              dm[1] = (h[c].y + edge_lin<FMA>(a[u], w[c].y, b[c].y) > 0.f) ? r[u][c].y : 0.f;
-              dm[2] = (h[c].z + edge_lin<FMA>(a[u], w[c].z, b[c].z) > 0.f) ? r[u][c].z : 0.f;
-              dm[3] = (h[c].w + edge_lin<FMA>(a[u], w[c].w, b[c].w) > 0.f) ? r[u][c].w : 0.f;
-              acc[c].x = acc[c].x + dm[0];
-              acc[c].y = acc[c].y + dm[1];
-              acc[c].z = acc[c].z + dm[2];
-              acc[c].w = acc[c].w + dm[3];
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                pw[c][k] += (double)dm[k] * ad;
-                pb[c][k] += (double)dm[k];
-              }
+              float4 dm;
+              dm.x = (h[c].x + edge_lin<FMA>(a[u], w[c].x, b[c].x) > 0.f) ? r[u][c].x : 0.f;
+              dm.y = (h[c].y + edge_lin<FMA>(a[u], w[c].y, b[c].y) > 0.f) ? r[u][c].y : 0.f;
+              dm.z = (h[c].z + edge_lin<FMA>(a[u], w[c].z, b[c].z) > 0.f) ? r[u][c].z : 0.f;
+              dm.w = (h[c].w + edge_lin<FMA>(a[u], w[c].w, b[c].w) > 0.f) ? r[u][c].w : 0.f;
+              acc[c].x = acc[c].x + dm.x;
+              acc[c].y = acc[c].y + dm.y;
+              acc[c].z = acc[c].z + dm.z;
+              acc[c].w = acc[c].w + dm.w;
+              // this node's fp32 share of dW_e = sum_e dm_e * a_e (fp64 across nodes)
+              accw[c].x = __builtin_fmaf(dm.x, a[u], accw[c].x);
+              accw[c].y = __builtin_fmaf(dm.y, a[u], accw[c].y);
+              accw[c].z = __builtin_fmaf(dm.z, a[u], accw[c].z);
+              accw[c].w = __builtin_fmaf(dm.w, a[u], accw[c].w);
             }
           }
         }
@@ -255,6 +255,15 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
       const int q = t + c * L;
       if (q < D4) {
         float4 o = acc[c];
+        // db_e = sum_e dm_e: each source node contributes its message-gradient sum
+        pb[c][0] += (double)acc[c].x;
+        pb[c][1] += (double)acc[c].y;
+        pb[c][2] += (double)acc[c].z;
+        pb[c][3] += (double)acc[c].w;
+        pw[c][0] += (double)accw[c].x;
+        pw[c][1] += (double)accw[c].y;
+        pw[c][2] += (double)accw[c].z;
+        pw[c][3] += (double)accw[c].w;
         if (add_self) {
           o.x = o.x + ope * g_self[c].x;
           o.y = o.y + ope * g_self[c].y;
