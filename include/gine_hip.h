@@ -114,6 +114,55 @@ int gine_mp_bwd_side(const float* dz, const float* x, const int32_t* out_rowptr,
                      float* db1, float* dw2, float* db2, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Window-staged message passing (same results as gine_mp_fwd / gine_mp_bwd, bit for bit
+ * for z and dx).  A PyG batch is a block-diagonal union of graphs (Batch.from_data_list,
+ * train.py:155), so the neighbours of a run of consecutive nodes lie in one short run of
+ * rows.  gine_graph_plan_windows (HOST pointers: a host copy of a CSR) cuts the nodes into
+ * tiles of at most max_nodes nodes / max_edges edges whose neighbour window
+ * [win_lo, win_lo + win_rows) spans at most max_rows rows; maxima[3] = the largest window
+ * rows, tile edges and tile nodes.  *num_tiles = 0 means no plan (some node's own neighbour
+ * span exceeds max_rows or its degree max_edges): use the gather entry points.
+ * The kernels stage each tile's window slice of slice_channels (8, 16 or 32) channels in
+ * LDS and read every neighbour row from there; channels % slice_channels == 0 and
+ * channels / slice_channels <= 8.  The plan arrays are device copies.
+ * gine_mp_bwd_win partials: num_tiles rows of fp64 [3][D]; gine_mp_bwd_win_finalize
+ * reduces them (fixed order) into dlin_w, dlin_b, deps.
+ * Replaces the same reference ops as gine_mp_fwd / gine_mp_bwd (models/gnn.py:41,44).
+ * ---------------------------------------------------------------------------------- */
+#define GINE_WINDOW_LDS_BYTES (80 * 1024)  /* two workgroups per CU (160 KiB LDS) */
+typedef struct gine_window_plan {
+  const int32_t* tile_begin; /* device [num_tiles + 1] */
+  const int32_t* win_lo;     /* device [num_tiles] */
+  const int32_t* win_rows;   /* device [num_tiles] */
+  int32_t num_tiles;
+  int32_t slice_channels;
+  int32_t max_rows, max_edges, max_nodes;
+} gine_window_plan;
+int gine_graph_plan_windows(const int32_t* rowptr, const int32_t* nbr, int64_t num_nodes,
+                            int32_t max_rows, int32_t max_nodes, int32_t max_edges,
+                            int32_t* tile_begin, int32_t* win_lo, int32_t* win_rows,
+                            int32_t* num_tiles, int32_t* maxima);
+int gine_mp_fwd_win(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                    const float* in_attr, const float* lin_w, const float* lin_b,
+                    const float* eps, float* z, int64_t num_nodes, int32_t channels,
+                    int32_t flags, const gine_window_plan* plan, void* stream);
+int gine_mp_bwd_win(const float* dz, const float* x, const int32_t* out_rowptr,
+                    const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                    const float* lin_b, const float* eps, const float* dres, float* dx,
+                    double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                    const gine_window_plan* plan, void* stream);
+int gine_mp_bwd_win_side(const float* dz, const float* x, const int32_t* out_rowptr,
+                         const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                         const float* lin_b, const float* eps, const float* dres, float* dx,
+                         double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                         const gine_window_plan* plan, const float* wg_slab, int32_t wg_chunks,
+                         int32_t mlp_channels, float* dw1, float* db1, float* dw2, float* db2,
+                         void* stream);
+int gine_mp_bwd_win_finalize(const double* partials, int32_t num_tiles, int32_t channels,
+                             int32_t slice_channels, float* dlin_w, float* dlin_b,
+                             float* deps, void* stream);
+
+/* ------------------------------------------------------------------------------------
  * Node MLP  nn = Sequential(Linear(D,D), BatchNorm1d(D), ReLU(), Linear(D,D))
  * (models/gnn.py:21-26), plus the ResGnn epilogue (models/gnn.py:38-44).
  * fp32 MFMA (v_mfma_f32_32x32x2_f32) row-tile GEMMs with fused prologues/epilogues.

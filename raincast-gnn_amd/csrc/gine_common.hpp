@@ -49,6 +49,13 @@ __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 
 // and a select.  A NaN comes out quieted (its payload may differ from the CPU's).
 __device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.0f); }
 
+// Edge Linear(1, D): a*w + b, rounded like the host CPU's PyG path (see gine_hip.h).
+template <bool FMA>
+__device__ __forceinline__ float edge_lin(float a, float w, float b) {
+  if constexpr (FMA) return __builtin_fmaf(a, w, b);
+  return a * w + b;  // -ffp-contract=off: two roundings
+}
+
 // Double-precision block reduction helper over the 32 lanes of one MFMA column half.
 __device__ __forceinline__ double shfl_xor_d(double v, int m) {
   return __shfl_xor(v, m, kWave);

@@ -16,6 +16,7 @@
 // destination's sum.  Accumulation order is the CSR order = original edge order, hence
 // bit-identical to CPU scatter_add_ / index_add_.
 #include "gine_common.hpp"
+#include "gine_edge.hpp"
 #include "gine_reduce.hpp"
 #include "gine_slab.hpp"
 
@@ -26,13 +27,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-
-// Edge Linear(1, D): a*w + b, rounded like the host CPU's PyG path (see gine_hip.h).
-template <bool FMA>
-__device__ __forceinline__ float edge_lin(float a, float w, float b) {
-  if constexpr (FMA) return __builtin_fmaf(a, w, b);
-  return a * w + b;  // -ffp-contract=off: two roundings
-}
 
 // Neighbour rows in flight per lane.  (16 -- one round for k <= 15 -- was measured slower
 // at cfg2: the extra VGPRs halve the waves per SIMD, and those hide more latency.)
@@ -72,17 +66,21 @@ __global__ __launch_bounds__(kThreads) void k_mp_fwd(
   if (node >= N) return;  // whole row group leaves together; no block barrier below
 
   // Lanes past the last float4 (D/4 not a multiple of L) duplicate the last chunk so that
-  // every load is issued unconditionally; only their stores are masked.
-  float4 w[C], b[C], self[C], acc[C];
-  int qc[C];
-  const int64_t row = node * D4;
+  // every load is issued unconditionally; only their stores are masked.  Neighbour rows
+  // are addressed by 32-bit byte offsets from the table base (N*D*4 < 2^32, host-checked).
+  const char* xb = reinterpret_cast<const char*>(x4);
+  const uint32_t rowb = (uint32_t)D4 * 16u;
+  f4v w[C], b[C], self[C], acc[C];
+  uint32_t qb[C];
+  const uint32_t own = (uint32_t)node * rowb;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    qc[c] = min(t + c * L, D4 - 1);
-    acc[c] = f4_zero();
-    w[c] = lw4[qc[c]];
-    b[c] = lb4[qc[c]];
-    self[c] = x4[row + qc[c]];
+    const int q = min(t + c * L, D4 - 1);
+    qb[c] = (uint32_t)q * 16u;
+    acc[c] = f4v_zero();
+    w[c] = ld_f4v(reinterpret_cast<const char*>(lw4), qb[c]);
+    b[c] = ld_f4v(reinterpret_cast<const char*>(lb4), qb[c]);
+    self[c] = ld_f4v(xb, own + qb[c]);
   }
   const float ope = 1.0f + eps[0];
   const int beg = rowptr[node], end = rowptr[node + 1];
@@ -96,53 +94,57 @@ __global__ __launch_bounds__(kThreads) void k_mp_fwd(
       my_attr[t] = attr[base + t];
     }
     __builtin_amdgcn_wave_barrier();
-    for (int j = 0; j < cnt; j += U) {
-      float4 r[U][C];
+    int j = 0;
+    // full batches of U neighbours: no per-edge test
+    for (; j + U <= cnt; j += U) {
+      f4v r[U][C];
       float a[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int jj = min(j + u, cnt - 1);  // clamp: loads are always issued (no branch)
-        const int64_t src_row = (int64_t)my_nbr[jj] * D4;
-        a[u] = my_attr[jj];
+        const uint32_t ro = (uint32_t)my_nbr[j + u] * rowb;
+        a[u] = my_attr[j + u];
 #pragma unroll
-        for (int c = 0; c < C; ++c) r[u][c] = x4[src_row + qc[c]];
+        for (int c = 0; c < C; ++c) r[u][c] = ld_f4v(xb, ro + qb[c]);
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < C; ++c) fwd_edge<FMA>(acc[c], r[u][c], a[u], w[c], b[c]);
+    }
+    // tail: loads clamped to the last neighbour (always issued), sums tested
+    if (j < cnt) {
+      f4v r[U][C];
+      float a[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        const int jj = min(j + u, cnt - 1);
+        const uint32_t ro = (uint32_t)my_nbr[jj] * rowb;
+        a[u] = my_attr[jj];
+#pragma unroll
+        for (int c = 0; c < C; ++c) r[u][c] = ld_f4v(xb, ro + qb[c]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
         if (j + u < cnt) {
 #pragma unroll
-          for (int c = 0; c < C; ++c) {
-            // m = relu(x_j + lin(a)); the add rounds once, the sum rounds once per edge in
-            // edge order.
-            acc[c].x = acc[c].x + relu_nan(r[u][c].x + edge_lin<FMA>(a[u], w[c].x, b[c].x));
-            acc[c].y = acc[c].y + relu_nan(r[u][c].y + edge_lin<FMA>(a[u], w[c].y, b[c].y));
-            acc[c].z = acc[c].z + relu_nan(r[u][c].z + edge_lin<FMA>(a[u], w[c].z, b[c].z));
-            acc[c].w = acc[c].w + relu_nan(r[u][c].w + edge_lin<FMA>(a[u], w[c].w, b[c].w));
-          }
+          for (int c = 0; c < C; ++c) fwd_edge<FMA>(acc[c], r[u][c], a[u], w[c], b[c]);
         }
-      }
     }
     __builtin_amdgcn_wave_barrier();
   }
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int q = t + c * L;
-    if (q < D4) {
-      float4 o;
-      o.x = acc[c].x + ope * self[c].x;
-      o.y = acc[c].y + ope * self[c].y;
-      o.z = acc[c].z + ope * self[c].z;
-      o.w = acc[c].w + ope * self[c].w;
-      z4[row + q] = o;
-    }
+    if (q < D4) z4[node * D4 + q] = to_float4(add_scaled(acc[c], ope, self[c]));
   }
 }
 
 // ----------------------------------------------------------------------------------------
 // Backward over the out-edge CSR (source-sorted, stable)
 // ----------------------------------------------------------------------------------------
+// (C == 1: 4 workgroups per CU, i.e. the kernel fits 128 VGPRs = 4 waves per SIMD)
 template <int L, int C, bool FMA>
-__global__ __launch_bounds__(kThreads) void k_mp_bwd(
+__global__ __launch_bounds__(kThreads, C == 1 ? 4 : 2) void k_mp_bwd(
     const float4* __restrict__ dz4, const float4* __restrict__ x4,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ nbr,
     const float* __restrict__ attr, const float4* __restrict__ lw4,
@@ -167,17 +169,24 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
   const int g = lane / L, t = lane % L;
   const float ope = 1.0f + eps[0];
   const bool add_self = (flags & GINE_MP_BWD_SELF) != 0;
+  const char* dzb = reinterpret_cast<const char*>(dz4);
+  const char* xb = reinterpret_cast<const char*>(x4);
+  // the residual gradient row is loaded with the node's own rows (unconditionally, from
+  // dz when there is none): a load behind the gather would add a round trip per tile
+  const char* rb = reinterpret_cast<const char*>(dres4 != nullptr ? dres4 : dz4);
+  const uint32_t rowb = (uint32_t)D4 * 16u;
 
-  float4 w[C], b[C];
-  int qc[C];
-  double pw[C][4], pb[C][4], pe[C][4];  // sum dm*a, sum dm, sum dz*x (per-node terms)
+  f4v w[C], b[C];
+  uint32_t qb[C];
+  double pw[C][4], pb[C][4];  // sum dm*a, sum dm (per channel, per-node terms)
+  double pe = 0.0;            // sum over nodes and channels of dz*x
 #pragma unroll
   for (int c = 0; c < C; ++c) {
-    qc[c] = min(t + c * L, D4 - 1);
-    w[c] = lw4[qc[c]];
-    b[c] = lb4[qc[c]];
+    qb[c] = (uint32_t)min(t + c * L, D4 - 1) * 16u;
+    w[c] = ld_f4v(reinterpret_cast<const char*>(lw4), qb[c]);
+    b[c] = ld_f4v(reinterpret_cast<const char*>(lb4), qb[c]);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) pw[c][k] = pb[c][k] = pe[c][k] = 0.0;
+    for (int k = 0; k < 4; ++k) pw[c][k] = pb[c][k] = 0.0;
   }
   int32_t* my_nbr = &s_nbr[wave][g * L];
   float* my_attr = &s_attr[wave][g * L];
@@ -191,18 +200,15 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
   for (int tile = t_begin + pos; tile < t_end; tile += blocks_here) {
     const int64_t node = (int64_t)tile * (kWaves * GPW) + wave * GPW + g;
     if (node >= N) continue;
-    const int64_t row = node * D4;
-    float4 h[C], g_self[C], acc[C], accw[C], r_self[C];
-    // the residual gradient row is loaded with the node's own rows (unconditionally, from
-    // dz when there is none): a load behind the gather would add a round trip per tile
-    const float4* rsrc = dres4 != nullptr ? dres4 : dz4;
+    const uint32_t own = (uint32_t)node * rowb;
+    f4v h[C], g_self[C], acc[C], accw[C], r_self[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      acc[c] = f4_zero();
-      accw[c] = f4_zero();
-      h[c] = x4[row + qc[c]];
-      g_self[c] = dz4[row + qc[c]];
-      r_self[c] = rsrc[row + qc[c]];
+      acc[c] = f4v_zero();
+      accw[c] = f4v_zero();
+      h[c] = ld_f4v(xb, own + qb[c]);
+      g_self[c] = ld_f4v(dzb, own + qb[c]);
+      r_self[c] = ld_f4v(rb, own + qb[c]);
     }
     // pre-activation of this node's outgoing messages: h + (a*W + b) depends on the edge
     // only through a, so h is loaded once per source node.
@@ -215,38 +221,23 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
       }
       __builtin_amdgcn_wave_barrier();
       for (int j = 0; j < cnt; j += U) {
-        float4 r[U][C];
+        f4v r[U][C];
         float a[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int jj = min(j + u, cnt - 1);
-          const int64_t dst_row = (int64_t)my_nbr[jj] * D4;
+          const uint32_t ro = (uint32_t)my_nbr[jj] * rowb;
           a[u] = my_attr[jj];
 #pragma unroll
-          for (int c = 0; c < C; ++c) r[u][c] = dz4[dst_row + qc[c]];
+          for (int c = 0; c < C; ++c) r[u][c] = ld_f4v(dzb, ro + qb[c]);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < U; ++u)
           if (j + u < cnt) {
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-              float4 dm;
-              dm.x = (h[c].x + edge_lin<FMA>(a[u], w[c].x, b[c].x) > 0.f) ? r[u][c].x : 0.f;
-              dm.y = (h[c].y + edge_lin<FMA>(a[u], w[c].y, b[c].y) > 0.f) ? r[u][c].y : 0.f;
-              dm.z = (h[c].z + edge_lin<FMA>(a[u], w[c].z, b[c].z) > 0.f) ? r[u][c].z : 0.f;
-              dm.w = (h[c].w + edge_lin<FMA>(a[u], w[c].w, b[c].w) > 0.f) ? r[u][c].w : 0.f;
-              acc[c].x = acc[c].x + dm.x;
-              acc[c].y = acc[c].y + dm.y;
-              acc[c].z = acc[c].z + dm.z;
-              acc[c].w = acc[c].w + dm.w;
-              // this node's fp32 share of dW_e = sum_e dm_e * a_e (fp64 across nodes)
-              accw[c].x = __builtin_fmaf(dm.x, a[u], accw[c].x);
-              accw[c].y = __builtin_fmaf(dm.y, a[u], accw[c].y);
-              accw[c].z = __builtin_fmaf(dm.z, a[u], accw[c].z);
-              accw[c].w = __builtin_fmaf(dm.w, a[u], accw[c].w);
-            }
+            for (int c = 0; c < C; ++c)
+              bwd_edge<FMA>(acc[c], accw[c], r[u][c], a[u], h[c], w[c], b[c]);
           }
-        }
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -254,34 +245,20 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
     for (int c = 0; c < C; ++c) {
       const int q = t + c * L;
       if (q < D4) {
-        float4 o = acc[c];
         // db_e = sum_e dm_e: each source node contributes its message-gradient sum
-        pb[c][0] += (double)acc[c].x;
-        pb[c][1] += (double)acc[c].y;
-        pb[c][2] += (double)acc[c].z;
-        pb[c][3] += (double)acc[c].w;
-        pw[c][0] += (double)accw[c].x;
-        pw[c][1] += (double)accw[c].y;
-        pw[c][2] += (double)accw[c].z;
-        pw[c][3] += (double)accw[c].w;
-        if (add_self) {
-          o.x = o.x + ope * g_self[c].x;
-          o.y = o.y + ope * g_self[c].y;
-          o.z = o.z + ope * g_self[c].z;
-          o.w = o.w + ope * g_self[c].w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          pb[c][k] += (double)acc[c][k];
+          pw[c][k] += (double)accw[c][k];
         }
+        f4v o = add_self ? add_scaled(acc[c], ope, g_self[c]) : acc[c];
         if (dres4 != nullptr) {
-          const float4 d = r_self[c];
-          o.x = o.x + d.x;
-          o.y = o.y + d.y;
-          o.z = o.z + d.z;
-          o.w = o.w + d.w;
+          o.xy = o.xy + r_self[c].xy;
+          o.zw = o.zw + r_self[c].zw;
         }
-        dx4[row + q] = o;
-        pe[c][0] += (double)g_self[c].x * (double)h[c].x;
-        pe[c][1] += (double)g_self[c].y * (double)h[c].y;
-        pe[c][2] += (double)g_self[c].z * (double)h[c].z;
-        pe[c][3] += (double)g_self[c].w * (double)h[c].w;
+        dx4[node * D4 + q] = to_float4(o);
+        pe += ((double)g_self[c].x * (double)h[c].x + (double)g_self[c].y * (double)h[c].y) +
+              ((double)g_self[c].z * (double)h[c].z + (double)g_self[c].w * (double)h[c].w);
       }
     }
   }
@@ -296,10 +273,11 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
       for (int m = L; m < kWave; m <<= 1) {
         pw[c][k] += shfl_xor_d(pw[c][k], m);
         pb[c][k] += shfl_xor_d(pb[c][k], m);
-        pe[c][k] += shfl_xor_d(pe[c][k], m);
       }
     }
   }
+#pragma unroll
+  for (int m = 1; m < kWave; m <<= 1) pe += shfl_xor_d(pe, m);
   for (int wv = 0; wv < kWaves; ++wv) {
     if (wave == wv && g == 0) {
 #pragma unroll
@@ -312,20 +290,24 @@ __global__ __launch_bounds__(kThreads) void k_mp_bwd(
             if (wv == 0) {
               s_red[ch] = pw[c][k];
               s_red[D + ch] = pb[c][k];
-              s_red[2 * D + ch] = pe[c][k];
             } else {
               s_red[ch] += pw[c][k];
               s_red[D + ch] += pb[c][k];
-              s_red[2 * D + ch] += pe[c][k];
             }
           }
         }
       }
+      if (lane == 0) s_red[2 * D + wv] = pe;
     }
     __syncthreads();
   }
-  // row layout [dW_e (D) | db_e (D) | sum over channels of dz*x (1) | unused]
-  block_tree_sum(s_red + 2 * D, D);
+  // row layout [dW_e (D) | db_e (D) | sum over nodes and channels of dz*x (1) | unused]
+  if (threadIdx.x == 0) {
+    double e = 0.0;
+    for (int wv = 0; wv < kWaves; ++wv) e += s_red[2 * D + wv];
+    s_red[2 * D] = e;
+  }
+  __syncthreads();
   double* out = partials + (size_t)vb * 3 * D;
   for (int i = threadIdx.x; i <= 2 * D; i += kThreads) out[i] = s_red[i];
 }
@@ -431,7 +413,7 @@ extern "C" int gine_mp_fwd(const float* x, const int32_t* in_rowptr, const int32
   Shape sh;
   if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
   if (num_nodes < 0 || (flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
-  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (num_nodes * channels * 4 >= (int64_t(1) << 32)) return GINE_ERR_TOO_LARGE;
   if (num_nodes == 0) return GINE_OK;
   if (!x || !in_rowptr || !lin_w || !lin_b || !eps || !z) return GINE_ERR_INVALID;
   const int D4 = channels / 4;
@@ -467,7 +449,7 @@ static int mp_bwd_launch(const float* dz, const float* x, const int32_t* out_row
   if (!pick_shape(channels, &sh)) return GINE_ERR_DIM;
   if (num_nodes < 0 || (flags & ~(GINE_MP_BWD_SELF | GINE_MP_LIN_MULADD)) != 0)
     return GINE_ERR_INVALID;
-  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (num_nodes * channels * 4 >= (int64_t(1) << 32)) return GINE_ERR_TOO_LARGE;
   if (!dz || !x || !out_rowptr || !lin_w || !lin_b || !eps || !dx || !partials)
     return GINE_ERR_INVALID;
   const int D4 = channels / 4;

@@ -1,0 +1,552 @@
+// Window-staged GINEConv message passing: neighbour feature rows gathered from LDS.
+//
+// Same arithmetic as gine_mp.hip (PyG GINEConv.message + SumAggregation, models/gnn.py:41,44;
+// bit-identical forward z and backward dx), different data movement.  A PyG batch is a
+// block-diagonal union of station graphs (Batch.from_data_list), so the in-neighbours of a
+// run of consecutive destination nodes all lie in one short run of source rows -- the
+// node's own graph.  gine_graph_plan_windows cuts the destinations into tiles whose source
+// window [lo, lo + rows) fits in LDS; a workgroup then owns (tile, column slice):
+//   1. stages the window's CS-channel slice of x (rows x CS x 4 bytes) and the tile's edge
+//      list (source offset in the window + attribute) in LDS with coalesced loads,
+//   2. walks the tile's destinations, Q = CS/4 lanes per destination (one float4 each),
+//      reading every neighbour row from LDS in the original edge order.
+// The per-edge gather of 512-byte rows from L2/MALL (11 neighbours per destination) becomes
+// one streaming read of each window slice per tile: HBM/L2 bytes per layer fall from
+// E*D*4 gathered to about (tiles per window) * N*D*4 staged.
+#include "gine_common.hpp"
+#include "gine_edge.hpp"
+#include "gine_slab.hpp"
+#include "gine_reduce.hpp"
+
+#include <climits>
+
+namespace gine {
+namespace {
+
+constexpr int kWinThreads = 512;
+constexpr int kWinWaves = kWinThreads / kWave;
+constexpr int kWinMaxSlices = 8;    // column slices per tile (= finalize columns per block)
+constexpr int kWinUnroll = 6;       // neighbour rows in flight per lane (LDS reads)
+constexpr int kWinTileNodes = 128;  // planner cap on nodes per tile
+constexpr int kWinRowBytes = 64 * 1024;
+// every thread's share of a tile's global loads, issued in one batch (bounds by construction:
+// window slice <= kWinRowBytes, tile edges <= kWinEdgeLoads * kWinThreads)
+constexpr int kWinRowLoads = kWinRowBytes / 16 / kWinThreads;  // float4 per thread
+constexpr int kWinEdgeLoads = 4;
+
+struct WinPlan {
+  const int32_t* tile_begin;  // [T + 1]
+  const int32_t* win_lo;      // [T]
+  const int32_t* win_rows;    // [T]
+  int max_rows, max_edges, max_nodes;
+};
+
+// Dynamic LDS: window [max_rows][Q] float4 | nbr [max_edges] | attr [max_edges] | rp [nodes+1]
+__host__ __device__ inline size_t win_lds_bytes(int cs, int max_rows, int max_edges,
+                                                int max_nodes) {
+  return (size_t)max_rows * cs * 4 + (size_t)max_edges * 8 + (size_t)(max_nodes + 1) * 4;
+}
+
+struct WinLds {
+  float4* win;
+  int32_t* nbr;  // neighbour's byte offset in the window (row * Q * 16)
+  float* attr;
+  int32_t* rp;
+  __device__ WinLds(float4* base, const WinPlan& p, int Q) {
+    win = base;
+    nbr = reinterpret_cast<int32_t*>(base + (size_t)p.max_rows * Q);
+    attr = reinterpret_cast<float*>(nbr + p.max_edges);
+    rp = reinterpret_cast<int32_t*>(attr + p.max_edges);
+  }
+};
+
+// One tile's staging: every global load of the window slice, the CSR segment and the row
+// pointers is issued before the first LDS store, so the tile pays one memory latency.
+template <int Q>
+__device__ __forceinline__ void stage_tile(const float4* __restrict__ tab4, int D4, int col4,
+                                           const int32_t* __restrict__ rowptr,
+                                           const int32_t* __restrict__ nbr,
+                                           const float* __restrict__ attr, int n0, int nodes,
+                                           int lo, int rows, const WinLds& lds) {
+  const int tid = threadIdx.x;
+  const int n = rows * Q;
+  float4 v[kWinRowLoads];
+#pragma unroll
+  for (int k = 0; k < kWinRowLoads; ++k) {
+    const int i = min(tid + k * kWinThreads, max(n - 1, 0));
+    v[k] = n > 0 ? tab4[(int64_t)(lo + i / Q) * D4 + col4 + i % Q] : f4_zero();
+  }
+  const int e0 = rowptr[n0];
+  const int ne = rowptr[n0 + nodes] - e0;
+  const int rp = rowptr[n0 + min(tid, nodes)];
+  int32_t nb[kWinEdgeLoads];
+  float at[kWinEdgeLoads];
+#pragma unroll
+  for (int k = 0; k < kWinEdgeLoads; ++k) {
+    const int i = min(tid + k * kWinThreads, max(ne - 1, 0));
+    nb[k] = ne > 0 ? nbr[e0 + i] : 0;
+    at[k] = ne > 0 ? attr[e0 + i] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < kWinRowLoads; ++k) {
+    const int i = tid + k * kWinThreads;
+    if (i < n) lds.win[i] = v[k];
+  }
+  if (tid <= nodes) lds.rp[tid] = rp - e0;
+#pragma unroll
+  for (int k = 0; k < kWinEdgeLoads; ++k) {
+    const int i = tid + k * kWinThreads;
+    if (i < ne) {
+      lds.nbr[i] = (nb[k] - lo) * Q * 16;
+      lds.attr[i] = at[k];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Forward: z = sum_{in-edges, edge order} relu(x[src] + lin(a)) + (1 + eps) x
+// ----------------------------------------------------------------------------------------
+template <int CS, bool FMA>
+__global__ __launch_bounds__(kWinThreads, 2) void k_mp_fwd_win(
+    const float4* __restrict__ x4, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ nbr, const float* __restrict__ attr,
+    const float4* __restrict__ lw4, const float4* __restrict__ lb4,
+    const float* __restrict__ eps, float4* __restrict__ z4, WinPlan plan, int D4, int S) {
+  constexpr int Q = CS / 4, G = kWinThreads / Q, U = kWinUnroll;
+  constexpr int P = (kWinTileNodes + G - 1) / G;  // destination passes per lane group
+  extern __shared__ float4 s_dyn[];
+  const WinLds lds(s_dyn, plan, Q);
+  // consecutive logical blocks (the slices of a tile, then the next tile of the same
+  // graph: the same window rows) stay on one XCD
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lb / S, col4 = (lb % S) * Q;
+  const int n0 = plan.tile_begin[tile], nodes = plan.tile_begin[tile + 1] - n0;
+  const int lo = plan.win_lo[tile];
+  const int g = threadIdx.x / Q, t = threadIdx.x % Q;
+  // the lane's own rows (x_i for the (1+eps) x_i term) join the staging batch
+  const char* xb = reinterpret_cast<const char*>(x4);
+  const uint32_t rowb = (uint32_t)D4 * 16u, tb = (uint32_t)(col4 + t) * 16u;
+  f4v self[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    self[p] = ld_f4v(xb, (uint32_t)(n0 + min(g + p * G, nodes - 1)) * rowb + tb);
+  const f4v w = ld_f4v(reinterpret_cast<const char*>(lw4), tb);
+  const f4v b = ld_f4v(reinterpret_cast<const char*>(lb4), tb);
+  const float ope = 1.0f + eps[0];
+  stage_tile<Q>(x4, D4, col4, rowptr, nbr, attr, n0, nodes, lo, plan.win_rows[tile], lds);
+  __syncthreads();
+  const char* wb = reinterpret_cast<const char*>(lds.win) + t * 16;
+
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int d = g + p * G;
+    if (d >= nodes) break;
+    const int eb = lds.rp[d], ee = lds.rp[d + 1];
+    f4v acc = f4v_zero();
+    int j = eb;
+    for (; j + U <= ee; j += U) {
+      f4v r[U];
+      float a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        r[u] = *reinterpret_cast<const f4v*>(wb + lds.nbr[j + u]);
+        a[u] = lds.attr[j + u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) fwd_edge<FMA>(acc, r[u], a[u], w, b);
+    }
+    if (j < ee) {
+      f4v r[U];
+      float a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = min(j + u, ee - 1);
+        r[u] = *reinterpret_cast<const f4v*>(wb + lds.nbr[jj]);
+        a[u] = lds.attr[jj];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j + u < ee) fwd_edge<FMA>(acc, r[u], a[u], w, b);
+    }
+    z4[(int64_t)(n0 + d) * D4 + col4 + t] = to_float4(add_scaled(acc, ope, self[p]));
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Backward over the out-edge CSR: the window holds dz rows of the tile's destinations.
+// partials row `tile` (fp64 [3][D]): columns [slice] of sum dm*a and sum dm, and at
+// 2D + slice the slice's sum of dz*x.
+// ----------------------------------------------------------------------------------------
+template <int CS, bool FMA>
+__global__ __launch_bounds__(kWinThreads, 2) void k_mp_bwd_win(
+    const float4* __restrict__ dz4, const float4* __restrict__ x4,
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ nbr,
+    const float* __restrict__ attr, const float4* __restrict__ lw4,
+    const float4* __restrict__ lb4, const float* __restrict__ eps,
+    const float4* __restrict__ dres4, float4* __restrict__ dx4, double* __restrict__ partials,
+    WinPlan plan, int D4, int S, int flags, MlpSlabJob job) {
+  constexpr int Q = CS / 4, G = kWinThreads / Q, U = kWinUnroll;
+  constexpr int P = (kWinTileNodes + G - 1) / G;
+  extern __shared__ float4 s_dyn[];
+  if ((int)blockIdx.x < job.nblocks) {  // side job: the node-MLP weight-gradient slab
+    if (threadIdx.x < 256)
+      job.run(blockIdx.x, reinterpret_cast<double(*)[kSlabQuads * 4 + 1]>(s_dyn));
+    return;
+  }
+  const WinLds lds(s_dyn, plan, Q);
+  const int lb = xcd_remap(blockIdx.x - job.nblocks, gridDim.x - job.nblocks);
+  const int tile = lb / S, slice = lb % S, col4 = slice * Q;
+  const int n0 = plan.tile_begin[tile], nodes = plan.tile_begin[tile + 1] - n0;
+  const int lo = plan.win_lo[tile];
+  const int g = threadIdx.x / Q, t = threadIdx.x % Q;
+  const char* xb = reinterpret_cast<const char*>(x4);
+  const char* dzb = reinterpret_cast<const char*>(dz4);
+  const char* rb = reinterpret_cast<const char*>(dres4 != nullptr ? dres4 : dz4);
+  const uint32_t rowb = (uint32_t)D4 * 16u, tb = (uint32_t)(col4 + t) * 16u;
+  f4v h[P], gs[P], rs[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const uint32_t off = (uint32_t)(n0 + min(g + p * G, nodes - 1)) * rowb + tb;
+    h[p] = ld_f4v(xb, off);
+    gs[p] = ld_f4v(dzb, off);
+    rs[p] = ld_f4v(rb, off);
+  }
+  const f4v w = ld_f4v(reinterpret_cast<const char*>(lw4), tb);
+  const f4v b = ld_f4v(reinterpret_cast<const char*>(lb4), tb);
+  const float ope = 1.0f + eps[0];
+  const bool add_self = (flags & GINE_MP_BWD_SELF) != 0;
+  stage_tile<Q>(dz4, D4, col4, rowptr, nbr, attr, n0, nodes, lo, plan.win_rows[tile], lds);
+  __syncthreads();
+  const char* wb = reinterpret_cast<const char*>(lds.win) + t * 16;
+
+  double pw[4] = {0.0, 0.0, 0.0, 0.0}, pb[4] = {0.0, 0.0, 0.0, 0.0};
+  double pe = 0.0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int d = g + p * G;
+    if (d >= nodes) break;
+    const int eb = lds.rp[d], ee = lds.rp[d + 1];
+    f4v acc = f4v_zero(), accw = f4v_zero();
+    int j = eb;
+    for (; j + U <= ee; j += U) {
+      f4v r[U];
+      float a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        r[u] = *reinterpret_cast<const f4v*>(wb + lds.nbr[j + u]);
+        a[u] = lds.attr[j + u];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) bwd_edge<FMA>(acc, accw, r[u], a[u], h[p], w, b);
+    }
+    if (j < ee) {
+      f4v r[U];
+      float a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = min(j + u, ee - 1);
+        r[u] = *reinterpret_cast<const f4v*>(wb + lds.nbr[jj]);
+        a[u] = lds.attr[jj];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j + u < ee) bwd_edge<FMA>(acc, accw, r[u], a[u], h[p], w, b);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pb[k] += (double)acc[k];
+      pw[k] += (double)accw[k];
+    }
+    f4v o = add_self ? add_scaled(acc, ope, gs[p]) : acc;
+    if (dres4 != nullptr) {
+      o.xy = o.xy + rs[p].xy;
+      o.zw = o.zw + rs[p].zw;
+    }
+    dx4[(int64_t)(n0 + d) * D4 + col4 + t] = to_float4(o);
+    pe += ((double)gs[p].x * (double)h[p].x + (double)gs[p].y * (double)h[p].y) +
+          ((double)gs[p].z * (double)h[p].z + (double)gs[p].w * (double)h[p].w);
+  }
+
+  // Fixed-order block reduction: the G destination groups of a wave by butterfly over the
+  // lane bits above Q, then the waves in order through LDS (the window is dead by now).
+#pragma unroll
+  for (int m = Q; m < kWave; m <<= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pw[k] += shfl_xor_d(pw[k], m);
+      pb[k] += shfl_xor_d(pb[k], m);
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < kWave; m <<= 1) pe += shfl_xor_d(pe, m);
+  __syncthreads();
+  double* s_red = reinterpret_cast<double*>(s_dyn);  // [kWinWaves][2 * CS + 1]
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  if (lane < Q) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s_red[wave * (2 * CS + 1) + 4 * lane + k] = pw[k];
+      s_red[wave * (2 * CS + 1) + CS + 4 * lane + k] = pb[k];
+    }
+  }
+  if (lane == 0) s_red[wave * (2 * CS + 1) + 2 * CS] = pe;
+  __syncthreads();
+  const int D = D4 * 4;
+  double* out = partials + (size_t)tile * 3 * D;
+  for (int i = threadIdx.x; i <= 2 * CS; i += kWinThreads) {
+    double v = 0.0;
+#pragma unroll
+    for (int wv = 0; wv < kWinWaves; ++wv) v += s_red[wv * (2 * CS + 1) + i];
+    if (i < CS) out[slice * CS + i] = v;
+    else if (i < 2 * CS) out[D + slice * CS + (i - CS)] = v;
+    else out[2 * D + slice] = v;
+  }
+}
+
+// Finish: blocks b < nb-1 own kWinMaxSlices of the 2D columns [dW_e | db_e]; the last one
+// sums the S eps columns of every tile, then the S totals in slice order.
+struct MpWinFin {
+  float *dlin_w, *dlin_b, *deps;
+  int D, S, nb;
+  __device__ int col(int b, int j) const {
+    if (b == nb - 1) return j < S ? 2 * D + j : -1;
+    const int c = kWinMaxSlices * b + j;
+    return c < 2 * D ? c : -1;
+  }
+  __device__ void finish(int b, const double* tot) const {
+    const int t = threadIdx.x;
+    if (b == nb - 1) {
+      if (t == 0) {
+        double s = 0.0;
+        for (int j = 0; j < S; ++j) s += tot[j];
+        deps[0] = (float)s;
+      }
+      return;
+    }
+    const int c = kWinMaxSlices * b + t;
+    if (t >= kWinMaxSlices || c >= 2 * D) return;
+    if (c < D) dlin_w[c] = (float)tot[t];
+    else dlin_b[c - D] = (float)tot[t];
+  }
+};
+
+// ----------------------------------------------------------------------------------------
+// Host side
+// ----------------------------------------------------------------------------------------
+bool valid_plan(const gine_window_plan* p, int64_t num_nodes, int32_t channels) {
+  if (!p || !p->tile_begin || !p->win_lo || !p->win_rows || p->num_tiles <= 0) return false;
+  const int cs = p->slice_channels;
+  if (!(cs == 8 || cs == 16 || cs == 32) || channels % cs != 0) return false;
+  if (channels / cs > kWinMaxSlices) return false;
+  if (p->max_rows < 0 || p->max_edges < 0 || p->max_nodes <= 0) return false;
+  if ((int64_t)p->max_rows * cs * 4 > kWinRowBytes) return false;
+  if (p->max_edges > kWinEdgeLoads * kWinThreads || p->max_nodes > kWinTileNodes) return false;
+  if (num_nodes <= 0 || num_nodes * channels * 4 >= (int64_t(1) << 32)) return false;
+  return win_lds_bytes(cs, p->max_rows, p->max_edges, p->max_nodes) <= GINE_WINDOW_LDS_BYTES;
+}
+
+WinPlan device_plan(const gine_window_plan* p) {
+  return WinPlan{p->tile_begin, p->win_lo, p->win_rows, p->max_rows, p->max_edges,
+                 p->max_nodes};
+}
+
+// Raise the kernel's dynamic-LDS ceiling once per instantiation (thread-safe static init).
+template <auto K>
+int set_lds_limit() {
+  static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(K),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  GINE_WINDOW_LDS_BYTES);
+  return e == hipSuccess ? GINE_OK : GINE_ERR_HIP_BASE + (int)e;
+}
+
+#define GINE_WIN_DISPATCH(CS_, FMA_FLAG, MACRO) \
+  switch (CS_) {                                \
+    case 8:                                     \
+      if (FMA_FLAG) MACRO(8, true);             \
+      else MACRO(8, false);                     \
+      break;                                    \
+    case 16:                                    \
+      if (FMA_FLAG) MACRO(16, true);            \
+      else MACRO(16, false);                    \
+      break;                                    \
+    default:                                    \
+      if (FMA_FLAG) MACRO(32, true);            \
+      else MACRO(32, false);                    \
+      break;                                    \
+  }
+
+int mp_bwd_win_launch(const float* dz, const float* x, const int32_t* out_rowptr,
+                      const int32_t* out_dst, const float* out_attr, const float* lin_w,
+                      const float* lin_b, const float* eps, const float* dres, float* dx,
+                      double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
+                      const gine_window_plan* plan, const MlpSlabJob& job, void* stream) {
+  if (!valid_plan(plan, num_nodes, channels)) return GINE_ERR_INVALID;
+  if ((flags & ~(GINE_MP_BWD_SELF | GINE_MP_LIN_MULADD)) != 0) return GINE_ERR_INVALID;
+  if (!dz || !x || !out_rowptr || !out_dst || !out_attr || !lin_w || !lin_b || !eps || !dx ||
+      !partials)
+    return GINE_ERR_INVALID;
+  const int cs = plan->slice_channels, S = channels / cs, D4 = channels / 4;
+  size_t smem = win_lds_bytes(cs, plan->max_rows, plan->max_edges, plan->max_nodes);
+  const size_t red = sizeof(double) * kWinWaves * (2 * (size_t)cs + 1);
+  const size_t jobb = job.nblocks > 0 ? sizeof(double) * kSlabGroups * (kSlabQuads * 4 + 1) : 0;
+  smem = smem > red ? smem : red;
+  smem = smem > jobb ? smem : jobb;
+  if (smem > GINE_WINDOW_LDS_BYTES) return GINE_ERR_INVALID;
+  const unsigned grid = (unsigned)(plan->num_tiles * S + job.nblocks);
+  const WinPlan wp = device_plan(plan);
+  hipStream_t s = as_stream(stream);
+  const bool fma = (flags & GINE_MP_LIN_MULADD) == 0;
+  int st = GINE_OK;
+#define LAUNCH_BWD_WIN(CS_, F_)                                                              \
+  do {                                                                                       \
+    st = set_lds_limit<k_mp_bwd_win<CS_, F_>>();                                               \
+    if (st == GINE_OK)                                                                       \
+      hipLaunchKernelGGL((k_mp_bwd_win<CS_, F_>), dim3(grid), dim3(kWinThreads), smem, s,    \
+                         (const float4*)dz, (const float4*)x, out_rowptr, out_dst, out_attr, \
+                         (const float4*)lin_w, (const float4*)lin_b, eps, (const float4*)dres, \
+                         (float4*)dx, partials, wp, D4, S, flags, job);                      \
+  } while (0)
+  GINE_WIN_DISPATCH(cs, fma, LAUNCH_BWD_WIN);
+#undef LAUNCH_BWD_WIN
+  if (st != GINE_OK) return st;
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_graph_plan_windows(const int32_t* rowptr, const int32_t* nbr,
+                                       int64_t num_nodes, int32_t max_rows, int32_t max_nodes,
+                                       int32_t max_edges, int32_t* tile_begin, int32_t* win_lo,
+                                       int32_t* win_rows, int32_t* num_tiles,
+                                       int32_t* maxima) {
+  if (!rowptr || !tile_begin || !win_lo || !win_rows || !num_tiles || !maxima)
+    return GINE_ERR_INVALID;
+  if (num_nodes < 0 || max_rows <= 0 || max_nodes <= 0 || max_edges <= 0)
+    return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  *num_tiles = 0;
+  maxima[0] = maxima[1] = maxima[2] = 0;
+  if (num_nodes == 0) return GINE_OK;
+  if (rowptr[num_nodes] > 0 && !nbr) return GINE_ERR_INVALID;
+  int T = 0, begin = 0, lo = INT_MAX, hi = -1, cnt = 0, ecnt = 0;
+  int mrows = 0, medges = 0, mnodes = 0;
+  auto close_tile = [&]() {
+    tile_begin[T] = begin;
+    win_lo[T] = hi >= lo ? lo : 0;
+    win_rows[T] = hi >= lo ? hi - lo + 1 : 0;
+    mrows = win_rows[T] > mrows ? win_rows[T] : mrows;
+    medges = ecnt > medges ? ecnt : medges;
+    mnodes = cnt > mnodes ? cnt : mnodes;
+    ++T;
+  };
+  for (int v = 0; v < (int)num_nodes; ++v) {
+    const int e0 = rowptr[v], e1 = rowptr[v + 1], deg = e1 - e0;
+    int vlo = INT_MAX, vhi = -1;
+    for (int e = e0; e < e1; ++e) {
+      vlo = nbr[e] < vlo ? nbr[e] : vlo;
+      vhi = nbr[e] > vhi ? nbr[e] : vhi;
+    }
+    if (deg > max_edges || (deg > 0 && vhi - vlo + 1 > max_rows)) return GINE_OK;  // no plan
+    const int nlo = vlo < lo ? vlo : lo, nhi = vhi > hi ? vhi : hi;
+    const bool too_wide = nhi >= nlo && nhi - nlo + 1 > max_rows;
+    if (cnt > 0 && (cnt == max_nodes || ecnt + deg > max_edges || too_wide)) {
+      close_tile();
+      begin = v;
+      lo = vlo;
+      hi = vhi;
+      cnt = 0;
+      ecnt = 0;
+    } else {
+      lo = nlo;
+      hi = nhi;
+    }
+    ++cnt;
+    ecnt += deg;
+  }
+  close_tile();
+  tile_begin[T] = (int32_t)num_nodes;
+  *num_tiles = T;
+  maxima[0] = mrows;
+  maxima[1] = medges;
+  maxima[2] = mnodes;
+  return GINE_OK;
+}
+
+extern "C" int gine_mp_fwd_win(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                               const float* in_attr, const float* lin_w, const float* lin_b,
+                               const float* eps, float* z, int64_t num_nodes, int32_t channels,
+                               int32_t flags, const gine_window_plan* plan, void* stream) {
+  if (!valid_plan(plan, num_nodes, channels)) return GINE_ERR_INVALID;
+  if ((flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
+  if (!x || !in_rowptr || !in_src || !in_attr || !lin_w || !lin_b || !eps || !z)
+    return GINE_ERR_INVALID;
+  const int cs = plan->slice_channels, S = channels / cs, D4 = channels / 4;
+  const size_t smem = win_lds_bytes(cs, plan->max_rows, plan->max_edges, plan->max_nodes);
+  const unsigned grid = (unsigned)(plan->num_tiles * S);
+  const WinPlan wp = device_plan(plan);
+  hipStream_t s = as_stream(stream);
+  const bool fma = (flags & GINE_MP_LIN_MULADD) == 0;
+  int st = GINE_OK;
+#define LAUNCH_FWD_WIN(CS_, F_)                                                              \
+  do {                                                                                       \
+    st = set_lds_limit<k_mp_fwd_win<CS_, F_>>();                                               \
+    if (st == GINE_OK)                                                                       \
+      hipLaunchKernelGGL((k_mp_fwd_win<CS_, F_>), dim3(grid), dim3(kWinThreads), smem, s,    \
+                         (const float4*)x, in_rowptr, in_src, in_attr, (const float4*)lin_w, \
+                         (const float4*)lin_b, eps, (float4*)z, wp, D4, S);                  \
+  } while (0)
+  GINE_WIN_DISPATCH(cs, fma, LAUNCH_FWD_WIN);
+#undef LAUNCH_FWD_WIN
+  if (st != GINE_OK) return st;
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_mp_bwd_win(const float* dz, const float* x, const int32_t* out_rowptr,
+                               const int32_t* out_dst, const float* out_attr,
+                               const float* lin_w, const float* lin_b, const float* eps,
+                               const float* dres, float* dx, double* partials,
+                               int64_t num_nodes, int32_t channels, int32_t flags,
+                               const gine_window_plan* plan, void* stream) {
+  const MlpSlabJob none{nullptr, 0, 0, 0, MlpWgradOut{nullptr, nullptr, nullptr, nullptr, 0}};
+  return mp_bwd_win_launch(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps, dres, dx,
+                           partials, num_nodes, channels, flags, plan, none, stream);
+}
+
+extern "C" int gine_mp_bwd_win_side(const float* dz, const float* x, const int32_t* out_rowptr,
+                                    const int32_t* out_dst, const float* out_attr,
+                                    const float* lin_w, const float* lin_b, const float* eps,
+                                    const float* dres, float* dx, double* partials,
+                                    int64_t num_nodes, int32_t channels, int32_t flags,
+                                    const gine_window_plan* plan, const float* wg_slab,
+                                    int32_t wg_chunks, int32_t mlp_channels, float* dw1,
+                                    float* db1, float* dw2, float* db2, void* stream) {
+  if (!wg_slab || wg_chunks <= 0 || mlp_channels <= 0) return GINE_ERR_INVALID;
+  const int64_t per = (int64_t)mlp_channels * mlp_channels + mlp_channels;
+  if (per % 4 != 0 || (reinterpret_cast<uintptr_t>(wg_slab) & 15) != 0) return GINE_ERR_INVALID;
+  const int cols = (int)ceil_div(per, kSlabQuads * 4);
+  const MlpSlabJob job{wg_slab, wg_chunks, cols, 2 * cols,
+                       MlpWgradOut{dw2, db2, dw1, db1, mlp_channels}};
+  return mp_bwd_win_launch(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps, dres, dx,
+                           partials, num_nodes, channels, flags, plan, job, stream);
+}
+
+extern "C" int gine_mp_bwd_win_finalize(const double* partials, int32_t num_tiles,
+                                        int32_t channels, int32_t slice_channels,
+                                        float* dlin_w, float* dlin_b, float* deps,
+                                        void* stream) {
+  if (num_tiles <= 0 || channels <= 0 || slice_channels <= 0) return GINE_ERR_INVALID;
+  if (channels % slice_channels != 0 || channels / slice_channels > kWinMaxSlices)
+    return GINE_ERR_INVALID;
+  if (!partials || !dlin_w || !dlin_b || !deps) return GINE_ERR_INVALID;
+  const int nb = (int)ceil_div(2 * channels, kWinMaxSlices) + 1;
+  const MpWinFin fin{dlin_w, dlin_b, deps, channels, channels / slice_channels, nb};
+  hipLaunchKernelGGL((k_colsum_fin<kWinMaxSlices, MpWinFin>), dim3(nb), dim3(256), 0,
+                     as_stream(stream), partials, num_tiles, 3 * channels, fin);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

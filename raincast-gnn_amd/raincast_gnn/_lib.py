@@ -29,6 +29,18 @@ _c_void_p = ctypes.c_void_p
 _i32, _i64, _f32, _size = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 _f64 = ctypes.c_double
 
+
+
+class WindowPlan(ctypes.Structure):
+    """``gine_window_plan`` (include/gine_hip.h): device tile arrays + LDS sizing."""
+    _fields_ = [("tile_begin", _c_void_p), ("win_lo", _c_void_p), ("win_rows", _c_void_p),
+                ("num_tiles", _i32), ("slice_channels", _i32), ("max_rows", _i32),
+                ("max_edges", _i32), ("max_nodes", _i32)]
+
+
+_plan_p = ctypes.POINTER(WindowPlan)
+WINDOW_LDS_BYTES = 80 * 1024
+
 # name -> argtypes (every entry point returns int status)
 _SIGNATURES = {
     "gine_graph_workspace_bytes": [_i64, _i64, ctypes.POINTER(_size)],
@@ -40,6 +52,14 @@ _SIGNATURES = {
     "gine_mp_bwd_side": [_c_void_p] * 11 + [_i64, _i32, _i32, _c_void_p, _i32, _i32]
                         + [_c_void_p] * 5,
     "gine_mp_bwd_finalize": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "gine_graph_plan_windows": [_c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p,
+                                _c_void_p, _c_void_p, ctypes.POINTER(_i32), _c_void_p],
+    "gine_mp_fwd_win": [_c_void_p] * 8 + [_i64, _i32, _i32, _plan_p, _c_void_p],
+    "gine_mp_bwd_win": [_c_void_p] * 11 + [_i64, _i32, _i32, _plan_p, _c_void_p],
+    "gine_mp_bwd_win_side": [_c_void_p] * 11 + [_i64, _i32, _i32, _plan_p, _c_void_p, _i32,
+                                                 _i32] + [_c_void_p] * 5,
+    "gine_mp_bwd_win_finalize": [_c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                 _c_void_p],
     "gine_mlp_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_fwd1": [_c_void_p] * 5 + [_i64, _i32, _c_void_p],
     "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,

@@ -84,6 +84,12 @@ def mp_forward(x, graph, lin_w, lin_b, eps, lin_flag=None):
     if N == 0:
         return z
     flag = edge_linear_flag() if lin_flag is None else lin_flag
+    plan = graph.window_plan("in", D)
+    if plan is not None:
+        call("gine_mp_fwd_win", ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src),
+             ptr(graph.in_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(z), N, D, flag,
+             ctypes.byref(plan), _lib.stream_handle(x.device))
+        return z
     call("gine_mp_fwd", ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
          ptr(lin_w), ptr(lin_b), ptr(eps), ptr(z), N, D, flag, _lib.stream_handle(x.device))
     return z
@@ -104,21 +110,33 @@ def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_
     deps = grad_out(p_e, (1,), dev) if p_e is not None else torch.empty(1, device=dev)
     if N == 0:
         return dx, dlw.zero_(), dlb.zero_(), deps.zero_()
-    P = _count("gine_mp_bwd_num_partials", N, D)
-    partials = torch.empty(P, 3, D, dtype=torch.float64, device=dev)
     stream = _lib.stream_handle(dev)
     flags = (_lib.GINE_MP_BWD_SELF if self_term else 0) | (
         edge_linear_flag() if lin_flag is None else lin_flag)
+    args = (ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst), ptr(graph.out_attr),
+            ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx))
+    plan = graph.window_plan("out", D)
+    if plan is not None:
+        P = plan.num_tiles
+        partials = torch.empty(P, 3, D, dtype=torch.float64, device=dev)
+        if side is None:
+            call("gine_mp_bwd_win", *args, ptr(partials), N, D, flags, ctypes.byref(plan),
+                 stream)
+        else:
+            slab, chunks, Dm, dw1, db1, dw2, db2 = side
+            call("gine_mp_bwd_win_side", *args, ptr(partials), N, D, flags, ctypes.byref(plan),
+                 ptr(slab), chunks, Dm, ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), stream)
+        call("gine_mp_bwd_win_finalize", ptr(partials), P, D, plan.slice_channels, ptr(dlw),
+             ptr(dlb), ptr(deps), stream)
+        return dx, dlw, dlb, deps
+    P = _count("gine_mp_bwd_num_partials", N, D)
+    partials = torch.empty(P, 3, D, dtype=torch.float64, device=dev)
     if side is None:
-        call("gine_mp_bwd", ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst),
-             ptr(graph.out_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx),
-             ptr(partials), N, D, flags, stream)
+        call("gine_mp_bwd", *args, ptr(partials), N, D, flags, stream)
     else:
         slab, chunks, Dm, dw1, db1, dw2, db2 = side
-        call("gine_mp_bwd_side", ptr(dz), ptr(x), ptr(graph.out_rowptr), ptr(graph.out_dst),
-             ptr(graph.out_attr), ptr(lin_w), ptr(lin_b), ptr(eps), ptr(dres), ptr(dx),
-             ptr(partials), N, D, flags, ptr(slab), chunks, Dm, ptr(dw1), ptr(db1), ptr(dw2),
-             ptr(db2), stream)
+        call("gine_mp_bwd_side", *args, ptr(partials), N, D, flags, ptr(slab), chunks, Dm,
+             ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), stream)
     call("gine_mp_bwd_finalize", ptr(partials), P, D, ptr(dlw), ptr(dlb), ptr(deps), stream)
     return dx, dlw, dlb, deps
 

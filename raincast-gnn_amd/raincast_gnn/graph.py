@@ -11,18 +11,77 @@ training run the same ``edge_index`` tensor (or a handful of them) recurs every 
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from collections import OrderedDict
 
 import torch
 
 from . import _lib
 
+# Window-staged message passing (gine_graph_plan_windows / gine_mp_*_win): channel-slice
+# widths tried, the LDS bytes a window slice may take, and the tile size in nodes.
+WINDOW_SLICES = (32, 16, 8)
+WINDOW_ROW_BYTES = 64 * 1024
+
+
+# A window launch has tiles x slices workgroups; below this many the gather kernels (one
+# workgroup per 8 nodes) fill the chip better (measured: cfg1, 4 tiles, is slower staged).
+WINDOW_MIN_WORKGROUPS = 256
+
+
+def window_settings() -> tuple[str, int]:
+    """(mode, max nodes per tile).  GINE_MP_WINDOW: "auto" (default) stages the backward
+    only -- measured faster than the gather kernel at cfg2, while the staged forward is
+    not --, "all" stages both directions, "0" uses the gather kernels everywhere."""
+    mode = os.environ.get("GINE_MP_WINDOW", "auto").lower()
+    if mode in ("0", "off", "false", "none"):
+        mode = "off"
+    elif mode in ("1", "all", "on"):
+        mode = "all"
+    elif mode != "auto":
+        raise ValueError(f"GINE_MP_WINDOW={mode!r}: expected auto, all or 0")
+    return mode, int(os.environ.get("GINE_MP_WINDOW_NODES", "128"))
+
+
+def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device,
+                 max_nodes: int) -> dict:
+    """slice channels -> (WindowPlan, device arrays) or None, from a host copy of one CSR.
+    Blocks on the device (a D2H copy): call outside graph capture."""
+    plans = {}
+    if num_nodes == 0:
+        return plans
+    rp = rowptr.cpu()
+    nb = nbr.cpu()
+    i32 = dict(dtype=torch.int32)
+    for cs in WINDOW_SLICES:
+        max_rows = WINDOW_ROW_BYTES // (cs * 4)
+        max_edges = (_lib.WINDOW_LDS_BYTES - max_rows * cs * 4 - (max_nodes + 1) * 4) // 8
+        tb = torch.empty(num_nodes + 1, **i32)
+        lo = torch.empty(num_nodes, **i32)
+        rows = torch.empty(num_nodes, **i32)
+        maxima = torch.zeros(3, **i32)
+        nt = ctypes.c_int32(0)
+        _lib.call("gine_graph_plan_windows", rp.data_ptr(), nb.data_ptr(), num_nodes, max_rows,
+                  max_nodes, max_edges, tb.data_ptr(), lo.data_ptr(), rows.data_ptr(),
+                  ctypes.byref(nt), maxima.data_ptr())
+        T = int(nt.value)
+        if T == 0:
+            plans[cs] = None
+            continue
+        arrays = (tb[:T + 1].to(device), lo[:T].to(device), rows[:T].to(device))
+        m = [int(v) for v in maxima]
+        plan = _lib.WindowPlan(arrays[0].data_ptr(), arrays[1].data_ptr(), arrays[2].data_ptr(),
+                               T, cs, m[0], m[1], max(m[2], 1))
+        plans[cs] = (plan, arrays)
+    return plans
+
 
 class GineGraph:
     """Stable CSR (by destination) + CSR (by source) of one edge list on one device."""
 
     __slots__ = ("num_nodes", "num_edges", "device", "in_rowptr", "in_src", "in_attr",
-                 "out_rowptr", "out_dst", "out_attr", "_error", "_checked")
+                 "out_rowptr", "out_dst", "out_attr", "_error", "_checked", "_windows")
 
     def __init__(self, edge_index: torch.Tensor, edge_attr: torch.Tensor | None,
                  num_nodes: int, flow: str = "source_to_target"):
@@ -65,8 +124,35 @@ class GineGraph:
         # ws / ei / attr are freed on return: they were allocated on the current stream, so
         # the caching allocator only hands them out again to work ordered after the sort.
         self._checked = False
+        self._windows = None
         if not torch.cuda.is_current_stream_capturing():
             self.check()
+            self._plan_windows()
+
+    def _plan_windows(self) -> None:
+        mode, max_nodes = window_settings()
+        self._windows = {"in": {}, "out": {}}
+        if mode == "off" or self.in_attr is None:
+            return
+        if mode == "all":
+            self._windows["in"] = plan_windows(self.in_rowptr, self.in_src, self.num_nodes,
+                                               self.device, max_nodes)
+        self._windows["out"] = plan_windows(self.out_rowptr, self.out_dst, self.num_nodes,
+                                            self.device, max_nodes)
+        self._windows["min_wg"] = 0 if mode == "all" else WINDOW_MIN_WORKGROUPS
+
+    def window_plan(self, side: str, channels: int):
+        """The widest-slice window plan usable at this channel count (``side`` "in" for the
+        forward, "out" for the backward), or None -> gather kernels."""
+        if self._windows is None:
+            return None
+        for cs, entry in self._windows[side].items():
+            if entry is not None and channels % cs == 0 and channels // cs <= 8:
+                plan = entry[0]
+                if plan.num_tiles * (channels // cs) < self._windows.get("min_wg", 0):
+                    return None
+                return plan
+        return None
 
     def check(self) -> None:
         """Raise IndexError (like torch.index_select) when an index was out of range."""

@@ -120,6 +120,106 @@ def test_mp_backward(case, D):
         assert_close_tiebreak(got.cpu(), ref32, ref64, TOL, name)
 
 
+@pytest.mark.parametrize("case", special_graphs(), ids=lambda c: c[0])
+@pytest.mark.parametrize("D,tile_nodes", [(128, 128), (64, 8), (32, 1), (16, 128), (256, 64),
+                                          (96, 128)])
+def test_mp_window_path_matches_gather_and_oracle(case, D, tile_nodes, monkeypatch):
+    """LDS-staged window kernels (gine_mp_*_win) vs the gather kernels and the oracle:
+    z and dx bit-identical, the parameter reductions at fp32 tolerance."""
+    _, ei, ea, n = case
+    monkeypatch.setenv("GINE_MP_WINDOW_NODES", str(tile_nodes))
+    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    gw = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    monkeypatch.setenv("GINE_MP_WINDOW", "0")
+    gg = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    assert gg.window_plan("in", D) is None and gg.window_plan("out", D) is None
+    plan_in, plan_out = gw.window_plan("in", D), gw.window_plan("out", D)
+    assert plan_in is not None and plan_out is not None
+    assert plan_in.max_nodes <= tile_nodes
+    torch.manual_seed(7 + D)
+    x = torch.randn(n, D, requires_grad=True)
+    dz, dres = torch.randn(n, D), torch.randn(n, D)
+    lw, lb, eps = _mp_params(D, seed=D + 3, eps=0.3)
+    lw.requires_grad_(True)
+    lb.requires_grad_(True)
+    eps.requires_grad_(True)
+    z_ref = O.gine_aggregate(x, ei, ea, lw, lb, eps)
+    (z_ref * dz).sum().backward()
+    dev_args = [t.detach().to(DEV) for t in (lw.reshape(-1), lb, eps)]
+    xd = x.detach().to(DEV)
+    z_w = Fn.mp_forward(xd, gw, *dev_args)
+    z_g = Fn.mp_forward(xd, gg, *dev_args)
+    assert torch.equal(z_w.cpu(), z_ref.detach())
+    assert torch.equal(z_w, z_g)
+    rw = Fn.mp_backward(dz.to(DEV), xd, gw, *dev_args, dres=dres.to(DEV))
+    rg = Fn.mp_backward(dz.to(DEV), xd, gg, *dev_args, dres=dres.to(DEV))
+    assert torch.equal(rw[0].cpu(), x.grad + dres)
+    assert torch.equal(rw[0], rg[0])
+    x64 = x.detach().double()
+    lw64, lb64, e64 = (t.detach().double().requires_grad_(True) for t in (lw, lb, eps))
+    O.gine_aggregate(x64, ei, ea.double(), lw64, lb64, e64).backward(dz.double())
+    for name, got, ref32, ref64 in (("dlin_w", rw[1], lw.grad.reshape(-1), lw64.grad.reshape(-1)),
+                                    ("dlin_b", rw[2], lb.grad, lb64.grad),
+                                    ("deps", rw[3], eps.grad, e64.grad)):
+        if ref32.abs().max() == 0:
+            assert got.abs().max().item() == 0
+            continue
+        assert_close_tiebreak(got.cpu(), ref32, ref64, TOL, name)
+    # deterministic: a second run is bit-identical
+    rw2 = Fn.mp_backward(dz.to(DEV), xd, gw, *dev_args, dres=dres.to(DEV))
+    for a, b in zip(rw, rw2):
+        assert torch.equal(a, b)
+
+
+def test_mp_window_auto_policy(monkeypatch):
+    """Default mode: the backward is staged when the launch has >= 256 workgroups, the
+    forward keeps the gather kernel; GINE_MP_WINDOW=0 disables staging."""
+    monkeypatch.delenv("GINE_MP_WINDOW", raising=False)
+    monkeypatch.delenv("GINE_MP_WINDOW_NODES", raising=False)
+    ei, ea, n = knn_batch_graph(500, 10, 32, seed=0)
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    assert g.window_plan("in", 128) is None
+    plan = g.window_plan("out", 128)
+    assert plan is not None and plan.num_tiles == 128 and plan.slice_channels == 32
+    ei1, ea1, n1 = knn_batch_graph(500, 10, 1, seed=0)
+    g1 = GineGraph(ei1.to(DEV), ea1.to(DEV), n1)
+    assert g1.window_plan("out", 128) is None      # 4 tiles x 4 slices: too few
+    monkeypatch.setenv("GINE_MP_WINDOW", "0")
+    g0 = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    assert g0.window_plan("out", 128) is None
+    monkeypatch.setenv("GINE_MP_WINDOW", "bogus")
+    with pytest.raises(ValueError):
+        GineGraph(ei.to(DEV), ea.to(DEV), n)
+
+
+def test_mp_nonfinite_inputs_follow_cpu():
+    """NaN / inf node features: relu keeps NaN (clamp_min), its backward passes the
+    gradient where relu(pre) is NaN (threshold_backward tests `result <= 0`)."""
+    ei, ea, n = knn_batch_graph(64, 4, 1, seed=3)
+    D = 64
+    torch.manual_seed(5)
+    x = torch.randn(n, D)
+    x[3, 5] = float("nan")
+    x[10, :7] = float("inf")
+    x[20, 40:] = float("-inf")
+    x[33, 1] = float("nan")
+    lw, lb, eps = _mp_params(D, seed=6, eps=0.2)
+    z_ref = O.gine_aggregate(x, ei, ea, lw, lb, eps)
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    z = Fn.mp_forward(x.to(DEV), g, lw.reshape(-1).to(DEV), lb.to(DEV), eps.to(DEV)).cpu()
+    assert torch.equal(z.isnan(), z_ref.isnan())
+    fin = ~z_ref.isnan()
+    assert torch.equal(z[fin], z_ref[fin])
+    xr = x.clone().requires_grad_(True)
+    dz = torch.randn(n, D)
+    O.gine_aggregate(xr, ei, ea, lw, lb, eps).backward(dz)
+    dx = Fn.mp_backward(dz.to(DEV), x.to(DEV), g, lw.reshape(-1).to(DEV), lb.to(DEV),
+                        eps.to(DEV))[0].cpu()
+    assert torch.equal(dx.isnan(), xr.grad.isnan())
+    fin = ~xr.grad.isnan()
+    assert torch.equal(dx[fin], xr.grad[fin])
+
+
 def test_mp_deterministic():
     ei, ea, n = random_graph(3000, 60000, seed=11)
     x = torch.randn(n, 128, device=DEV)

@@ -50,6 +50,16 @@ for s in $STEPS; do
              GINE_HIP_LIB=${v}libgine_hip.so run var_${n}_base 300 python bench.py --no-cpu --steps 30 ${VARARGS:-}
            done ;;
     varbase) run var_base 300 python bench.py --no-cpu --steps 30 ${VARARGS:-} ;;
+    mpmicro) run mp_micro 300 python tools/mp_micro.py ${MPARGS:-} ;;
+    mpvar) for v in raincast-gnn_amd/csrc/build/var/*/; do n=$(basename "$v")
+             GINE_HIP_LIB=${v}libgine_hip.so run mp_micro_${n} 300 python tools/mp_micro.py ${MPARGS:-}
+           done ;;
+    mpsq)  run mp_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d "$OUT/mp_sq1" -o run -- \
+               python3 tools/mp_micro.py --eager --reps 5 ${MPARGS:-}
+           run mp_sq2 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/mp_sq2" -o run -- \
+               python3 tools/mp_micro.py --eager --reps 5 ${MPARGS:-}
+           run mp_l2 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum --output-format csv -d "$OUT/mp_l2" -o run -- \
+               python3 tools/mp_micro.py --eager --reps 5 ${MPARGS:-} ;;
     floor) run launch_floor 300 python tools/launch_floor.py ;;
     counters) run list_counters 300 rocprofv3 -L ;;
     dsmicro) run ds_micro 300 python tools/ds_micro.py ;;
