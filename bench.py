@@ -17,6 +17,7 @@ CPU baseline (oracle, rank 0, N=1 only) are measured in the same process.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -157,6 +158,9 @@ def time_kernels(tr: Trainer, reps: int):
     slab = torch.empty(2 * C * (D * D + D), device=dev)
     dw1, dw2 = torch.empty(D, D, device=dev), torch.empty(D, D, device=dev)
     db1, db2 = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    win = g.window_plan("out", D)
+    win_part = (torch.empty(win.num_tiles, 3, D, dtype=torch.float64, device=dev)
+                if win is not None else None)
     Pm = Fn._count("gine_mp_bwd_num_partials", N, D)
     mp_part = torch.empty(Pm, 3, D, dtype=torch.float64, device=dev)
     dx = torch.empty_like(x)
@@ -179,10 +183,17 @@ def time_kernels(tr: Trainer, reps: int):
                                      ptr(g.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(z), N, D,
                                      lin, S[0]),
                         {"bytes": 4 * (2 * N * D + 2 * E + N + 1)}),
-        "gine_mp_bwd": (lambda: call("gine_mp_bwd", ptr(dz), ptr(x), ptr(g.out_rowptr),
-                                     ptr(g.out_dst), ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep),
-                                     ptr(dz), ptr(dx), ptr(mp_part), N, D, 1 | lin, S[0]),
-                        {"bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D}),
+        # the backward the training step runs: LDS-staged window kernel when the graph
+        # has a plan (GINE_MP_WINDOW policy, raincast_gnn/graph.py), else the gather kernel
+        "gine_mp_bwd": (
+            (lambda: call("gine_mp_bwd_win", ptr(dz), ptr(x), ptr(g.out_rowptr),
+                          ptr(g.out_dst), ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep), ptr(dz),
+                          ptr(dx), ptr(win_part), N, D, 1 | lin, ctypes.byref(win), S[0]))
+            if win is not None else
+            (lambda: call("gine_mp_bwd", ptr(dz), ptr(x), ptr(g.out_rowptr), ptr(g.out_dst),
+                          ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep), ptr(dz), ptr(dx),
+                          ptr(mp_part), N, D, 1 | lin, S[0])),
+            {"bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D}),
         "gine_mlp_fwd1": (lambda: call("gine_mlp_fwd1", ptr(z), ptr(w1), ptr(b1), ptr(a1),
                                        ptr(partials), N, D, S[0]),
                           {"flops": 2 * N * D * D, "bytes": 8 * N * D}),
@@ -196,6 +207,12 @@ def time_kernels(tr: Trainer, reps: int):
         "gine_mlp_bwd1": (lambda: call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save),
                                        ptr(coef), ptr(w1), ptr(dx), N, D, S[0]),
                           {"flops": 2 * N * D * D, "bytes": 12 * N * D}),
+        # what the step runs: dz = da1 W1 beside dW1 = da1^T z, dW2 = do^T r (+ biases)
+        "gine_mlp_bwd1_wgrad": (lambda: call("gine_mlp_bwd1_wgrad", ptr(dz), None, ptr(mask),
+                                             ptr(a1), ptr(bn_save), ptr(dbn), ptr(coef), ptr(z),
+                                             ptr(w1), ptr(dx), ptr(slab), None, None, None,
+                                             None, N, D, 2, S[0]),
+                                {"flops": 6 * N * D * D, "bytes": 4 * 5 * N * D + 5 * N * D}),
         "gine_mlp_wgrad": (lambda: call("gine_mlp_wgrad", ptr(dz), None, ptr(mask), ptr(a1),
                                         ptr(bn_save), ptr(dbn), ptr(coef), ptr(z), ptr(slab),
                                         ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), N, D, 2, S[0]),
@@ -248,37 +265,73 @@ def time_kernels(tr: Trainer, reps: int):
     return out
 
 
-def roofline_for(kernels: dict, layers: int):
-    # launches per step: every kernel once per layer
-    timed = [k for k in kernels if "alg_bytes" in kernels[k] or "alg_flops" in kernels[k]]
-    dominant = max(timed, key=lambda k: kernels[k]["us"])
-    rec = kernels[dominant]
-    if "flops" in rec or "alg_flops" in rec:
+STEP_KERNELS = ("gine_mp_fwd", "gine_mp_bwd", "gine_mlp_fwd1", "gine_mlp_fwd2",
+                "gine_mlp_bwd2", "gine_mlp_bwd1_wgrad")  # each runs once per GINE layer
+
+
+def _roof(name: str, rec: dict, bound: str, layers: int) -> dict:
+    if bound == "mfma":
         achieved = rec["TFLOPps"]
-        roof = {"kernel": dominant, "bound": "mfma", "achieved": achieved,
+        roof = {"kernel": name, "bound": "mfma", "achieved": achieved,
                 "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)}
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                "work_per_launch": rec["alg_flops"]}
     else:
         achieved = rec["GBps"]
-        roof = {"kernel": dominant, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4)}
+        roof = {"kernel": name, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "work_per_launch": rec["alg_bytes"]}
     roof["avg_us"] = rec["us"]
     roof["launches_per_step"] = layers
-    t = pmc_traffic(dominant)
+    t = pmc_traffic(name)
     roof["traffic"] = t["bytes"] if t else None
     roof["traffic_source"] = t["source"] if t else None
     return roof
+
+
+def roofline_for(kernels: dict, layers: int):
+    """The dominant kernel of the step (largest time per step among the per-layer kernels
+    the training step launches), against its bound: fp32 MFMA for the node-MLP GEMMs, HBM
+    for message passing."""
+    timed = [k for k in STEP_KERNELS if k in kernels]
+    dominant = max(timed, key=lambda k: kernels[k]["us"])
+    rec = kernels[dominant]
+    return _roof(dominant, rec, "mfma" if "alg_flops" in rec else "hbm", layers)
+
+
+def roofline_mp(kernels: dict, layers: int):
+    """The message-passing backward (the north-star gather/segmented-scatter path) against
+    HBM, with the measured copy ceiling beside the 8 TB/s spec."""
+    rec = kernels.get("gine_mp_bwd")
+    return _roof("gine_mp_bwd", rec, "hbm", layers) if rec else None
+
+
+def copy_ceiling_gbps(device, nbytes=1 << 30, reps=10):
+    """Measured HBM ceiling: device-to-device copy of a 1 GiB buffer (read + write bytes)."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=device).fill_(1.0)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    ev1.record()
+    ev1.synchronize()
+    sec = ev0.elapsed_time(ev1) * 1e-3 / reps
+    del src, dst
+    return round(2 * nbytes / sec / 1e9, 1)
 
 
 # entry point -> the kernels one call launches (names as in the rocprofv3 PMC summary; D=128,
 # the residual epilogue of layers >= 1)
 PMC_KERNELS = {
     "gine_mp_fwd": ["gine::k_mp_fwd<32, 1, "],
-    "gine_mp_bwd": ["gine::k_mp_bwd<32, 1, "],
+    "gine_mp_bwd": ["gine::k_mp_bwd_win<32, "],
     "gine_mlp_fwd1": ["gine::k_rowgemm<128, 0, 0, true>"],
     "gine_mlp_fwd2": ["gine::k_rowgemm<128, 1, 5, true>"],
     "gine_mlp_bwd2": ["gine::k_rowgemm<128, 5, 2, false>"],
     "gine_mlp_bwd1": ["gine::k_rowgemm<128, 3, 3, false>"],
+    "gine_mlp_bwd1_wgrad": ["gine::k_bwd1_wgrad<5>"],
     "gine_mlp_wgrad": ["gine::k_wgrad_engine<gine::MlpWgradSrc<5>, 64, 8>",
                        "gine::k_slab_sum<true, gine::MlpWgradOut>"],
 }
@@ -308,7 +361,20 @@ def pmc_traffic(kernel: str):
 # -----------------------------------------------------------------------------------------
 # CPU baseline (oracle, rank 0, N=1)
 # -----------------------------------------------------------------------------------------
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(cfg, graphs, seconds):
+    """The oracle (CPU restatement of the reference's training step) on this host: all
+    threads torch uses, then one thread for a quarter of the time."""
     from oracle import gine_cpu as O
     params = cfg.params()
     torch.manual_seed(42)
@@ -323,20 +389,32 @@ def cpu_baseline(cfg, graphs, seconds):
         loss.backward()
         opt.step()
 
-    step()  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step()
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 200:
-            break
+    def run(limit):
+        step()  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            step()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= limit or n >= 200:
+                return n, el
+
+    threads = torch.get_num_threads()
+    n, el = run(seconds)
+    torch.set_num_threads(1)
+    try:
+        n1, el1 = run(seconds / 4)
+    finally:
+        torch.set_num_threads(threads)
     return {"value": round(graphs * n / el, 3), "unit": "graphs/s",
-            "cores": torch.get_num_threads(), "kind": "port",
+            "cores": threads, "kind": "port",
             "sample": f"{n} full training steps (oracle CPU restatement, fp32) on the cfg "
                       f"{cfg.name} batch of {graphs} graphs x {cfg.num_stations} stations, "
-                      f"after 1 warm-up step; {el:.1f} s; cpu={platform.processor() or platform.machine()}",
-            "ms_per_step": round(el / n * 1e3, 2)}
+                      f"after 1 warm-up step; {el:.1f} s on {threads} threads; "
+                      f"cpu={cpu_model()}",
+            "ms_per_step": round(el / n * 1e3, 2),
+            "one_thread": {"value": round(graphs * n1 / el1, 3), "unit": "graphs/s",
+                           "steps": n1, "seconds": round(el1, 1)}}
 
 
 # -----------------------------------------------------------------------------------------
@@ -374,13 +452,22 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
+    # HIP events between steps on the stream the steps run on (distribution only; the
+    # reported time is the wall clock between the synchronised barriers)
+    stream = torch.cuda.current_stream(device)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record(stream)
+    for i in range(args.steps):
         tr.step()
+        evs[i + 1].record(stream)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    pct = {q: round(per_step[min(len(per_step) - 1, int(q / 100 * len(per_step)))], 4)
+           for q in (10, 50, 90)}
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -397,6 +484,11 @@ def main():
     result = None
     if rank == 0:
         roof = roofline_for(kernels, layers)
+        roof_mp = roofline_mp(kernels, layers)
+        if roof_mp is not None:
+            roof_mp["measured_copy_GBps"] = copy_ceiling_gbps(device)
+            roof_mp["frac_of_measured"] = round(roof_mp["achieved"] /
+                                                roof_mp["measured_copy_GBps"], 4)
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(cfg, graphs_per_rank, args.cpu_seconds)
@@ -413,7 +505,9 @@ def main():
                        "nodes_per_gpu": tr.batch.num_nodes, "edges_per_gpu": E_rank,
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
             "edges_aggregated_per_s": round(edges_per_s, 1),
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+            "step_ms_p10_p50_p90": [pct[10], pct[50], pct[90]],
+            "roofline": roof, "roofline_message_passing": roof_mp,
+            "cpu_baseline": cpu, "kernels": kernels,
             "final_loss": loss_val,
         }
         print(json.dumps(result), flush=True)
