@@ -107,7 +107,7 @@ __device__ __forceinline__ void stage_tile(const float4* __restrict__ tab4, int 
 // Forward: z = sum_{in-edges, edge order} relu(x[src] + lin(a)) + (1 + eps) x
 // ----------------------------------------------------------------------------------------
 template <int CS, bool FMA>
-__global__ __launch_bounds__(kWinThreads, 2) void k_mp_fwd_win(
+__global__ __launch_bounds__(kWinThreads, CS == 32 ? 2 : 3) void k_mp_fwd_win(
     const float4* __restrict__ x4, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ nbr, const float* __restrict__ attr,
     const float4* __restrict__ lw4, const float4* __restrict__ lb4,

@@ -54,7 +54,11 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
     rp = rowptr.cpu()
     nb = nbr.cpu()
     i32 = dict(dtype=torch.int32)
-    for cs in WINDOW_SLICES:
+    slices = WINDOW_SLICES
+    pref = os.environ.get("GINE_MP_WINDOW_SLICE")  # tuning experiments: force one width
+    if pref:
+        slices = (int(pref),)
+    for cs in slices:
         max_rows = WINDOW_ROW_BYTES // (cs * 4)
         max_edges = (_lib.WINDOW_LDS_BYTES - max_rows * cs * 4 - (max_nodes + 1) * 4) // 8
         tb = torch.empty(num_nodes + 1, **i32)

@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--tiles", default="128,64,32")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--slice", type=int, default=0, help="force a window slice width")
     ap.add_argument("--eager", action="store_true", help="no graphs (for rocprofv3 --pmc)")
     args = ap.parse_args()
     global EAGER
@@ -84,6 +85,8 @@ def main():
         for name, on, tiles in variants:
             os.environ["GINE_MP_WINDOW"] = on
             os.environ["GINE_MP_WINDOW_NODES"] = str(tiles)
+            if args.slice:
+                os.environ["GINE_MP_WINDOW_SLICE"] = str(args.slice)
             g = GineGraph(ei, ea, N)
             plan = g.window_plan("in", D)
             if on == "all" and plan is None:
