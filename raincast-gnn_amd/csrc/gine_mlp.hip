@@ -726,7 +726,10 @@ __global__ __launch_bounds__(256) void k_bwd1_wgrad(const float* __restrict__ w1
   __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
   const int b = blockIdx.x;
   if (b < eng_blocks) {
-    wgrad_block<MlpWgradSrc<PDO>, 64, 4>(src, N, 128, 128, b % chunks, b / chunks,
+    // the output tiles of one row chunk run back to back on ONE XCD: they read the same
+    // rows (a1 by all four, z by the two dW1 tiles), which that XCD's L2 then serves
+    const int lb = xcd_remap(b, eng_blocks), tiles = eng_blocks / chunks;
+    wgrad_block<MlpWgradSrc<PDO>, 64, 4>(src, N, 128, 128, lb / tiles, lb % tiles,
                                          rows_per_chunk, zstride, cstride, slab, sP, sQ);
   } else {
     static_assert(kRowTile * (128 + 4) <= kWgRows * kWgLdQ, "row tile fits in sQ");

@@ -298,16 +298,20 @@ __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, in
   }
 }
 
-// grid = (chunks, sum over z of the product's output tiles); blockIdx.y -> (z, tile).
+// 1-D grid of chunks x tiles (tiles = sum over z of the product's output tiles).  The
+// tiles of one row chunk run back to back on ONE XCD (xcd_remap): they read the same rows,
+// which that XCD's L2 then serves.
 template <class Src, int TO, int NW>
 __global__ __launch_bounds__(64 * NW) void k_wgrad_engine(Src src, int64_t R, int O, int I,
                                                           int rows_per_chunk, size_t zstride,
                                                           size_t cstride,
-                                                          float* __restrict__ slab) {
+                                                          float* __restrict__ slab,
+                                                          int total_tiles) {
   __shared__ __attribute__((aligned(16))) float sP[kWgRows * (TO + 4)];
   __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
-  wgrad_block<Src, TO, NW>(src, R, O, I, blockIdx.x, blockIdx.y, rows_per_chunk, zstride,
-                           cstride, slab, sP, sQ);
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  wgrad_block<Src, TO, NW>(src, R, O, I, lb / total_tiles, lb % total_tiles, rows_per_chunk,
+                           zstride, cstride, slab, sP, sQ);
 }
 
 // Z must equal Src::kZ; total_tiles = sum of the products' output tiles (the plan's).
@@ -316,9 +320,9 @@ inline int launch_wgrad_engine(const Src& src, int64_t R, int O, int I, int tota
                                const WgPlan& p, size_t zstride, size_t cstride, float* slab,
                                hipStream_t s) {
   constexpr int NW = TO == 64 ? kWgWaves64 : 4;
-  hipLaunchKernelGGL((k_wgrad_engine<Src, TO, NW>), dim3(p.chunks, total_tiles), dim3(64 * NW),
-                     0, s,
-                     src, R, O, I, p.rows_per_chunk, zstride, cstride, slab);
+  hipLaunchKernelGGL((k_wgrad_engine<Src, TO, NW>), dim3(p.chunks * total_tiles),
+                     dim3(64 * NW), 0, s, src, R, O, I, p.rows_per_chunk, zstride, cstride,
+                     slab, total_tiles);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
