@@ -163,6 +163,51 @@ int gine_mp_bwd_win_finalize(const double* partials, int32_t num_tiles, int32_t 
                              float* deps, void* stream);
 
 /* ------------------------------------------------------------------------------------
+ * Batched gradient finish.  The parameter-gradient reductions that nothing reads before
+ * the optimizer -- dW_e/db_e/eps of every GINE layer (gine_mp_bwd*_finalize), the head's
+ * and the dense chain's weight-gradient slabs, the DeepSet dW1 slab -- in ONE launch at the
+ * end of the backward instead of one launch each (autograd of the Linear/GINEConv
+ * parameters, models/gnn.py; reduced by the reference's autograd as separate mm/sum ops).
+ *   GINE_GRAD_JOB_MP:   src = fp64 partial rows [rows][3*channels] as gine_mp_bwd (eps at
+ *                       column 2D, eps_cols = 1) or gine_mp_bwd_win (eps at 2D + slice,
+ *                       eps_cols = slices) write them; w[0] = dlin_w [D], w[1] = dlin_b
+ *                       [D], w[2] = deps [1].
+ *   GINE_GRAD_JOB_SLAB: src = fp32 slab, element e of product z < nz at
+ *                       src + z*zstride + c*cstride + e for chunks c < rows; product z has
+ *                       per[z] elements: e < wsize[z] -> w[z][e], else b[z][e - wsize[z]]
+ *                       (times bscale[z]).  Sums in fp64, fixed order.
+ * The *_grad_job entry points (host only) describe the slab a producer left when called
+ * with NULL gradient outputs.  At most GINE_GRAD_MAX_JOBS jobs per launch.
+ * ---------------------------------------------------------------------------------- */
+#define GINE_GRAD_JOB_MP 1
+#define GINE_GRAD_JOB_SLAB 2
+#define GINE_GRAD_MAX_JOBS 12
+typedef struct gine_grad_job {
+  int32_t kind;
+  int32_t rows;      /* MP: partial rows; SLAB: chunks */
+  int32_t channels;  /* MP: D */
+  int32_t eps_cols;  /* MP: eps columns */
+  int32_t nz;        /* SLAB: products (<= 4) */
+  int32_t pad_;
+  const void* src;
+  int64_t cstride, zstride;  /* SLAB, in floats */
+  int64_t per[4];
+  int64_t wsize[4];
+  float bscale[4];
+  float* w[4];
+  float* b[4];
+} gine_grad_job;
+int gine_grad_finalize_batch(const gine_grad_job* jobs, int32_t num_jobs, void* stream);
+int gine_head_bwd_grad_job(int64_t num_nodes, int32_t channels, int32_t kind, const float* slab,
+                           float* dw, float* db, gine_grad_job* job);
+int gine_chain_wgrad_grad_job(int64_t num_nodes, int32_t hidden, int32_t in_features,
+                              const float* slab, float bias_scale, float* dwp2, float* dbp2,
+                              float* dwr0, float* dbr0, float* dwr1, float* dbr1, float* dwdr,
+                              float* dbdr, gine_grad_job* job);
+int gine_deepset_bwd_grad_job(int64_t num_nodes, int32_t in_features, int32_t hidden,
+                              const float* slab, float* dw1, float* db1, gine_grad_job* job);
+
+/* ------------------------------------------------------------------------------------
  * Node MLP  nn = Sequential(Linear(D,D), BatchNorm1d(D), ReLU(), Linear(D,D))
  * (models/gnn.py:21-26), plus the ResGnn epilogue (models/gnn.py:38-44).
  * fp32 MFMA (v_mfma_f32_32x32x2_f32) row-tile GEMMs with fused prologues/epilogues.

@@ -408,9 +408,10 @@ extern "C" int gine_chain_wgrad(const float* dh0, const float* x, const float* r
                                 void* stream) {
   if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
   if (num_nodes <= 0) return GINE_ERR_INVALID;
-  if (!dh0 || !x || !r || !s || !u || !e || !de || !dt || !ds || !slab || !dwp2 || !dwr0 ||
-      !dwr1 || !dwdr)
-    return GINE_ERR_INVALID;
+  if (!dh0 || !x || !r || !s || !u || !e || !de || !dt || !ds || !slab) return GINE_ERR_INVALID;
+  // all four weight outputs NULL: the slab is left for gine_grad_finalize_batch
+  const bool reduce = dwp2 || dwr0 || dwr1 || dwdr;
+  if (reduce && (!dwp2 || !dwr0 || !dwr1 || !dwdr)) return GINE_ERR_INVALID;
   hipStream_t st = as_stream(stream);
   const int D = hidden, F = in_features;
   int rc;
@@ -420,8 +421,40 @@ extern "C" int gine_chain_wgrad(const float* dh0, const float* x, const float* r
   rc = launch_wgrad_engine<64>(src, num_nodes, D, D + F, chain_wgrad_tiles(D, F), p,
                                 per * p.chunks, per, slab, st);
   if (rc != GINE_OK) return rc;
+  if (!reduce) return GINE_OK;
   return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 4,
                          ChainWgradOut{{dwdr, dwr1, dwr0, dwp2}, {dbdr, dbr1, dbr0, dbp2}, D,
                                        F, bias_scale},
                          st);
+}
+
+extern "C" int gine_chain_wgrad_grad_job(int64_t num_nodes, int32_t hidden, int32_t in_features,
+                                         const float* slab, float bias_scale, float* dwp2,
+                                         float* dbp2, float* dwr0, float* dbr0, float* dwr1,
+                                         float* dbr1, float* dwdr, float* dbdr,
+                                         gine_grad_job* job) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !slab || !dwp2 || !dwr0 || !dwr1 || !dwdr || !job)
+    return GINE_ERR_INVALID;
+  const int64_t D = hidden, F = in_features;
+  const WgPlan p = chain_wgrad_plan(num_nodes, hidden, in_features);
+  const int64_t per = D * (D + F) + D;
+  *job = gine_grad_job{};
+  job->kind = GINE_GRAD_JOB_SLAB;
+  job->src = slab;
+  job->rows = p.chunks;
+  job->cstride = per;
+  job->zstride = per * p.chunks;
+  job->nz = 4;
+  float* w[4] = {dwdr, dwr1, dwr0, dwp2};  // product order of ChainWgradSrc
+  float* b[4] = {dbdr, dbr1, dbr0, dbp2};
+  for (int z = 0; z < 4; ++z) {
+    const int64_t ws = D * (z == 0 ? F + D : D);
+    job->per[z] = ws + D;
+    job->wsize[z] = ws;
+    job->w[z] = w[z];
+    job->b[z] = b[z];
+    job->bscale[z] = z == 3 ? bias_scale : 1.0f;
+  }
+  return GINE_OK;
 }

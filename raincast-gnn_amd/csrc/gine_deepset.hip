@@ -514,7 +514,7 @@ extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const fl
                                 void* stream) {
   const int KP = pad_bwd(in_features);
   if (!hidden_ok(hidden) || KP < 0 || in_features <= 0) return GINE_ERR_DIM;
-  if (num_nodes < 0 || members <= 0 || !slab || !dw1) return GINE_ERR_INVALID;
+  if (num_nodes < 0 || members <= 0 || !slab) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!ens || !mask || !dr)) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   const int groups = (int)ceil_div(num_nodes > 0 ? num_nodes : 1, kNodes);
@@ -531,9 +531,30 @@ extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const fl
 #undef LAUNCH_BWD
     GINE_LAUNCH_STATUS();
   }
+  if (!dw1) return GINE_OK;  // slab left for gine_grad_finalize_batch
   hipLaunchKernelGGL(k_deepset_slab_reduce, dim3((unsigned)ceil_div(per, 16)), dim3(256), 0, s,
                      slab, grid, per, (int64_t)hidden * in_features, dw1, db1);
   GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_deepset_bwd_grad_job(int64_t num_nodes, int32_t in_features, int32_t hidden,
+                                         const float* slab, float* dw1, float* db1,
+                                         gine_grad_job* job) {
+  if (!hidden_ok(hidden) || pad_bwd(in_features) < 0 || in_features <= 0) return GINE_ERR_DIM;
+  if (num_nodes < 0 || !slab || !dw1 || !job) return GINE_ERR_INVALID;
+  const int64_t per = (int64_t)hidden * in_features + hidden;
+  *job = gine_grad_job{};
+  job->kind = GINE_GRAD_JOB_SLAB;
+  job->src = slab;
+  job->rows = bwd_grid(num_nodes);
+  job->cstride = per;
+  job->nz = 1;
+  job->per[0] = per;
+  job->wsize[0] = (int64_t)hidden * in_features;
+  job->w[0] = dw1;
+  job->b[0] = db1;
+  job->bscale[0] = 1.0f;
   return GINE_OK;
 }
 

@@ -306,3 +306,24 @@ extern "C" int gine_head_bwd_reduce(const float* slab, float* dw, float* db, int
   return launch_slab_sum(slab, num_nodes == 0 ? 1 : head_bwd_grid(num_nodes), per, (size_t)per,
                          0, 1, HeadOut{dw, db, (int64_t)K * channels}, as_stream(stream));
 }
+
+extern "C" int gine_head_bwd_grad_job(int64_t num_nodes, int32_t channels, int32_t kind,
+                                      const float* slab, float* dw, float* db,
+                                      gine_grad_job* job) {
+  const int K = k_of(kind);
+  if (K < 0 || num_nodes < 0 || !head_dim_ok(channels) || !slab || !dw || !job)
+    return GINE_ERR_INVALID;
+  const int64_t per = (int64_t)K * channels + K;
+  *job = gine_grad_job{};
+  job->kind = GINE_GRAD_JOB_SLAB;
+  job->src = slab;
+  job->rows = num_nodes == 0 ? 1 : head_bwd_grid(num_nodes);
+  job->cstride = per;
+  job->nz = 1;
+  job->per[0] = per;
+  job->wsize[0] = (int64_t)K * channels;
+  job->w[0] = dw;
+  job->b[0] = db;
+  job->bscale[0] = 1.0f;
+  return GINE_OK;
+}

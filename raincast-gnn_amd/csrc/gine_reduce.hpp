@@ -105,13 +105,12 @@ __device__ inline void block_tree_sum(double* v, int n) {
 // workgroups (few columns, many row groups) keep each thread's dependent chain short, so
 // one launch of many small workgroups replaces the slice + single-block two-launch form.
 template <int COLS, class Fin>
-__global__ __launch_bounds__(256) void k_colsum_fin(const double* __restrict__ a, int P, int ld,
-                                                    Fin fin) {
+__device__ __forceinline__ void colsum_fin_block(const double* __restrict__ a, int P, int ld,
+                                                 const Fin& fin, int b,
+                                                 double (*s_part)[COLS], double* s_tot) {
   constexpr int G = 256 / COLS;
-  __shared__ double s_part[G][COLS];
-  __shared__ double s_tot[COLS];
   const int j = threadIdx.x % COLS, g = threadIdx.x / COLS;
-  const int c = fin.col(blockIdx.x, j);
+  const int c = fin.col(b, j);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (c >= 0) {
     const double* colp = a + c;
@@ -135,7 +134,15 @@ __global__ __launch_bounds__(256) void k_colsum_fin(const double* __restrict__ a
     s_tot[threadIdx.x] = t;
   }
   __syncthreads();
-  fin.finish(blockIdx.x, s_tot);
+  fin.finish(b, s_tot);
+}
+
+template <int COLS, class Fin>
+__global__ __launch_bounds__(256) void k_colsum_fin(const double* __restrict__ a, int P, int ld,
+                                                    Fin fin) {
+  __shared__ double s_part[256 / COLS][COLS];
+  __shared__ double s_tot[COLS];
+  colsum_fin_block<COLS, Fin>(a, P, ld, fin, blockIdx.x, s_part, s_tot);
 }
 
 }  // namespace gine

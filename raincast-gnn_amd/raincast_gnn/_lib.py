@@ -39,6 +39,18 @@ class WindowPlan(ctypes.Structure):
 
 
 _plan_p = ctypes.POINTER(WindowPlan)
+
+
+class GradJob(ctypes.Structure):
+    """``gine_grad_job`` (include/gine_hip.h): one reduction of gine_grad_finalize_batch."""
+    _fields_ = [("kind", _i32), ("rows", _i32), ("channels", _i32), ("eps_cols", _i32),
+                ("nz", _i32), ("pad_", _i32), ("src", _c_void_p), ("cstride", _i64),
+                ("zstride", _i64), ("per", _i64 * 4), ("wsize", _i64 * 4),
+                ("bscale", _f32 * 4), ("w", _c_void_p * 4), ("b", _c_void_p * 4)]
+
+
+GRAD_JOB_MP, GRAD_JOB_SLAB, GRAD_MAX_JOBS = 1, 2, 12
+_job_p = ctypes.POINTER(GradJob)
 WINDOW_LDS_BYTES = 80 * 1024
 
 # name -> argtypes (every entry point returns int status)
@@ -60,6 +72,11 @@ _SIGNATURES = {
                                                  _i32] + [_c_void_p] * 5,
     "gine_mp_bwd_win_finalize": [_c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                                  _c_void_p],
+    "gine_grad_finalize_batch": [_job_p, _i32, _c_void_p],
+    "gine_head_bwd_grad_job": [_i64, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _job_p],
+    "gine_chain_wgrad_grad_job": [_i64, _i32, _i32, _c_void_p, _f32] + [_c_void_p] * 8
+                                 + [_job_p],
+    "gine_deepset_bwd_grad_job": [_i64, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _job_p],
     "gine_mlp_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_fwd1": [_c_void_p] * 5 + [_i64, _i32, _c_void_p],
     "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,

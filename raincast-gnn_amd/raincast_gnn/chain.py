@@ -17,7 +17,7 @@ import ctypes
 
 import torch
 
-from . import _lib, sidework
+from . import _lib, gradbuf, sidework
 from .gradbuf import grad_out
 
 HIDDEN = (64, 128)
@@ -77,8 +77,19 @@ class _ChainFn(torch.autograd.Function):
         _lib.call("gine_chain_bwd", P(dh0), P(x), P(r), P(s), P(u), P(e), P(wp2), P(wr0),
                   P(wr1), P(wdr), P(de), P(dt), P(ds), P(dr), None, None, None, ctx.members,
                   None, None, None, None, None, None, N, D, F, _lib.stream_handle(dev))
-        # ... while the four weight gradients run beside it on the side stream
         members = ctx.members
+        if gradbuf.deferrable(*g):
+            # the engine leaves its slab; the end-of-backward batch reduces it
+            _lib.call("gine_chain_wgrad", P(dh0), P(x), P(r), P(s), P(u), P(e), P(de),
+                      P(dt), P(ds), P(slab), None, None, members, None, None, None, None,
+                      None, None, N, D, F, _lib.stream_handle(dev))
+            job = _lib.GradJob()
+            _lib.call("gine_chain_wgrad_grad_job", N, D, F, P(slab), members, P(g[0]),
+                      P(g[1]), P(g[2]), P(g[3]), P(g[4]), P(g[5]), P(g[6]), P(g[7]),
+                      ctypes.byref(job))
+            gradbuf.defer(job, dev, (slab,))
+            return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
+        # ... while the four weight gradients run beside it on the side stream
         sidework.launch(dev, lambda sh: _lib.call(
             "gine_chain_wgrad", P(dh0), P(x), P(r), P(s), P(u), P(e), P(de), P(dt), P(ds),
             P(slab), P(g[0]), P(g[1]), members, P(g[2]), P(g[3]), P(g[4]), P(g[5]), P(g[6]),

@@ -17,6 +17,7 @@ import ctypes
 import torch
 
 from . import _lib
+from . import gradbuf
 from .gradbuf import grad_out
 
 HIDDEN = (32, 64, 128, 256)
@@ -62,9 +63,16 @@ class _PhiSumFn(torch.autograd.Function):
         slab = torch.empty(parts.value * (H * Fdim + H), dtype=torch.float32, device=dr.device)
         dw = grad_out(ctx.params[0], (H, Fdim), dr.device)
         db = grad_out(ctx.params[1], (H,), dr.device)
+        defer = gradbuf.deferrable(dw, db)  # slab reduced in the end-of-backward batch
         _lib.call("gine_deepset_bwd", _lib.ptr(ens), _lib.ptr(mask), _lib.ptr(dr),
-                  _lib.ptr(slab), _lib.ptr(dw), _lib.ptr(db), N, M, Fdim, H,
+                  _lib.ptr(slab), None if defer else _lib.ptr(dw),
+                  None if defer else _lib.ptr(db), N, M, Fdim, H,
                   _lib.stream_handle(dr.device))
+        if defer:
+            job = _lib.GradJob()
+            _lib.call("gine_deepset_bwd_grad_job", N, Fdim, H, _lib.ptr(slab), _lib.ptr(dw),
+                      _lib.ptr(db), ctypes.byref(job))
+            gradbuf.defer(job, dr.device, (slab,))
         return None, dw, db
 
 

@@ -23,6 +23,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr
+from . import gradbuf
 from .gradbuf import grad_out
 
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = _lib.EPI_NONE, _lib.EPI_RELU, _lib.EPI_RESIDUAL_RELU
@@ -126,8 +127,12 @@ def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_
             slab, chunks, Dm, dw1, db1, dw2, db2 = side
             call("gine_mp_bwd_win_side", *args, ptr(partials), N, D, flags, ctypes.byref(plan),
                  ptr(slab), chunks, Dm, ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), stream)
-        call("gine_mp_bwd_win_finalize", ptr(partials), P, D, plan.slice_channels, ptr(dlw),
-             ptr(dlb), ptr(deps), stream)
+        if gradbuf.deferrable(dlw, dlb, deps):  # in the end-of-backward batch
+            gradbuf.defer(gradbuf.mp_job(partials, P, D, D // plan.slice_channels, dlw, dlb,
+                                         deps), dev, (partials,))
+        else:
+            call("gine_mp_bwd_win_finalize", ptr(partials), P, D, plan.slice_channels,
+                 ptr(dlw), ptr(dlb), ptr(deps), stream)
         return dx, dlw, dlb, deps
     P = _count("gine_mp_bwd_num_partials", N, D)
     partials = torch.empty(P, 3, D, dtype=torch.float64, device=dev)
@@ -137,7 +142,11 @@ def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_
         slab, chunks, Dm, dw1, db1, dw2, db2 = side
         call("gine_mp_bwd_side", *args, ptr(partials), N, D, flags, ptr(slab), chunks, Dm,
              ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), stream)
-    call("gine_mp_bwd_finalize", ptr(partials), P, D, ptr(dlw), ptr(dlb), ptr(deps), stream)
+    if gradbuf.deferrable(dlw, dlb, deps):
+        gradbuf.defer(gradbuf.mp_job(partials, P, D, 1, dlw, dlb, deps), dev, (partials,))
+    else:
+        call("gine_mp_bwd_finalize", ptr(partials), P, D, ptr(dlw), ptr(dlb), ptr(deps),
+             stream)
     return dx, dlw, dlb, deps
 
 

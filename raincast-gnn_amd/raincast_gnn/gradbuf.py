@@ -13,15 +13,36 @@ using the buffer that every ``param.grad`` really is its slice and copies it in 
 """
 from __future__ import annotations
 
+import os
+import threading
+import weakref
+
 import torch
 from torch.utils.weak import WeakIdKeyDictionary  # identity keys (Tensor.__eq__ is elementwise)
 
+from . import _lib
+
 _slots = WeakIdKeyDictionary()   # param -> (flat buffer, offset)
 _issued = WeakIdKeyDictionary()  # params whose slice was handed out this step
+_flats: list = []                # weak references to the registered flat buffers
 
 
 def register(param: torch.Tensor, flat: torch.Tensor, offset: int) -> None:
     _slots[param] = (flat, offset)
+    if not any(r() is flat for r in _flats):
+        _flats.append(weakref.ref(flat))
+
+
+def in_flat_buffer(t: torch.Tensor | None) -> bool:
+    """True when ``t`` lies inside a registered flat gradient buffer."""
+    if t is None:
+        return False
+    p = t.data_ptr()
+    for r in _flats:
+        f = r()
+        if f is not None and f.data_ptr() <= p < f.data_ptr() + 4 * f.numel():
+            return True
+    return False
 
 
 def slice_of(param: torch.Tensor):
@@ -48,3 +69,63 @@ def grad_out(param: torch.Tensor | None, shape=None, device=None) -> torch.Tenso
     shp = param.shape if shape is None else shape
     dev = param.device if device is None else device
     return torch.empty(shp, dtype=torch.float32, device=dev)
+
+
+# ---------------------------------------------------------------------------------------
+# Deferred gradient reductions (gine_grad_finalize_batch, include/gine_hip.h)
+# ---------------------------------------------------------------------------------------
+# Reductions whose outputs only the optimizer reads -- dW_e/db_e/eps of every GINE layer,
+# the head / dense-chain / DeepSet weight-gradient slabs -- are collected during a backward
+# pass and run as ONE launch when the pass ends (an autograd final callback, so
+# ``param.grad`` is complete when ``backward()`` returns and before any accumulation).  Only
+# outputs that are flat-buffer slices adopted as ``param.grad`` qualify: autograd then
+# never reads them during the pass.  RAINCAST_BATCH_GRAD_FINISH=0 turns it off.
+
+BATCH_ENABLED = os.environ.get("RAINCAST_BATCH_GRAD_FINISH", "1") != "0"
+_pending: list = []
+_pending_lock = threading.Lock()
+
+
+def deferrable(*outs) -> bool:
+    """True when every gradient output is a flat-buffer slice and a backward pass is
+    running (its end-of-pass callback will run the batch)."""
+    if not BATCH_ENABLED or not outs:
+        return False
+    if not all(in_flat_buffer(t) for t in outs if t is not None):
+        return False
+    return torch._C._current_graph_task_id() != -1
+
+
+def defer(job: "_lib.GradJob", device: torch.device, keep_alive=()) -> None:
+    """Queue ``job`` (its buffers kept alive) for the end-of-backward batch launch."""
+    stream = _lib.stream_handle(device)
+    with _pending_lock:
+        first = not _pending
+        _pending.append((job, stream, tuple(keep_alive)))
+    if first:
+        torch.autograd.Variable._execution_engine.queue_callback(flush)
+
+
+def flush() -> None:
+    """Run every queued reduction (one launch per stream and per GRAD_MAX_JOBS jobs)."""
+    with _pending_lock:
+        items = list(_pending)
+        _pending.clear()
+    by_stream: dict = {}
+    for job, stream, keep in items:
+        by_stream.setdefault(stream, []).append(job)
+    for stream, jobs in by_stream.items():
+        for i in range(0, len(jobs), _lib.GRAD_MAX_JOBS):
+            part = jobs[i:i + _lib.GRAD_MAX_JOBS]
+            arr = (_lib.GradJob * len(part))(*part)
+            _lib.call("gine_grad_finalize_batch", arr, len(part), stream)
+    # the buffers in ``items`` are released here, after their consumer is enqueued
+
+
+def mp_job(partials: torch.Tensor, rows: int, channels: int, eps_cols: int, dlw, dlb, deps):
+    j = _lib.GradJob()
+    j.kind = _lib.GRAD_JOB_MP
+    j.src = partials.data_ptr()
+    j.rows, j.channels, j.eps_cols = int(rows), int(channels), int(eps_cols)
+    j.w[0], j.w[1], j.w[2] = dlw.data_ptr(), dlb.data_ptr(), deps.data_ptr()
+    return j

@@ -14,6 +14,7 @@ import ctypes
 import torch
 
 from . import _lib
+from . import gradbuf
 from .gradbuf import grad_out
 
 MAX_CHANNELS = 256
@@ -69,9 +70,15 @@ class _HeadFn(torch.autograd.Function):
         dh = torch.empty_like(h)
         dw = grad_out(ctx.params[0], (K, D), dev)
         db = grad_out(ctx.params[1], (K,), dev)
+        defer = gradbuf.deferrable(dw, db)  # slab reduced in the end-of-backward batch
         _lib.call("gine_head_bwd", _lib.ptr(gpred), _lib.ptr(raw), _lib.ptr(h), _lib.ptr(w),
-                  _lib.ptr(dh), _lib.ptr(slab), _lib.ptr(dw), _lib.ptr(db), N, D, ctx.kind,
-                  _lib.stream_handle(dev))
+                  _lib.ptr(dh), _lib.ptr(slab), None if defer else _lib.ptr(dw),
+                  None if defer else _lib.ptr(db), N, D, ctx.kind, _lib.stream_handle(dev))
+        if defer:
+            job = _lib.GradJob()
+            _lib.call("gine_head_bwd_grad_job", N, D, ctx.kind, _lib.ptr(slab), _lib.ptr(dw),
+                      _lib.ptr(db), ctypes.byref(job))
+            gradbuf.defer(job, dev, (slab,))
         return dh, dw, db, None
 
 

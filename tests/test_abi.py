@@ -63,3 +63,24 @@ def test_host_validation_without_device():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(_lib.GineError, match="not found"):
         _lib.load(str(tmp_path / "nope.so"))
+
+
+def test_grad_batch_validation_without_device():
+    lib = _lib.load()
+    jobs = (_lib.GradJob * 1)()
+    assert lib.gine_grad_finalize_batch(jobs, 0, None) == 0          # nothing to do
+    assert lib.gine_grad_finalize_batch(jobs, _lib.GRAD_MAX_JOBS + 1, None) == 1
+    jobs[0].kind = 99
+    assert lib.gine_grad_finalize_batch(jobs, 1, None) == 1          # unknown kind
+    jobs[0].kind = _lib.GRAD_JOB_MP
+    assert lib.gine_grad_finalize_batch(jobs, 1, None) == 1          # no source
+    job = _lib.GradJob()
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.addressof(buf)
+    assert lib.gine_head_bwd_grad_job(100, 128, 2, p, p, p, ctypes.byref(job)) == 0
+    assert job.kind == _lib.GRAD_JOB_SLAB and job.nz == 1 and job.per[0] == 4 * 128 + 4
+    assert lib.gine_chain_wgrad_grad_job(16000, 128, 35, p, 11.0, *([p] * 8),
+                                         ctypes.byref(job)) == 0
+    assert job.nz == 4 and job.wsize[0] == 128 * 163 and job.bscale[3] == 11.0
+    assert lib.gine_deepset_bwd_grad_job(16000, 35, 128, p, p, p, ctypes.byref(job)) == 0
+    assert job.wsize[0] == 128 * 35 and job.per[0] == 128 * 36

@@ -198,3 +198,35 @@ def test_device_loader_training_builds_graph_once():
         losses.append(loss.item())
     assert len(losses) == 3 and all(l == l for l in losses)
     assert len(graph_cache._entries) == 1
+
+
+def test_batched_grad_finish_matches_per_kernel_reductions(monkeypatch):
+    """The end-of-backward batch (gine_grad_finalize_batch: dW_e/db_e/eps of every layer, the
+    head / chain / DeepSet slabs) gives the gradients of the per-kernel reductions, complete
+    when backward() returns, in fewer launches."""
+    from raincast_gnn import gradbuf
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.models import GNN
+    torch.manual_seed(9)
+    base = GNN(35, 128, 128, 4, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5)
+    batch = synthetic_batch(500, 32, k=10, seed=4).to(DEV)   # window backward active
+    grads = {}
+    for on in (False, True):
+        monkeypatch.setattr(gradbuf, "BATCH_ENABLED", on)
+        m = copy.deepcopy(base).to(DEV)
+        opt = FlatAdamW(m.parameters(), lr=1e-3)
+        opt.zero_grad()
+        m.loss_fn.crps(m(batch), batch.y).backward()
+        assert not gradbuf._pending
+        grads[on] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    for n, g in grads[False].items():
+        assert rel_err(grads[True][n], g) <= 1e-6, n
+    # a second backward accumulates onto complete gradients (nothing deferred then)
+    monkeypatch.setattr(gradbuf, "BATCH_ENABLED", True)
+    m = copy.deepcopy(base).to(DEV)
+    opt = FlatAdamW(m.parameters(), lr=1e-3)
+    opt.zero_grad()
+    for _ in range(2):
+        m.loss_fn.crps(m(batch), batch.y).backward()
+    for n, p in m.named_parameters():
+        assert rel_err(p.grad, 2 * grads[True][n]) <= 1e-6, n

@@ -14,6 +14,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "raincast-gnn_amd"), os.path.join(ROOT, "tests")]
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from raincast_gnn import functional as Fn  # noqa: E402
@@ -21,6 +22,22 @@ from raincast_gnn.graph import GineGraph  # noqa: E402
 from helpers import knn_batch_graph  # noqa: E402
 
 CONFIGS = {1: (500, 10, 1), 2: (500, 10, 32), 3: (2000, 16, 64), 5: (10000, 32, 8)}
+
+
+def morton_batch_graph(n, k, batch, seed=0):
+    """knn_batch_graph with the stations renumbered along a Z-order curve of (lat, lon):
+    graph neighbours become index neighbours (locality experiment)."""
+    from raincast_gnn import data as rdata
+    lat, lon = rdata.synthetic_stations(n, seed)
+    qa = ((lat - 43.0) / 12.0 * 65535).astype(np.int64)
+    qo = ((lon + 5.0) / 22.0 * 65535).astype(np.int64)
+    key = np.zeros(n, dtype=np.int64)
+    for b in range(16):
+        key |= ((qa >> b) & 1) << (2 * b + 1) | ((qo >> b) & 1) << (2 * b)
+    order = np.argsort(key, kind="stable")
+    ei, ea = rdata.knn_edge_index_and_attr(rdata.haversine_matrix(lat[order], lon[order]), k)
+    eis = [ei + g * n for g in range(batch)]
+    return torch.cat(eis, 1), torch.cat([ea] * batch), n * batch
 
 
 EAGER = False
@@ -60,6 +77,7 @@ def main():
     ap.add_argument("--tiles", default="128,64,32")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--D", type=int, default=128)
+    ap.add_argument("--morton", action="store_true", help="Z-order station numbering")
     ap.add_argument("--slice", type=int, default=0, help="force a window slice width")
     ap.add_argument("--eager", action="store_true", help="no graphs (for rocprofv3 --pmc)")
     args = ap.parse_args()
@@ -70,7 +88,7 @@ def main():
     out = []
     for c in (int(v) for v in args.configs.split(",")):
         n, k, B = CONFIGS[c]
-        ei, ea, N = knn_batch_graph(n, k, B, seed=0)
+        ei, ea, N = (morton_batch_graph if args.morton else knn_batch_graph)(n, k, B, seed=0)
         E = ei.size(1)
         ei, ea = ei.to(dev), ea.to(dev)
         x = torch.randn(N, D, device=dev)
