@@ -275,7 +275,8 @@ int gine_mlp_bwd1_wgrad(const float* dy, const float* y, const uint8_t* mask, co
  * step, train.py:67-69 with torch.optim.AdamW, lr from params.json).  Bumps the device
  * step counter `step` (fp32 [2]: the count, then a ticket word that must start at 0 and is
  * left at 0) and updates param / exp_avg / exp_avg_sq in place with torch.optim.AdamW's
- * default (amsgrad=False) formulation.  One launch, graph-safe.
+ * default (amsgrad=False) formulation.  One launch, graph-safe; the four buffers must be
+ * 16-byte aligned (float4 accesses).
  * ---------------------------------------------------------------------------------- */
 int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                     float* step, int64_t n, float lr, float beta1, float beta2, float eps,
@@ -290,8 +291,10 @@ int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_
  *   GINE_LOSS_MIXED_U       MixedLoss(grad_u=True)                      K = 5, u learned
  * gine_crps_fwd: per node the closed form and its exact gradient w.r.t. pred (fp64
  * forward-mode duals) into dpred [N, K]; per-block partials [P][2]; loss_out[0] = mean over
- * non-NaN targets, count_out[0] = their number.  c = censoring point (log 0.01), t =
- * sigmoid temperature of grad_u, xi = GPD shape, u = fixed threshold.
+ * non-NaN targets, count_out[0] = their number, written by the workgroup that finishes
+ * last (ticket: a device uint32 the caller zeroes ONCE; every call leaves it at 0 again;
+ * calls sharing a ticket must not overlap).  c = censoring point (log 0.01), t = sigmoid
+ * temperature of grad_u, xi = GPD shape, u = fixed threshold.
  * gine_crps_bwd: grad_pred = gloss[0] * dpred / count (fp32).
  * ---------------------------------------------------------------------------------- */
 #define GINE_LOSS_NORMAL 0
@@ -301,7 +304,7 @@ int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_
 int gine_crps_num_partials(int64_t num_nodes, int32_t* num_partials);
 int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t kind, double u,
                   double xi, double c, double t, double* dpred, double* partials,
-                  double* loss_out, double* count_out, void* stream);
+                  double* loss_out, double* count_out, uint32_t* ticket, void* stream);
 int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
                   int64_t num_nodes, int32_t kind, float* grad_pred, void* stream);
 

@@ -204,16 +204,21 @@ struct LossK {
 };
 
 // One thread per node.  Writes d crps_n / d pred_n (0 for NaN targets) and per-block
-// [sum crps, count] partials.
+// [sum crps, count] partials; the workgroup that finishes last (ticket) reduces the partials
+// into the loss -- no separate finalize launch.
 template <int KIND>
 __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pred,
                                                    const float* __restrict__ y, int64_t n,
                                                    double u_fixed, double xi, double c,
                                                    double t, double* __restrict__ dpred,
-                                                   double* __restrict__ partials) {
+                                                   double* __restrict__ partials,
+                                                   double* __restrict__ loss_out,
+                                                   double* __restrict__ count_out,
+                                                   unsigned int* __restrict__ ticket) {
   constexpr int K = LossK<KIND>::value;
   __shared__ double s_sum[kThreads];
   __shared__ double s_cnt[kThreads];
+  __shared__ int s_last;
   const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
   double val = 0.0, cnt = 0.0;
   if (i < n) {
@@ -254,22 +259,46 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
     }
     __syncthreads();
   }
+  // publish the partial, then draw a ticket (MI355X_MICROARCH.md hand-off recipe: drain,
+  // agent-scope release, drain, relaxed agent-scope add; the last arriver acquires)
   if (threadIdx.x == 0) {
     partials[2 * blockIdx.x] = s_sum[0];
     partials[2 * blockIdx.x + 1] = s_cnt[0];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned int prev =
+        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == gridDim.x - 1;
   }
-}
-
-// loss = sum / count (NaN when no target is valid, like torch.mean of an empty tensor)
-__global__ __launch_bounds__(kColsumThreads) void k_crps_finalize(
-    const double* __restrict__ partials, int P, double* __restrict__ loss_out,
-    double* __restrict__ count_out) {
-  __shared__ double s_tmp[kColsumThreads];
-  __shared__ double s_out[2];
-  block_colsum(partials, P, 2, 2, s_tmp, s_out);
+  __syncthreads();
+  if (!s_last) return;
   if (threadIdx.x == 0) {
-    loss_out[0] = s_out[0] / s_out[1];
-    count_out[0] = s_out[1];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // fixed order: thread j sums partial rows j, j + 256, ... then the same tree as above
+  const int P = gridDim.x;
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < P; p += kThreads) {
+    a += partials[2 * p];
+    b += partials[2 * p + 1];
+  }
+  s_sum[threadIdx.x] = a;
+  s_cnt[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      s_sum[threadIdx.x] += s_sum[threadIdx.x + s];
+      s_cnt[threadIdx.x] += s_cnt[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    loss_out[0] = s_sum[0] / s_cnt[0];  // NaN when no target is valid (torch.mean of empty)
+    count_out[0] = s_cnt[0];
+    *ticket = 0u;  // re-armed for the next call (stream order)
   }
 }
 
@@ -298,15 +327,15 @@ extern "C" int gine_crps_num_partials(int64_t num_nodes, int32_t* num_partials) 
 extern "C" int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
                              double u, double xi, double c, double t, double* dpred,
                              double* partials, double* loss_out, double* count_out,
-                             void* stream) {
-  if (num_nodes < 0 || !partials || !loss_out || !count_out) return GINE_ERR_INVALID;
+                             uint32_t* ticket, void* stream) {
+  if (num_nodes < 0 || !partials || !loss_out || !count_out || !ticket) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!pred || !y || !dpred)) return GINE_ERR_INVALID;
   if (kind < GINE_LOSS_NORMAL || kind > GINE_LOSS_MIXED_U) return GINE_ERR_INVALID;
   hipStream_t s = as_stream(stream);
   const int64_t blocks = ceil_div(num_nodes, kThreads) > 0 ? ceil_div(num_nodes, kThreads) : 1;
 #define LAUNCH_CRPS(KIND_)                                                                  \
   hipLaunchKernelGGL(k_crps<KIND_>, dim3((unsigned)blocks), dim3(kThreads), 0, s, pred, y,  \
-                     num_nodes, u, xi, c, t, dpred, partials)
+                     num_nodes, u, xi, c, t, dpred, partials, loss_out, count_out, ticket)
   switch (kind) {
     case GINE_LOSS_NORMAL: LAUNCH_CRPS(GINE_LOSS_NORMAL); break;
     case GINE_LOSS_MIXED_NORMAL: LAUNCH_CRPS(GINE_LOSS_MIXED_NORMAL); break;
@@ -314,9 +343,6 @@ extern "C" int gine_crps_fwd(const float* pred, const float* y, int64_t num_node
     default: LAUNCH_CRPS(GINE_LOSS_MIXED_U); break;
   }
 #undef LAUNCH_CRPS
-  GINE_LAUNCH_STATUS();
-  hipLaunchKernelGGL(k_crps_finalize, dim3(1), dim3(kColsumThreads), 0, s, partials,
-                     (int)blocks, loss_out, count_out);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

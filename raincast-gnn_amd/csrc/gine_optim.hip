@@ -18,6 +18,20 @@
 namespace gine {
 namespace {
 
+struct AdamW {
+  float decay, neg_step_size, bc2_sqrt, w1, w2, beta2, eps;
+  __device__ __forceinline__ void operator()(float gi, float& pi, float& mi, float& vi) const {
+    pi = pi * decay;
+    mi = mi + w1 * (gi - mi);
+    vi = vi * beta2;
+    vi = vi + w2 * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi + neg_step_size * (mi / denom);  // addcdiv: p + value * (m / denom)
+  }
+};
+
+// One float4 of every buffer per thread (16-byte loads, all four issued before any use);
+// the last n % 4 elements by the first threads of the grid.
 __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                float* __restrict__ m, float* __restrict__ v,
                                                float* __restrict__ step, int64_t n,
@@ -25,21 +39,30 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
                                                float weight_decay) {
   const float t_new = step[0] + 1.0f;
   const double t = (double)t_new;
-  const float decay = (float)(1.0 - (double)lr * (double)weight_decay);
-  const float neg_step_size = (float)(-((double)lr / (1.0 - pow((double)beta1, t))));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, t));
-  const float w1 = 1.0f - beta1;
-  const float w2 = 1.0f - beta2;
+  const AdamW op{(float)(1.0 - (double)lr * (double)weight_decay),
+                 (float)(-((double)lr / (1.0 - pow((double)beta1, t)))),
+                 (float)sqrt(1.0 - pow((double)beta2, t)), 1.0f - beta1, 1.0f - beta2, beta2,
+                 eps};
+  const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float gi = g[i];
-    float pi = p[i] * decay;
-    float mi = m[i];
-    mi = mi + w1 * (gi - mi);
-    float vi = v[i] * beta2;
-    vi = vi + w2 * gi * gi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    pi = pi + neg_step_size * (mi / denom);  // addcdiv: p + value * (m / denom)
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (int64_t i = tid; i < n4; i += stride) {
+    const float4 gi = reinterpret_cast<const float4*>(g)[i];
+    float4 pi = reinterpret_cast<float4*>(p)[i];
+    float4 mi = reinterpret_cast<float4*>(m)[i];
+    float4 vi = reinterpret_cast<float4*>(v)[i];
+    op(gi.x, pi.x, mi.x, vi.x);
+    op(gi.y, pi.y, mi.y, vi.y);
+    op(gi.z, pi.z, mi.z, vi.z);
+    op(gi.w, pi.w, mi.w, vi.w);
+    reinterpret_cast<float4*>(p)[i] = pi;
+    reinterpret_cast<float4*>(m)[i] = mi;
+    reinterpret_cast<float4*>(v)[i] = vi;
+  }
+  if (tid < n - 4 * n4) {
+    const int64_t i = 4 * n4 + tid;
+    float pi = p[i], mi = m[i], vi = v[i];
+    op(g[i], pi, mi, vi);
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
@@ -66,9 +89,14 @@ extern "C" int gine_adamw_step(float* param, const float* grad, float* exp_avg,
   if (n < 0 || !step) return GINE_ERR_INVALID;
   if (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)) return GINE_ERR_INVALID;
   hipStream_t s = as_stream(stream);
-  // grid-stride over at most 256 workgroups: few tickets to serialise on one word
-  int64_t blocks = ceil_div(n > 0 ? n : 1, 256);
-  if (blocks > 256) blocks = 256;
+  // one float4 per thread up to 512 workgroups (few tickets to serialise on one word);
+  // 16-byte accesses need 16-byte aligned buffers
+  const uintptr_t al = reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
+                       reinterpret_cast<uintptr_t>(exp_avg) |
+                       reinterpret_cast<uintptr_t>(exp_avg_sq);
+  if (n > 0 && (al & 15) != 0) return GINE_ERR_INVALID;
+  int64_t blocks = ceil_div(n > 0 ? ceil_div(n, 4) : 1, 256);
+  if (blocks > 512) blocks = 512;
   hipLaunchKernelGGL(k_adamw, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg,
                      exp_avg_sq, step, n, lr, beta1, beta2, eps, weight_decay);
   GINE_LAUNCH_STATUS();

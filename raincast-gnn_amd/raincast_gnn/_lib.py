@@ -94,7 +94,7 @@ _SIGNATURES = {
     "gine_adamw_step": [_c_void_p] * 5 + [_i64, _f32, _f32, _f32, _f32, _f32, _c_void_p],
     "gine_crps_num_partials": [_i64, ctypes.POINTER(_i32)],
     "gine_crps_fwd": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64, _c_void_p,
-                      _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+                      _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "gine_crps_bwd": [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
     "gine_linear_wgrad_num_chunks": [_i64, _i32, _i32, ctypes.POINTER(_i32)],
     "gine_linear_wgrad": [_c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p,

@@ -59,6 +59,19 @@ class _Consts:
 
 _consts = _Consts()
 
+_tickets: dict = {}
+
+
+def _ticket(device) -> torch.Tensor:
+    """Per-device uint32 work counter of gine_crps_fwd's last-workgroup finish (zeroed once;
+    every launch leaves it at 0 again)."""
+    key = str(device)
+    t = _tickets.get(key)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int32, device=device)
+        _tickets[key] = t
+    return t
+
 
 def _finish(crps: torch.Tensor, mask: torch.Tensor, reduce: bool) -> torch.Tensor:
     if not reduce:  # reference shape: only the rows with a target, [M, 1]
@@ -89,7 +102,7 @@ class _FusedCRPS(torch.autograd.Function):
         count = torch.empty(1, dtype=torch.float64, device=dev)
         _lib.call("gine_crps_fwd", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c, t,
                   _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss), _lib.ptr(count),
-                  _lib.stream_handle(dev))
+                  _lib.ptr(_ticket(dev)), _lib.stream_handle(dev))
         ctx.save_for_backward(dpred, count)
         ctx.kind = kind
         return loss
