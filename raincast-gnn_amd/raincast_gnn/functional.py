@@ -259,15 +259,27 @@ class GineLayer(torch.autograd.Function):
         slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
         dw1, db1 = grad_out(p_w1, (D, D), dev), grad_out(p_b1, (D,), dev)
         dw2, db2 = grad_out(p_w2, (D, D), dev), grad_out(p_b2, (D,), dev)
-        # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch; the slabs
-        # are reduced by extra workgroups of the message-passing backward launch
+        # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch
         call("gine_mlp_bwd1_wgrad", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save),
              ptr(dbn), ptr(coef), ptr(z), ptr(w1c), ptr(dz), ptr(slab), None, None, None,
              None, N, D, epi, stream)
         dres = dy if epi == EPI_RESIDUAL_RELU else None
+        if gradbuf.deferrable(dw1, db1, dw2, db2):
+            # only the optimizer reads dW1/db1/dW2/db2: the slab joins the end-of-backward
+            # batch, off the critical path of the message-passing backward
+            per = D * D + D
+            job = _lib.GradJob()
+            job.kind, job.src, job.rows, job.nz = _lib.GRAD_JOB_SLAB, slab.data_ptr(), C, 2
+            job.cstride, job.zstride = per, per * C
+            for zi, (wg, bg) in enumerate(((dw2, db2), (dw1, db1))):  # MlpWgradOut order
+                job.per[zi], job.wsize[zi], job.bscale[zi] = per, D * D, 1.0
+                job.w[zi], job.b[zi] = wg.data_ptr(), bg.data_ptr()
+            gradbuf.defer(job, dev, (slab,))
+            side = None
+        else:  # reduced by extra workgroups of the message-passing backward launch
+            side = (slab, C, D, dw1, db1, dw2, db2)
         dx, dlw, dlb, deps = mp_backward(dz, x, ctx.graph, lw, lb, ep, dres=dres,
-                                         params=(p_lw, p_lb, p_eps),
-                                         side=(slab, C, D, dw1, db1, dw2, db2))
+                                         params=(p_lw, p_lb, p_eps), side=side)
         lin_w_shape, affine = ctx.shapes
         return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1, dgamma, dbeta,
                 dw2, db2, None, None, None)
