@@ -80,20 +80,25 @@ struct Stager {
       dst[i] = has ? (16 * c + j) * LD + f : -1;
     }
   }
-  // base: ens + (first group row of the tile) * F;  lim: rows left from that row (clamped)
-  __device__ __forceinline__ void load(float (&v)[PER], const float* __restrict__ base,
-                                       int lim) const {
+  // base: ens + (first group row of the tile) * F;  lim: rows left from that row (clamped).
+  // Returns the rows-in-range bits: the zeroing of out-of-range rows waits for store(), so
+  // nothing consumes the loaded registers before the tile is staged -- a select right
+  // behind each load made the compiler wait for it there and serialised the prefetch.
+  __device__ __forceinline__ uint32_t load(float (&v)[PER], const float* __restrict__ base,
+                                           int lim) const {
+    uint32_t ok = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const bool ok = row[i] < lim;
-      const float x = base[ok ? src[i] : 0];
-      v[i] = ok ? x : 0.f;
+      const bool in = row[i] < lim;
+      v[i] = base[in ? src[i] : 0];
+      ok |= (in ? 1u : 0u) << i;
     }
+    return ok;
   }
-  __device__ __forceinline__ void store(float* s_e, const float (&v)[PER]) const {
+  __device__ __forceinline__ void store(float* s_e, const float (&v)[PER], uint32_t ok) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-      if (dst[i] >= 0) s_e[dst[i]] = v[i];
+      if (dst[i] >= 0) s_e[dst[i]] = ((ok >> i) & 1u) ? v[i] : 0.f;
   }
 };
 
@@ -198,29 +203,29 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
     return mask_in ? (uint32_t)mask_in[((int64_t)c.g * M + c.t) * NT + threadIdx.x] : 0u;
   };
   float va[PER], vb[PER];
-  uint32_t ma = 0, mb = 0;
-  st.load(va, ens + pf.row * F, rows_left(rows_total, pf.row));
+  uint32_t ma = 0, mb = 0, oa = 0, ob = 0;
+  oa = st.load(va, ens + pf.row * F, rows_left(rows_total, pf.row));
   ma = mload(pf);
-  st.store(buf0, va);
+  st.store(buf0, va, oa);
   if (count > 1) {
     pf.advance(M, gr.step);
-    st.load(vb, ens + pf.row * F, rows_left(rows_total, pf.row));
+    ob = st.load(vb, ens + pf.row * F, rows_left(rows_total, pf.row));
     mb = mload(pf);
   }
   pf.advance(M, gr.step);  // pf: tile k+2
   __syncthreads();
-  auto step = [&](int k, float (&vcur)[PER], uint32_t& mcur, float (&vnxt)[PER], float* bcur,
-                  float* bnxt) {
+  auto step = [&](int k, float (&vcur)[PER], uint32_t& mcur, uint32_t& ocur,
+                  float (&vnxt)[PER], uint32_t onxt, float* bcur, float* bnxt) {
     const uint32_t bits = mcur;
     DS_MARK(0);
     if (k + 2 < count) {
-      st.load(vcur, ens + pf.row * F, rows_left(rows_total, pf.row));
+      ocur = st.load(vcur, ens + pf.row * F, rows_left(rows_total, pf.row));
       mcur = mload(pf);
     }
     DS_MARK(1);
     tile(cur, bcur, bits);
     DS_MARK(4);
-    if (k + 1 < count) st.store(bnxt, vnxt);
+    if (k + 1 < count) st.store(bnxt, vnxt, onxt);
     DS_MARK(5);
     __syncthreads();
     DS_MARK(6);
@@ -228,15 +233,20 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
     pf.advance(M, gr.step);
   };
   for (int k = 0; k < count; k += 2) {
-    step(k, va, ma, vb, buf0, buf1);
-    if (k + 1 < count) step(k + 1, vb, mb, va, buf1, buf0);
+    step(k, va, ma, oa, vb, ob, buf0, buf1);
+    if (k + 1 < count) step(k + 1, vb, mb, ob, va, oa, buf1, buf0);
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// Forward.  mask_out (optional): bit q of word [(g*M + t)*NT + thread] = ReLU active for the
+// Forward.  mask_out (MASK): bit q of word [(g*M + t)*NT + thread] = ReLU active for the
 // row in accumulator register q -- what the backward needs instead of the activation.
-template <int H, int KP>
+// Node sums go to LDS as nodes complete and to HBM once per group (32 nodes): no global
+// store sits in a data-dependent branch of the tile loop, so the compiler can count the
+// memory operations in flight and the next tiles' loads stay in flight under the MFMAs
+// (a conditional store there made it drain the whole queue -- s_waitcnt vmcnt(0) -- every
+// tile).
+template <int H, int KP, bool MASK>
 __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__ ens,
                                                        const float* __restrict__ w1,
                                                        const float* __restrict__ b1,
@@ -247,6 +257,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
   constexpr int NT = 2 * H;
   constexpr int LD = KP + 4;
   __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
+  __shared__ float s_r[kNodes * H];  // node sums of the current group
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
@@ -262,14 +273,10 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
   // uniform walk state: node (0..15 within each half's 16) and rows left in it
   int node = 0, rem = M;
   float run = 0.f;
-  float* rout = r;        // this lane's column of the current half's first node
-  int64_t nvalid = 0;     // nodes of this half that exist
+  float* s_mine = s_r + (16 * h) * H + col;  // this lane's column of its half's 16 nodes
   walk_tiles(gr, M, st, ens, N * M, F, s_e[0], s_e[1], nullptr,
              [&](const Cursor& c, const float* buf, uint32_t) {
     if (c.t == 0) {
-      const int64_t n0 = (int64_t)c.g * kNodes + 16 * h;
-      rout = r + n0 * H + col;
-      nvalid = N - n0;
       node = 0;
       rem = M;
       run = 0.f;
@@ -282,15 +289,22 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
       const float v = acc[q] + bias;
       bits |= (v > 0.f ? 1u : 0u) << q;
       run += relu_nan(v);
-      if (--rem == 0) {  // last member of this node: write its sum
-        if (node < nvalid) rout[(int64_t)node * H] = run;
+      if (--rem == 0) {  // last member of this node: keep its sum
+        s_mine[node * H] = run;
         run = 0.f;
         ++node;
         rem = M;
       }
     }
     DS_MARK(3 + 0 * (int)run);
-    if (mask_out) mask_out[((int64_t)c.g * M + c.t) * NT + threadIdx.x] = (uint16_t)bits;
+    if constexpr (MASK) mask_out[((int64_t)c.g * M + c.t) * NT + threadIdx.x] = (uint16_t)bits;
+    if (c.t == M - 1) {  // the group is complete: its 2 x 16 node sums to HBM
+      const int64_t n0 = (int64_t)c.g * kNodes + 16 * h;
+      const int64_t nvalid = N - n0;
+#pragma unroll
+      for (int n = 0; n < 16; ++n)
+        if (n < nvalid) r[(n0 + n) * H + col] = s_mine[n * H];
+    }
   });
 }
 
@@ -493,11 +507,17 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   const int groups = (int)ceil_div(num_nodes, kNodes);
   const int grid = std::min(groups, 1024);
   hipStream_t s = as_stream(stream);
-#define LAUNCH_FWD(H_, KP_)                                                                 \
-  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, b1, \
+#define LAUNCH_FWD_M(H_, KP_, MK_)                                                            \
+  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, MK_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, b1, \
                      r, mask, num_nodes, members, in_features, groups)
+#define LAUNCH_FWD(H_, KP_)                     \
+  do {                                          \
+    if (mask) LAUNCH_FWD_M(H_, KP_, true);      \
+    else LAUNCH_FWD_M(H_, KP_, false);          \
+  } while (0)
   DS_DISPATCH_H(hidden, KP, DS_FWD_KP, LAUNCH_FWD);
 #undef LAUNCH_FWD
+#undef LAUNCH_FWD_M
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
