@@ -174,8 +174,9 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
         const int r = idx / FP, c = idx % FP;
         int64_t n = n0 + r;
         n = n < N ? n : N - 1;
-        const float v = a.x[n * a.F + min(c, a.F - 1)];
-        xr[i] = (c < a.F && idx < kRowTile * FP) ? v : 0.f;
+        // raw value only: the padding columns are zeroed at the LDS store (a select right
+        // behind the load would make the compiler wait for it here, ending the prefetch)
+        xr[i] = a.x[n * a.F + min(c, a.F - 1)];
       }
     }
   };
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
 #pragma unroll
       for (int i = 0; i < XITEMS; ++i) {
         const int idx = threadIdx.x + i * NT;
-        if (idx < kRowTile * FP) sB[(idx / FP) * LDB + idx % FP] = xr[i];
+        if (idx < kRowTile * FP) sB[(idx / FP) * LDB + idx % FP] = idx % FP < a.F ? xr[i] : 0.f;
       }
     }
     __syncthreads();
@@ -265,10 +266,19 @@ struct ChainWgradSrc {
   struct Raw {
     float4 v;
   };
-  struct Col {};
+  struct Col {
+    float keep[4];  // Q of z = 0: 1 for the columns inside [x | e], 0 for the padding
+  };
   template <int Z> __device__ int i_dim(int) const { return Z == 0 ? F + D : D; }
-  template <int Z> __device__ Col p_col(int) const { return Col{}; }
-  template <int Z> __device__ Col q_col(int) const { return Col{}; }
+  template <int Z> __device__ Col p_col(int) const { return Col{{1.f, 1.f, 1.f, 1.f}}; }
+  template <int Z> __device__ Col q_col(int q) const {
+    Col c{{1.f, 1.f, 1.f, 1.f}};
+    if constexpr (Z == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c.keep[j] = 4 * q + j < F + D ? 1.f : 0.f;
+    }
+    return c;
+  }
   template <int Z> __device__ Raw p_load(int64_t n, int q) const {
     const float* p = Z == 0 ? dh0 : (Z == 1 ? de : (Z == 2 ? dt : ds));
     return Raw{reinterpret_cast<const float4*>(p + n * D)[q]};
@@ -281,7 +291,7 @@ struct ChainWgradSrc {
       for (int j = 0; j < 4; ++j) {
         const int c = min(4 * q + j, I - 1);
         const float* src = c < F ? x + n * F + c : e + n * D + (c - F);
-        v[j] = (4 * q + j < I) ? *src : 0.f;
+        v[j] = *src;  // raw: the padding is zeroed in q_xform, when the tile is staged
       }
       return Raw{make_float4(v[0], v[1], v[2], v[3])};
     } else {
@@ -290,7 +300,12 @@ struct ChainWgradSrc {
     }
   }
   template <int Z> __device__ float4 p_xform(const Raw& r, const Col&) const { return r.v; }
-  template <int Z> __device__ float4 q_xform(const Raw& r, const Col&) const { return r.v; }
+  template <int Z> __device__ float4 q_xform(const Raw& r, const Col& c) const {
+    if constexpr (Z == 0)
+      return make_float4(c.keep[0] != 0.f ? r.v.x : 0.f, c.keep[1] != 0.f ? r.v.y : 0.f,
+                         c.keep[2] != 0.f ? r.v.z : 0.f, c.keep[3] != 0.f ? r.v.w : 0.f);
+    return r.v;
+  }
 };
 
 struct ChainWgradOut {
