@@ -247,6 +247,21 @@ int gine_mlp_fwd2(const float* a1, const float* bn_save, const float* w2, const 
                   const float* x, float* y, uint8_t* mask, int64_t num_nodes, int32_t channels,
                   int32_t epilogue, void* stream);
 
+/* Fused forward message passing + first Linear (D = 128 only): z exactly as gine_mp_fwd and
+ * a1 / partials exactly as gine_mlp_fwd1 (bit-identical; partials has gine_mlp_num_partials
+ * rows), in one launch whose workgroups gather the next 32-row tile of z while the matrix
+ * cores multiply the current one (csrc/gine_mpmlp.hip).  Requires every in-degree <=
+ * GINE_MP_FUSED_MAX_DEGREE: the caller passes the graph's maximum in-degree and gets
+ * GINE_ERR_INVALID above it (-> the unfused pair); GINE_ERR_DIM for channels != 128.
+ * flags: GINE_MP_LIN_MULADD as for gine_mp_fwd.
+ * Replaces models/gnn.py:41,44 (GINEConv.propagate + nn[0] Linear + BN batch statistics). */
+#define GINE_MP_FUSED_MAX_DEGREE 32
+int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                     const float* in_attr, const float* lin_w, const float* lin_b,
+                     const float* eps, const float* w1, const float* b1, float* z, float* a1,
+                     double* partials, int64_t num_nodes, int32_t channels,
+                     int32_t max_in_degree, int32_t flags, void* stream);
+
 int gine_mlp_bwd2(const float* dy, const float* y, const uint8_t* mask, const float* a1,
                   const float* bn_save, const float* w2, float* dbn, double* partials,
                   int64_t num_nodes, int32_t channels, int32_t epilogue, void* stream);

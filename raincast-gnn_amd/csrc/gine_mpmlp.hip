@@ -1,0 +1,359 @@
+// GINEConv forward message passing fused with the first node-MLP Linear (D = 128).
+//
+// Replaces, in one launch (models/gnn.py:41,44 -> PyG GINEConv.forward -> nn[0]):
+//   z  = scatter_add(relu(x[src] + Linear(1,D)(edge_attr)), dst) + (1 + eps) x
+//   a1 = z W1^T + b1,   per-workgroup fp64 partial sums of a1 and a1^2 (BatchNorm1d stats)
+// which otherwise are gine_mp_fwd (gather, L2-bound, no matrix work) followed by
+// gine_mlp_fwd1 (row-tile GEMM, matrix-bound, one HBM read of z).  The two are
+// complementary, so one 768-thread workgroup per CU runs both on the same 32-row tiles,
+// split by wave role:
+//   waves 4-11 ("gather"): tile k+1's destinations -- each half-wave owns 2 rows, lane t
+//            the 16-byte column chunk t; edge lists run two stages ahead, 22 neighbour
+//            rows in flight per lane -- written to an LDS z tile and to HBM;
+//   waves 0-3 ("matrix"): tile k's 64-step v_mfma_f32_32x32x2_f32 chain against W1
+//            fragments held in VGPRs, then bias + BN statistics + a1 store, transposed
+//            through a per-wave LDS tile (no cross-wave barrier).
+// One __syncthreads per tile hands the z tile over (double-buffered).
+//
+// Measured (tools/fused_micro.py, HIP-graph replay, MI355X): cfg1 7.5 us vs 8.1 for the
+// pair, cfg2 15.1 vs 16.9; at cfg3 (4,000 tiles) 121 vs 96 -- the gather waves keep fewer
+// loads in flight than the standalone gather kernel's 32 waves per CU, which only the
+// short per-workgroup tile runs hide.  The host uses it up to 2 tiles per workgroup.
+//
+// Results are bit-identical to the unfused pair: z follows k_mp_fwd's per-edge rounding
+// sequence in CSR order (gine_edge.hpp), a1 the row-tile GEMM's MFMA order, and the BN
+// partials its row-group summation order over the same tile -> workgroup assignment
+// (xcd_tile_range, grid = gine_mlp_num_partials).  Every in-degree must be at most
+// GINE_MP_FUSED_MAX_DEGREE (one 32-slot edge list per row; the host checks).
+#include "gine_common.hpp"
+#include "gine_edge.hpp"
+
+namespace gine {
+namespace {
+
+constexpr int kD = 128, kD4 = kD / 4;
+constexpr int kTileRows = 32;
+constexpr int kLD = kD + 4;                 // padded z-tile / W row (floats)
+constexpr int kKS = kD / 2;                 // MFMA k-steps per lane half
+#ifndef GINE_FUSED_GATHER_WAVES
+#define GINE_FUSED_GATHER_WAVES 8
+#endif
+constexpr int kMatThreads = 256;                                 // waves 0-3
+constexpr int kGatherWaves = GINE_FUSED_GATHER_WAVES;            // waves 4-...
+constexpr int kThreads = kMatThreads + kWave * kGatherWaves;
+constexpr int kHalves = 2 * kGatherWaves;                        // gather half-waves
+constexpr int kRowsPerHalf = kTileRows / kHalves;
+static_assert(kRowsPerHalf % 2 == 0, "rows are gathered in pairs");
+constexpr int kSlots = GINE_MP_FUSED_MAX_DEGREE;
+constexpr int kU = 11;  // neighbour rows in flight per row, 2 rows per round (k=10: one)
+constexpr int kTLD = 36;                    // per-wave transposition tile row (floats)
+constexpr uint32_t kRowBytes = kD * 4;
+// experiment builds only (make variant VDEFS=-DGINE_FUSED_DBG=n): 1 = no neighbour loads,
+// 2 = no MFMA chain -- the two roles timed without each other
+#ifndef GINE_FUSED_DBG
+#define GINE_FUSED_DBG 0
+#endif
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct TileSeq {
+  int first, end, step;
+  __device__ int count() const { return first < end ? (end - first + step - 1) / step : 0; }
+  __device__ int at(int k) const { return first + k * step; }
+};
+// The row-tile GEMM's tile -> workgroup assignment (gine_mlp.hip xcd_tile_range): the tiles
+// of one XCD form a contiguous range, its workgroups stride it.
+__device__ __forceinline__ TileSeq tile_seq(int num_tiles, int vb, int nb) {
+  const int xcd = vb % kNumXcd, pos = vb / kNumXcd;
+  const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
+  const int span = (num_tiles + kNumXcd - 1) / kNumXcd;
+  const int b = xcd * span;
+  return TileSeq{b + pos, min(num_tiles, b + span), here};
+}
+
+// Edge lists run two stages ahead of their use, with nothing waiting on a load until the
+// tile that consumes it: rowptr of tile k+2 and the edge slots of tile k+1 are issued while
+// tile k is gathered.  Lane t keeps slot t of each of its half-wave's 4 rows; the selects
+// that depend on loaded values (slot past the in-degree -> the row itself, a valid index)
+// run when the slots are written to LDS, not right behind the loads.
+struct RowptrStage {
+  int32_t beg[kRowsPerHalf], end[kRowsPerHalf];
+};
+struct EdgeStage {
+  int32_t nbr[kRowsPerHalf];
+  float attr[kRowsPerHalf];
+  int cnt[kRowsPerHalf];
+};
+
+// acc += relu(r + lin(a)) when ok (else + 0: acc is never -0, so adding +0 is exact)
+template <bool FMA>
+__device__ __forceinline__ void edge_acc(f4v& acc, f4v r, float a, f4v w, f4v b, bool ok) {
+  const f2v lo = relu2(r.xy + edge_lin2<FMA>(a, w.xy, b.xy));
+  const f2v hi = relu2(r.zw + edge_lin2<FMA>(a, w.zw, b.zw));
+  const f2v zero = {0.f, 0.f};
+  acc.xy = acc.xy + (ok ? lo : zero);
+  acc.zw = acc.zw + (ok ? hi : zero);
+}
+
+struct FusedArgs {
+  const float* x;
+  const int32_t* rowptr;
+  const int32_t* nbr;
+  const float* attr;
+  const float* lin_w;
+  const float* lin_b;
+  const float* eps;
+  const float* W1;
+  const float* b1;
+  float* z;
+  float* a1;
+  double* partials;
+  int N, num_tiles;
+};
+
+struct FusedLds {
+  // W1 staging (prologue only), then the matrix waves' transposition tiles and, at the end,
+  // their statistics scratch (disjoint regions)
+  float w[kD * kLD];
+  float z[2][kTileRows * kLD];  // z tiles, gather -> matrix, double-buffered
+  int32_t nbr[kHalves][kRowsPerHalf][kSlots];
+  float attr[kHalves][kRowsPerHalf][kSlots];
+};
+static_assert(4 * 32 * kTLD * 4 + 2 * 8 * kD * 8 <= kD * kLD * 4, "scratch fits in w");
+
+// Matrix role (waves 0-3).  Barriers: 1 + (nt + 1), as the gather role.
+__device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, const TileSeq& ts,
+                                            int nt) {
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int cq = lane & 7, grp = lane >> 3;  // transposed epilogue: 4-column chunk, row group
+  {
+    const float4* w4 = reinterpret_cast<const float4*>(A.W1);
+    float4 wt[kD * kD4 / kMatThreads];
+#pragma unroll
+    for (int j = 0; j < kD * kD4 / kMatThreads; ++j) wt[j] = w4[tid + kMatThreads * j];
+#pragma unroll
+    for (int j = 0; j < kD * kD4 / kMatThreads; ++j) {
+      const int idx = tid + kMatThreads * j;
+      *reinterpret_cast<float4*>(&L.w[(idx / kD4) * kLD + 4 * (idx % kD4)]) = wt[j];
+    }
+  }
+  const float4 bias4 = *reinterpret_cast<const float4*>(A.b1 + 32 * wave + 4 * cq);
+  __syncthreads();
+  // W1^T fragments: B[k][j] = W1[j][k], lane half h takes k in [h*64, h*64+64)
+  float bf[kKS];
+  {
+    const float* wr = &L.w[(32 * wave + c32) * kLD + h * kKS];
+#pragma unroll
+    for (int q = 0; q < kKS / 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(&wr[4 * q]);
+      bf[4 * q] = v.x;
+      bf[4 * q + 1] = v.y;
+      bf[4 * q + 2] = v.z;
+      bf[4 * q + 3] = v.w;
+    }
+  }
+  __syncthreads();  // (iteration 0: the gather role stages the first tile)
+  double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
+  const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
+  float* tt = &L.w[wave * 32 * kTLD];
+  for (int it = 1; it <= nt; ++it) {
+    const int T = ts.at(it - 1);
+    const float* arow = &L.z[(it - 1) & 1][c32 * kLD + h * kKS];
+    floatx16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int q = 0; q < (GINE_FUSED_DBG == 2 ? 1 : kKS / 4); ++q) {
+      const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+    }
+    // this wave's 32x32 block -> row-major through its own LDS tile
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tt[((r & 3) + 8 * (r >> 2) + 4 * h) * kTLD + c32] = acc[r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = grp + 8 * i;
+      const int64_t n = (int64_t)T * kTileRows + row;
+      const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * cq]);
+      if (n >= A.N) continue;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      float o4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o4[k] = vv[k] + bb[k];
+        st1[k] += (double)o4[k];
+        st2[k] += (double)o4[k] * (double)o4[k];
+      }
+      *reinterpret_cast<float4*>(A.a1 + n * kD + 32 * wave + 4 * cq) =
+          make_float4(o4[0], o4[1], o4[2], o4[3]);
+    }
+    __builtin_amdgcn_wave_barrier();  // the next tile's transposition writes come after
+    __syncthreads();
+  }
+  // per-column partials: the 8 row groups added in fixed order (row-tile GEMM order)
+  double* sr = reinterpret_cast<double*>(&L.w[4 * 32 * kTLD]);  // [2][8][kD]
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = 32 * wave + 4 * cq + k;
+    sr[(0 * 8 + grp) * kD + c] = st1[k];
+    sr[(1 * 8 + grp) * kD + c] = st2[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int which = lane >> 5, cc = 32 * wave + (lane & 31);
+  double s = 0.0;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) s += sr[(which * 8 + g) * kD + cc];
+  A.partials[(size_t)blockIdx.x * 2 * kD + which * kD + cc] = s;
+}
+
+// Gather role (waves 4-11).  Barriers: 1 + (nt + 1), as the matrix role.
+template <bool FMA>
+__device__ __forceinline__ void gather_role(const FusedArgs& A, FusedLds& L, const TileSeq& ts,
+                                            int nt) {
+  const int p = threadIdx.x - kMatThreads;
+  const int hw = p >> 5, t = p & 31;
+  const int N = A.N;
+  const uint32_t qb = (uint32_t)t * 16u;
+  const char* xb = reinterpret_cast<const char*>(A.x);
+  RowptrStage rp;
+  EdgeStage es;
+#pragma unroll
+  for (int i = 0; i < kRowsPerHalf; ++i) {
+    rp.beg[i] = rp.end[i] = 0;
+    es.nbr[i] = 0;
+    es.attr[i] = 0.f;
+    es.cnt[i] = 0;
+  }
+  auto row_of = [&](int T, int i) { return T * kTileRows + hw + kHalves * i; };
+  auto clamp_row = [&](int n) { return n < N ? n : N - 1; };
+  auto issue_rowptr = [&](int T) {  // -> rp (no wait)
+#pragma unroll
+    for (int i = 0; i < kRowsPerHalf; ++i) {
+      const int n = clamp_row(row_of(T, i));
+      rp.beg[i] = A.rowptr[n];
+      rp.end[i] = A.rowptr[n + 1];
+    }
+  };
+  auto issue_edges = [&](int T) {  // rp (of tile T, arrived) -> es (no wait)
+#pragma unroll
+    for (int i = 0; i < kRowsPerHalf; ++i) {
+      const int cnt = row_of(T, i) < N ? min(rp.end[i] - rp.beg[i], kSlots) : 0;
+      const int e = cnt > 0 ? rp.beg[i] + min(t, cnt - 1) : 0;  // always a valid index
+      es.nbr[i] = A.nbr[e];
+      es.attr[i] = A.attr[e];
+      es.cnt[i] = cnt;
+    }
+  };
+  const f4v lw = ld_f4v(reinterpret_cast<const char*>(A.lin_w), qb);
+  const f4v lb = ld_f4v(reinterpret_cast<const char*>(A.lin_b), qb);
+  const float ope = 1.0f + A.eps[0];
+  if (nt > 0) {
+    issue_rowptr(ts.at(0));
+    issue_edges(ts.at(0));
+  }
+  if (nt > 1) issue_rowptr(ts.at(1));
+  __syncthreads();
+
+  for (int it = 0; it < nt; ++it) {
+    const int T = ts.at(it);
+    float* sz = L.z[it & 1];
+    int cnt[kRowsPerHalf];
+#pragma unroll
+    for (int i = 0; i < kRowsPerHalf; ++i) {
+      L.nbr[hw][i][t] = t < es.cnt[i] ? es.nbr[i] : clamp_row(row_of(T, i));
+      L.attr[hw][i][t] = es.attr[i];
+      cnt[i] = es.cnt[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (it + 1 < nt) issue_edges(ts.at(it + 1));
+    if (it + 2 < nt) issue_rowptr(ts.at(it + 2));
+    f4v self[kRowsPerHalf], acc[kRowsPerHalf];
+#pragma unroll
+    for (int i = 0; i < kRowsPerHalf; ++i) {
+      self[i] = ld_f4v(xb, (uint32_t)clamp_row(row_of(T, i)) * kRowBytes + qb);
+      acc[i] = f4v_zero();
+    }
+#pragma unroll
+    for (int pr = 0; pr < kRowsPerHalf; pr += 2) {
+      const int m = GINE_FUSED_DBG == 1 ? 0 : max(cnt[pr], cnt[pr + 1]);
+      for (int j0 = 0; j0 < m; j0 += kU) {
+        f4v r0[kU], r1[kU];
+        float a0[kU], a1v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int j = min(j0 + u, kSlots - 1);
+          r0[u] = ld_f4v(xb, (uint32_t)L.nbr[hw][pr][j] * kRowBytes + qb);
+          r1[u] = ld_f4v(xb, (uint32_t)L.nbr[hw][pr + 1][j] * kRowBytes + qb);
+          a0[u] = L.attr[hw][pr][j];
+          a1v[u] = L.attr[hw][pr + 1][j];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          edge_acc<FMA>(acc[pr], r0[u], a0[u], lw, lb, j0 + u < cnt[pr]);
+          edge_acc<FMA>(acc[pr + 1], r1[u], a1v[u], lw, lb, j0 + u < cnt[pr + 1]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRowsPerHalf; ++i) {
+      const int r = hw + kHalves * i;
+      const int64_t n = (int64_t)T * kTileRows + r;
+      const f4v zv = add_scaled(acc[i], ope, self[i]);
+      *reinterpret_cast<f4v*>(&sz[r * kLD + 4 * t]) = zv;
+      if (n < N) *reinterpret_cast<f4v*>(A.z + n * kD + 4 * t) = zv;
+    }
+    __builtin_amdgcn_wave_barrier();  // edge-list reads done before the next tile's writes
+    __syncthreads();
+  }
+  __syncthreads();  // (iteration nt: the matrix role multiplies the last tile)
+}
+
+template <bool FMA>
+__global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_mlp1(FusedArgs A) {
+  __shared__ __attribute__((aligned(16))) FusedLds L;
+  const TileSeq ts = tile_seq(A.num_tiles, blockIdx.x, gridDim.x);
+  const int nt = ts.count();
+  // the role is wave-uniform (an SGPR): each wave branches, none runs the other's barriers
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  if (wave < kMatThreads / kWave) matrix_role(A, L, ts, nt);
+  else gather_role<FMA>(A, L, ts, nt);
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                                const float* in_attr, const float* lin_w, const float* lin_b,
+                                const float* eps, const float* w1, const float* b1, float* z,
+                                float* a1, double* partials, int64_t num_nodes,
+                                int32_t channels, int32_t max_in_degree, int32_t flags,
+                                void* stream) {
+  if (channels != kD) return GINE_ERR_DIM;
+  if ((flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
+  if (max_in_degree < 0 || max_in_degree > GINE_MP_FUSED_MAX_DEGREE) return GINE_ERR_INVALID;
+  if (num_nodes <= 0 || !x || !in_rowptr || !in_src || !in_attr || !lin_w || !lin_b || !eps ||
+      !w1 || !b1 || !z || !a1 || !partials)
+    return GINE_ERR_INVALID;
+  if (num_nodes * channels * 4 >= (int64_t(1) << 32)) return GINE_ERR_TOO_LARGE;
+  int32_t grid = 0;
+  const int st = gine_mlp_num_partials(num_nodes, channels, &grid);
+  if (st != GINE_OK) return st;
+  const int tiles = (int)ceil_div(num_nodes, kTileRows);
+  hipStream_t s = as_stream(stream);
+  const FusedArgs A{x,  in_rowptr, in_src, in_attr, lin_w,    lin_b,          eps,
+                    w1, b1,        z,      a1,      partials, (int)num_nodes, tiles};
+  if (flags & GINE_MP_LIN_MULADD)
+    hipLaunchKernelGGL(k_mp_fwd_mlp1<false>, dim3((unsigned)grid), dim3(kThreads), 0, s, A);
+  else
+    hipLaunchKernelGGL(k_mp_fwd_mlp1<true>, dim3((unsigned)grid), dim3(kThreads), 0, s, A);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

@@ -50,6 +50,7 @@ class GradJob(ctypes.Structure):
 
 
 GRAD_JOB_MP, GRAD_JOB_SLAB, GRAD_MAX_JOBS = 1, 2, 12
+MP_FUSED_MAX_DEGREE = 32  # GINE_MP_FUSED_MAX_DEGREE
 _job_p = ctypes.POINTER(GradJob)
 WINDOW_LDS_BYTES = 80 * 1024
 
@@ -79,6 +80,7 @@ _SIGNATURES = {
     "gine_deepset_bwd_grad_job": [_i64, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _job_p],
     "gine_mlp_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_fwd1": [_c_void_p] * 5 + [_i64, _i32, _c_void_p],
+    "gine_mp_fwd_mlp1": [_c_void_p] * 12 + [_i64, _i32, _i32, _i32, _c_void_p],
     "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,
                                                                    _i32, _c_void_p],
     "gine_mlp_fwd2": [_c_void_p] * 7 + [_i64, _i32, _i32, _c_void_p],

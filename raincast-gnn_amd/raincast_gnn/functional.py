@@ -189,6 +189,23 @@ class BnConfig:
         self.update_running = bn.training and bn.track_running_stats
 
 
+# gine_mp_fwd_mlp1 wins while each workgroup has at most 2 row tiles (256 workgroups of
+# 32-row tiles): 15.1 vs 16.9 us at cfg2, but 121 vs 96 us at cfg3 (csrc/gine_mpmlp.hip).
+FUSED_MAX_NODES = 2 * 256 * 32
+
+
+def fused_forward_ok(graph, N: int, D: int) -> bool:
+    """gine_mp_fwd_mlp1 applies: D = 128, edge attributes, every in-degree within
+    GINE_MP_FUSED_MAX_DEGREE, N <= FUSED_MAX_NODES, no forward window plan.
+    GINE_MP_FUSED=0 turns it off, =all lifts the size limit (tests, experiments)."""
+    mode = os.environ.get("GINE_MP_FUSED", "1")
+    if mode == "0" or (N > FUSED_MAX_NODES and mode != "all"):
+        return False
+    deg = graph.max_in_degree
+    return (D == 128 and N > 0 and graph.in_attr is not None and deg is not None
+            and deg <= _lib.MP_FUSED_MAX_DEGREE and graph.window_plan("in", D) is None)
+
+
 class GineLayer(torch.autograd.Function):
     """y = epilogue( Linear2( ReLU( BN( Linear1( z ) ) ) ) ),  z = GINE message passing.
 
@@ -210,11 +227,19 @@ class GineLayer(torch.autograd.Function):
                 f"Expected more than 1 value per channel when training, got input size "
                 f"{torch.Size([N, D])}")
 
-        z = mp_forward(x, graph, lw, lb, ep)
         a1 = torch.empty_like(x)
         P = _count("gine_mlp_num_partials", N, D)
         partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
-        call("gine_mlp_fwd1", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), ptr(partials), N, D, stream)
+        if fused_forward_ok(graph, N, D):
+            # gather of the next tile beside the matrix chain of this one: one launch
+            z = torch.empty_like(x)
+            call("gine_mp_fwd_mlp1", ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src),
+                 ptr(graph.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(w1c), ptr(b1c), ptr(z),
+                 ptr(a1), ptr(partials), N, D, graph.max_in_degree, edge_linear_flag(), stream)
+        else:
+            z = mp_forward(x, graph, lw, lb, ep)
+            call("gine_mlp_fwd1", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), ptr(partials), N, D,
+                 stream)
         bn_save = torch.empty(4, D, dtype=torch.float32, device=dev)
         call("gine_bn_fwd_finalize", ptr(partials), P, ptr(g), ptr(bt), ptr(bn.running_mean),
              ptr(bn.running_var), ptr(bn.num_batches_tracked) if bn.update_running else None,

@@ -85,7 +85,8 @@ class GineGraph:
     """Stable CSR (by destination) + CSR (by source) of one edge list on one device."""
 
     __slots__ = ("num_nodes", "num_edges", "device", "in_rowptr", "in_src", "in_attr",
-                 "out_rowptr", "out_dst", "out_attr", "_error", "_checked", "_windows")
+                 "out_rowptr", "out_dst", "out_attr", "_error", "_checked", "_windows",
+                 "max_in_degree")
 
     def __init__(self, edge_index: torch.Tensor, edge_attr: torch.Tensor | None,
                  num_nodes: int, flow: str = "source_to_target"):
@@ -129,9 +130,11 @@ class GineGraph:
         # the caching allocator only hands them out again to work ordered after the sort.
         self._checked = False
         self._windows = None
+        self.max_in_degree = None  # host copy; None when built inside a stream capture
         if not torch.cuda.is_current_stream_capturing():
             self.check()
             self._plan_windows()
+            self.max_in_degree = int(self.in_degree().max()) if self.num_nodes > 0 else 0
 
     def _plan_windows(self) -> None:
         mode, max_nodes = window_settings()

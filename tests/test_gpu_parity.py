@@ -511,3 +511,93 @@ def test_eval_mode_prediction_and_ensemble_match_oracle(tmp_path):
     c = ensemble_crps(make(), preds, y)
     c_ref = ensemble_crps(make(), ref_mean, y)
     assert abs(c.item() - c_ref.item()) <= 1e-5 * abs(c_ref.item())
+
+
+# ---------------------------------------------------------------------------------------
+# fused message passing + first Linear (gine_mp_fwd_mlp1)
+# ---------------------------------------------------------------------------------------
+def _fused_cases():
+    out = [c for c in special_graphs()]
+    ei, ea, n = knn_batch_graph(500, 10, 32, seed=5)        # cfg2: ~2 tiles per workgroup
+    out.append(("knn500_k10_b32", ei, ea, n))
+    ei, ea, n = knn_batch_graph(2000, 16, 16, seed=6)       # 1000 tiles: 4 per workgroup
+    out.append(("knn2000_k16_b16", ei, ea, n))
+    ei, ea, n = knn_batch_graph(37, 31, 3, seed=7)          # in-degree 32: the limit
+    out.append(("knn37_k31_b3", ei, ea, n))
+    return out
+
+
+@pytest.mark.parametrize("case", _fused_cases(), ids=lambda c: c[0])
+@pytest.mark.parametrize("rounding", [0, _lib.GINE_MP_LIN_MULADD], ids=["fma", "muladd"])
+def test_mp_fwd_mlp1_fused_matches_unfused(case, rounding, monkeypatch):
+    """One-launch gather + Linear1 + BN partials == gine_mp_fwd then gine_mlp_fwd1, bit for
+    bit (z, a1 and every partial row); above the degree limit it refuses."""
+    monkeypatch.setenv("GINE_MP_FUSED", "all")
+    _, ei, ea, n = case
+    D = 128
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    torch.manual_seed(n)
+    x = torch.randn(n, D, device=DEV)
+    lw, lb, eps = (t.to(DEV) for t in _mp_params(D, seed=n, eps=0.25))
+    lw = lw.reshape(-1).contiguous()
+    w1 = (torch.randn(D, D) / 11).to(DEV)
+    b1 = torch.randn(D).to(DEV)
+    P = Fn._count("gine_mlp_num_partials", n, D)
+    z1, a1f = torch.full_like(x, 7.0), torch.full_like(x, 7.0)
+    part1 = torch.full((P, 2, D), 7.0, dtype=torch.float64, device=DEV)
+    args = (Fn.ptr(x), Fn.ptr(g.in_rowptr), Fn.ptr(g.in_src), Fn.ptr(g.in_attr), Fn.ptr(lw),
+            Fn.ptr(lb), Fn.ptr(eps), Fn.ptr(w1), Fn.ptr(b1), Fn.ptr(z1), Fn.ptr(a1f),
+            Fn.ptr(part1), n, D)
+    stream = _lib.stream_handle(DEV)
+    if g.max_in_degree > _lib.MP_FUSED_MAX_DEGREE:
+        with pytest.raises(_lib.GineError):
+            _lib.call("gine_mp_fwd_mlp1", *args, g.max_in_degree, rounding, stream)
+        assert not Fn.fused_forward_ok(g, n, D)
+        return
+    assert Fn.fused_forward_ok(g, n, D)
+    _lib.call("gine_mp_fwd_mlp1", *args, g.max_in_degree, rounding, stream)
+    z0 = Fn.mp_forward(x, g, lw, lb, eps, lin_flag=rounding)
+    a10 = torch.empty_like(x)
+    part0 = torch.empty(P, 2, D, dtype=torch.float64, device=DEV)
+    _lib.call("gine_mlp_fwd1", Fn.ptr(z0), Fn.ptr(w1), Fn.ptr(b1), Fn.ptr(a10), Fn.ptr(part0),
+              n, D, stream)
+    torch.cuda.synchronize()
+    assert torch.equal(z1, z0)
+    assert torch.equal(a1f, a10)
+    assert torch.equal(part1, part0)
+
+
+def test_mp_fwd_mlp1_rejects_bad_arguments():
+    ei, ea, n = knn_batch_graph(64, 4, 1, seed=3)
+    g = GineGraph(ei.to(DEV), ea.to(DEV), n)
+    D = 128
+    x = torch.randn(n, D, device=DEV)
+    t = torch.zeros(D, device=DEV)
+    P = Fn._count("gine_mlp_num_partials", n, D)
+    part = torch.zeros(P, 2, D, dtype=torch.float64, device=DEV)
+    base = [Fn.ptr(x), Fn.ptr(g.in_rowptr), Fn.ptr(g.in_src), Fn.ptr(g.in_attr), Fn.ptr(t),
+            Fn.ptr(t), Fn.ptr(t), Fn.ptr(x), Fn.ptr(t), Fn.ptr(x), Fn.ptr(x), Fn.ptr(part)]
+    s = _lib.stream_handle(DEV)
+    for bad in ([*base, n, 64, 5, 0, s], [*base, n, D, 33, 0, s], [*base, n, D, 5, 8, s],
+                [*base[:3], None, *base[4:], n, D, 5, 0, s], [*base, 0, D, 5, 0, s]):
+        with pytest.raises(_lib.GineError):
+            _lib.call("gine_mp_fwd_mlp1", *bad)
+
+
+def test_layer_fused_forward_equals_unfused(monkeypatch):
+    """A training GINE layer (forward + backward) gives identical bits with the fused
+    forward on and off."""
+    ei, ea, n = knn_batch_graph(500, 10, 4, seed=9)
+    assert n <= Fn.FUSED_MAX_NODES
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GINE_MP_FUSED", flag)
+        torch.manual_seed(0)
+        net = ResGnn(128, 128, 2, 128).to(DEV).train()
+        x = torch.randn(n, 128, device=DEV, requires_grad=True)
+        y = net(x, ei.to(DEV), ea.to(DEV))
+        y.backward(torch.ones_like(y))
+        outs.append([y.detach(), x.grad] + [p.grad for p in net.parameters()]
+                    + [b for b in net.buffers()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -26,6 +26,7 @@ run() {  # run <name> <seconds> cmd...
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
+    ktests) run pytest_k 600 python -u -m pytest tests -m gpu -q -rf -k "${KTESTS:-window}" --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench1) run bench_cfg1 600 python bench.py --config 1 ;;
