@@ -604,6 +604,14 @@ __global__ __launch_bounds__(kColsumThreads) void k_bn_fwd_finalize(
 //   z = 1: P = da1 (PRO_DA1 of dbn), Q = z               -> dW1, db1
 // on the shared engine (gine_wgrad.hpp); this is its operand source.
 // ----------------------------------------------------------------------------------------
+// Output-tile height of the node-MLP weight gradients (experiment switch: TO = 128 reads
+// each operand row once per chunk, TO = 64 twice, with twice the workgroups; at cfg2
+// TO = 128 measured 28.2 vs 25.0 us for gine_mlp_bwd1_wgrad, 26.3 vs 22.1 standalone).
+#ifndef GINE_MLP_WG_TO
+#define GINE_MLP_WG_TO 64
+#endif
+constexpr int kMlpWgTO = GINE_MLP_WG_TO;
+
 template <int PDO>  // PRO_PLAIN | PRO_DOR | PRO_DOM: how do is formed from dy
 struct MlpWgradSrc {
   static constexpr int kZ = 2;
@@ -722,14 +730,14 @@ __global__ __launch_bounds__(256) void k_bwd1_wgrad(const float* __restrict__ w1
                                                     int chunks, int rows_per_chunk,
                                                     size_t zstride, size_t cstride,
                                                     float* __restrict__ slab, int eng_blocks) {
-  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (64 + 4)];
+  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (kMlpWgTO + 4)];
   __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
   const int b = blockIdx.x;
   if (b < eng_blocks) {
     // the output tiles of one row chunk run back to back on ONE XCD: they read the same
     // rows (a1 by all four, z by the two dW1 tiles), which that XCD's L2 then serves
     const int lb = xcd_remap(b, eng_blocks), tiles = eng_blocks / chunks;
-    wgrad_block<MlpWgradSrc<PDO>, 64, 4>(src, N, 128, 128, lb / tiles, lb % tiles,
+    wgrad_block<MlpWgradSrc<PDO>, kMlpWgTO, 4>(src, N, 128, 128, lb / tiles, lb % tiles,
                                          rows_per_chunk, zstride, cstride, slab, sP, sQ);
   } else {
     static_assert(kRowTile * (128 + 4) <= kWgRows * kWgLdQ, "row tile fits in sQ");
@@ -740,7 +748,7 @@ __global__ __launch_bounds__(256) void k_bwd1_wgrad(const float* __restrict__ w1
 
 inline bool mlp_dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
-inline WgPlan mlp_wgrad_plan(int64_t N, int D) { return wg_plan(N, D, D, 2, 64); }
+inline WgPlan mlp_wgrad_plan(int64_t N, int D) { return wg_plan(N, D, D, 2, kMlpWgTO); }
 
 }  // namespace
 }  // namespace gine
@@ -901,13 +909,16 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   int st;
   if (epilogue == GINE_EPI_NONE) {
     const MlpWgradSrc<PRO_PLAIN> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<kMlpWgTO>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
+                                       per * p.chunks, per, slab, s);
   } else if (epilogue == GINE_EPI_RELU) {
     const MlpWgradSrc<PRO_DOR> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<kMlpWgTO>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
+                                       per * p.chunks, per, slab, s);
   } else {
     const MlpWgradSrc<PRO_DOM> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<64>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p, per * p.chunks, per, slab, s);
+    st = launch_wgrad_engine<kMlpWgTO>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
+                                       per * p.chunks, per, slab, s);
   }
   if (st != GINE_OK) return st;
   if (st != GINE_OK) return st;
