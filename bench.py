@@ -226,6 +226,15 @@ def time_kernels(tr: Trainer, reps: int):
         "gine_mp_bwd_finalize": (lambda: call("gine_mp_bwd_finalize", ptr(mp_part), Pm, D,
                                               ptr(lw_g), ptr(lb_g), ptr(eps_g), S[0]), {}),
     }
+
+    def mp_fwd_mlp1():  # the fused forward (gather + Linear1 + BN partials)
+        call("gine_mp_fwd_mlp1", ptr(x), ptr(g.in_rowptr), ptr(g.in_src), ptr(g.in_attr),
+             ptr(lw), ptr(lb), ptr(ep), ptr(w1), ptr(b1), ptr(z), ptr(a1), ptr(partials), N,
+             D, g.max_in_degree, lin, S[0])
+
+    if Fn.fused_forward_ok(g, N, D):  # what the training step's forward runs at this size
+        kernels["gine_mp_fwd_mlp1"] = (mp_fwd_mlp1, {
+            "flops": 2 * N * D * D, "bytes": 4 * (2 * N * D + 2 * E + N + 1) + 4 * N * D})
     out = {}
     for name, (fn, work) in kernels.items():
         for _ in range(3):
@@ -267,6 +276,9 @@ def time_kernels(tr: Trainer, reps: int):
 
 STEP_KERNELS = ("gine_mp_fwd", "gine_mp_bwd", "gine_mlp_fwd1", "gine_mlp_fwd2",
                 "gine_mlp_bwd2", "gine_mlp_bwd1_wgrad")  # each runs once per GINE layer
+# ... or, where the fused forward applies (raincast_gnn.functional.fused_forward_ok):
+FUSED_STEP_KERNELS = ("gine_mp_fwd_mlp1", "gine_mp_bwd", "gine_mlp_fwd2", "gine_mlp_bwd2",
+                      "gine_mlp_bwd1_wgrad")
 
 
 def _roof(name: str, rec: dict, bound: str, layers: int) -> dict:
@@ -293,7 +305,8 @@ def roofline_for(kernels: dict, layers: int):
     """The dominant kernel of the step (largest time per step among the per-layer kernels
     the training step launches), against its bound: fp32 MFMA for the node-MLP GEMMs, HBM
     for message passing."""
-    timed = [k for k in STEP_KERNELS if k in kernels]
+    step = FUSED_STEP_KERNELS if "gine_mp_fwd_mlp1" in kernels else STEP_KERNELS
+    timed = [k for k in step if k in kernels]
     dominant = max(timed, key=lambda k: kernels[k]["us"])
     rec = kernels[dominant]
     return _roof(dominant, rec, "mfma" if "alg_flops" in rec else "hbm", layers)
@@ -326,6 +339,7 @@ def copy_ceiling_gbps(device, nbytes=1 << 30, reps=10):
 # the residual epilogue of layers >= 1)
 PMC_KERNELS = {
     "gine_mp_fwd": ["gine::k_mp_fwd<32, 1, "],
+    "gine_mp_fwd_mlp1": ["gine::k_mp_fwd_mlp1<"],
     "gine_mp_bwd": ["gine::k_mp_bwd_win<32, "],
     "gine_mlp_fwd1": ["gine::k_rowgemm<128, 0, 0, true>"],
     "gine_mlp_fwd2": ["gine::k_rowgemm<128, 1, 5, true>"],

@@ -25,6 +25,7 @@
 #include "gine_wgrad.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace gine {
 namespace {
@@ -239,9 +240,15 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   }
 }
 
+// Persistent grid, one workgroup per CU (two per CU measured slower at cfg2: 0.614 vs
+// 0.589 ms per step).  GINE_CHAIN_BLOCKS (tuning experiments only) overrides the cap.
 inline int chain_grid(int64_t N) {
+  static const int cap = [] {
+    const char* e = getenv("GINE_CHAIN_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : kNumCu;
+  }();
   const int64_t tiles = ceil_div(N, kRowTile);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, 256));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cap));
 }
 
 template <int D, int FP, int KIND>
