@@ -158,6 +158,23 @@ int gine_mp_bwd_win_side(const float* dz, const float* x, const int32_t* out_row
                          const gine_window_plan* plan, const float* wg_slab, int32_t wg_chunks,
                          int32_t mlp_channels, float* dw1, float* db1, float* dw2, float* db2,
                          void* stream);
+/* gine_mp_bwd_win + the node-MLP weight-gradient engine of the same GINE layer in ONE launch
+ * (D = 128, slice_channels = 32): extra workgroups write the fp32 slab
+ * [2][gine_mlp_wgrad_num_chunks][D*D + D] exactly as gine_mlp_wgrad does with NULL outputs
+ * (operands dy, y, mask, a1, bn_save, dbn, coef, z, epilogue as for gine_mlp_wgrad), while
+ * the window workgroups run the message-passing backward; the slab is then reduced by
+ * gine_grad_finalize_batch.  Replaces the same reference ops as gine_mp_bwd and
+ * gine_mlp_wgrad (models/gnn.py:21-26,41,44 autograd).  GINE_ERR_INVALID when the plan's
+ * slice is not 32 channels. */
+int gine_mp_bwd_win_mlp_wgrad(const float* dz, const float* x, const int32_t* out_rowptr,
+                              const int32_t* out_dst, const float* out_attr,
+                              const float* lin_w, const float* lin_b, const float* eps,
+                              const float* dres, float* dx, double* partials,
+                              int64_t num_nodes, int32_t channels, int32_t flags,
+                              const gine_window_plan* plan, const float* dy, const float* y,
+                              const uint8_t* mask, const float* a1, const float* bn_save,
+                              const float* dbn, const float* coef, const float* z, float* slab,
+                              int32_t epilogue, void* stream);
 int gine_mp_bwd_win_finalize(const double* partials, int32_t num_tiles, int32_t channels,
                              int32_t slice_channels, float* dlin_w, float* dlin_b,
                              float* deps, void* stream);
@@ -272,6 +289,8 @@ int gine_mlp_bwd1(const float* dbn, const float* a1, const float* bn_save, const
                   const float* w1, float* dz, int64_t num_nodes, int32_t channels,
                   void* stream);
 int gine_mlp_wgrad_num_chunks(int64_t num_nodes, int32_t channels, int32_t* num_chunks);
+/* dw1, db1, dw2, db2 all NULL: only the fp32 slab [2][chunks][D*D + D] is written (for a
+ * batched reduction, gine_grad_finalize_batch). */
 int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* mask, const float* a1,
                    const float* bn_save, const float* dbn, const float* coef, const float* z,
                    float* slab, float* dw1, float* db1, float* dw2, float* db2,

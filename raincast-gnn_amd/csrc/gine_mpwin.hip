@@ -16,6 +16,8 @@
 #include "gine_common.hpp"
 #include "gine_edge.hpp"
 #include "gine_slab.hpp"
+#include "gine_wgrad.hpp"
+#include "gine_mlpsrc.hpp"
 #include "gine_reduce.hpp"
 
 #include <climits>
@@ -177,24 +179,52 @@ __global__ __launch_bounds__(kWinThreads, CS == 32 ? 2 : 3) void k_mp_fwd_win(
 // partials row `tile` (fp64 [3][D]): columns [slice] of sum dm*a and sum dm, and at
 // 2D + slice the slice's sum of dz*x.
 // ----------------------------------------------------------------------------------------
-template <int CS, bool FMA>
+// The node-MLP weight-gradient engine (dW1 = da1^T z, dW2 = do^T r of this GINE layer,
+// gine_wgrad.hpp with 8 waves) as extra workgroups of the message-passing backward: the
+// engine is matrix- and HBM-bound, the window kernel LDS- and VALU-bound, so they share
+// the CUs instead of the engine sharing them with the dz GEMM (gine_mlp_bwd1_wgrad).
+template <int PDO>
+struct WinEngine {
+  MlpWgradSrc<PDO> src;
+  float* slab;
+  int64_t N;
+  size_t zstride, cstride;
+  int nblocks, tiles, rows_per_chunk;
+};
+constexpr size_t kWinEngineLds = sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
+
+template <int CS, bool FMA, bool ENG = false, int PDO = PRO_PLAIN>
 __global__ __launch_bounds__(kWinThreads, 2) void k_mp_bwd_win(
     const float4* __restrict__ dz4, const float4* __restrict__ x4,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ nbr,
     const float* __restrict__ attr, const float4* __restrict__ lw4,
     const float4* __restrict__ lb4, const float* __restrict__ eps,
     const float4* __restrict__ dres4, float4* __restrict__ dx4, double* __restrict__ partials,
-    WinPlan plan, int D4, int S, int flags, MlpSlabJob job) {
+    WinPlan plan, int D4, int S, int flags, MlpSlabJob job, WinEngine<PDO> eng) {
   constexpr int Q = CS / 4, G = kWinThreads / Q, U = kWinUnroll;
   constexpr int P = (kWinTileNodes + G - 1) / G;
   extern __shared__ float4 s_dyn[];
-  if ((int)blockIdx.x < job.nblocks) {  // side job: the node-MLP weight-gradient slab
+  int eb = 0;  // engine workgroups (first: the longest job starts first)
+  if constexpr (ENG) {
+    static_assert(kWinThreads == 512, "the engine runs 8 waves");
+    if ((int)blockIdx.x < eng.nblocks) {
+      float* sP = reinterpret_cast<float*>(s_dyn);
+      float* sQ = sP + kWgRows * (64 + 4);
+      const int e = xcd_remap(blockIdx.x, eng.nblocks);
+      wgrad_block<MlpWgradSrc<PDO>, 64, 8>(eng.src, eng.N, 128, 128, e / eng.tiles,
+                                           e % eng.tiles, eng.rows_per_chunk, eng.zstride,
+                                           eng.cstride, eng.slab, sP, sQ);
+      return;
+    }
+    eb = eng.nblocks;
+  }
+  if ((int)blockIdx.x - eb < job.nblocks) {  // side job: the node-MLP weight-gradient slab
     if (threadIdx.x < 256)
-      job.run(blockIdx.x, reinterpret_cast<double(*)[kSlabQuads * 4 + 1]>(s_dyn));
+      job.run(blockIdx.x - eb, reinterpret_cast<double(*)[kSlabQuads * 4 + 1]>(s_dyn));
     return;
   }
   const WinLds lds(s_dyn, plan, Q);
-  const int lb = xcd_remap(blockIdx.x - job.nblocks, gridDim.x - job.nblocks);
+  const int lb = xcd_remap(blockIdx.x - eb - job.nblocks, gridDim.x - eb - job.nblocks);
   const int tile = lb / S, slice = lb % S, col4 = slice * Q;
   const int n0 = plan.tile_begin[tile], nodes = plan.tile_begin[tile + 1] - n0;
   const int lo = plan.win_lo[tile];
@@ -375,11 +405,13 @@ int set_lds_limit() {
       break;                                    \
   }
 
+template <int PDO>
 int mp_bwd_win_launch(const float* dz, const float* x, const int32_t* out_rowptr,
                       const int32_t* out_dst, const float* out_attr, const float* lin_w,
                       const float* lin_b, const float* eps, const float* dres, float* dx,
                       double* partials, int64_t num_nodes, int32_t channels, int32_t flags,
-                      const gine_window_plan* plan, const MlpSlabJob& job, void* stream) {
+                      const gine_window_plan* plan, const MlpSlabJob& job,
+                      const WinEngine<PDO>* eng, void* stream) {
   if (!valid_plan(plan, num_nodes, channels)) return GINE_ERR_INVALID;
   if ((flags & ~(GINE_MP_BWD_SELF | GINE_MP_LIN_MULADD)) != 0) return GINE_ERR_INVALID;
   if (!dz || !x || !out_rowptr || !out_dst || !out_attr || !lin_w || !lin_b || !eps || !dx ||
@@ -391,23 +423,39 @@ int mp_bwd_win_launch(const float* dz, const float* x, const int32_t* out_rowptr
   const size_t jobb = job.nblocks > 0 ? sizeof(double) * kSlabGroups * (kSlabQuads * 4 + 1) : 0;
   smem = smem > red ? smem : red;
   smem = smem > jobb ? smem : jobb;
+  if (eng) {  // the engine: D = 128, 32-channel slices, no slab side job in the same launch
+    if (channels != 128 || cs != 32 || job.nblocks != 0 || eng->nblocks <= 0)
+      return GINE_ERR_INVALID;
+    smem = smem > kWinEngineLds ? smem : kWinEngineLds;
+  }
   if (smem > GINE_WINDOW_LDS_BYTES) return GINE_ERR_INVALID;
-  const unsigned grid = (unsigned)(plan->num_tiles * S + job.nblocks);
+  const unsigned grid =
+      (unsigned)(plan->num_tiles * S + job.nblocks + (eng ? eng->nblocks : 0));
   const WinPlan wp = device_plan(plan);
   hipStream_t s = as_stream(stream);
   const bool fma = (flags & GINE_MP_LIN_MULADD) == 0;
   int st = GINE_OK;
-#define LAUNCH_BWD_WIN(CS_, F_)                                                              \
+  const WinEngine<PDO> e0 = eng ? *eng : WinEngine<PDO>{};
+#define LAUNCH_BWD_WIN_K(KER)                                                                 \
   do {                                                                                       \
-    st = set_lds_limit<k_mp_bwd_win<CS_, F_>>();                                               \
+    st = set_lds_limit<KER>();                                                               \
     if (st == GINE_OK)                                                                       \
-      hipLaunchKernelGGL((k_mp_bwd_win<CS_, F_>), dim3(grid), dim3(kWinThreads), smem, s,    \
-                         (const float4*)dz, (const float4*)x, out_rowptr, out_dst, out_attr, \
+      hipLaunchKernelGGL((KER), dim3(grid), dim3(kWinThreads), smem, s, (const float4*)dz,   \
+                         (const float4*)x, out_rowptr, out_dst, out_attr,                    \
                          (const float4*)lin_w, (const float4*)lin_b, eps, (const float4*)dres, \
-                         (float4*)dx, partials, wp, D4, S, flags, job);                      \
+                         (float4*)dx, partials, wp, D4, S, flags, job, e0);                  \
   } while (0)
-  GINE_WIN_DISPATCH(cs, fma, LAUNCH_BWD_WIN);
+#define LAUNCH_BWD_WIN(CS_, F_) LAUNCH_BWD_WIN_K((k_mp_bwd_win<CS_, F_, false, PDO>))
+  if (eng) {
+    if (fma) LAUNCH_BWD_WIN_K((k_mp_bwd_win<32, true, true, PDO>));
+    else LAUNCH_BWD_WIN_K((k_mp_bwd_win<32, false, true, PDO>));
+  } else if constexpr (PDO == PRO_PLAIN) {  // (the engine's type is unused here)
+    GINE_WIN_DISPATCH(cs, fma, LAUNCH_BWD_WIN);
+  } else {
+    return GINE_ERR_INVALID;
+  }
 #undef LAUNCH_BWD_WIN
+#undef LAUNCH_BWD_WIN_K
   if (st != GINE_OK) return st;
   GINE_LAUNCH_STATUS();
   return GINE_OK;
@@ -513,8 +561,9 @@ extern "C" int gine_mp_bwd_win(const float* dz, const float* x, const int32_t* o
                                int64_t num_nodes, int32_t channels, int32_t flags,
                                const gine_window_plan* plan, void* stream) {
   const MlpSlabJob none{nullptr, 0, 0, 0, MlpWgradOut{nullptr, nullptr, nullptr, nullptr, 0}};
-  return mp_bwd_win_launch(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps, dres, dx,
-                           partials, num_nodes, channels, flags, plan, none, stream);
+  return mp_bwd_win_launch<PRO_PLAIN>(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps,
+                                      dres, dx, partials, num_nodes, channels, flags, plan,
+                                      none, nullptr, stream);
 }
 
 extern "C" int gine_mp_bwd_win_side(const float* dz, const float* x, const int32_t* out_rowptr,
@@ -531,8 +580,45 @@ extern "C" int gine_mp_bwd_win_side(const float* dz, const float* x, const int32
   const int cols = (int)ceil_div(per, kSlabQuads * 4);
   const MlpSlabJob job{wg_slab, wg_chunks, cols, 2 * cols,
                        MlpWgradOut{dw2, db2, dw1, db1, mlp_channels}};
-  return mp_bwd_win_launch(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps, dres, dx,
-                           partials, num_nodes, channels, flags, plan, job, stream);
+  return mp_bwd_win_launch<PRO_PLAIN>(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps,
+                                      dres, dx, partials, num_nodes, channels, flags, plan,
+                                      job, nullptr, stream);
+}
+
+extern "C" int gine_mp_bwd_win_mlp_wgrad(
+    const float* dz, const float* x, const int32_t* out_rowptr, const int32_t* out_dst,
+    const float* out_attr, const float* lin_w, const float* lin_b, const float* eps,
+    const float* dres, float* dx, double* partials, int64_t num_nodes, int32_t channels,
+    int32_t flags, const gine_window_plan* plan, const float* dy, const float* y,
+    const uint8_t* mask, const float* a1, const float* bn_save, const float* dbn,
+    const float* coef, const float* z, float* slab, int32_t epilogue, void* stream) {
+  if (!dy || !a1 || !bn_save || !dbn || !coef || !z || !slab) return GINE_ERR_INVALID;
+  if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
+  if (channels != 128) return GINE_ERR_DIM;
+  static_assert(kMlpWgTO == 64, "the fused engine runs 64-row output tiles");
+  const int D = channels;
+  const WgPlan p = wg_plan(num_nodes, D, D, 2, kMlpWgTO);  // = gine_mlp_wgrad's plan
+  const size_t per = (size_t)D * D + D;
+  const int tiles = 2 * p.tiles_o * p.tiles_i;
+  const ProArgs p_do{dy, y, mask, nullptr, nullptr};
+  const ProArgs q_r{a1, nullptr, nullptr, bn_save, nullptr};
+  const ProArgs p_da1{dbn, a1, nullptr, bn_save, coef};
+  const ProArgs q_z{z, nullptr, nullptr, nullptr, nullptr};
+  const MlpSlabJob none{nullptr, 0, 0, 0, MlpWgradOut{nullptr, nullptr, nullptr, nullptr, 0}};
+#define MP_ENG(PD)                                                                           \
+  do {                                                                                       \
+    const WinEngine<PD> e{MlpWgradSrc<PD>{p_do, q_r, p_da1, q_z, D}, slab, num_nodes,        \
+                          per * p.chunks, per, p.chunks * tiles, tiles, p.rows_per_chunk};   \
+    return mp_bwd_win_launch<PD>(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps,    \
+                                 dres, dx, partials, num_nodes, channels, flags, plan, none,  \
+                                 &e, stream);                                                \
+  } while (0)
+  if (epilogue == GINE_EPI_NONE) MP_ENG(PRO_PLAIN);
+  if (epilogue == GINE_EPI_RELU) MP_ENG(PRO_DOR);
+  MP_ENG(PRO_DOM);
+#undef MP_ENG
 }
 
 extern "C" int gine_mp_bwd_win_finalize(const double* partials, int32_t num_tiles,

@@ -69,6 +69,8 @@ _SIGNATURES = {
                                 _c_void_p, _c_void_p, ctypes.POINTER(_i32), _c_void_p],
     "gine_mp_fwd_win": [_c_void_p] * 8 + [_i64, _i32, _i32, _plan_p, _c_void_p],
     "gine_mp_bwd_win": [_c_void_p] * 11 + [_i64, _i32, _i32, _plan_p, _c_void_p],
+    "gine_mp_bwd_win_mlp_wgrad": [_c_void_p] * 11 + [_i64, _i32, _i32, _plan_p]
+                                 + [_c_void_p] * 9 + [_i32, _c_void_p],
     "gine_mp_bwd_win_side": [_c_void_p] * 11 + [_i64, _i32, _i32, _plan_p, _c_void_p, _i32,
                                                  _i32] + [_c_void_p] * 5,
     "gine_mp_bwd_win_finalize": [_c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,

@@ -97,11 +97,14 @@ def mp_forward(x, graph, lin_w, lin_b, eps, lin_flag=None):
 
 
 def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_flag=None,
-                params=(None, None, None), side=None):
+                params=(None, None, None), side=None, engine=None):
     """Returns (dx, dlin_w, dlin_b, deps); ``params`` = the (lin.weight, lin.bias, eps)
     Parameters, whose gradients then go straight to their flat-buffer slices if any.
     ``side`` = (slab, chunks, D, dw1, db1, dw2, db2): a node-MLP weight-gradient slab left
-    by gine_mlp_bwd1_wgrad, reduced by extra workgroups of the same launch."""
+    by gine_mlp_bwd1_wgrad, reduced by extra workgroups of the same launch.
+    ``engine`` = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epilogue): the node-MLP
+    weight-gradient engine run by extra workgroups of the window launch (the caller checked
+    engine_in_mp_ok)."""
     N, D = x.shape
     dev = x.device
     dx = torch.empty_like(x)
@@ -120,7 +123,12 @@ def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_
     if plan is not None:
         P = plan.num_tiles
         partials = torch.empty(P, 3, D, dtype=torch.float64, device=dev)
-        if side is None:
+        if engine is not None:
+            e_dy, e_y, e_mask, e_a1, e_bn, e_dbn, e_coef, e_z, e_slab, e_epi = engine
+            call("gine_mp_bwd_win_mlp_wgrad", *args, ptr(partials), N, D, flags,
+                 ctypes.byref(plan), ptr(e_dy), ptr(e_y), ptr(e_mask), ptr(e_a1), ptr(e_bn),
+                 ptr(e_dbn), ptr(e_coef), ptr(e_z), ptr(e_slab), e_epi, stream)
+        elif side is None:
             call("gine_mp_bwd_win", *args, ptr(partials), N, D, flags, ctypes.byref(plan),
                  stream)
         else:
@@ -206,6 +214,15 @@ def fused_forward_ok(graph, N: int, D: int) -> bool:
             and deg <= _lib.MP_FUSED_MAX_DEGREE and graph.window_plan("in", D) is None)
 
 
+def engine_in_mp_ok(graph, D: int) -> bool:
+    """gine_mp_bwd_win_mlp_wgrad applies: D = 128 and a 32-channel window plan for the
+    backward.  GINE_MLP_WGRAD_IN_MP=0 keeps the engine in the dz launch."""
+    if os.environ.get("GINE_MLP_WGRAD_IN_MP", "1") == "0" or D != 128:
+        return False
+    plan = graph.window_plan("out", D)
+    return plan is not None and plan.slice_channels == 32
+
+
 class GineLayer(torch.autograd.Function):
     """y = epilogue( Linear2( ReLU( BN( Linear1( z ) ) ) ) ),  z = GINE message passing.
 
@@ -284,12 +301,21 @@ class GineLayer(torch.autograd.Function):
         slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
         dw1, db1 = grad_out(p_w1, (D, D), dev), grad_out(p_b1, (D,), dev)
         dw2, db2 = grad_out(p_w2, (D, D), dev), grad_out(p_b2, (D,), dev)
-        # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch
-        call("gine_mlp_bwd1_wgrad", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save),
-             ptr(dbn), ptr(coef), ptr(z), ptr(w1c), ptr(dz), ptr(slab), None, None, None,
-             None, N, D, epi, stream)
+        deferrable = gradbuf.deferrable(dw1, db1, dw2, db2)
+        engine = None
+        if deferrable and engine_in_mp_ok(ctx.graph, D):
+            # dz = da1 W1 alone; the dW1, dW2 slab from extra workgroups of the
+            # message-passing backward launch below
+            call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save), ptr(coef), ptr(w1c),
+                 ptr(dz), N, D, stream)
+            engine = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epi)
+        else:
+            # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch
+            call("gine_mlp_bwd1_wgrad", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save),
+                 ptr(dbn), ptr(coef), ptr(z), ptr(w1c), ptr(dz), ptr(slab), None, None, None,
+                 None, N, D, epi, stream)
         dres = dy if epi == EPI_RESIDUAL_RELU else None
-        if gradbuf.deferrable(dw1, db1, dw2, db2):
+        if deferrable:
             # only the optimizer reads dW1/db1/dW2/db2: the slab joins the end-of-backward
             # batch, off the critical path of the message-passing backward
             per = D * D + D
@@ -304,7 +330,7 @@ class GineLayer(torch.autograd.Function):
         else:  # reduced by extra workgroups of the message-passing backward launch
             side = (slab, C, D, dw1, db1, dw2, db2)
         dx, dlw, dlb, deps = mp_backward(dz, x, ctx.graph, lw, lb, ep, dres=dres,
-                                         params=(p_lw, p_lb, p_eps), side=side)
+                                         params=(p_lw, p_lb, p_eps), side=side, engine=engine)
         lin_w_shape, affine = ctx.shapes
         return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1, dgamma, dbeta,
                 dw2, db2, None, None, None)

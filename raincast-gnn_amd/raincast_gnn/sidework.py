@@ -47,12 +47,27 @@ def side_stream(device: torch.device) -> torch.cuda.Stream:
         return s
 
 
-def launch(device: torch.device, fn, keep_alive=(), params=()) -> None:
+_unjoined: list = []  # (main, side) stream pairs with side work not yet joined
+
+
+def wait_all() -> None:
+    """Make every main stream wait for the side work queued from it (the end-of-backward
+    gradient batch calls this before it reads slabs written on a side stream)."""
+    with _lock:
+        pairs = list(_unjoined)
+        _unjoined.clear()
+    for main, side in pairs:
+        main.wait_stream(side)
+
+
+def launch(device: torch.device, fn, keep_alive=(), params=(), force=False) -> None:
     """``fn(stream_handle)`` on the side stream of ``device``, ordered after the current
     stream's queued work and joined back into it at the end of the backward pass (inline
-    on the current stream when a parameter in ``params`` already has a gradient)."""
+    on the current stream when a parameter in ``params`` already has a gradient).
+    ``force`` uses the side stream even when RAINCAST_SIDE_STREAMS is off."""
     main = torch.cuda.current_stream(device)
-    if not ENABLED or any(p is not None and p.grad is not None for p in params):
+    if (not ENABLED and not force) or any(p is not None and p.grad is not None
+                                          for p in params):
         fn(main.cuda_stream)
         return
     side = side_stream(device)
@@ -60,6 +75,8 @@ def launch(device: torch.device, fn, keep_alive=(), params=()) -> None:
     with torch.cuda.stream(side):
         fn(side.cuda_stream)
     held = tuple(keep_alive)
+    with _lock:
+        _unjoined.append((main, side))
 
     def join():
         main.wait_stream(side)

@@ -230,3 +230,29 @@ def test_batched_grad_finish_matches_per_kernel_reductions(monkeypatch):
         m.loss_fn.crps(m(batch), batch.y).backward()
     for n, p in m.named_parameters():
         assert rel_err(p.grad, 2 * grads[True][n]) <= 1e-6, n
+
+
+def test_mlp_weight_grads_in_message_passing_launch(monkeypatch):
+    """The node-MLP weight-gradient engine run by extra workgroups of the window
+    message-passing backward (gine_mp_bwd_win_mlp_wgrad) gives the gradients of the engine
+    run beside the dz GEMM (gine_mlp_bwd1_wgrad): dW bit for bit (same MFMA order), the
+    bias sums to fp32 rounding."""
+    from raincast_gnn import functional as Fn
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.models import GNN
+    torch.manual_seed(11)
+    base = GNN(35, 128, 128, 4, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5)
+    batch = synthetic_batch(500, 32, k=10, seed=5).to(DEV)   # window backward active
+    grads = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GINE_MLP_WGRAD_IN_MP", flag)
+        m = copy.deepcopy(base).to(DEV)
+        opt = FlatAdamW(m.parameters(), lr=1e-3)
+        opt.zero_grad()
+        m.loss_fn.crps(m(batch), batch.y).backward()
+        grads[flag] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    for n, gref in grads["0"].items():
+        got = grads["1"][n]
+        if n.endswith("nn.0.weight") or n.endswith("nn.3.weight"):
+            assert torch.equal(got, gref), n
+        assert rel_err(got, gref) <= 1e-6, n
