@@ -235,6 +235,16 @@ def time_kernels(tr: Trainer, reps: int):
     if Fn.fused_forward_ok(g, N, D):  # what the training step's forward runs at this size
         kernels["gine_mp_fwd_mlp1"] = (mp_fwd_mlp1, {
             "flops": 2 * N * D * D, "bytes": 4 * (2 * N * D + 2 * E + N + 1) + 4 * N * D})
+
+    def mp_bwd_mlp_wgrad():  # the window backward + the node-MLP weight-gradient engine
+        call("gine_mp_bwd_win_mlp_wgrad", ptr(dz), ptr(x), ptr(g.out_rowptr), ptr(g.out_dst),
+             ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep), ptr(dz), ptr(dx), ptr(win_part), N, D,
+             1 | lin, ctypes.byref(win), ptr(dz), None, ptr(mask), ptr(a1), ptr(bn_save),
+             ptr(dbn), ptr(coef), ptr(z), ptr(slab), 2, S[0])
+
+    if Fn.engine_in_mp_ok(g, D):  # what the training step's backward runs at this size
+        kernels["gine_mp_bwd_mlp_wgrad"] = (mp_bwd_mlp_wgrad, {
+            "flops": 4 * N * D * D, "bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D})
     out = {}
     for name, (fn, work) in kernels.items():
         for _ in range(3):
@@ -305,11 +315,19 @@ def roofline_for(kernels: dict, layers: int):
     """The dominant kernel of the step (largest time per step among the per-layer kernels
     the training step launches), against its bound: fp32 MFMA for the node-MLP GEMMs, HBM
     for message passing."""
-    step = FUSED_STEP_KERNELS if "gine_mp_fwd_mlp1" in kernels else STEP_KERNELS
+    step = list(FUSED_STEP_KERNELS if "gine_mp_fwd_mlp1" in kernels else STEP_KERNELS)
+    if "gine_mp_bwd_mlp_wgrad" in kernels:  # engine in the message-passing launch
+        step = [k for k in step if k not in ("gine_mp_bwd", "gine_mlp_bwd1_wgrad")]
+        step += ["gine_mlp_bwd1", "gine_mp_bwd_mlp_wgrad"]
     timed = [k for k in step if k in kernels]
     dominant = max(timed, key=lambda k: kernels[k]["us"])
     rec = kernels[dominant]
-    return _roof(dominant, rec, "mfma" if "alg_flops" in rec else "hbm", layers)
+    roof = _roof(dominant, rec, "mfma" if "alg_flops" in rec else "hbm", layers)
+    if dominant == "gine_mp_bwd_mlp_wgrad":
+        roof["note"] = ("one launch = node-MLP weight-gradient engine (work_per_launch flops, "
+                        "fp32 MFMA) + the message-passing backward (alg_bytes of "
+                        "kernels.gine_mp_bwd_mlp_wgrad); achieved counts the engine flops only")
+    return roof
 
 
 def roofline_mp(kernels: dict, layers: int):
@@ -340,6 +358,8 @@ def copy_ceiling_gbps(device, nbytes=1 << 30, reps=10):
 PMC_KERNELS = {
     "gine_mp_fwd": ["gine::k_mp_fwd<32, 1, "],
     "gine_mp_fwd_mlp1": ["gine::k_mp_fwd_mlp1<"],
+    # (the GPU box's host rounds the edge Linear mul-then-add: FMA = false)
+    "gine_mp_bwd_mlp_wgrad": ["gine::k_mp_bwd_win<32, false, true, 5>"],
     "gine_mp_bwd": ["gine::k_mp_bwd_win<32, "],
     "gine_mlp_fwd1": ["gine::k_rowgemm<128, 0, 0, true>"],
     "gine_mlp_fwd2": ["gine::k_rowgemm<128, 1, 5, true>"],
