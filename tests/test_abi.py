@@ -84,3 +84,24 @@ def test_grad_batch_validation_without_device():
     assert job.nz == 4 and job.wsize[0] == 128 * 163 and job.bscale[3] == 11.0
     assert lib.gine_deepset_bwd_grad_job(16000, 35, 128, p, p, p, ctypes.byref(job)) == 0
     assert job.wsize[0] == 128 * 35 and job.per[0] == 128 * 36
+
+
+def test_fused_entry_points_validate_without_device():
+    """gine_mp_fwd_mlp1 and gine_mp_bwd_win_mlp_wgrad reject bad arguments before any HIP
+    call (channels, degree limit, flags, NULL operands, missing plan)."""
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.addressof(buf)
+    f = lib.gine_mp_fwd_mlp1
+    assert f(*([p] * 12), 100, 64, 5, 0, None) == 2                       # D != 128
+    assert f(*([p] * 12), 100, 128, _lib.MP_FUSED_MAX_DEGREE + 1, 0, None) == 1
+    assert f(*([p] * 12), 100, 128, 5, 8, None) == 1                       # bad flag
+    assert f(*([p] * 3), None, *([p] * 8), 100, 128, 5, 0, None) == 1      # no edge attrs
+    assert f(*([p] * 12), 0, 128, 5, 0, None) == 1                         # no nodes
+    g = lib.gine_mp_bwd_win_mlp_wgrad
+    plan = _lib.WindowPlan()
+    args = [p] * 11 + [100, 128, 1, ctypes.byref(plan)] + [p] * 9
+    assert g(*args, 2, None) == 1                                          # empty plan
+    assert g(*([p] * 11 + [100, 128, 1, ctypes.byref(plan)] + [None] + [p] * 8), 2, None) == 1
+    assert g(*args, 7, None) == 1                                          # bad epilogue
+    assert g(*([p] * 11 + [100, 64, 1, ctypes.byref(plan)] + [p] * 9), 2, None) == 2
