@@ -256,3 +256,32 @@ def test_mlp_weight_grads_in_message_passing_launch(monkeypatch):
         if n.endswith("nn.0.weight") or n.endswith("nn.3.weight"):
             assert torch.equal(got, gref), n
         assert rel_err(got, gref) <= 1e-6, n
+
+
+@pytest.mark.parametrize("graphs,stations,k", [(1, 64, 4), (3, 500, 10), (2, 37, 36)])
+def test_mlp_weight_grads_in_mp_launch_small_graphs(graphs, stations, k, monkeypatch):
+    """The combined launch at sizes where the engine has few row chunks and the window plan
+    is forced (GINE_MP_WINDOW=all): same gradients as the engine beside the dz GEMM."""
+    from raincast_gnn import functional as Fn
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.models import GNN
+    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    torch.manual_seed(graphs + stations)
+    base = GNN(35, 128, 128, 2, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5)
+    batch = synthetic_batch(stations, graphs, k=k, seed=6).to(DEV)
+    grads = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GINE_MLP_WGRAD_IN_MP", flag)
+        m = copy.deepcopy(base).to(DEV)
+        opt = FlatAdamW(m.parameters(), lr=1e-3)
+        opt.zero_grad()
+        m.loss_fn.crps(m(batch), batch.y).backward()
+        grads[flag] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    from raincast_gnn.graph import get_graph
+    g = get_graph(batch.edge_index, batch.edge_attr.float(), batch.num_nodes)
+    assert Fn.engine_in_mp_ok(g, 128)   # the combined launch really ran
+    for n, gref in grads["0"].items():
+        got = grads["1"][n]
+        if n.endswith("nn.0.weight") or n.endswith("nn.3.weight"):
+            assert torch.equal(got, gref), n
+        assert rel_err(got, gref) <= 1e-6, n
