@@ -243,8 +243,12 @@ def time_kernels(tr: Trainer, reps: int):
              ptr(dbn), ptr(coef), ptr(z), ptr(slab), 2, S[0])
 
     if Fn.engine_in_mp_ok(g, D):  # what the training step's backward runs at this size
+        # bytes: the message-passing backward's B_b (dz, x, dx, CSR, dres = dy) + the
+        # engine's other operands read once (mask u8, dbn, a1, z) + its fp32 slab
         kernels["gine_mp_bwd_mlp_wgrad"] = (mp_bwd_mlp_wgrad, {
-            "flops": 4 * N * D * D, "bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D})
+            "flops": 4 * N * D * D,
+            "bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D + 13 * N * D
+                     + 4 * slab.numel()})
     out = {}
     for name, (fn, work) in kernels.items():
         for _ in range(3):
@@ -322,11 +326,14 @@ def roofline_for(kernels: dict, layers: int):
     timed = [k for k in step if k in kernels]
     dominant = max(timed, key=lambda k: kernels[k]["us"])
     rec = kernels[dominant]
-    roof = _roof(dominant, rec, "mfma" if "alg_flops" in rec else "hbm", layers)
+    # the binding resource at the ideal: the larger of flops / MFMA peak and bytes / HBM peak
+    t_mfma = rec.get("alg_flops", 0) / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+    t_hbm = rec.get("alg_bytes", 0) / (HBM_PEAK_GBS * 1e9)
+    roof = _roof(dominant, rec, "mfma" if t_mfma >= t_hbm else "hbm", layers)
     if dominant == "gine_mp_bwd_mlp_wgrad":
-        roof["note"] = ("one launch = node-MLP weight-gradient engine (work_per_launch flops, "
-                        "fp32 MFMA) + the message-passing backward (alg_bytes of "
-                        "kernels.gine_mp_bwd_mlp_wgrad); achieved counts the engine flops only")
+        roof["note"] = ("one launch = the message-passing backward + the node-MLP weight-"
+                        "gradient engine (alg_flops of kernels.gine_mp_bwd_mlp_wgrad on fp32 "
+                        "MFMA); work_per_launch = all algorithmic bytes of the launch")
     return roof
 
 
