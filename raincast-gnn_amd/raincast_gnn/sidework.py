@@ -60,14 +60,12 @@ def wait_all() -> None:
         main.wait_stream(side)
 
 
-def launch(device: torch.device, fn, keep_alive=(), params=(), force=False) -> None:
+def launch(device: torch.device, fn, keep_alive=(), params=()) -> None:
     """``fn(stream_handle)`` on the side stream of ``device``, ordered after the current
     stream's queued work and joined back into it at the end of the backward pass (inline
-    on the current stream when a parameter in ``params`` already has a gradient).
-    ``force`` uses the side stream even when RAINCAST_SIDE_STREAMS is off."""
+    on the current stream when a parameter in ``params`` already has a gradient)."""
     main = torch.cuda.current_stream(device)
-    if (not ENABLED and not force) or any(p is not None and p.grad is not None
-                                          for p in params):
+    if not ENABLED or any(p is not None and p.grad is not None for p in params):
         fn(main.cuda_stream)
         return
     side = side_stream(device)
