@@ -279,6 +279,35 @@ int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in
                      double* partials, int64_t num_nodes, int32_t channels,
                      int32_t max_in_degree, int32_t flags, void* stream);
 
+/* BatchNorm statistics without a finish launch (training, momentum >= 0; csrc/gine_bnacc.hpp).
+ * bn_acc: int64[gine_bn_acc_words(D) = 40D + 1], zeroed once by the caller at allocation,
+ * then owned by the kernels (the sums only grow; each consumer differences them against a
+ * snapshot the previous consumer left), so one buffer serves every step of one BatchNorm,
+ * HIP-graph replays included.  Every producer launch must be followed by exactly one
+ * gine_mlp_fwd2_bn on the same buffer; not shared by layers whose launches interleave.
+ *   gine_mlp_fwd1_acc / gine_mp_fwd_mlp1_acc: as gine_mlp_fwd1 / gine_mp_fwd_mlp1, and the
+ *     per-workgroup sums are also added into bn_acc as 2-word fixed point with integer
+ *     atomics (order-independent: same bits every run).  partials may be NULL.
+ *   gine_mlp_fwd2_bn: gine_bn_fwd_finalize (from bn_acc) + gine_mlp_fwd2 in one launch;
+ *     writes bn_save, the running statistics and num_batches_tracked as the finalize does.
+ * The statistics agree with the partials path to ~1e-15 relative (sums are rounded to
+ * 2^-48 per workgroup), so bn_save can differ from it in the last fp32 bit. */
+int gine_bn_acc_words(int32_t channels, int64_t* words);
+int gine_mlp_fwd1_acc(const float* z, const float* w1, const float* b1, float* a1,
+                      double* partials, int64_t* bn_acc, int64_t num_nodes, int32_t channels,
+                      void* stream);
+int gine_mp_fwd_mlp1_acc(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                         const float* in_attr, const float* lin_w, const float* lin_b,
+                         const float* eps, const float* w1, const float* b1, float* z,
+                         float* a1, double* partials, int64_t* bn_acc, int64_t num_nodes,
+                         int32_t channels, int32_t max_in_degree, int32_t flags, void* stream);
+int gine_mlp_fwd2_bn(const float* a1, int64_t* bn_acc, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                     float* bn_save, float momentum, float bn_eps, int32_t update_running,
+                     const float* w2, const float* b2, const float* x, float* y,
+                     uint8_t* mask, int64_t num_nodes, int32_t channels, int32_t epilogue,
+                     void* stream);
+
 int gine_mlp_bwd2(const float* dy, const float* y, const uint8_t* mask, const float* a1,
                   const float* bn_save, const float* w2, float* dbn, double* partials,
                   int64_t num_nodes, int32_t channels, int32_t epilogue, void* stream);

@@ -25,8 +25,10 @@
 #include "gine_slab.hpp"
 #include "gine_wgrad.hpp"
 #include "gine_mlpsrc.hpp"
+#include "gine_bnacc.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace gine {
@@ -87,8 +89,9 @@ struct EpiArgs {
   const float* resid;  // OUT, residual epilogue: the layer input x
   const float* a1;     // DBN
   const float* bn;     // DBN
-  double* partials;    // A1STATS / DBN: [grid][2][D]
+  double* partials;    // A1STATS / DBN: [grid][2][D]  (A1STATS: may be NULL with bnacc)
   int mode;            // OUT: GINE_EPI_*
+  long long* bnacc = nullptr;  // A1STATS: fixed-point accumulator (gine_bnacc.hpp)
 };
 
 // Tiles of one XCD form a contiguous range; its blocks stride that range.
@@ -119,10 +122,17 @@ __device__ __forceinline__ TileRange xcd_tile_range(int num_tiles, int vb, int n
 // ----------------------------------------------------------------------------------------
 // One persistent workgroup (virtual index vb of vgrid) of the row-tile GEMM; s_x: LDS of
 // kRowTile * (D + 4) floats.
-template <int D, int PRO, int EPI, bool BT, bool WL = false>
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+// hook: runs once per workgroup after the weight staging and before the prologue constants
+// are read (k_fwd2_bnacc: the BatchNorm finish, overlapping the first tile's loads).
+template <int D, int PRO, int EPI, bool BT, bool WL = false, class Hook = NoHook>
 __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const ProArgs& pa,
                                              const EpiArgs& ea, int64_t N, int num_tiles,
-                                             float* __restrict__ s_x, int vb, int vgrid) {
+                                             float* __restrict__ s_x, int vb, int vgrid,
+                                             const Hook& hook = Hook{}) {
   constexpr int NT = 2 * D;      // threads: D/32 waves
   constexpr int KS = D / 2;      // k-steps per lane half
   constexpr int LD = D + 4;      // padded LDS row (floats)
@@ -165,7 +175,11 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
 #pragma unroll
     for (int s = 0; s < KS; ++s) bf[s] = W[(size_t)(h * KS + s) * D + col];
   }
-  const ColConst kc = col_const<PRO>(pa, D, q_me);
+  // With a hook the prologue constants come after the weight staging: the hook's barriers
+  // and stores in the middle of the live weight registers put them in scratch.
+  constexpr bool kHook = !std::is_same<Hook, NoHook>::value;
+  ColConst kc;
+  if constexpr (!kHook) kc = col_const<PRO>(pa, D, q_me);
 
   // Epilogue in the row-major domain: after the MFMA chain the accumulator tile goes
   // through LDS (s_x, free by then), and each thread finishes the float4 column group q_me
@@ -213,6 +227,10 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
       bf[4 * q + 3] = v.w;
     }
     // the first tile's __syncthreads() below orders these reads before the staging writes
+  }
+  if constexpr (kHook) {
+    hook();
+    kc = col_const<PRO>(pa, D, q_me);
   }
   for (int tile = tr.first; tile < tr.end; tile += tr.step) {
     const int64_t n0 = (int64_t)tile * kRowTile;
@@ -335,7 +353,9 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
       double t = 0.0;
 #pragma unroll
       for (int g = 0; g < RSTEP; ++g) t += sr[(which * RSTEP + g) * D + cc];
-      ea.partials[(size_t)vb * 2 * D + c] = t;
+      if (EPI == EPI_DBN || ea.partials) ea.partials[(size_t)vb * 2 * D + c] = t;
+      if constexpr (EPI == EPI_A1STATS)
+        if (ea.bnacc) bnacc_add(ea.bnacc, 2 * D, c, t);
     }
   }
   RG_MARK(5);
@@ -393,6 +413,66 @@ int launch_rowgemm(int D, const float* W, const ProArgs& pa, const EpiArgs& ea, 
     case 256:
       hipLaunchKernelGGL((k_rowgemm<256, PRO, EPI, BT>), dim3(grid), dim3(512), 0, s, W, pa,
                          ea, N, tiles);
+      break;
+    default:
+      return GINE_ERR_DIM;
+  }
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+// Second GEMM with the BatchNorm finish in its prologue (training, momentum given): every
+// workgroup turns the fixed-point totals of gine_bnacc.hpp into alpha / shift in LDS
+// (workgroup 0 also writes bn_save, the running statistics and num_batches_tracked -- the
+// arithmetic of BnFwdFin), the last one to have read them re-zeroes the accumulator, then
+// the row-tile GEMM runs with its prologue constants read from LDS.
+template <int D, int EPI>
+__global__ __launch_bounds__(2 * D) void k_fwd2_bnacc(const float* __restrict__ W, ProArgs pa,
+                                                      EpiArgs ea, BnFwdParams q,
+                                                      long long* acc, int64_t N,
+                                                      int num_tiles) {
+  constexpr bool WL = D <= 128;
+  __shared__ __attribute__((aligned(16))) float s_x[(WL ? D : kRowTile) * (D + 4)];
+  __shared__ __attribute__((aligned(16))) float s_bn[4 * D];
+  __shared__ double s_tot[2 * D];
+  auto finish = [=]() {  // by value: a reference to a kernel argument puts it in scratch
+    const int t = threadIdx.x;  // 2D threads: word t = (sum | sum of squares) of column t % D
+    s_tot[t] = bnacc_total(acc, 2 * D, t, blockIdx.x == 0);
+    __syncthreads();
+    if (t < D)
+      bn_finish_channel(q, D, t, s_tot[t], s_tot[D + t], blockIdx.x == 0, &s_bn[2 * D + t],
+                        &s_bn[3 * D + t]);
+    if (blockIdx.x == 0 && t == 0 && q.update_running && q.nbt != nullptr)
+      q.nbt[0] = q.nbt[0] + 1;
+    __syncthreads();
+  };
+  ProArgs p2 = pa;
+  p2.bn = s_bn;
+  rowgemm_body<D, PRO_BNRELU, EPI, true, WL>(W, p2, ea, N, num_tiles, s_x, blockIdx.x,
+                                             gridDim.x, finish);
+}
+
+template <int EPI>
+int launch_fwd2_bnacc(int D, const float* W, const ProArgs& pa, const EpiArgs& ea,
+                      const BnFwdParams& q, long long* acc, int64_t N, hipStream_t s) {
+  const int grid = rowgemm_grid(N, D);
+  const int tiles = (int)ceil_div(N, kRowTile);
+  switch (D) {
+    case 32:
+      hipLaunchKernelGGL((k_fwd2_bnacc<32, EPI>), dim3(grid), dim3(64), 0, s, W, pa, ea, q, acc,
+                         N, tiles);
+      break;
+    case 64:
+      hipLaunchKernelGGL((k_fwd2_bnacc<64, EPI>), dim3(grid), dim3(128), 0, s, W, pa, ea, q,
+                         acc, N, tiles);
+      break;
+    case 128:
+      hipLaunchKernelGGL((k_fwd2_bnacc<128, EPI>), dim3(grid), dim3(256), 0, s, W, pa, ea, q,
+                         acc, N, tiles);
+      break;
+    case 256:
+      hipLaunchKernelGGL((k_fwd2_bnacc<256, EPI>), dim3(grid), dim3(512), 0, s, W, pa, ea, q,
+                         acc, N, tiles);
       break;
     default:
       return GINE_ERR_DIM;
@@ -578,6 +658,55 @@ extern "C" int gine_mlp_fwd1(const float* z, const float* w1, const float* b1, f
   EpiArgs ea{b1, a1, nullptr, nullptr, nullptr, nullptr, partials, 0};
   return launch_rowgemm<PRO_PLAIN, EPI_A1STATS, true>(channels, w1, pa, ea, num_nodes,
                                                       as_stream(stream));
+}
+
+extern "C" int gine_bn_acc_words(int32_t channels, int64_t* words) {
+  if (!words || channels <= 0) return GINE_ERR_INVALID;
+  *words = (int64_t)kBnAccReplicas * 4 * channels + 8 * (int64_t)channels + 1;
+  return GINE_OK;
+}
+
+extern "C" int gine_mlp_fwd1_acc(const float* z, const float* w1, const float* b1, float* a1,
+                                 double* partials, int64_t* bn_acc, int64_t num_nodes,
+                                 int32_t channels, void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !z || !w1 || !b1 || !a1 || !bn_acc) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  ProArgs pa{z, nullptr, nullptr, nullptr, nullptr};
+  EpiArgs ea{b1, a1, nullptr, nullptr, nullptr, nullptr, partials, 0,
+             reinterpret_cast<long long*>(bn_acc)};
+  return launch_rowgemm<PRO_PLAIN, EPI_A1STATS, true>(channels, w1, pa, ea, num_nodes,
+                                                      as_stream(stream));
+}
+
+extern "C" int gine_mlp_fwd2_bn(const float* a1, int64_t* bn_acc, const float* gamma,
+                                const float* beta, float* running_mean, float* running_var,
+                                int64_t* num_batches_tracked, float* bn_save, float momentum,
+                                float bn_eps, int32_t update_running, const float* w2,
+                                const float* b2, const float* x, float* y, uint8_t* mask,
+                                int64_t num_nodes, int32_t channels, int32_t epilogue,
+                                void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !a1 || !bn_acc || !bn_save || !w2 || !b2 || !y) return GINE_ERR_INVALID;
+  if (!(momentum >= 0.f)) return GINE_ERR_INVALID;  // momentum=None: gine_bn_fwd_finalize
+  if (update_running && (!running_mean || !running_var)) return GINE_ERR_INVALID;
+  if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && (!x || !mask)) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  ProArgs pa{a1, nullptr, nullptr, nullptr, nullptr};
+  EpiArgs ea{b2, y, mask, x, nullptr, nullptr, nullptr, epilogue};
+  const BnFwdParams q{gamma,   beta,      running_mean, running_var,   num_batches_tracked,
+                      bn_save, num_nodes, momentum,     bn_eps,        update_running};
+  long long* acc = reinterpret_cast<long long*>(bn_acc);
+  hipStream_t s = as_stream(stream);
+  switch (epilogue) {
+    case GINE_EPI_NONE:
+      return launch_fwd2_bnacc<EPI_OUT>(channels, w2, pa, ea, q, acc, num_nodes, s);
+    case GINE_EPI_RELU:
+      return launch_fwd2_bnacc<EPI_OUT_RELU>(channels, w2, pa, ea, q, acc, num_nodes, s);
+    default:
+      return launch_fwd2_bnacc<EPI_OUT_RES>(channels, w2, pa, ea, q, acc, num_nodes, s);
+  }
 }
 
 extern "C" int gine_bn_fwd_finalize(const double* partials, int32_t num_partials,

@@ -26,6 +26,7 @@
 // (xcd_tile_range, grid = gine_mlp_num_partials).  Every in-degree must be at most
 // GINE_MP_FUSED_MAX_DEGREE (one 32-slot edge list per row; the host checks).
 #include "gine_common.hpp"
+#include "gine_bnacc.hpp"
 #include "gine_edge.hpp"
 
 namespace gine {
@@ -107,7 +108,8 @@ struct FusedArgs {
   const float* b1;
   float* z;
   float* a1;
-  double* partials;
+  double* partials;      // NULL: bnacc only
+  long long* bnacc;      // NULL: partials only (gine_bnacc.hpp)
   int N, num_tiles;
 };
 
@@ -209,7 +211,8 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
   double s = 0.0;
 #pragma unroll
   for (int g = 0; g < 8; ++g) s += sr[(which * 8 + g) * kD + cc];
-  A.partials[(size_t)blockIdx.x * 2 * kD + which * kD + cc] = s;
+  if (A.partials) A.partials[(size_t)blockIdx.x * 2 * kD + which * kD + cc] = s;
+  if (A.bnacc) bnacc_add(A.bnacc, 2 * kD, which * kD + cc, s);
 }
 
 // Gather role (waves 4-11).  Barriers: 1 + (nt + 1), as the matrix role.
@@ -330,17 +333,17 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_mlp1(FusedArgs A) {
 
 using namespace gine;
 
-extern "C" int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
-                                const float* in_attr, const float* lin_w, const float* lin_b,
-                                const float* eps, const float* w1, const float* b1, float* z,
-                                float* a1, double* partials, int64_t num_nodes,
-                                int32_t channels, int32_t max_in_degree, int32_t flags,
-                                void* stream) {
+namespace {
+int mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                const float* in_attr, const float* lin_w, const float* lin_b, const float* eps,
+                const float* w1, const float* b1, float* z, float* a1, double* partials,
+                int64_t* bn_acc, int64_t num_nodes, int32_t channels, int32_t max_in_degree,
+                int32_t flags, void* stream) {
   if (channels != kD) return GINE_ERR_DIM;
   if ((flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
   if (max_in_degree < 0 || max_in_degree > GINE_MP_FUSED_MAX_DEGREE) return GINE_ERR_INVALID;
   if (num_nodes <= 0 || !x || !in_rowptr || !in_src || !in_attr || !lin_w || !lin_b || !eps ||
-      !w1 || !b1 || !z || !a1 || !partials)
+      !w1 || !b1 || !z || !a1 || (!partials && !bn_acc))
     return GINE_ERR_INVALID;
   if (num_nodes * channels * 4 >= (int64_t(1) << 32)) return GINE_ERR_TOO_LARGE;
   int32_t grid = 0;
@@ -348,12 +351,37 @@ extern "C" int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const 
   if (st != GINE_OK) return st;
   const int tiles = (int)ceil_div(num_nodes, kTileRows);
   hipStream_t s = as_stream(stream);
-  const FusedArgs A{x,  in_rowptr, in_src, in_attr, lin_w,    lin_b,          eps,
-                    w1, b1,        z,      a1,      partials, (int)num_nodes, tiles};
+  const FusedArgs A{x,  in_rowptr, in_src, in_attr,  lin_w, lin_b,
+                    eps, w1,       b1,     z,        a1,    partials,
+                    reinterpret_cast<long long*>(bn_acc), (int)num_nodes, tiles};
   if (flags & GINE_MP_LIN_MULADD)
     hipLaunchKernelGGL(k_mp_fwd_mlp1<false>, dim3((unsigned)grid), dim3(kThreads), 0, s, A);
   else
     hipLaunchKernelGGL(k_mp_fwd_mlp1<true>, dim3((unsigned)grid), dim3(kThreads), 0, s, A);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
+}
+}  // namespace
+
+extern "C" int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                                const float* in_attr, const float* lin_w, const float* lin_b,
+                                const float* eps, const float* w1, const float* b1, float* z,
+                                float* a1, double* partials, int64_t num_nodes,
+                                int32_t channels, int32_t max_in_degree, int32_t flags,
+                                void* stream) {
+  if (!partials) return GINE_ERR_INVALID;
+  return mp_fwd_mlp1(x, in_rowptr, in_src, in_attr, lin_w, lin_b, eps, w1, b1, z, a1, partials,
+                     nullptr, num_nodes, channels, max_in_degree, flags, stream);
+}
+
+extern "C" int gine_mp_fwd_mlp1_acc(const float* x, const int32_t* in_rowptr,
+                                    const int32_t* in_src, const float* in_attr,
+                                    const float* lin_w, const float* lin_b, const float* eps,
+                                    const float* w1, const float* b1, float* z, float* a1,
+                                    double* partials, int64_t* bn_acc, int64_t num_nodes,
+                                    int32_t channels, int32_t max_in_degree, int32_t flags,
+                                    void* stream) {
+  if (!bn_acc) return GINE_ERR_INVALID;
+  return mp_fwd_mlp1(x, in_rowptr, in_src, in_attr, lin_w, lin_b, eps, w1, b1, z, a1, partials,
+                     bn_acc, num_nodes, channels, max_in_degree, flags, stream);
 }

@@ -83,6 +83,11 @@ _SIGNATURES = {
     "gine_mlp_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_fwd1": [_c_void_p] * 5 + [_i64, _i32, _c_void_p],
     "gine_mp_fwd_mlp1": [_c_void_p] * 12 + [_i64, _i32, _i32, _i32, _c_void_p],
+    "gine_mp_fwd_mlp1_acc": [_c_void_p] * 13 + [_i64, _i32, _i32, _i32, _c_void_p],
+    "gine_mlp_fwd1_acc": [_c_void_p] * 6 + [_i64, _i32, _c_void_p],
+    "gine_mlp_fwd2_bn": [_c_void_p] * 8 + [_f32, _f32, _i32] + [_c_void_p] * 5
+                        + [_i64, _i32, _i32, _c_void_p],
+    "gine_bn_acc_words": [_i32, _c_void_p],
     "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,
                                                                    _i32, _c_void_p],
     "gine_mlp_fwd2": [_c_void_p] * 7 + [_i64, _i32, _i32, _c_void_p],

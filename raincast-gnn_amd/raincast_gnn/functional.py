@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 import warnings
 
 import torch
@@ -71,6 +72,12 @@ def edge_linear_flag() -> int:
 def _count(fn: str, n: int, d: int) -> int:
     out = ctypes.c_int32(0)
     call(fn, n, d, ctypes.byref(out))
+    return int(out.value)
+
+
+def _count64(fn: str, d: int) -> int:
+    out = ctypes.c_int64(0)
+    call(fn, d, ctypes.byref(out))
     return int(out.value)
 
 
@@ -184,9 +191,10 @@ class BnConfig:
     """What GineLayer needs from a BatchNorm1d module (torch semantics)."""
 
     __slots__ = ("running_mean", "running_var", "num_batches_tracked", "momentum", "eps",
-                 "use_batch_stats", "update_running")
+                 "use_batch_stats", "update_running", "module")
 
     def __init__(self, bn: torch.nn.BatchNorm1d):
+        self.module = bn
         self.running_mean = bn.running_mean
         self.running_var = bn.running_var
         self.num_batches_tracked = bn.num_batches_tracked
@@ -223,6 +231,25 @@ def engine_in_mp_ok(graph, D: int) -> bool:
     return plan is not None and plan.slice_channels == 32
 
 
+_BN_ACC = weakref.WeakKeyDictionary()
+
+
+def bn_accumulator(bn: "BnConfig", D: int, dev) -> "torch.Tensor | None":
+    """The int64 fixed-point accumulator of gine_mlp_fwd2_bn for this BatchNorm (one per
+    module and device, zeroed at allocation, then owned by the kernels), or None when the
+    finish launch is needed: eval mode, momentum=None, or GINE_BN_ACC=0."""
+    if (not bn.use_batch_stats or bn.momentum < 0 or bn.module is None
+            or os.environ.get("GINE_BN_ACC", "1") == "0"):
+        return None
+    per_dev = _BN_ACC.setdefault(bn.module, {})
+    acc = per_dev.get(dev)
+    words = _count64("gine_bn_acc_words", D)
+    if acc is None or acc.numel() != words:
+        acc = torch.zeros(words, dtype=torch.int64, device=dev)
+        per_dev[dev] = acc
+    return acc
+
+
 class GineLayer(torch.autograd.Function):
     """y = epilogue( Linear2( ReLU( BN( Linear1( z ) ) ) ) ),  z = GINE message passing.
 
@@ -245,28 +272,47 @@ class GineLayer(torch.autograd.Function):
                 f"{torch.Size([N, D])}")
 
         a1 = torch.empty_like(x)
-        P = _count("gine_mlp_num_partials", N, D)
-        partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
+        acc = bn_accumulator(bn, D, dev)
+        if acc is None:
+            P = _count("gine_mlp_num_partials", N, D)
+            partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
+        else:  # statistics summed by integer atomics, finished inside the second GEMM
+            partials = None
         if fused_forward_ok(graph, N, D):
             # gather of the next tile beside the matrix chain of this one: one launch
             z = torch.empty_like(x)
-            call("gine_mp_fwd_mlp1", ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src),
-                 ptr(graph.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(w1c), ptr(b1c), ptr(z),
-                 ptr(a1), ptr(partials), N, D, graph.max_in_degree, edge_linear_flag(), stream)
+            args = (ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
+                    ptr(lw), ptr(lb), ptr(ep), ptr(w1c), ptr(b1c), ptr(z), ptr(a1),
+                    ptr(partials))
+            tail = (N, D, graph.max_in_degree, edge_linear_flag(), stream)
+            if acc is None:
+                call("gine_mp_fwd_mlp1", *args, *tail)
+            else:
+                call("gine_mp_fwd_mlp1_acc", *args, ptr(acc), *tail)
         else:
             z = mp_forward(x, graph, lw, lb, ep)
-            call("gine_mlp_fwd1", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), ptr(partials), N, D,
-                 stream)
+            if acc is None:
+                call("gine_mlp_fwd1", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), ptr(partials), N,
+                     D, stream)
+            else:
+                call("gine_mlp_fwd1_acc", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), None,
+                     ptr(acc), N, D, stream)
         bn_save = torch.empty(4, D, dtype=torch.float32, device=dev)
-        call("gine_bn_fwd_finalize", ptr(partials), P, ptr(g), ptr(bt), ptr(bn.running_mean),
-             ptr(bn.running_var), ptr(bn.num_batches_tracked) if bn.update_running else None,
-             ptr(bn_save), N, D, bn.momentum, bn.eps, int(bn.use_batch_stats),
-             int(bn.update_running and bn.running_mean is not None), stream)
+        nbt = ptr(bn.num_batches_tracked) if bn.update_running else None
+        update_running = int(bn.update_running and bn.running_mean is not None)
         y = torch.empty_like(x)
         mask = (torch.empty(N, D, dtype=torch.uint8, device=dev)
                 if epilogue == EPI_RESIDUAL_RELU else None)
-        call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2c), ptr(b2c), ptr(x), ptr(y),
-             ptr(mask), N, D, epilogue, stream)
+        if acc is None:
+            call("gine_bn_fwd_finalize", ptr(partials), P, ptr(g), ptr(bt),
+                 ptr(bn.running_mean), ptr(bn.running_var), nbt, ptr(bn_save), N, D,
+                 bn.momentum, bn.eps, int(bn.use_batch_stats), update_running, stream)
+            call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2c), ptr(b2c), ptr(x), ptr(y),
+                 ptr(mask), N, D, epilogue, stream)
+        else:
+            call("gine_mlp_fwd2_bn", ptr(a1), ptr(acc), ptr(g), ptr(bt), ptr(bn.running_mean),
+                 ptr(bn.running_var), nbt, ptr(bn_save), bn.momentum, bn.eps, update_running,
+                 ptr(w2c), ptr(b2c), ptr(x), ptr(y), ptr(mask), N, D, epilogue, stream)
 
         ctx.save_for_backward(x, z, a1, y if epilogue == EPI_RELU else None, mask, bn_save,
                               lw, lb, ep, w1c, w2c, g)

@@ -1,0 +1,143 @@
+"""GPU: BatchNorm statistics summed by fixed-point integer atomics and finished inside the
+second node-MLP GEMM (gine_mlp_fwd1_acc / gine_mp_fwd_mlp1_acc + gine_mlp_fwd2_bn,
+csrc/gine_bnacc.hpp) against the finish-launch path (partials -> gine_bn_fwd_finalize ->
+gine_mlp_fwd2).  The layer uses it by default in training mode (GINE_BN_ACC=0 turns it
+off), so test_gpu_parity.py's test_gine_layer_fused also checks it against the oracle.
+
+Tolerance: the fixed-point sums round each workgroup's fp64 partial to 2^-48, so mean and
+variance agree with the fp64 partials path to ~1e-15 relative; alpha / shift may differ in
+their last fp32 bit, y by a few ulp (1e-5 relative bound written below).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import knn_batch_graph
+from raincast_gnn import GINEConv, _lib, functional as Fn
+from raincast_gnn.graph import GineGraph
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL = 1e-5
+
+
+def _conv(D, seed):
+    torch.manual_seed(seed)
+    mlp = torch.nn.Sequential(torch.nn.Linear(D, D), torch.nn.BatchNorm1d(D), torch.nn.ReLU(),
+                              torch.nn.Linear(D, D))
+    conv = GINEConv(nn=mlp, train_eps=True, edge_dim=1)
+    with torch.no_grad():
+        mlp[1].weight.uniform_(0.5, 1.5)
+        mlp[1].bias.uniform_(-0.2, 0.2)
+    return conv.to(DEV).train()
+
+
+def _run(conv, state, x, ei, ea, steps, epilogue):
+    conv.load_state_dict(state)
+    fn = {"none": conv.forward, "relu": conv.forward_relu,
+          "residual": conv.forward_residual_relu}[epilogue]
+    ys = [fn(x, ei, ea) for _ in range(steps)]
+    torch.cuda.synchronize()
+    bn = conv.nn[1]
+    return ys, bn.running_mean.clone(), bn.running_var.clone(), int(bn.num_batches_tracked)
+
+
+@pytest.mark.parametrize("D", [32, 64, 128, 256])
+@pytest.mark.parametrize("epilogue", ["none", "relu", "residual"])
+def test_bn_acc_matches_finish_launch(D, epilogue, monkeypatch):
+    ei, ea, n = knn_batch_graph(400, 8, 3, seed=D)
+    conv = _conv(D, seed=D)
+    state = {k: v.clone() for k, v in conv.state_dict().items()}
+    x = torch.randn(n, D, device=DEV) * 2 + 0.5
+    eid, ead = ei.to(DEV), ea.to(DEV)
+    monkeypatch.setenv("GINE_BN_ACC", "0")
+    ref = _run(conv, state, x, eid, ead, 3, epilogue)
+    monkeypatch.setenv("GINE_BN_ACC", "1")
+    got = _run(conv, state, x, eid, ead, 3, epilogue)
+    for a, b in zip(got[0], ref[0]):   # three steps: the accumulator is re-zeroed each time
+        assert ((a - b).abs() <= TOL * (1 + b.abs())).all()
+    torch.testing.assert_close(got[1], ref[1], rtol=TOL, atol=TOL)
+    torch.testing.assert_close(got[2], ref[2], rtol=TOL, atol=TOL)
+    assert got[3] == ref[3] == 3
+    acc = Fn._BN_ACC[conv.nn[1]][DEV]
+    assert acc.numel() == 40 * D + 1 and int(acc[-1]) == 3   # phase: one per producer launch
+
+
+def test_bn_acc_deterministic(monkeypatch):
+    monkeypatch.setenv("GINE_BN_ACC", "1")
+    ei, ea, n = knn_batch_graph(2000, 16, 4, seed=7)
+    conv = _conv(128, seed=3)
+    state = {k: v.clone() for k, v in conv.state_dict().items()}
+    x = torch.randn(n, 128, device=DEV)
+    eid, ead = ei.to(DEV), ea.to(DEV)
+    runs = [_run(conv, state, x, eid, ead, 2, "residual") for _ in range(3)]
+    for r in runs[1:]:
+        for a, b in zip(r[0], runs[0][0]):
+            assert torch.equal(a, b)
+        assert torch.equal(r[1], runs[0][1]) and torch.equal(r[2], runs[0][2])
+
+
+def test_bn_acc_eval_and_momentum_none_use_finish_launch(monkeypatch):
+    monkeypatch.setenv("GINE_BN_ACC", "1")
+    conv = _conv(64, seed=1)
+    bn = Fn.BnConfig(conv.nn[1])
+    assert Fn.bn_accumulator(bn, 64, DEV) is not None
+    conv.eval()
+    assert Fn.bn_accumulator(Fn.BnConfig(conv.nn[1]), 64, DEV) is None
+    conv.train()
+    conv.nn[1].momentum = None
+    assert Fn.bn_accumulator(Fn.BnConfig(conv.nn[1]), 64, DEV) is None
+
+
+@pytest.mark.parametrize("n,max_deg", [(33, 3), (2049, 7), (16000, 11)])
+def test_fused_forward_acc_equals_unfused(n, max_deg):
+    """gine_mp_fwd_mlp1_acc and gine_mlp_fwd1_acc add the same workgroup sums: the integer
+    accumulators agree word for word; z / a1 as the partials forms."""
+    rng = np.random.default_rng(n)
+    deg = rng.integers(0, max_deg + 1, n)
+    dst = np.repeat(np.arange(n), deg)
+    src = rng.integers(0, n, dst.size)
+    ei = torch.tensor(np.stack([src, dst]), dtype=torch.long, device=DEV)
+    ea = torch.from_numpy(rng.uniform(0.2, 5.0, (dst.size, 1)).astype(np.float32)).to(DEV)
+    g = GineGraph(ei, ea, n)
+    D = 128
+    x = torch.randn(n, D, device=DEV)
+    lw, lb = torch.randn(D, device=DEV), torch.randn(D, device=DEV)
+    eps = torch.tensor([0.1], device=DEV)
+    w1, b1 = torch.randn(D, D, device=DEV) / 11, torch.randn(D, device=DEV)
+    p, s = _lib.ptr, _lib.stream_handle(DEV)
+    acc1 = torch.zeros(40 * D + 1, dtype=torch.int64, device=DEV)
+    acc0 = torch.zeros_like(acc1)
+    z1, a11 = torch.empty_like(x), torch.empty_like(x)
+    _lib.call("gine_mp_fwd_mlp1_acc", p(x), p(g.in_rowptr), p(g.in_src), p(g.in_attr), p(lw),
+              p(lb), p(eps), p(w1), p(b1), p(z1), p(a11), None, p(acc1), n, D,
+              g.max_in_degree, 0, s)
+    z0 = Fn.mp_forward(x, g, lw, lb, eps, lin_flag=0)
+    a10 = torch.empty_like(x)
+    _lib.call("gine_mlp_fwd1_acc", p(z0), p(w1), p(b1), p(a10), None, p(acc0), n, D, s)
+    torch.cuda.synchronize()
+    assert torch.equal(z1, z0) and torch.equal(a11, a10)
+    assert torch.equal(acc1, acc0)
+    # the totals are the column sums of a1 and a1^2
+    a64 = a10.double()
+    rep = acc0[:8 * 4 * D].view(8, 2, 2 * D).sum(0)          # replicas: [hi | lo] x (sum | sumsq)
+    tot = (rep[0].double() / 2**16 + rep[1].double() / 2**48).view(2, D)
+    torch.testing.assert_close(tot[0], a64.sum(0), rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(tot[1], (a64 * a64).sum(0), rtol=1e-12, atol=1e-9)
+    assert int(acc0[8 * 4 * D:-1].abs().sum()) == 0 and int(acc0[-1]) == 1
+
+
+def test_bn_acc_entry_points_validate():
+    p, s = _lib.ptr, _lib.stream_handle(DEV)
+    a = torch.zeros(64, 64, device=DEV)
+    acc = torch.zeros(40 * 64 + 1, dtype=torch.int64, device=DEV)
+    save = torch.empty(4, 64, device=DEV)
+    w = torch.zeros(64, 64, device=DEV)
+    b = torch.zeros(64, device=DEV)
+    lib = _lib.load()
+    # momentum=None (negative) and a missing accumulator are refused
+    assert lib.gine_mlp_fwd2_bn(p(a), p(acc), None, None, None, None, None, p(save), -1.0,
+                                1e-5, 0, p(w), p(b), None, p(a), None, 64, 64, 0, s) != 0
+    assert lib.gine_mlp_fwd2_bn(p(a), None, None, None, None, None, None, p(save), 0.1,
+                                1e-5, 0, p(w), p(b), None, p(a), None, 64, 64, 0, s) != 0
+    assert lib.gine_mlp_fwd1_acc(p(a), p(w), p(b), p(a), None, None, 64, 64, s) != 0
