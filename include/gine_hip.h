@@ -293,6 +293,18 @@ int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in
  * The statistics agree with the partials path to ~1e-15 relative (sums are rounded to
  * 2^-48 per workgroup), so bn_save can differ from it in the last fp32 bit. */
 int gine_bn_acc_words(int32_t channels, int64_t* words);
+/* Backward, same scheme (a second accumulator per BatchNorm): gine_mlp_bwd2_acc = gine_mlp_bwd2
+ * with the [sum dbn | sum dbn*xhat] sums into bn_acc (partials may be NULL);
+ * gine_mlp_bwd1_bn = gine_bn_bwd_finalize (training) + gine_mlp_bwd1 in one launch (writes
+ * coef, dgamma, dbeta; dgamma / dbeta may be NULL). */
+int gine_mlp_bwd2_acc(const float* dy, const float* y, const uint8_t* mask, const float* a1,
+                      const float* bn_save, const float* w2, float* dbn, double* partials,
+                      int64_t* bn_acc, int64_t num_nodes, int32_t channels, int32_t epilogue,
+                      void* stream);
+int gine_mlp_bwd1_bn(const float* dbn, const float* a1, const float* bn_save, int64_t* bn_acc,
+                     const float* gamma, float* dgamma, float* dbeta, float* coef,
+                     const float* w1, float* dz, int64_t num_nodes, int32_t channels,
+                     void* stream);
 int gine_mlp_fwd1_acc(const float* z, const float* w1, const float* b1, float* a1,
                       double* partials, int64_t* bn_acc, int64_t num_nodes, int32_t channels,
                       void* stream);

@@ -91,7 +91,7 @@ struct EpiArgs {
   const float* bn;     // DBN
   double* partials;    // A1STATS / DBN: [grid][2][D]  (A1STATS: may be NULL with bnacc)
   int mode;            // OUT: GINE_EPI_*
-  long long* bnacc = nullptr;  // A1STATS: fixed-point accumulator (gine_bnacc.hpp)
+  long long* bnacc = nullptr;  // A1STATS / DBN: fixed-point accumulator (gine_bnacc.hpp)
 };
 
 // Tiles of one XCD form a contiguous range; its blocks stride that range.
@@ -353,9 +353,8 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
       double t = 0.0;
 #pragma unroll
       for (int g = 0; g < RSTEP; ++g) t += sr[(which * RSTEP + g) * D + cc];
-      if (EPI == EPI_DBN || ea.partials) ea.partials[(size_t)vb * 2 * D + c] = t;
-      if constexpr (EPI == EPI_A1STATS)
-        if (ea.bnacc) bnacc_add(ea.bnacc, 2 * D, c, t);
+      if (ea.partials) ea.partials[(size_t)vb * 2 * D + c] = t;
+      if (ea.bnacc) bnacc_add(ea.bnacc, 2 * D, c, t);
     }
   }
   RG_MARK(5);
@@ -450,6 +449,48 @@ __global__ __launch_bounds__(2 * D) void k_fwd2_bnacc(const float* __restrict__ 
   p2.bn = s_bn;
   rowgemm_body<D, PRO_BNRELU, EPI, true, WL>(W, p2, ea, N, num_tiles, s_x, blockIdx.x,
                                              gridDim.x, finish);
+}
+
+// dz = da1 W1 with the BatchNorm backward finish in its prologue (training): the totals
+// [sum dbn | sum dbn*xhat] of gine_bnacc.hpp -> coef = [c1 | c2 | c3] in LDS (workgroup 0
+// also writes coef, dgamma, dbeta -- the arithmetic of BnBwdFin).
+template <int D>
+__global__ __launch_bounds__(2 * D) void k_bwd1_bnacc(const float* __restrict__ W, ProArgs pa,
+                                                      EpiArgs ea, const float* gamma,
+                                                      float* dgamma, float* dbeta, float* coef,
+                                                      long long* acc, int64_t N,
+                                                      int num_tiles) {
+  __shared__ __attribute__((aligned(16))) float s_x[kRowTile * (D + 4)];
+  __shared__ __attribute__((aligned(16))) float s_coef[3 * D];
+  __shared__ double s_tot[2 * D];
+  const float* bn_save = pa.bn;
+  auto finish = [=]() {  // by value: a reference to a kernel argument puts it in scratch
+    const int t = threadIdx.x;
+    s_tot[t] = bnacc_total(acc, 2 * D, t, blockIdx.x == 0);
+    __syncthreads();
+    if (t < D) {
+      const double sd = s_tot[t], sx = s_tot[D + t];
+      const double g = gamma ? (double)gamma[t] : 1.0;
+      const double c1 = g * (double)bn_save[D + t];
+      const float k1 = (float)c1, k2 = (float)(-c1 * sx / (double)N),
+                  k3 = (float)(-c1 * sd / (double)N);
+      s_coef[t] = k1;
+      s_coef[D + t] = k2;
+      s_coef[2 * D + t] = k3;
+      if (blockIdx.x == 0) {
+        if (dgamma) dgamma[t] = (float)sx;
+        if (dbeta) dbeta[t] = (float)sd;
+        coef[t] = k1;
+        coef[D + t] = k2;
+        coef[2 * D + t] = k3;
+      }
+    }
+    __syncthreads();
+  };
+  ProArgs p2 = pa;
+  p2.coef = s_coef;
+  rowgemm_body<D, PRO_DA1, EPI_PLAIN, false, false>(W, p2, ea, N, num_tiles, s_x, blockIdx.x,
+                                                    gridDim.x, finish);
 }
 
 template <int EPI>
@@ -812,6 +853,67 @@ extern "C" int gine_mlp_bwd1(const float* dbn, const float* a1, const float* bn_
   EpiArgs ea{nullptr, dz, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   return launch_rowgemm<PRO_DA1, EPI_PLAIN, false>(channels, w1, pa, ea, num_nodes,
                                                    as_stream(stream));
+}
+
+extern "C" int gine_mlp_bwd2_acc(const float* dy, const float* y, const uint8_t* mask,
+                                 const float* a1, const float* bn_save, const float* w2,
+                                 float* dbn, double* partials, int64_t* bn_acc,
+                                 int64_t num_nodes, int32_t channels, int32_t epilogue,
+                                 void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !dy || !a1 || !bn_save || !w2 || !dbn || !bn_acc)
+    return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  ProArgs pa{dy, y, mask, nullptr, nullptr};
+  EpiArgs ea{nullptr, dbn, nullptr, nullptr, a1, bn_save, partials, 0,
+             reinterpret_cast<long long*>(bn_acc)};
+  hipStream_t s = as_stream(stream);
+  switch (epilogue) {
+    case GINE_EPI_NONE:
+      return launch_rowgemm<PRO_PLAIN, EPI_DBN, false>(channels, w2, pa, ea, num_nodes, s);
+    case GINE_EPI_RELU:
+      return launch_rowgemm<PRO_DOR, EPI_DBN, false>(channels, w2, pa, ea, num_nodes, s);
+    default:
+      return launch_rowgemm<PRO_DOM, EPI_DBN, false>(channels, w2, pa, ea, num_nodes, s);
+  }
+}
+
+extern "C" int gine_mlp_bwd1_bn(const float* dbn, const float* a1, const float* bn_save,
+                                int64_t* bn_acc, const float* gamma, float* dgamma,
+                                float* dbeta, float* coef, const float* w1, float* dz,
+                                int64_t num_nodes, int32_t channels, void* stream) {
+  if (!mlp_dim_ok(channels)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !dbn || !a1 || !bn_save || !bn_acc || !coef || !w1 || !dz)
+    return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  ProArgs pa{dbn, a1, nullptr, bn_save, nullptr};
+  EpiArgs ea{nullptr, dz, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  long long* acc = reinterpret_cast<long long*>(bn_acc);
+  const int grid = rowgemm_grid(num_nodes, channels);
+  const int tiles = (int)ceil_div(num_nodes, kRowTile);
+  hipStream_t s = as_stream(stream);
+  switch (channels) {
+    case 32:
+      hipLaunchKernelGGL(k_bwd1_bnacc<32>, dim3(grid), dim3(64), 0, s, w1, pa, ea, gamma,
+                         dgamma, dbeta, coef, acc, num_nodes, tiles);
+      break;
+    case 64:
+      hipLaunchKernelGGL(k_bwd1_bnacc<64>, dim3(grid), dim3(128), 0, s, w1, pa, ea, gamma,
+                         dgamma, dbeta, coef, acc, num_nodes, tiles);
+      break;
+    case 128:
+      hipLaunchKernelGGL(k_bwd1_bnacc<128>, dim3(grid), dim3(256), 0, s, w1, pa, ea, gamma,
+                         dgamma, dbeta, coef, acc, num_nodes, tiles);
+      break;
+    default:
+      hipLaunchKernelGGL(k_bwd1_bnacc<256>, dim3(grid), dim3(512), 0, s, w1, pa, ea, gamma,
+                         dgamma, dbeta, coef, acc, num_nodes, tiles);
+      break;
+  }
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
 }
 
 extern "C" int gine_mlp_wgrad_num_chunks(int64_t num_nodes, int32_t channels,

@@ -88,6 +88,8 @@ _SIGNATURES = {
     "gine_mlp_fwd2_bn": [_c_void_p] * 8 + [_f32, _f32, _i32] + [_c_void_p] * 5
                         + [_i64, _i32, _i32, _c_void_p],
     "gine_bn_acc_words": [_i32, _c_void_p],
+    "gine_mlp_bwd2_acc": [_c_void_p] * 9 + [_i64, _i32, _i32, _c_void_p],
+    "gine_mlp_bwd1_bn": [_c_void_p] * 10 + [_i64, _i32, _c_void_p],
     "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,
                                                                    _i32, _c_void_p],
     "gine_mlp_fwd2": [_c_void_p] * 7 + [_i64, _i32, _i32, _c_void_p],

@@ -234,7 +234,7 @@ def engine_in_mp_ok(graph, D: int) -> bool:
 _BN_ACC = weakref.WeakKeyDictionary()
 
 
-def bn_accumulator(bn: "BnConfig", D: int, dev) -> "torch.Tensor | None":
+def bn_accumulator(bn: "BnConfig", D: int, dev, kind: str = "fwd") -> "torch.Tensor | None":
     """The int64 fixed-point accumulator of gine_mlp_fwd2_bn for this BatchNorm (one per
     module and device, zeroed at allocation, then owned by the kernels), or None when the
     finish launch is needed: eval mode, momentum=None, or GINE_BN_ACC=0."""
@@ -242,11 +242,11 @@ def bn_accumulator(bn: "BnConfig", D: int, dev) -> "torch.Tensor | None":
             or os.environ.get("GINE_BN_ACC", "1") == "0"):
         return None
     per_dev = _BN_ACC.setdefault(bn.module, {})
-    acc = per_dev.get(dev)
+    acc = per_dev.get((dev, kind))
     words = _count64("gine_bn_acc_words", D)
     if acc is None or acc.numel() != words:
         acc = torch.zeros(words, dtype=torch.int64, device=dev)
-        per_dev[dev] = acc
+        per_dev[(dev, kind)] = acc
     return acc
 
 
@@ -318,6 +318,7 @@ class GineLayer(torch.autograd.Function):
                               lw, lb, ep, w1c, w2c, g)
         ctx.graph, ctx.epilogue = graph, epilogue
         ctx.use_batch_stats = bn.use_batch_stats
+        ctx.bn_acc_bwd = bn_accumulator(bn, D, dev, "bwd")  # allocated outside backward
         ctx.params = (lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2)
         ctx.shapes = (lin_w.shape, gamma is not None)
         return y
@@ -331,29 +332,41 @@ class GineLayer(torch.autograd.Function):
         stream = _lib.stream_handle(dev)
         epi = ctx.epilogue
 
-        dbn = torch.empty_like(x)
-        P = _count("gine_mlp_num_partials", N, D)
-        partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
-        call("gine_mlp_bwd2", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save), ptr(w2c),
-             ptr(dbn), ptr(partials), N, D, epi, stream)
         p_lw, p_lb, p_eps, p_w1, p_b1, p_g, p_bt, p_w2, p_b2 = ctx.params
         dgamma = grad_out(p_g, (D,), dev) if p_g is not None else None
         dbeta = grad_out(p_bt, (D,), dev) if p_bt is not None else None
-        coef = torch.empty(3, D, dtype=torch.float32, device=dev)
-        call("gine_bn_bwd_finalize", ptr(partials), P, ptr(g), ptr(bn_save), ptr(dgamma),
-             ptr(dbeta), ptr(coef), N, D, int(ctx.use_batch_stats), stream)
-        dz = torch.empty_like(x)
-        C = _count("gine_mlp_wgrad_num_chunks", N, D)
-        slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
         dw1, db1 = grad_out(p_w1, (D, D), dev), grad_out(p_b1, (D,), dev)
         dw2, db2 = grad_out(p_w2, (D, D), dev), grad_out(p_b2, (D,), dev)
         deferrable = gradbuf.deferrable(dw1, db1, dw2, db2)
+        use_engine = deferrable and engine_in_mp_ok(ctx.graph, D)
+        # BatchNorm backward sums as fixed-point atomics, finished in the dz GEMM
+        acc = ctx.bn_acc_bwd if use_engine else None
+
+        dbn = torch.empty_like(x)
+        coef = torch.empty(3, D, dtype=torch.float32, device=dev)
+        if acc is None:
+            P = _count("gine_mlp_num_partials", N, D)
+            partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
+            call("gine_mlp_bwd2", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save), ptr(w2c),
+                 ptr(dbn), ptr(partials), N, D, epi, stream)
+            call("gine_bn_bwd_finalize", ptr(partials), P, ptr(g), ptr(bn_save), ptr(dgamma),
+                 ptr(dbeta), ptr(coef), N, D, int(ctx.use_batch_stats), stream)
+        else:
+            call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save),
+                 ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi, stream)
+        dz = torch.empty_like(x)
+        C = _count("gine_mlp_wgrad_num_chunks", N, D)
+        slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
         engine = None
-        if deferrable and engine_in_mp_ok(ctx.graph, D):
+        if use_engine:
             # dz = da1 W1 alone; the dW1, dW2 slab from extra workgroups of the
             # message-passing backward launch below
-            call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save), ptr(coef), ptr(w1c),
-                 ptr(dz), N, D, stream)
+            if acc is None:
+                call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save), ptr(coef), ptr(w1c),
+                     ptr(dz), N, D, stream)
+            else:
+                call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc), ptr(g),
+                     ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz), N, D, stream)
             engine = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epi)
         else:
             # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch

@@ -59,7 +59,7 @@ def test_bn_acc_matches_finish_launch(D, epilogue, monkeypatch):
     torch.testing.assert_close(got[1], ref[1], rtol=TOL, atol=TOL)
     torch.testing.assert_close(got[2], ref[2], rtol=TOL, atol=TOL)
     assert got[3] == ref[3] == 3
-    acc = Fn._BN_ACC[conv.nn[1]][DEV]
+    acc = Fn._BN_ACC[conv.nn[1]][(DEV, "fwd")]
     assert acc.numel() == 40 * D + 1 and int(acc[-1]) == 3   # phase: one per producer launch
 
 
@@ -141,3 +141,32 @@ def test_bn_acc_entry_points_validate():
     assert lib.gine_mlp_fwd2_bn(p(a), None, None, None, None, None, None, p(save), 0.1,
                                 1e-5, 0, p(w), p(b), None, p(a), None, 64, 64, 0, s) != 0
     assert lib.gine_mlp_fwd1_acc(p(a), p(w), p(b), p(a), None, None, 64, 64, s) != 0
+
+
+@pytest.mark.parametrize("epilogue", ["none", "relu", "residual"])
+def test_bn_acc_backward_matches_finish_launch(epilogue, monkeypatch):
+    """gine_mlp_bwd2_acc + gine_mlp_bwd1_bn (taken with the window-plan backward, D = 128)
+    against gine_mlp_bwd2 + gine_bn_bwd_finalize + gine_mlp_bwd1, over two steps."""
+    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    ei, ea, n = knn_batch_graph(500, 10, 4, seed=11)
+    conv = _conv(128, seed=5)
+    state = {k: v.clone() for k, v in conv.state_dict().items()}
+    eid, ead = ei.to(DEV), ea.to(DEV)
+    x0 = torch.randn(n, 128, device=DEV)
+    dy = torch.randn(n, 128, device=DEV)
+    fn = {"none": "forward", "relu": "forward_relu", "residual": "forward_residual_relu"}
+    grads = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GINE_BN_ACC", mode)
+        conv.load_state_dict(state)
+        out = []
+        for _ in range(2):
+            conv.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            getattr(conv, fn[epilogue])(x, eid, ead).backward(dy)
+            out.append([x.grad.clone()] + [p.grad.clone() for p in conv.parameters()])
+        torch.cuda.synchronize()
+        grads[mode] = out
+    for a_step, b_step in zip(grads["1"], grads["0"]):
+        for a, b in zip(a_step, b_step):
+            assert ((a - b).abs() <= 1e-4 * (1 + b.abs())).all()
