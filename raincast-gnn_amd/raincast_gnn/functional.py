@@ -318,7 +318,10 @@ class GineLayer(torch.autograd.Function):
                               lw, lb, ep, w1c, w2c, g)
         ctx.graph, ctx.epilogue = graph, epilogue
         ctx.use_batch_stats = bn.use_batch_stats
-        ctx.bn_acc_bwd = bn_accumulator(bn, D, dev, "bwd")  # allocated outside backward
+        # backward form: opt-in (GINE_BN_ACC_BWD=1) -- a test sequence with it faults a later
+        # kernel; allocated here, outside backward
+        ctx.bn_acc_bwd = (bn_accumulator(bn, D, dev, "bwd")
+                          if os.environ.get("GINE_BN_ACC_BWD", "0") == "1" else None)
         ctx.params = (lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2)
         ctx.shapes = (lin_w.shape, gamma is not None)
         return y
