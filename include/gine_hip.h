@@ -280,18 +280,22 @@ int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in
                      int32_t max_in_degree, int32_t flags, void* stream);
 
 /* BatchNorm statistics without a finish launch (training, momentum >= 0; csrc/gine_bnacc.hpp).
- * bn_acc: int64[gine_bn_acc_words(D) = 40D + 1], zeroed once by the caller at allocation,
+ * bn_acc: int64[gine_bn_acc_words(D) = 78D + 3], zeroed once by the caller at allocation,
  * then owned by the kernels (the sums only grow; each consumer differences them against a
  * snapshot the previous consumer left), so one buffer serves every step of one BatchNorm,
  * HIP-graph replays included.  Every producer launch must be followed by exactly one
- * gine_mlp_fwd2_bn on the same buffer; not shared by layers whose launches interleave.
+ * gine_mlp_fwd2_bn on the same buffer; not shared by layers whose launches interleave.  A
+ * consumer that finds the pairing broken (the producer's phase moved by more than one since
+ * the last consumer) emits NaN statistics for that step; re-zero the buffer to recover.
  *   gine_mlp_fwd1_acc / gine_mp_fwd_mlp1_acc: as gine_mlp_fwd1 / gine_mp_fwd_mlp1, and the
- *     per-workgroup sums are also added into bn_acc as 2-word fixed point with integer
- *     atomics (order-independent: same bits every run).  partials may be NULL.
+ *     per-workgroup sums are also added into bn_acc as 3-word fixed point (2^0 / 2^-32 /
+ *     2^-64) with integer atomics (order-independent: same bits every run); NaN / +Inf /
+ *     -Inf workgroup sums are counted instead and give NaN / +Inf / -Inf column sums, as
+ *     ATen's do.  partials may be NULL.
  *   gine_mlp_fwd2_bn: gine_bn_fwd_finalize (from bn_acc) + gine_mlp_fwd2 in one launch;
  *     writes bn_save, the running statistics and num_batches_tracked as the finalize does.
  * The statistics agree with the partials path to ~1e-15 relative (sums are rounded to
- * 2^-48 per workgroup), so bn_save can differ from it in the last fp32 bit. */
+ * 2^-64 per workgroup), so bn_save can differ from it in the last fp32 bit. */
 int gine_bn_acc_words(int32_t channels, int64_t* words);
 /* Backward, same scheme (a second accumulator per BatchNorm): gine_mlp_bwd2_acc = gine_mlp_bwd2
  * with the [sum dbn | sum dbn*xhat] sums into bn_acc (partials may be NULL);

@@ -1,19 +1,33 @@
 // BatchNorm1d batch statistics without a finish launch (training mode, momentum given).
 //
 // The producer of the statistics (the first node-MLP GEMM: k_rowgemm EPI_A1STATS or the
-// fused gather kernel) adds each workgroup's fp64 per-column sums into a device-wide
-// accumulator as 2-word fixed-point integers (hi = v * 2^16 rounded, lo = the remainder *
-// 2^32 rounded) with agent-scope integer atomics: integer addition is order-independent, so
-// the totals -- and everything computed from them -- are the same bits on every run, with
-// no release fence (an agent-scope release writes the XCD's L2 back).  The consumer (the
-// second GEMM, whose prologue needs alpha / shift) reads the 2-word totals in every
-// workgroup and finishes the statistics itself (workgroup 0 also writes bn_save and the
-// running statistics); the accumulator is never reset (see bnacc_total).
-// Exact for |sum| < 2^37 per column (beyond that the conversion to double rounds, still
-// deterministically); the per-workgroup rounding is below 2^-49.
-// Layout of acc (int64): [replica: 8][hi: W][lo: W], [snapshot: 2][hi: W][lo: W], phase;
-// W = 2 * D (sum | sum of squares).  Every producer launch must be followed by exactly one
-// consumer launch on the same accumulator.
+// fused gather kernel; in the backward the dbn GEMM, EPI_DBN) adds each workgroup's fp64
+// per-column sums into a device-wide accumulator as 3-word fixed-point integers
+//   v = hi + mid * 2^-32 + lo * 2^-64   (hi = rint(v), then the remainder in two words)
+// with agent-scope integer atomics: integer addition is order-independent, so the totals --
+// and everything computed from them -- are the same bits on every run, with no release
+// fence (an agent-scope release writes the XCD's L2 back).  The consumer (the next GEMM,
+// whose prologue needs the finished statistics) reads the totals in every workgroup and
+// finishes the statistics itself; the accumulator is never reset (see bnacc_total).
+// Range and resolution: a per-step column total must stay below 2^63 in magnitude
+// (guaranteed: a workgroup sum of 2^52 or more is not added, see below, and grids are
+// <= 2048 workgroups); the resolution is 2^-64 absolute, so a column sum of 1e-10 (tiny
+// gradients in the backward) keeps ~31 significant bits.
+// Non-finite sums follow IEEE/ATen: a NaN, +Inf or -Inf workgroup sum is counted in its
+// own word (single copy; rare) instead of being converted, and the consumer rebuilds the
+// column total as NaN (a NaN, or both infinities), +Inf or -Inf -- so mean / var / alpha
+// come out non-finite exactly where ATen's batch_norm does.  A finite workgroup sum of
+// magnitude >= 2^52 (an activation column far beyond fp32 BatchNorm's useful range) is
+// counted as NaN: the statistics turn NaN, loudly, instead of wrapping.
+// Pairing: every producer launch must be followed by exactly one consumer launch on the
+// same accumulator.  The producer bumps a phase word; the consumer records the phase it
+// consumed and, if the phase moved by anything but 1 since the last consumer (a producer
+// ran without its consumer, e.g. after a host-side error between the two), emits NaN
+// statistics for that step instead of silently mixing steps.
+// Layout of acc (int64), W = 2 * D words per quantity (sum | sum of squares, or in the
+// backward sum dbn | sum dbn * xhat):
+//   [replica: 8][hi | mid | lo: W]   [count: nan | +inf | -inf: W]
+//   [snapshot: 2][hi | mid | lo | nan | +inf | -inf: W]   phase   consumed[2]
 #pragma once
 
 #include "gine_common.hpp"
@@ -25,52 +39,97 @@ namespace gine {
 // copy cost ~4 us at the end of the producer; 8 replicas make 32-deep chains.  The consumer
 // sums the replicas' integers (exact) before the one conversion to double.
 constexpr int kBnAccReplicas = 8;
+constexpr int kBnAccWords = 3;   // hi, mid, lo
+constexpr int kBnAccCounts = 3;  // nan, +inf, -inf
+constexpr int kBnAccSnap = kBnAccWords + kBnAccCounts;
 
-// Word offsets after the replicas: snapshots [2][hi W | lo W], then the phase counter.
+__host__ __device__ constexpr int64_t bnacc_words(int D) {
+  return (int64_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * 2 * D + 3;
+}
+
+__device__ __forceinline__ long long* bnacc_counts(long long* acc, int W) {
+  return acc + (size_t)kBnAccReplicas * kBnAccWords * W;
+}
 __device__ __forceinline__ long long* bnacc_snap(long long* acc, int W) {
-  return acc + (size_t)kBnAccReplicas * 2 * W;
+  return acc + (size_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts) * W;
 }
 __device__ __forceinline__ long long* bnacc_phase(long long* acc, int W) {
-  return acc + (size_t)kBnAccReplicas * 2 * W + 4 * W;
+  return acc + (size_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * W;
 }
 
 __device__ __forceinline__ void bnacc_add(long long* acc, int W, int c, double v) {
-  long long* r = acc + (size_t)(blockIdx.x % kBnAccReplicas) * 2 * W;
-  const double sv = v * 65536.0;                  // 2^16
-  const double h = rint(sv);
-  const double l = rint((sv - h) * 4294967296.0);  // 2^32: |l| <= 2^31
-  __hip_atomic_fetch_add(r + c, (long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_fetch_add(r + W + c, (long long)l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__builtin_fabs(v) < 4503599627370496.0) {  // 2^52; false for NaN
+    long long* r = acc + (size_t)(blockIdx.x % kBnAccReplicas) * kBnAccWords * W;
+    const double h = __builtin_rint(v);
+    const double f = (v - h) * 4294967296.0;  // exact: |v - h| <= 1/2, power-of-2 scale
+    const double m = __builtin_rint(f);
+    const double l = __builtin_rint((f - m) * 4294967296.0);
+    __hip_atomic_fetch_add(r + c, (long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(r + W + c, (long long)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(r + 2 * W + c, (long long)l, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  } else {  // NaN, +-Inf, or out of range (counted as NaN)
+    const int k = (v == __builtin_inf()) ? 1 : (v == -__builtin_inf()) ? 2 : 0;
+    __hip_atomic_fetch_add(bnacc_counts(acc, W) + k * W + c, 1ll, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (blockIdx.x == 0 && c == 0) {  // one producer launch = one phase (read by the consumer)
     long long* ph = bnacc_phase(acc, W);
     *ph = *ph + 1;
   }
 }
 
-// This step's total of word t (< W).  The replicas only ever grow (mod 2^64): the step's sum
-// is the replicas' total minus the snapshot the previous consumer took.  The snapshot slot
-// alternates with the phase, so workgroup 0 (write_snap) stores this step's totals into the
-// slot nobody reads in this launch -- no atomics, no reset, nothing host-side (HIP-graph
-// replays keep working).  Plain (L2-cached) loads: the producer's atomics were performed at
-// the memory side and the consumer is a later kernel on the stream, whose start invalidates
-// the L2s.
+// This step's total of word t (< W).  The replicas and counts only ever grow (mod 2^64):
+// the step's sum is the current total minus the snapshot the previous consumer took.  The
+// snapshot slot alternates with the phase, so workgroup 0 (write_snap) stores this step's
+// totals into the slot nobody reads in this launch -- no atomics, no reset, nothing
+// host-side (HIP-graph replays keep working).  Plain (L2-cached) loads: the producer's
+// atomics were performed at the memory side and the consumer is a later kernel on the
+// stream, whose start invalidates the L2s.  The consumed phase is kept the same way: a
+// consumer at phase p checks slot (p-1)&1 == p-1 (what a correctly paired previous
+// consumer wrote) and workgroup 0 writes p into slot p&1 (bnacc_mark_consumed).
 __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool write_snap) {
-  unsigned long long h = 0, l = 0;
+  unsigned long long cur_v[kBnAccSnap];
+#pragma unroll
+  for (int k = 0; k < kBnAccSnap; ++k) cur_v[k] = 0;
 #pragma unroll
   for (int r = 0; r < kBnAccReplicas; ++r) {
-    h += (unsigned long long)acc[(size_t)r * 2 * W + t];
-    l += (unsigned long long)acc[(size_t)r * 2 * W + W + t];
+#pragma unroll
+    for (int k = 0; k < kBnAccWords; ++k)
+      cur_v[k] += (unsigned long long)acc[(size_t)(r * kBnAccWords + k) * W + t];
   }
-  const long long ph = *bnacc_phase(acc, W);
-  long long* prev = bnacc_snap(acc, W) + ((ph - 1) & 1) * 2 * W;
-  long long* cur = bnacc_snap(acc, W) + (ph & 1) * 2 * W;
-  const long long dh = (long long)(h - (unsigned long long)prev[t]);
-  const long long dl = (long long)(l - (unsigned long long)prev[W + t]);
+  const long long* cnt = bnacc_counts(acc, W);
+#pragma unroll
+  for (int k = 0; k < kBnAccCounts; ++k) cur_v[kBnAccWords + k] = (unsigned long long)cnt[k * W + t];
+  long long* phw = bnacc_phase(acc, W);
+  const long long ph = phw[0], consumed = phw[1 + ((ph - 1) & 1)];
+  long long* prev = bnacc_snap(acc, W) + ((ph - 1) & 1) * kBnAccSnap * W;
+  long long* cur = bnacc_snap(acc, W) + (ph & 1) * kBnAccSnap * W;
+  long long d[kBnAccSnap];
+#pragma unroll
+  for (int k = 0; k < kBnAccSnap; ++k)
+    d[k] = (long long)(cur_v[k] - (unsigned long long)prev[k * W + t]);
   if (write_snap) {
-    cur[t] = (long long)h;
-    cur[W + t] = (long long)l;
+    // read-before-write within the thread: slot `cur` is not read in this launch
+#pragma unroll
+    for (int k = 0; k < kBnAccSnap; ++k) cur[k * W + t] = (long long)cur_v[k];
   }
-  return (double)dh * (1.0 / 65536.0) + (double)dl * (1.0 / 281474976710656.0);
+  const bool nan = d[3] != 0 || (d[4] != 0 && d[5] != 0) || ph - consumed != 1;
+  double v;
+  if (nan) v = __builtin_nan("");
+  else if (d[4] != 0) v = __builtin_inf();
+  else if (d[5] != 0) v = -__builtin_inf();
+  else
+    v = ((double)d[2] * 5.421010862427522e-20 + (double)d[1] * 2.3283064365386963e-10) +
+        (double)d[0];  // lo * 2^-64 + mid * 2^-32 + hi, smallest first
+  return v;
+}
+
+// Record the consumed phase (one thread of workgroup 0 of the consumer).
+__device__ __forceinline__ void bnacc_mark_consumed(long long* acc, int W) {
+  long long* phw = bnacc_phase(acc, W);
+  const long long ph = phw[0];
+  phw[1 + (ph & 1)] = ph;
 }
 
 struct BnFwdParams {

@@ -80,17 +80,33 @@ struct Stager {
       dst[i] = has ? (16 * c + j) * LD + f : -1;
     }
   }
-  // base: ens + (first group row of the tile) * F;  lim: rows left from that row (clamped).
+  // Stage the tile whose first group row is `row0` (rows_total = N*M rows exist).
   // Returns the rows-in-range bits: the zeroing of out-of-range rows waits for store(), so
   // nothing consumes the loaded registers before the tile is staged -- a select right
   // behind each load made the compiler wait for it there and serialised the prefetch.
-  __device__ __forceinline__ uint32_t load(float (&v)[PER], const float* __restrict__ base,
-                                           int lim) const {
+  // A short last group has whole tiles past rows_total: their base is clamped to `ens`
+  // (every lane then loads ens[0], which exists since N*M > 0), so no address outside
+  // [ens, ens + N*M*F) is ever formed.
+  __device__ __forceinline__ uint32_t load(float (&v)[PER], const float* __restrict__ ens,
+                                           int64_t row0, int64_t rows_total, int F) const {
+    const int64_t d = rows_total - row0;
+    const int lim = d <= 0 ? 0 : (d > 0x7fffffff ? 0x7fffffff : (int)d);
+    const float* __restrict__ base = lim > 0 ? ens + row0 * F : ens;
     uint32_t ok = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const bool in = row[i] < lim;
-      v[i] = base[in ? src[i] : 0];
+      const int off = in ? src[i] : 0;
+#ifdef GINE_BOUNDS_CHECK
+      const int64_t a = (base - ens) + off;
+      if (a < 0 || a >= rows_total * F) {
+        printf("GINE_BOUNDS_CHECK deepset Stager::load: block %d thread %d reads ens[%lld] "
+               "outside [0, %lld)\n", (int)blockIdx.x, (int)threadIdx.x, (long long)a,
+               (long long)(rows_total * F));
+        __builtin_trap();
+      }
+#endif
+      v[i] = base[off];
       ok |= (in ? 1u : 0u) << i;
     }
     return ok;
@@ -179,11 +195,6 @@ struct Cursor {
   }
 };
 
-__device__ __forceinline__ int rows_left(int64_t rows_total, int64_t row) {
-  const int64_t d = rows_total - row;
-  return d > 0x7fffffff ? 0x7fffffff : (int)d;
-}
-
 // Drive `tile(cursor, buf, mbits)` over the workgroup's tiles with a two-deep register ring
 // and a double-buffered LDS tile: tile k+2 is loaded while tile k computes, tile k+1 is
 // stored after it, one barrier per tile.  With `mask_in`, each thread's 16-bit ReLU mask
@@ -204,12 +215,12 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
   };
   float va[PER], vb[PER];
   uint32_t ma = 0, mb = 0, oa = 0, ob = 0;
-  oa = st.load(va, ens + pf.row * F, rows_left(rows_total, pf.row));
+  oa = st.load(va, ens, pf.row, rows_total, F);
   ma = mload(pf);
   st.store(buf0, va, oa);
   if (count > 1) {
     pf.advance(M, gr.step);
-    ob = st.load(vb, ens + pf.row * F, rows_left(rows_total, pf.row));
+    ob = st.load(vb, ens, pf.row, rows_total, F);
     mb = mload(pf);
   }
   pf.advance(M, gr.step);  // pf: tile k+2
@@ -219,7 +230,7 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
     const uint32_t bits = mcur;
     DS_MARK(0);
     if (k + 2 < count) {
-      ocur = st.load(vcur, ens + pf.row * F, rows_left(rows_total, pf.row));
+      ocur = st.load(vcur, ens, pf.row, rows_total, F);
       mcur = mload(pf);
     }
     DS_MARK(1);

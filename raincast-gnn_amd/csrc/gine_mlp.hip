@@ -379,7 +379,7 @@ inline int rowgemm_cap(int D, int64_t tiles) {
     const char* e = getenv("GINE_ROWGEMM_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  if (env > 0) return env;
+  if (env > 0) return std::min(env, 2048);  // gine_bnacc.hpp range bound
   const int per_cu = (D == 128 && tiles > 4 * kNumCu) ? 2 : 1;
   return std::max(kNumCu * per_cu, 1024 / (D / 32));
 }
@@ -423,8 +423,8 @@ int launch_rowgemm(int D, const float* W, const ProArgs& pa, const EpiArgs& ea, 
 // Second GEMM with the BatchNorm finish in its prologue (training, momentum given): every
 // workgroup turns the fixed-point totals of gine_bnacc.hpp into alpha / shift in LDS
 // (workgroup 0 also writes bn_save, the running statistics and num_batches_tracked -- the
-// arithmetic of BnFwdFin), the last one to have read them re-zeroes the accumulator, then
-// the row-tile GEMM runs with its prologue constants read from LDS.
+// arithmetic of BnFwdFin -- and its snapshot / consumed-phase words), then the row-tile
+// GEMM runs with its prologue constants read from LDS.
 template <int D, int EPI>
 __global__ __launch_bounds__(2 * D) void k_fwd2_bnacc(const float* __restrict__ W, ProArgs pa,
                                                       EpiArgs ea, BnFwdParams q,
@@ -441,8 +441,10 @@ __global__ __launch_bounds__(2 * D) void k_fwd2_bnacc(const float* __restrict__ 
     if (t < D)
       bn_finish_channel(q, D, t, s_tot[t], s_tot[D + t], blockIdx.x == 0, &s_bn[2 * D + t],
                         &s_bn[3 * D + t]);
-    if (blockIdx.x == 0 && t == 0 && q.update_running && q.nbt != nullptr)
-      q.nbt[0] = q.nbt[0] + 1;
+    if (blockIdx.x == 0 && t == 0) {
+      if (q.update_running && q.nbt != nullptr) q.nbt[0] = q.nbt[0] + 1;
+      bnacc_mark_consumed(acc, 2 * D);
+    }
     __syncthreads();
   };
   ProArgs p2 = pa;
@@ -478,6 +480,7 @@ __global__ __launch_bounds__(2 * D) void k_bwd1_bnacc(const float* __restrict__ 
       s_coef[D + t] = k2;
       s_coef[2 * D + t] = k3;
       if (blockIdx.x == 0) {
+        if (t == 0) bnacc_mark_consumed(acc, 2 * D);
         if (dgamma) dgamma[t] = (float)sx;
         if (dbeta) dbeta[t] = (float)sd;
         coef[t] = k1;
@@ -703,7 +706,7 @@ extern "C" int gine_mlp_fwd1(const float* z, const float* w1, const float* b1, f
 
 extern "C" int gine_bn_acc_words(int32_t channels, int64_t* words) {
   if (!words || channels <= 0) return GINE_ERR_INVALID;
-  *words = (int64_t)kBnAccReplicas * 4 * channels + 8 * (int64_t)channels + 1;
+  *words = bnacc_words(channels);
   return GINE_OK;
 }
 

@@ -250,6 +250,25 @@ def bn_accumulator(bn: "BnConfig", D: int, dev, kind: str = "fwd") -> "torch.Ten
     return acc
 
 
+class _paired:
+    """Producer/consumer launches on one BatchNorm accumulator (csrc/gine_bnacc.hpp): if
+    anything raises between the two, the accumulator is re-zeroed so the next step starts a
+    fresh pairing instead of differencing against a stale snapshot."""
+
+    __slots__ = ("acc",)
+
+    def __init__(self, acc):
+        self.acc = acc
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is not None and self.acc is not None:
+            self.acc.zero_()
+        return False
+
+
 class GineLayer(torch.autograd.Function):
     """y = epilogue( Linear2( ReLU( BN( Linear1( z ) ) ) ) ),  z = GINE message passing.
 
@@ -273,55 +292,58 @@ class GineLayer(torch.autograd.Function):
 
         a1 = torch.empty_like(x)
         acc = bn_accumulator(bn, D, dev)
-        if acc is None:
-            P = _count("gine_mlp_num_partials", N, D)
-            partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
-        else:  # statistics summed by integer atomics, finished inside the second GEMM
-            partials = None
-        if fused_forward_ok(graph, N, D):
-            # gather of the next tile beside the matrix chain of this one: one launch
-            z = torch.empty_like(x)
-            args = (ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
-                    ptr(lw), ptr(lb), ptr(ep), ptr(w1c), ptr(b1c), ptr(z), ptr(a1),
-                    ptr(partials))
-            tail = (N, D, graph.max_in_degree, edge_linear_flag(), stream)
-            if acc is None:
-                call("gine_mp_fwd_mlp1", *args, *tail)
-            else:
-                call("gine_mp_fwd_mlp1_acc", *args, ptr(acc), *tail)
-        else:
-            z = mp_forward(x, graph, lw, lb, ep)
-            if acc is None:
-                call("gine_mlp_fwd1", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), ptr(partials), N,
-                     D, stream)
-            else:
-                call("gine_mlp_fwd1_acc", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), None,
-                     ptr(acc), N, D, stream)
+        # everything the consumer needs exists before the producer launches (gine_bnacc.hpp:
+        # a producer without its consumer breaks the pairing)
         bn_save = torch.empty(4, D, dtype=torch.float32, device=dev)
         nbt = ptr(bn.num_batches_tracked) if bn.update_running else None
         update_running = int(bn.update_running and bn.running_mean is not None)
         y = torch.empty_like(x)
         mask = (torch.empty(N, D, dtype=torch.uint8, device=dev)
                 if epilogue == EPI_RESIDUAL_RELU else None)
+        fused = fused_forward_ok(graph, N, D)
+        # fused: the gather runs inside the Linear1 launch; else the gather first, unpaired
+        z = torch.empty_like(x) if fused else mp_forward(x, graph, lw, lb, ep)
         if acc is None:
-            call("gine_bn_fwd_finalize", ptr(partials), P, ptr(g), ptr(bt),
-                 ptr(bn.running_mean), ptr(bn.running_var), nbt, ptr(bn_save), N, D,
-                 bn.momentum, bn.eps, int(bn.use_batch_stats), update_running, stream)
-            call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2c), ptr(b2c), ptr(x), ptr(y),
-                 ptr(mask), N, D, epilogue, stream)
-        else:
-            call("gine_mlp_fwd2_bn", ptr(a1), ptr(acc), ptr(g), ptr(bt), ptr(bn.running_mean),
-                 ptr(bn.running_var), nbt, ptr(bn_save), bn.momentum, bn.eps, update_running,
-                 ptr(w2c), ptr(b2c), ptr(x), ptr(y), ptr(mask), N, D, epilogue, stream)
+            P = _count("gine_mlp_num_partials", N, D)
+            partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
+        else:  # statistics summed by integer atomics, finished inside the second GEMM
+            partials = None
+        with _paired(acc):
+            if fused:
+                # gather of the next tile beside the matrix chain of this one: one launch
+                args = (ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
+                        ptr(lw), ptr(lb), ptr(ep), ptr(w1c), ptr(b1c), ptr(z), ptr(a1),
+                        ptr(partials))
+                tail = (N, D, graph.max_in_degree, edge_linear_flag(), stream)
+                if acc is None:
+                    call("gine_mp_fwd_mlp1", *args, *tail)
+                else:
+                    call("gine_mp_fwd_mlp1_acc", *args, ptr(acc), *tail)
+            elif acc is None:
+                call("gine_mlp_fwd1", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), ptr(partials), N,
+                     D, stream)
+            else:
+                call("gine_mlp_fwd1_acc", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), None,
+                     ptr(acc), N, D, stream)
+            if acc is None:
+                call("gine_bn_fwd_finalize", ptr(partials), P, ptr(g), ptr(bt),
+                     ptr(bn.running_mean), ptr(bn.running_var), nbt, ptr(bn_save), N, D,
+                     bn.momentum, bn.eps, int(bn.use_batch_stats), update_running, stream)
+                call("gine_mlp_fwd2", ptr(a1), ptr(bn_save), ptr(w2c), ptr(b2c), ptr(x),
+                     ptr(y), ptr(mask), N, D, epilogue, stream)
+            else:
+                call("gine_mlp_fwd2_bn", ptr(a1), ptr(acc), ptr(g), ptr(bt),
+                     ptr(bn.running_mean), ptr(bn.running_var), nbt, ptr(bn_save),
+                     bn.momentum, bn.eps, update_running, ptr(w2c), ptr(b2c), ptr(x), ptr(y),
+                     ptr(mask), N, D, epilogue, stream)
 
         ctx.save_for_backward(x, z, a1, y if epilogue == EPI_RELU else None, mask, bn_save,
                               lw, lb, ep, w1c, w2c, g)
         ctx.graph, ctx.epilogue = graph, epilogue
         ctx.use_batch_stats = bn.use_batch_stats
-        # backward form: opt-in (GINE_BN_ACC_BWD=1) -- a test sequence with it faults a later
-        # kernel; allocated here, outside backward
+        # backward form (GINE_BN_ACC_BWD=0 turns it off); allocated here, outside backward
         ctx.bn_acc_bwd = (bn_accumulator(bn, D, dev, "bwd")
-                          if os.environ.get("GINE_BN_ACC_BWD", "0") == "1" else None)
+                          if os.environ.get("GINE_BN_ACC_BWD", "1") != "0" else None)
         ctx.params = (lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2)
         ctx.shapes = (lin_w.shape, gamma is not None)
         return y
@@ -347,6 +369,9 @@ class GineLayer(torch.autograd.Function):
 
         dbn = torch.empty_like(x)
         coef = torch.empty(3, D, dtype=torch.float32, device=dev)
+        dz = torch.empty_like(x)
+        C = _count("gine_mlp_wgrad_num_chunks", N, D)
+        slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
         if acc is None:
             P = _count("gine_mlp_num_partials", N, D)
             partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
@@ -354,12 +379,6 @@ class GineLayer(torch.autograd.Function):
                  ptr(dbn), ptr(partials), N, D, epi, stream)
             call("gine_bn_bwd_finalize", ptr(partials), P, ptr(g), ptr(bn_save), ptr(dgamma),
                  ptr(dbeta), ptr(coef), N, D, int(ctx.use_batch_stats), stream)
-        else:
-            call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1), ptr(bn_save),
-                 ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi, stream)
-        dz = torch.empty_like(x)
-        C = _count("gine_mlp_wgrad_num_chunks", N, D)
-        slab = torch.empty(2 * C * (D * D + D), dtype=torch.float32, device=dev)
         engine = None
         if use_engine:
             # dz = da1 W1 alone; the dW1, dW2 slab from extra workgroups of the
@@ -368,8 +387,12 @@ class GineLayer(torch.autograd.Function):
                 call("gine_mlp_bwd1", ptr(dbn), ptr(a1), ptr(bn_save), ptr(coef), ptr(w1c),
                      ptr(dz), N, D, stream)
             else:
-                call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc), ptr(g),
-                     ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz), N, D, stream)
+                with _paired(acc):  # producer + consumer back to back
+                    call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1),
+                         ptr(bn_save), ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi, stream)
+                    call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc),
+                         ptr(g), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz), N, D,
+                         stream)
             engine = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epi)
         else:
             # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch

@@ -4,10 +4,11 @@ csrc/gine_bnacc.hpp) against the finish-launch path (partials -> gine_bn_fwd_fin
 gine_mlp_fwd2).  The layer uses it by default in training mode (GINE_BN_ACC=0 turns it
 off), so test_gpu_parity.py's test_gine_layer_fused also checks it against the oracle.
 
-Tolerance: the fixed-point sums round each workgroup's fp64 partial to 2^-48, so mean and
+Tolerance: the fixed-point sums round each workgroup's fp64 partial to 2^-64, so mean and
 variance agree with the fp64 partials path to ~1e-15 relative; alpha / shift may differ in
 their last fp32 bit, y by a few ulp (1e-5 relative bound written below).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -21,6 +22,12 @@ from raincast_gnn.graph import GineGraph
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 TOL = 1e-5
+
+
+def _words(D):
+    w = ctypes.c_int64(0)
+    assert _lib.load().gine_bn_acc_words(D, ctypes.byref(w)) == 0
+    return w.value
 
 
 def _conv(D, seed):
@@ -62,7 +69,8 @@ def test_bn_acc_matches_finish_launch(D, epilogue, monkeypatch):
     torch.testing.assert_close(got[2], ref[2], rtol=TOL, atol=TOL)
     assert got[3] == ref[3] == 3
     acc = Fn._BN_ACC[conv.nn[1]][(DEV, "fwd")]
-    assert acc.numel() == 40 * D + 1 and int(acc[-1]) == 3   # phase: one per producer launch
+    assert acc.numel() == _words(D) and int(acc[-3]) == 3   # phase: one per producer launch
+    assert int(acc[-2 + (3 & 1)]) == 3                       # consumed: the last consumer
 
 
 def test_bn_acc_deterministic(monkeypatch):
@@ -108,7 +116,7 @@ def test_fused_forward_acc_equals_unfused(n, max_deg):
     eps = torch.tensor([0.1], device=DEV)
     w1, b1 = torch.randn(D, D, device=DEV) / 11, torch.randn(D, device=DEV)
     p, s = _lib.ptr, _lib.stream_handle(DEV)
-    acc1 = torch.zeros(40 * D + 1, dtype=torch.int64, device=DEV)
+    acc1 = torch.zeros(_words(D), dtype=torch.int64, device=DEV)
     acc0 = torch.zeros_like(acc1)
     z1, a11 = torch.empty_like(x), torch.empty_like(x)
     _lib.call("gine_mp_fwd_mlp1_acc", p(x), p(g.in_rowptr), p(g.in_src), p(g.in_attr), p(lw),
@@ -122,17 +130,22 @@ def test_fused_forward_acc_equals_unfused(n, max_deg):
     assert torch.equal(acc1, acc0)
     # the totals are the column sums of a1 and a1^2
     a64 = a10.double()
-    rep = acc0[:8 * 4 * D].view(8, 2, 2 * D).sum(0)          # replicas: [hi | lo] x (sum | sumsq)
-    tot = (rep[0].double() / 2**16 + rep[1].double() / 2**48).view(2, D)
+    W = 2 * D
+    rep = acc0[:8 * 3 * W].view(8, 3, W).sum(0)   # replicas: [hi | mid | lo] x (sum | sumsq)
+    tot = (rep[0].double() + rep[1].double() / 2**32 + rep[2].double() / 2**64).view(2, D)
     torch.testing.assert_close(tot[0], a64.sum(0), rtol=1e-12, atol=1e-9)
     torch.testing.assert_close(tot[1], (a64 * a64).sum(0), rtol=1e-12, atol=1e-9)
-    assert int(acc0[8 * 4 * D:-1].abs().sum()) == 0 and int(acc0[-1]) == 1
+    assert int(acc0[8 * 3 * W:-3].abs().sum()) == 0       # no non-finite counts, no snapshot
+    assert int(acc0[-3]) == 1 and int(acc0[-2:].abs().sum()) == 0
 
 
 def test_bn_acc_entry_points_validate():
     p, s = _lib.ptr, _lib.stream_handle(DEV)
     a = torch.zeros(64, 64, device=DEV)
-    acc = torch.zeros(40 * 64 + 1, dtype=torch.int64, device=DEV)
+    words = ctypes.c_int64(0)
+    assert _lib.load().gine_bn_acc_words(64, ctypes.byref(words)) == 0
+    assert words.value == 78 * 64 + 3
+    acc = torch.zeros(words.value, dtype=torch.int64, device=DEV)
     save = torch.empty(4, 64, device=DEV)
     w = torch.zeros(64, 64, device=DEV)
     b = torch.zeros(64, device=DEV)
@@ -145,9 +158,6 @@ def test_bn_acc_entry_points_validate():
     assert lib.gine_mlp_fwd1_acc(p(a), p(w), p(b), p(a), None, None, 64, 64, s) != 0
 
 
-@pytest.mark.skipif(os.environ.get("GINE_BN_ACC_BWD") != "1",
-                    reason="backward accumulator path is opt-in: after this test a later "
-                           "kernel faults (illegal address), cause not yet found")
 @pytest.mark.parametrize("epilogue", ["none", "relu", "residual"])
 def test_bn_acc_backward_matches_finish_launch(epilogue, monkeypatch):
     """gine_mlp_bwd2_acc + gine_mlp_bwd1_bn (taken with the window-plan backward, D = 128)
@@ -176,3 +186,152 @@ def test_bn_acc_backward_matches_finish_launch(epilogue, monkeypatch):
     for a_step, b_step in zip(grads["1"], grads["0"]):
         for a, b in zip(a_step, b_step):
             assert ((a - b).abs() <= 1e-4 * (1 + b.abs())).all()
+
+
+def _fwd_pair(x, acc, bn, D, N, w1=None):
+    """gine_mlp_fwd1_acc (a1 = x W1^T, W1 = I by default so a1 = x exactly), then
+    gine_mlp_fwd2_bn; returns a1 and bn_save [mean | invstd | alpha | shift]."""
+    p, s = _lib.ptr, _lib.stream_handle(DEV)
+    eye, zero = torch.eye(D, device=DEV), torch.zeros(D, device=DEV)
+    w1 = eye if w1 is None else w1
+    a1 = torch.empty_like(x)
+    _lib.call("gine_mlp_fwd1_acc", p(x), p(w1), p(zero), p(a1), None, p(acc), N, D, s)
+    save = torch.empty(4, D, device=DEV)
+    y = torch.empty_like(x)
+    _lib.call("gine_mlp_fwd2_bn", p(a1), p(acc), p(bn["g"]), p(bn["b"]), p(bn["rm"]),
+              p(bn["rv"]), None, p(save), 0.1, 1e-5, 1, p(eye), p(zero), None, p(y), None,
+              N, D, 0, s)
+    torch.cuda.synchronize()
+    return a1, save
+
+
+def _cls(t):
+    """NaN / +Inf / -Inf classification of a tensor (for exact pattern comparisons)."""
+    return torch.stack([t.isnan(), t == float("inf"), t == float("-inf")])
+
+
+def _bn_state(D):
+    return {"g": torch.rand(D, device=DEV) + 0.5, "b": torch.randn(D, device=DEV),
+            "rm": torch.zeros(D, device=DEV), "rv": torch.ones(D, device=DEV)}
+
+
+@pytest.mark.parametrize("case", ["nan", "+inf", "-inf", "both_inf"])
+def test_bn_acc_nonfinite_follows_aten(case):
+    """Non-finite column sums (csrc/gine_bnacc.hpp counts them): mean and the running
+    statistics come out NaN / +Inf / -Inf exactly where ATen's train-mode batch_norm (CPU,
+    on the same a1) puts them, finite entries within 1e-5; the next step is clean again."""
+    N, D = 1000, 64
+    x = torch.randn(N, D, device=DEV) * 3 + 1
+    bad = {"nan": [(17, 0, float("nan"))], "+inf": [(5, 1, float("inf"))],
+           "-inf": [(900, 2, float("-inf"))],
+           "both_inf": [(3, 3, float("inf")), (600, 5, float("-inf"))]}[case]
+    for r, c, v in bad:
+        x[r, c] = v
+    # W1 > 0 everywhere: a non-finite entry spreads over its a1 row with one sign
+    w1 = torch.eye(D, device=DEV) + 1e-3
+    bn = _bn_state(D)
+    acc = torch.zeros(_words(D), dtype=torch.int64, device=DEV)
+    a1, save = _fwd_pair(x, acc, bn, D, N, w1)
+    a64 = a1.cpu().double()
+    rm, rv = torch.zeros(D, dtype=torch.float64), torch.ones(D, dtype=torch.float64)
+    torch.nn.functional.batch_norm(a64, rm, rv, training=True, momentum=0.1, eps=1e-5)
+    assert not bool(torch.isfinite(a64.sum(0)).any())          # the case reached every column
+    assert torch.equal(_cls(save[0].cpu()), _cls(a64.mean(0).float()))
+    assert torch.equal(_cls(bn["rm"].cpu()), _cls(rm.float()))
+    assert torch.equal(_cls(bn["rv"].cpu()), _cls(rv.float()))
+    # the accumulator carries nothing into the next step
+    bn2 = _bn_state(D)
+    x2 = torch.randn(N, D, device=DEV)
+    _, save2 = _fwd_pair(x2, acc, bn2, D, N)
+    torch.testing.assert_close(save2[0].cpu().double(), x2.cpu().double().mean(0),
+                               rtol=TOL, atol=TOL)
+
+
+def test_bn_acc_out_of_range_column_is_nan():
+    """The documented divergence: a finite workgroup column sum of 2^52 or more is counted as
+    NaN (no silent fixed-point wrap); other columns are unaffected."""
+    N, D = 1000, 64
+    x = torch.randn(N, D, device=DEV)
+    x[:, 4] = 3e16
+    bn = _bn_state(D)
+    acc = torch.zeros(_words(D), dtype=torch.int64, device=DEV)
+    a1, save = _fwd_pair(x, acc, bn, D, N)
+    assert torch.equal(a1, x)
+    assert bool(save[0, 4].isnan()) and bool(bn["rm"][4].isnan())
+    fin = [c for c in range(D) if c != 4]
+    x64 = x.cpu().double()
+    torch.testing.assert_close(save[0].cpu()[fin].double(), x64.mean(0)[fin], rtol=TOL,
+                               atol=TOL)
+    rv = 0.9 + 0.1 * x64.var(0, unbiased=True)
+    torch.testing.assert_close(bn["rv"].cpu()[fin].double(), rv[fin], rtol=TOL, atol=TOL)
+
+
+def test_bn_acc_layer_with_nonfinite_input_matches_oracle():
+    """Train-mode GINE layer (default accumulator path) with +Inf / NaN in x against the CPU
+    oracle: equal NaN / Inf pattern of y and of the running statistics, finite running
+    means within 1e-5."""
+    from oracle import gine_cpu as O
+    import copy
+    ei, ea, n = knn_batch_graph(300, 8, 2, seed=4)
+    for bad in (float("inf"), float("nan"), float("-inf")):
+        conv = _conv(64, seed=9)
+        ref = O.OracleGINEConv(copy.deepcopy(conv.nn).cpu(), train_eps=True, edge_dim=1)
+        ref.load_state_dict({k: v.cpu() for k, v in conv.state_dict().items()})
+        ref.train()
+        x = torch.randn(n, 64)
+        x[123, 7] = bad
+        y = conv.forward_residual_relu(x.to(DEV), ei.to(DEV), ea.to(DEV))
+        yr = x + torch.relu(ref(x, ei, ea))
+        torch.cuda.synchronize()
+        assert torch.equal(_cls(y.cpu()), _cls(yr)), bad
+        for buf in ("running_mean", "running_var"):
+            g, r = getattr(conv.nn[1], buf).cpu(), getattr(ref.nn[1], buf)
+            assert torch.equal(_cls(g), _cls(r)), (bad, buf)
+            f = torch.isfinite(r)
+            torch.testing.assert_close(g[f], r[f], rtol=TOL, atol=TOL)
+
+
+def test_bn_acc_pairing_break_gives_nan_then_recovers():
+    """A producer launch without its consumer (the pairing gine_bnacc.hpp requires) makes
+    the next consumer emit NaN statistics instead of mixing two steps; the pair after it is
+    exact again."""
+    N, D = 512, 32
+    p, s = _lib.ptr, _lib.stream_handle(DEV)
+    acc = torch.zeros(_words(D), dtype=torch.int64, device=DEV)
+    bn = {"g": None, "b": None, "rm": torch.zeros(D, device=DEV),
+          "rv": torch.ones(D, device=DEV)}
+    x = torch.randn(N, D, device=DEV)
+    _, save = _fwd_pair(x, acc, bn, D, N)
+    torch.testing.assert_close(save[0].double(), x.double().mean(0), rtol=TOL, atol=TOL)
+    eye, zero = torch.eye(D, device=DEV), torch.zeros(D, device=DEV)
+    a1 = torch.empty_like(x)
+    _lib.call("gine_mlp_fwd1_acc", p(x), p(eye), p(zero), p(a1), None, p(acc), N, D, s)
+    _, save = _fwd_pair(x, acc, bn, D, N)      # two producers, one consumer
+    assert bool(save[0].isnan().all())
+    x3 = torch.randn(N, D, device=DEV) + 2
+    _, save = _fwd_pair(x3, acc, bn, D, N)
+    torch.testing.assert_close(save[0].double(), x3.double().mean(0), rtol=TOL, atol=TOL)
+
+
+def test_bn_acc_backward_small_gradients(monkeypatch):
+    """Gradients of order 1e-10 (the ADVICE case): the backward accumulator's 2^-64
+    resolution keeps them within 1e-5 (max-norm relative) of the fp64-partials path."""
+    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    ei, ea, n = knn_batch_graph(500, 10, 4, seed=12)
+    conv = _conv(128, seed=6)
+    state = {k: v.clone() for k, v in conv.state_dict().items()}
+    eid, ead = ei.to(DEV), ea.to(DEV)
+    x0 = torch.randn(n, 128, device=DEV)
+    dy = torch.randn(n, 128, device=DEV) * 1e-10
+    grads = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GINE_BN_ACC_BWD", mode)
+        conv.load_state_dict(state)
+        conv.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        conv.forward_residual_relu(x, eid, ead).backward(dy)
+        torch.cuda.synchronize()
+        grads[mode] = [x.grad.clone()] + [p.grad.clone() for p in conv.parameters()]
+    for a, b in zip(grads["1"], grads["0"]):
+        den = float(b.abs().max())
+        assert float((a - b).abs().max()) <= TOL * den + 1e-30

@@ -41,7 +41,9 @@ def _run(N, M, F, H, seed=0, scale=1.0):
 @pytest.mark.parametrize("N,M,F,H", [
     (1, 1, 1, 32), (31, 11, 35, 128), (33, 11, 35, 128), (1000, 11, 35, 128),
     (16000, 11, 35, 128), (257, 1, 16, 64), (100, 33, 64, 256), (77, 5, 20, 32),
-    (500, 51, 35, 128), (64, 2, 40, 128), (65, 3, 48, 64), (90, 7, 33, 128), (40, 4, 61, 32)])
+    (500, 51, 35, 128), (64, 2, 40, 128), (65, 3, 48, 64), (90, 7, 33, 128), (40, 4, 61, 32),
+    # short last groups (whole tiles past N*M rows): N % 32 != 0
+    (65, 11, 35, 128), (610, 10, 35, 128), (33, 10, 35, 128), (97, 11, 35, 256)])
 def test_phi_sum_forward_and_weight_grads(N, M, F, H):
     ens, lin = _run(N, M, F, H, seed=N + M + F + H)
     r = deepset.phi_sum(ens, lin)

@@ -25,9 +25,11 @@ run() {  # run <name> <seconds> cmd...
 
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15 ;;
+    tests) run pytest_gpu 660 python -u -m pytest tests -m gpu -q -rf --durations=15 --timeout 120 --timeout-method thread ;;
+    btests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/bounds/libgine_hip.so \
+            run pytest_bounds 300 python -u -m pytest tests/test_gpu_bnacc.py tests/test_gpu_deepset.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     ktests) run pytest_k 600 python -u -m pytest tests -m gpu -q -rf -k "${KTESTS:-window}" --timeout 120 --timeout-method thread ;;
-    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    smoke) run smoke 150 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench1) run bench_cfg1 600 python bench.py --config 1 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 20 ;;
