@@ -295,18 +295,62 @@ FUSED_STEP_KERNELS = ("gine_mp_fwd_mlp1", "gine_mp_bwd", "gine_mlp_fwd2", "gine_
                       "gine_mlp_bwd1_wgrad")
 
 
-def _roof(name: str, rec: dict, bound: str, layers: int) -> dict:
-    if bound == "mfma":
-        achieved = rec["TFLOPps"]
-        roof = {"kernel": name, "bound": "mfma", "achieved": achieved,
-                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "work_per_launch": rec["alg_flops"]}
+def sec8d_work(N: int, E: int, D: int) -> dict:
+    """SURVEY.md 8(d)'s algorithmic quantities per GINE layer: B_f (read h once, src index
+    and attribute per edge, rowptr, write z), B_b (read dz, read h for the ReLU mask, write
+    dh, dst index + attribute per edge, rowptr) and the node-MLP flops (fwd 4ND^2, bwd
+    8ND^2, of which the weight gradients are 4ND^2)."""
+    return {"B_f": 4 * (2 * N * D + 2 * E + N + 1), "B_b": 4 * (3 * N * D + 2 * E + N + 1),
+            "mlp_fwd_flops": 4 * N * D * D, "mlp_bwd_flops": 8 * N * D * D}
+
+
+# per entry point: its 8(d) work per launch (bytes, flops) -- only what 8(d) counts:
+# message-passing bytes for the gather / scatter kernels, GEMM flops for the node MLP
+# (operands of a GEMM re-read from L2, split-K slabs and the residual-gradient read are
+# NOT algorithmic work; they show up in `traffic`)
+def sec8d_launch_work(name: str, w: dict) -> dict:
+    half_fwd, half_bwd = w["mlp_fwd_flops"] // 2, w["mlp_bwd_flops"] // 4
+    return {
+        "gine_mp_fwd": {"bytes": w["B_f"]},
+        "gine_mp_bwd": {"bytes": w["B_b"]},
+        "gine_mp_fwd_mlp1": {"bytes": w["B_f"], "flops": half_fwd},
+        "gine_mp_bwd_mlp_wgrad": {"bytes": w["B_b"], "flops": 2 * half_bwd},
+        "gine_mlp_fwd1": {"flops": half_fwd}, "gine_mlp_fwd2": {"flops": half_fwd},
+        "gine_mlp_bwd2": {"flops": half_bwd}, "gine_mlp_bwd1": {"flops": half_bwd},
+        "gine_mlp_bwd1_wgrad": {"flops": 3 * half_bwd},
+        "gine_mlp_wgrad": {"flops": 2 * half_bwd},
+    }.get(name, {})
+
+
+def roofline_for(kernels: dict, layers: int, work: dict):
+    """The dominant kernel of the step (largest time per step among the per-layer kernels
+    the training step launches) against SURVEY.md 8(d)'s roofline: its ideal time is
+    max(8(d) bytes / 8 TB/s, 8(d) flops / 157.3 TFLOP/s fp32 MFMA), frac = ideal / measured
+    average launch time; `achieved` is the binding quantity per second."""
+    step = list(FUSED_STEP_KERNELS if "gine_mp_fwd_mlp1" in kernels else STEP_KERNELS)
+    if "gine_mp_bwd_mlp_wgrad" in kernels:  # engine in the message-passing launch
+        step = [k for k in step if k not in ("gine_mp_bwd", "gine_mlp_bwd1_wgrad")]
+        step += ["gine_mlp_bwd1", "gine_mp_bwd_mlp_wgrad"]
+    timed = [k for k in step if k in kernels]
+    dominant = max(timed, key=lambda k: kernels[k]["us"])
+    return roof_of(dominant, kernels[dominant], layers, work)
+
+
+def roof_of(name: str, rec: dict, layers: int, work: dict) -> dict:
+    wl = sec8d_launch_work(name, work)
+    b, f = wl.get("bytes", 0), wl.get("flops", 0)
+    t_hbm = b / (HBM_PEAK_GBS * 1e9)
+    t_mfma = f / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+    sec = rec["us"] * 1e-6
+    if t_mfma > t_hbm:
+        roof = {"kernel": name, "bound": "mfma", "achieved": round(f / sec * 1e-12, 2),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s"}
     else:
-        achieved = rec["GBps"]
-        roof = {"kernel": name, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "work_per_launch": rec["alg_bytes"]}
+        roof = {"kernel": name, "bound": "hbm", "achieved": round(b / sec * 1e-9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof["frac"] = round(max(t_hbm, t_mfma) / sec, 4)
+    roof["alg_bytes_per_launch"] = b
+    roof["alg_flops_per_launch"] = f
     roof["avg_us"] = rec["us"]
     roof["launches_per_step"] = layers
     t = pmc_traffic(name)
@@ -315,33 +359,24 @@ def _roof(name: str, rec: dict, bound: str, layers: int) -> dict:
     return roof
 
 
-def roofline_for(kernels: dict, layers: int):
-    """The dominant kernel of the step (largest time per step among the per-layer kernels
-    the training step launches), against its bound: fp32 MFMA for the node-MLP GEMMs, HBM
-    for message passing."""
-    step = list(FUSED_STEP_KERNELS if "gine_mp_fwd_mlp1" in kernels else STEP_KERNELS)
-    if "gine_mp_bwd_mlp_wgrad" in kernels:  # engine in the message-passing launch
-        step = [k for k in step if k not in ("gine_mp_bwd", "gine_mlp_bwd1_wgrad")]
-        step += ["gine_mlp_bwd1", "gine_mp_bwd_mlp_wgrad"]
-    timed = [k for k in step if k in kernels]
-    dominant = max(timed, key=lambda k: kernels[k]["us"])
-    rec = kernels[dominant]
-    # the binding resource at the ideal: the larger of flops / MFMA peak and bytes / HBM peak
-    t_mfma = rec.get("alg_flops", 0) / (FP32_MFMA_PEAK_TFLOPS * 1e12)
-    t_hbm = rec.get("alg_bytes", 0) / (HBM_PEAK_GBS * 1e9)
-    roof = _roof(dominant, rec, "mfma" if t_mfma >= t_hbm else "hbm", layers)
-    if dominant == "gine_mp_bwd_mlp_wgrad":
-        roof["note"] = ("one launch = the message-passing backward + the node-MLP weight-"
-                        "gradient engine (alg_flops of kernels.gine_mp_bwd_mlp_wgrad on fp32 "
-                        "MFMA); work_per_launch = all algorithmic bytes of the launch")
-    return roof
+def roofline_step(work: dict, layers: int, ms_per_step: float) -> dict:
+    """SURVEY.md 8(d)'s per-step figure: sum over layers of (B_f + B_b) / step time, against
+    HBM (the message-passing bytes of the whole step; the rest of the step -- DeepSet,
+    dense chain, node-MLP GEMMs, head, loss, optimizer -- is time without 8(d) bytes)."""
+    b = (work["B_f"] + work["B_b"]) * layers
+    gbs = b / (ms_per_step * 1e-3) * 1e-9
+    return {"bytes_per_step": b, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
-def roofline_mp(kernels: dict, layers: int):
-    """The message-passing backward (the north-star gather/segmented-scatter path) against
-    HBM, with the measured copy ceiling beside the 8 TB/s spec."""
-    rec = kernels.get("gine_mp_bwd")
-    return _roof("gine_mp_bwd", rec, "hbm", layers) if rec else None
+def roofline_mp(kernels: dict, layers: int, work: dict):
+    """The message-passing kernels (the north-star gather / segmented-scatter path) alone
+    against HBM, with the measured copy ceiling beside the 8 TB/s spec."""
+    out = {}
+    for name in ("gine_mp_fwd", "gine_mp_bwd"):
+        if name in kernels:
+            out[name] = roof_of(name, kernels[name], layers, work)
+    return out or None
 
 
 def copy_ceiling_gbps(device, nbytes=1 << 30, reps=10):
@@ -440,7 +475,14 @@ def cpu_baseline(cfg, graphs, seconds):
             if el >= limit or n >= 200:
                 return n, el
 
+    # threads: the cores this process may use.  On the GPU pool one GPU's job gets a 16-CPU
+    # share (OMP_NUM_THREADS=16 is set there and the pool asks that it be left as is), so
+    # torch's intra-op pool is that share even when the affinity mask shows every CPU.
     threads = torch.get_num_threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     n, el = run(seconds)
     torch.set_num_threads(1)
     try:
@@ -454,6 +496,12 @@ def cpu_baseline(cfg, graphs, seconds):
                       f"after 1 warm-up step; {el:.1f} s on {threads} threads; "
                       f"cpu={cpu_model()}",
             "ms_per_step": round(el / n * 1e3, 2),
+            "host": {"cpu_count": os.cpu_count(), "affinity_cpus": affinity,
+                     "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+                     "threads_used": threads,
+                     "why": "torch intra-op threads = the job's CPU share (OMP_NUM_THREADS, "
+                            "set by the GPU pool: 16 CPUs per GPU); the affinity mask and "
+                            "cpu_count show the whole host"},
             "one_thread": {"value": round(graphs * n1 / el1, 3), "unit": "graphs/s",
                            "steps": n1, "seconds": round(el1, 1)}}
 
@@ -524,12 +572,15 @@ def main():
     kernels = time_kernels(tr, args.kernel_reps) if rank == 0 else {}
     result = None
     if rank == 0:
-        roof = roofline_for(kernels, layers)
-        roof_mp = roofline_mp(kernels, layers)
+        work = sec8d_work(tr.batch.num_nodes, E_rank, tr.params["gnn_hidden"])
+        roof = roofline_for(kernels, layers, work)
+        roof_mp = roofline_mp(kernels, layers, work)
         if roof_mp is not None:
-            roof_mp["measured_copy_GBps"] = copy_ceiling_gbps(device)
-            roof_mp["frac_of_measured"] = round(roof_mp["achieved"] /
-                                                roof_mp["measured_copy_GBps"], 4)
+            copy_gbs = copy_ceiling_gbps(device)
+            for r in roof_mp.values():
+                r["measured_copy_GBps"] = copy_gbs
+                r["frac_of_measured"] = round(r["achieved"] / copy_gbs, 4)
+        roof_step = roofline_step(work, layers, ms)
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(cfg, graphs_per_rank, args.cpu_seconds)
@@ -547,7 +598,8 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
             "edges_aggregated_per_s": round(edges_per_s, 1),
             "step_ms_p10_p50_p90": [pct[10], pct[50], pct[90]],
-            "roofline": roof, "roofline_message_passing": roof_mp,
+            "roofline": roof, "roofline_step": roof_step,
+            "roofline_message_passing": roof_mp,
             "cpu_baseline": cpu, "kernels": kernels,
             "final_loss": loss_val,
         }

@@ -1,0 +1,104 @@
+"""GPU: the training step at the benchmark configurations of BASELINE.json / SURVEY.md 8.
+
+Oracle parity (tests/helpers.py: check_training_step -- predictions, loss and the BatchNorm
+running statistics within 1e-5 of the CPU oracle, fp64 tie-break; every parameter gradient
+within twice the reference restatement's own fp32 envelope, i.e. the largest error against
+the fp64 oracle of the fp32 oracle run at 1, 2, 4 and all threads -- at these sizes fp32
+ReLU decisions near zero make the reference's gradient itself uncertain at 1e-4..5e-3,
+see check_training_step) on each config's own station graph, experiment head and layer
+count, at batch sizes the CPU oracle finishes in seconds:
+
+* cfg2 at full size (32 x 500 stations, k=10): the fused gather + Linear1 forward, the
+  LDS-window backward with the weight-gradient engine in the same launch, BatchNorm sums
+  by fixed-point accumulators in both directions;
+* cfg3's graph (2,000 stations, k=16, 72h_mixed_u: MixedLoss with a learned u) at 4 graphs
+  (8,000 nodes: fused forward) and 9 graphs (18,000 nodes: the standalone gather forward,
+  no window plan -> the gather backward with dz and the weight gradients in one launch);
+* cfg5's graph (10,000 stations, k=32: in-degree 33, above the fused forward's limit;
+  3 GINE layers; 120h_normal_mixed) at 1 graph.
+
+At the configs' full sizes (cfg3: 64 graphs, 128,000 nodes; cfg5: 8 graphs, 80,000 nodes),
+where an oracle step would take minutes, size-independent properties: the step is finite
+and bit-identical when re-run from the same state, and the fused and unfused forward
+kernels give bit-identical gradients (same z / a1 / BatchNorm integer sums).
+"""
+import copy
+
+import pytest
+import torch
+
+from helpers import check_training_step
+from raincast_gnn.data import synthetic_batch
+from raincast_gnn.params import BENCH_CONFIGS
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+TOL = 1e-5
+
+
+@pytest.mark.parametrize("cfg,graphs", [(2, 32), (3, 4), (3, 9), (5, 1)],
+                         ids=["cfg2-full", "cfg3-b4-fused", "cfg3-b9-gather", "cfg5-b1"])
+def test_training_step_matches_oracle_at_config(cfg, graphs):
+    c = BENCH_CONFIGS[cfg]
+    params = c.params()
+    batch = synthetic_batch(c.num_stations, graphs, k=c.k, seed=100 + cfg)
+    worst = check_training_step(params, batch, DEV, TOL, envelope_threads=(1, 2, 4))
+    print(f"{c.name} x{graphs}: worst grad rel err vs fp32 oracle {worst:.2e}")
+
+
+def _grads_after_step(model, batch):
+    model.zero_grad(set_to_none=True)
+    loss = model.loss_fn.crps(model(batch), batch.y)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach().clone(), [p.grad.detach().clone() for p in model.parameters()]
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_full_size_step_deterministic_and_fused_equal(cfg, monkeypatch):
+    from raincast_gnn.models import gnn_from_params
+    c = BENCH_CONFIGS[cfg]
+    torch.manual_seed(42)
+    base = gnn_from_params(c.params()).to(DEV).train()
+    batch = synthetic_batch(c.num_stations, c.graphs_per_gpu, k=c.k, seed=1000).to(DEV)
+    assert batch.num_nodes == c.num_stations * c.graphs_per_gpu
+
+    def run(mode):
+        monkeypatch.setenv("GINE_MP_FUSED", mode)
+        return _grads_after_step(copy.deepcopy(base), batch)
+
+    l0, g0 = run("1")       # what the training step runs at this size
+    l1, g1 = run("1")
+    assert torch.isfinite(l0) and all(torch.isfinite(g).all() for g in g0)
+    assert torch.equal(l0, l1) and all(torch.equal(a, b) for a, b in zip(g0, g1))
+    # cfg3: in-degree 17 -> the fused forward applies once the size gate is lifted;
+    # cfg5: in-degree 33 is beyond it, so "all" must fall back to the same kernels
+    l2, g2 = run("all")
+    l3, g3 = run("0")
+    assert torch.equal(l2, l3) and all(torch.equal(a, b) for a, b in zip(g2, g3))
+    assert torch.equal(l0, l3) and all(torch.equal(a, b) for a, b in zip(g0, g3))
+
+
+def test_device_collation_on_gpu_matches_collate():
+    """Row a9: DeviceDataset.batch on the HIP device equals PyG-style collation."""
+    from raincast_gnn.batching import DeviceDataset
+    from raincast_gnn.data import collate, synthetic_samples
+    samples = synthetic_samples(500, 12, k=10, seed=5)
+    ds = DeviceDataset(samples, DEV)
+    idx = torch.tensor([11, 3, 3, 0, 7, 9], device=DEV)
+    got = ds.batch(idx)
+    ref = collate([samples[i] for i in idx.tolist()])
+    for name in ("x", "ensemble", "edge_index", "edge_attr", "batch", "ptr"):
+        a = getattr(got, name)
+        assert a.device.type == "cuda", name
+        assert torch.equal(a.cpu(), getattr(ref, name)), name
+    assert torch.equal(got.y.isnan().cpu(), ref.y.isnan())
+    assert torch.equal(torch.nan_to_num(got.y).cpu(), torch.nan_to_num(ref.y))
+    assert got.num_graphs == ref.num_graphs == 6
+    # ...and the model gives the same bits on either batch
+    from raincast_gnn.models import gnn_from_params
+    from raincast_gnn.params import EXPERIMENTS
+    torch.manual_seed(0)
+    m = gnn_from_params(EXPERIMENTS["24h_mixed"]).to(DEV).eval()
+    with torch.no_grad():
+        assert torch.equal(m(got), m(ref.to(DEV)))

@@ -10,7 +10,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import assert_close_tiebreak, knn_batch_graph, random_graph, rel_err, special_graphs
+from helpers import (assert_close_tiebreak, check_training_step, knn_batch_graph, random_graph,
+                     rel_err, special_graphs)
 from oracle import gine_cpu as O
 from raincast_gnn import GINEConv, _lib, functional as Fn
 from raincast_gnn.graph import GineGraph
@@ -349,68 +350,16 @@ def test_layer_deterministic_and_errors():
 # ---------------------------------------------------------------------------------------
 # full models
 # ---------------------------------------------------------------------------------------
-def _oracle_gnn_from(model: GNN, params) -> O.OracleGNN:
-    ref = O.OracleGNN(35, params["gnn_hidden"], params["gnn_layers"], params["loss"],
-                      params["grad_u"], params["u"], params["xi"])
-    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()},
-                        strict=True)
-    return ref
-
-
-def _oracle_step(ref, batch, dtype, record=False):
-    r = copy.deepcopy(ref).to(dtype)
-    if record:
-        for conv in r.conv.convolutions:
-            conv.record = []
-    b = copy.copy(batch)
-    b.x, b.ensemble, b.edge_attr = (t.to(dtype) for t in (batch.x, batch.ensemble,
-                                                          batch.edge_attr))
-    pred = r(b)
-    loss = r.crps(pred, batch.y)
-    loss.backward()
-    return r, pred, loss
-
-
 @pytest.mark.parametrize("experiment", ["24h_mixed", "72h_mixed_u", "120h_normal_mixed",
                                         "24h_normal"])
 def test_training_step_matches_oracle(experiment):
-    """Full train-step gradients (DeepSet + 4 GINE layers + head + loss) vs the oracle.
-    Linear1's bias gradient is analytically zero (train-mode BN follows it), so every
-    comparison goes through the fp64 tie-break."""
+    """Full train-step gradients (DeepSet + 4 GINE layers + head + loss) vs the oracle
+    (tests/helpers.py: check_training_step; the benchmark shapes are in
+    tests/test_gpu_configs.py)."""
     from raincast_gnn.data import synthetic_batch
     from raincast_gnn.params import EXPERIMENTS
-    params = dict(EXPERIMENTS[experiment])
-    torch.manual_seed(42)
-    model = GNN(35, params["gnn_hidden"], params["gnn_hidden"], params["gnn_layers"],
-                loss=params["loss"], grad_u=params["grad_u"], u=params["u"], xi=params["xi"])
-    ref = _oracle_gnn_from(model, params)
-    batch = synthetic_batch(500, 2, k=10, seed=7)
-    model = model.to(DEV).train()
-    pred = model(batch.to(DEV))
-    loss = model.loss_fn.crps(pred, batch.y.to(DEV))
-    loss.backward()
-    r32, pred32, loss32 = _oracle_step(ref, batch, torch.float32)
-    r64, pred64, loss64 = _oracle_step(ref, batch, torch.float64, record=True)
-    assert loss.dtype == loss32.dtype
-    assert_close_tiebreak(pred.detach().cpu(), pred32.detach(), pred64.detach(), TOL, "pred")
-    assert_close_tiebreak(loss.detach().cpu().reshape(1), loss32.detach().reshape(1),
-                          loss64.detach().reshape(1), TOL, "loss")
-    p32, p64 = dict(r32.named_parameters()), dict(r64.named_parameters())
-    worst = 0.0
-    for name, p in model.named_parameters():
-        if name.endswith(".eps"):
-            # d eps = sum_{n,c} dz*x: one cancelling reduction over N*D terms, whose relative
-            # error is ill-conditioned in any fp32 implementation (the fp32 CPU oracle itself
-            # is up to ~1e-4 off the exact value).  Check it against its condition scale:
-            # |gpu - exact| <= TOL * sum |dz*x|  (exact = fp64 oracle).
-            i = int(name.split(".")[2])
-            x64, dz64 = r64.conv.convolutions[i].record[0]
-            scale = (dz64 * x64).abs().sum().item()
-            err = abs(p.grad.item() - p64[name].grad.item())
-            assert err <= TOL * scale, f"{name}: |err| {err:.3e} > {TOL} * {scale:.3e}"
-            continue
-        e = assert_close_tiebreak(p.grad.cpu(), p32[name].grad, p64[name].grad, TOL, name)
-        worst = max(worst, e)
+    worst = check_training_step(dict(EXPERIMENTS[experiment]),
+                                synthetic_batch(500, 2, k=10, seed=7), DEV, TOL)
     print(f"{experiment}: worst grad rel err vs fp32 oracle {worst:.2e}")
 
 
