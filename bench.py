@@ -6,7 +6,9 @@ One step = one full training step exactly as train.py:55-74 does it -- DeepSet +
 4 GINE layers (HIP engine) + head + PostProcess + MixedLoss + backward + AdamW -- on one
 pre-collated batch resident in HBM.  N=1 runs configs[1] (500-station k=10 graphs, 32 per
 GPU); with N>1 every rank runs its own 32 graphs (weak scaling) and the gradient is
-averaged with one RCCL all-reduce per step.
+averaged with one RCCL all-reduce per step, captured in the step's HIP graph.  The same run
+also measures cfg4 (global batch 256 split over the N ranks: strong scaling) and reports
+it as ``strong_scaling_cfg4``.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -60,6 +62,15 @@ def parse():
                     help="target duration of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the cfg4 strong-scaling line (global batch 256) that the "
+                         "default cfg2 run adds")
+    ap.add_argument("--allreduce", choices=("graph", "split"), default="graph",
+                    help="graph: the gradient all-reduce captured inside the step's HIP "
+                         "graph (falls back to split if capture fails); split: fwd+bwd "
+                         "graph, eager all-reduce, optimizer graph")
+    ap.add_argument("--force-allreduce", action="store_true",
+                    help="run the all-reduce even with one rank (rehearsal of the capture)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm, the benchmark) | gloo (multi-rank rehearsal on "
                          "one GPU: ranks share the device)")
@@ -70,8 +81,11 @@ def parse():
 # training step
 # -----------------------------------------------------------------------------------------
 class Trainer:
-    def __init__(self, cfg, device, rank, world, graphs_per_rank):
+    def __init__(self, cfg, device, rank, world, graphs_per_rank, allreduce="graph",
+                 force_allreduce=False):
         self.cfg, self.device, self.world = cfg, device, world
+        self.allreduce = allreduce
+        self.collective = world > 1 or force_allreduce
         params = cfg.params()
         self.params = params
         torch.manual_seed(42)
@@ -82,9 +96,11 @@ class Trainer:
         # AdamW (train.py:185, torch defaults betas/eps/weight_decay) over one flat buffer;
         # the same flat gradient buffer is what the data-parallel all-reduce reduces
         self.opt = FlatAdamW(self.model.parameters(), lr=params["lr"])
-        self.reducer = FlatGradReducer(self.model.parameters(), flat=self.opt.flat_grad)
+        self.reducer = FlatGradReducer(self.model.parameters(), flat=self.opt.flat_grad,
+                                       force=force_allreduce)
         self.graph_fb = self.graph_opt = None
         self.loss = None
+        self.allreduce_in_graph = False
 
     def fwd_bwd(self):
         self.opt.zero_grad()            # set_to_none: kernels write grads into flat slices
@@ -101,23 +117,40 @@ class Trainer:
         return loss
 
     def capture(self):
-        """fwd+bwd (+ optimizer when there is no collective) as HIP graphs."""
+        """The whole step as ONE HIP graph -- fwd + bwd, the RCCL gradient all-reduce (when
+        there is a collective) and AdamW.  If the collective cannot be captured (or
+        ``allreduce="split"``), fwd+bwd and AdamW are two graphs with the all-reduce
+        launched between them."""
+        if not self.collective or self.allreduce == "graph":
+            try:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.loss = self.fwd_bwd()
+                    if self.collective:
+                        self.reducer.all_reduce_()
+                    self.opt.step()
+                self.graph_fb, self.graph_opt = g, None
+                self.allreduce_in_graph = self.collective
+                assert self.opt.views_intact()
+                return
+            except Exception as e:  # noqa: BLE001 -- fall back to the split form
+                if not self.collective:
+                    raise
+                log(f"all-reduce capture failed ({type(e).__name__}: {e}); split graphs")
+                torch.cuda.synchronize(self.device)
         self.graph_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph_fb):
             self.loss = self.fwd_bwd()
-            if self.world == 1:
-                self.opt.step()
-        if self.world > 1:
-            self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt):
-                self.opt.step()
+        self.graph_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_opt):
+            self.opt.step()
         assert self.opt.views_intact()
 
     def step(self):
         if self.graph_fb is None:
             return self.eager_step()
         self.graph_fb.replay()
-        if self.world > 1:
+        if self.graph_opt is not None:
             self.reducer.all_reduce_()
             self.graph_opt.replay()
         return self.loss
@@ -507,24 +540,11 @@ def cpu_baseline(cfg, graphs, seconds):
 
 
 # -----------------------------------------------------------------------------------------
-def main():
-    args = parse()
-    rank, local_rank, world = env_rank()
-    if world > 1:
-        dist.init_process_group(args.dist_backend)
-    device = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(device)
-    cfg = BENCH_CONFIGS[args.config]
-    if args.config == 4:  # global batch fixed -> strong scaling
-        graphs_per_rank = cfg.graphs_per_gpu // world
-        scaling = "strong"
-    else:
-        graphs_per_rank = cfg.graphs_per_gpu
-        scaling = "weak"
-    tr = Trainer(cfg, device, rank, world, graphs_per_rank)
-    layers = tr.params["gnn_layers"]
-    E_rank = tr.batch.edge_index.size(1)
-
+def measure(cfg, graphs_per_rank, args, device, rank, world):
+    """Build the trainer, warm up, capture, then time ``args.steps`` steps between barriers
+    + synchronisations; returns (trainer, max-over-ranks seconds, HIP-event percentiles)."""
+    tr = Trainer(cfg, device, rank, world, graphs_per_rank, args.allreduce,
+                 args.force_allreduce)
     side = torch.cuda.Stream(device)
     side.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(side):
@@ -561,6 +581,26 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    return tr, elapsed, pct
+
+
+def main():
+    args = parse()
+    rank, local_rank, world = env_rank()
+    if world > 1 or args.force_allreduce:
+        dist.init_process_group(args.dist_backend)
+    device = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(device)
+    cfg = BENCH_CONFIGS[args.config]
+    if args.config == 4:  # global batch fixed -> strong scaling
+        graphs_per_rank = cfg.graphs_per_gpu // world
+        scaling = "strong"
+    else:
+        graphs_per_rank = cfg.graphs_per_gpu
+        scaling = "weak"
+    tr, elapsed, pct = measure(cfg, graphs_per_rank, args, device, rank, world)
+    layers = tr.params["gnn_layers"]
+    E_rank = tr.batch.edge_index.size(1)
     loss_val = float(tr.loss.item()) if tr.loss is not None else float("nan")
 
     graphs_global = graphs_per_rank * world
@@ -568,6 +608,23 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = graphs_global * args.steps / elapsed
     edges_per_s = edges_global * layers * args.steps / elapsed
+
+    strong = None
+    if args.config == 2 and not args.no_strong:
+        # the same model at a fixed global batch of 256 graphs split over
+        # the ranks (strong scaling), measured in the same run as the weak-scaling line
+        c4 = BENCH_CONFIGS[4]
+        g4 = c4.graphs_per_gpu // world
+        tr4, el4, pct4 = measure(c4, g4, args, device, rank, world)
+        strong = {"config": "cfg4", "global_batch": g4 * world, "graphs_per_gpu": g4,
+                  "value": round(g4 * world * args.steps / el4, 2), "unit": "graphs/s",
+                  "ms_per_step": round(el4 / args.steps * 1e3, 4),
+                  "step_ms_p10_p50_p90": [pct4[10], pct4[50], pct4[90]],
+                  "scaling": "strong",
+                  "edges_aggregated_per_s": round(tr4.batch.edge_index.size(1) * world
+                                                  * layers * args.steps / el4, 1)}
+        del tr4
+        torch.cuda.empty_cache()
 
     kernels = time_kernels(tr, args.kernel_reps) if rank == 0 else {}
     result = None
@@ -595,16 +652,18 @@ def main():
                                    f"{layers} GINE layers, D={tr.params['gnn_hidden']}",
                        "global_batch": graphs_global, "graphs_per_gpu": graphs_per_rank,
                        "nodes_per_gpu": tr.batch.num_nodes, "edges_per_gpu": E_rank,
-                       "parallelism": f"dp{world}", "hip_graph": not args.no_graph},
+                       "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
+                       "allreduce_in_graph": tr.allreduce_in_graph},
             "edges_aggregated_per_s": round(edges_per_s, 1),
             "step_ms_p10_p50_p90": [pct[10], pct[50], pct[90]],
             "roofline": roof, "roofline_step": roof_step,
             "roofline_message_passing": roof_mp,
+            "strong_scaling_cfg4": strong,
             "cpu_baseline": cpu, "kernels": kernels,
             "final_loss": loss_val,
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

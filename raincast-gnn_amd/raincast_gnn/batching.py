@@ -43,6 +43,19 @@ class DeviceDataset:
     def __len__(self) -> int:
         return self.x.size(0)
 
+    def subset(self, indices) -> "DeviceDataset":
+        """The samples ``indices`` (any order) as a dataset sharing this one's graph
+        (``torch.utils.data.Subset`` after ``random_split``, train.py:150)."""
+        idx = torch.as_tensor(indices, dtype=torch.long).to(self.device)
+        out = DeviceDataset.__new__(DeviceDataset)
+        out.device, out.num_stations = self.device, self.num_stations
+        out.x = self.x.index_select(0, idx)
+        out.ensemble = self.ensemble.index_select(0, idx)
+        out.y = self.y.index_select(0, idx)
+        out.edge_index, out.edge_attr = self.edge_index, self.edge_attr
+        out._blocks = self._blocks   # same station graph: share the per-size edge lists
+        return out
+
     def block_graph(self, num_graphs: int):
         """(edge_index, edge_attr, batch, ptr) of ``num_graphs`` copies of the station graph,
         built once per size and returned as the same tensors afterwards."""
@@ -73,14 +86,19 @@ class DeviceDataset:
 
 
 class DeviceLoader:
-    """Epoch iterator over a :class:`DeviceDataset` (train.py:155: shuffle=True,
-    batch_size from params.json); the permutation is drawn on the device."""
+    """Epoch iterator over a :class:`DeviceDataset` (train.py:155-156: ``shuffle=True``,
+    ``batch_size`` from params.json).  The permutation is drawn from a seeded CPU generator
+    (``torch.randperm``, as PyG's DataLoader's RandomSampler does), so the batch order is the
+    same whatever the dataset's device.  With ``world > 1`` every rank walks the same global
+    batches and yields its contiguous shard of graphs (:func:`~raincast_gnn.distributed.
+    shard_range`); a (short, last) batch with fewer graphs than ranks is skipped by all."""
 
     def __init__(self, dataset: DeviceDataset, batch_size: int, shuffle: bool = True,
-                 seed: int = 0, drop_last: bool = False):
+                 seed: int = 0, drop_last: bool = False, rank: int = 0, world: int = 1):
         self.dataset, self.batch_size = dataset, int(batch_size)
         self.shuffle, self.drop_last = shuffle, drop_last
-        self._gen = torch.Generator(device=dataset.device)
+        self.rank, self.world = int(rank), int(world)
+        self._gen = torch.Generator()
         self._gen.manual_seed(seed)
 
     def __len__(self) -> int:
@@ -88,12 +106,16 @@ class DeviceLoader:
         return T // self.batch_size if self.drop_last else -(-T // self.batch_size)
 
     def __iter__(self):
+        from .distributed import shard_range
         T = len(self.dataset)
-        dev = self.dataset.device
-        order = (torch.randperm(T, generator=self._gen, device=dev) if self.shuffle
-                 else torch.arange(T, device=dev))
+        order = torch.randperm(T, generator=self._gen) if self.shuffle else torch.arange(T)
         for i in range(0, T, self.batch_size):
             idx = order[i:i + self.batch_size]
             if self.drop_last and idx.numel() < self.batch_size:
                 return
+            if self.world > 1:
+                if idx.numel() < self.world:  # some rank would get no graph: every rank
+                    continue                  # skips it (they all see the same order)
+                lo, hi = shard_range(idx.numel(), self.rank, self.world)
+                idx = idx[lo:hi]
             yield self.dataset.batch(idx)

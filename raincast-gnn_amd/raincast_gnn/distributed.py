@@ -6,7 +6,9 @@ graphs across ranks needs no halo exchange; the only exchange is the gradient.  
 holds ~0.2 M fp32 parameters (209,800 for 24h_mixed = 839 KB), far below what a ring needs to
 become bandwidth-bound on xGMI, so the gradient lives in ONE flat buffer and is reduced with
 ONE RCCL all-reduce per step (no bucketing, no per-parameter collectives).  BatchNorm keeps
-per-rank batch statistics, like the reference's single-process BN over its own batch.
+per-rank batch statistics, like the reference's single-process BN over its own batch; the
+running buffers are broadcast from rank 0 before they are read (validation, checkpoints:
+raincast_gnn/train.py), which gives DistributedDataParallel's buffer semantics there.
 """
 from __future__ import annotations
 
@@ -30,7 +32,9 @@ class FlatGradReducer:
     single collective.  Optimisers see ordinary ``.grad`` tensors.
     """
 
-    def __init__(self, params, group=None, flat: torch.Tensor | None = None):
+    def __init__(self, params, group=None, flat: torch.Tensor | None = None,
+                 force: bool = False):
+        self.force = force  # all-reduce even in a 1-rank group (rehearsing the collective)
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("no trainable parameters")
@@ -62,7 +66,7 @@ class FlatGradReducer:
         if not (dist.is_available() and dist.is_initialized()):
             return
         world = dist.get_world_size(self.group)
-        if world == 1:
+        if world == 1 and not self.force:
             return
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.div_(world)
