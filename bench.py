@@ -36,7 +36,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from raincast_gnn import functional as Fn  # noqa: E402
-from raincast_gnn.data import synthetic_batch  # noqa: E402
+from raincast_gnn.data import relabel_stations, synthetic_batch  # noqa: E402
+from raincast_gnn.data import station_order as station_order_of  # noqa: E402
 from raincast_gnn.distributed import FlatGradReducer, broadcast_parameters, env_rank  # noqa: E402
 from raincast_gnn.graph import get_graph  # noqa: E402
 from raincast_gnn.models import gnn_from_params  # noqa: E402
@@ -69,6 +70,10 @@ def parse():
                     help="graph: the gradient all-reduce captured inside the step's HIP "
                          "graph (falls back to split if capture fails); split: fwd+bwd "
                          "graph, eager all-reduce, optimizer graph")
+    ap.add_argument("--station-order", choices=("locality", "dataset"), default="locality",
+                    help="locality: the batch in the engine's station order (reverse "
+                         "Cuthill-McKee, raincast_gnn.data.station_order -- the device "
+                         "loader's layout); dataset: the reference's collated order")
     ap.add_argument("--force-allreduce", action="store_true",
                     help="run the all-reduce even with one rank (rehearsal of the capture)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -82,7 +87,7 @@ def parse():
 # -----------------------------------------------------------------------------------------
 class Trainer:
     def __init__(self, cfg, device, rank, world, graphs_per_rank, allreduce="graph",
-                 force_allreduce=False):
+                 force_allreduce=False, station_order="locality"):
         self.cfg, self.device, self.world = cfg, device, world
         self.allreduce = allreduce
         self.collective = world > 1 or force_allreduce
@@ -91,8 +96,14 @@ class Trainer:
         torch.manual_seed(42)
         self.model = gnn_from_params(params).to(device).train()
         broadcast_parameters(self.model)
-        self.batch = synthetic_batch(cfg.num_stations, graphs_per_rank, k=cfg.k,
-                                     seed=1000 + rank).to(device)
+        batch = synthetic_batch(cfg.num_stations, graphs_per_rank, k=cfg.k, seed=1000 + rank)
+        if station_order == "locality":
+            # the layout DeviceDataset stores samples in (raincast_gnn/batching.py): every
+            # graph's stations in reverse Cuthill-McKee order, edges relabelled, edge order
+            # kept; collation itself stays outside the timed step, as in the reference
+            graph0 = batch.edge_index[:, :batch.edge_index.size(1) // graphs_per_rank]
+            batch = relabel_stations(batch, station_order_of(graph0, cfg.num_stations))
+        self.batch = batch.to(device)
         # AdamW (train.py:185, torch defaults betas/eps/weight_decay) over one flat buffer;
         # the same flat gradient buffer is what the data-parallel all-reduce reduces
         self.opt = FlatAdamW(self.model.parameters(), lr=params["lr"])
@@ -260,6 +271,17 @@ def time_kernels(tr: Trainer, reps: int):
                                               ptr(lw_g), ptr(lb_g), ptr(eps_g), S[0]), {}),
     }
 
+    # the LDS-window forward (GINE_MP_WINDOW=all), for comparison with the gather forward
+    from raincast_gnn.graph import plan_windows
+    fwin = plan_windows(g.in_rowptr, g.in_src, N, dev, 128).get(32)
+    if fwin is not None:
+        fplan = fwin[0]
+        kernels["gine_mp_fwd_win"] = (
+            lambda: call("gine_mp_fwd_win", ptr(x), ptr(g.in_rowptr), ptr(g.in_src),
+                         ptr(g.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(z), N, D, lin,
+                         ctypes.byref(fplan), S[0]),
+            {"bytes": 4 * (2 * N * D + 2 * E + N + 1)})
+
     def mp_fwd_mlp1():  # the fused forward (gather + Linear1 + BN partials)
         call("gine_mp_fwd_mlp1", ptr(x), ptr(g.in_rowptr), ptr(g.in_src), ptr(g.in_attr),
              ptr(lw), ptr(lb), ptr(ep), ptr(w1), ptr(b1), ptr(z), ptr(a1), ptr(partials), N,
@@ -344,7 +366,7 @@ def sec8d_work(N: int, E: int, D: int) -> dict:
 def sec8d_launch_work(name: str, w: dict) -> dict:
     half_fwd, half_bwd = w["mlp_fwd_flops"] // 2, w["mlp_bwd_flops"] // 4
     return {
-        "gine_mp_fwd": {"bytes": w["B_f"]},
+        "gine_mp_fwd": {"bytes": w["B_f"]}, "gine_mp_fwd_win": {"bytes": w["B_f"]},
         "gine_mp_bwd": {"bytes": w["B_b"]},
         "gine_mp_fwd_mlp1": {"bytes": w["B_f"], "flops": half_fwd},
         "gine_mp_bwd_mlp_wgrad": {"bytes": w["B_b"], "flops": 2 * half_bwd},
@@ -406,7 +428,7 @@ def roofline_mp(kernels: dict, layers: int, work: dict):
     """The message-passing kernels (the north-star gather / segmented-scatter path) alone
     against HBM, with the measured copy ceiling beside the 8 TB/s spec."""
     out = {}
-    for name in ("gine_mp_fwd", "gine_mp_bwd"):
+    for name in ("gine_mp_fwd", "gine_mp_fwd_win", "gine_mp_bwd"):
         if name in kernels:
             out[name] = roof_of(name, kernels[name], layers, work)
     return out or None
@@ -544,7 +566,7 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     """Build the trainer, warm up, capture, then time ``args.steps`` steps between barriers
     + synchronisations; returns (trainer, max-over-ranks seconds, HIP-event percentiles)."""
     tr = Trainer(cfg, device, rank, world, graphs_per_rank, args.allreduce,
-                 args.force_allreduce)
+                 args.force_allreduce, args.station_order)
     side = torch.cuda.Stream(device)
     side.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(side):
@@ -653,6 +675,7 @@ def main():
                        "global_batch": graphs_global, "graphs_per_gpu": graphs_per_rank,
                        "nodes_per_gpu": tr.batch.num_nodes, "edges_per_gpu": E_rank,
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
+                       "station_order": args.station_order,
                        "allreduce_in_graph": tr.allreduce_in_graph},
             "edges_aggregated_per_s": round(edges_per_s, 1),
             "step_ms_p10_p50_p90": [pct[10], pct[50], pct[90]],

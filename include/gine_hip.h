@@ -142,6 +142,15 @@ int gine_graph_plan_windows(const int32_t* rowptr, const int32_t* nbr, int64_t n
                             int32_t max_rows, int32_t max_nodes, int32_t max_edges,
                             int32_t* tile_begin, int32_t* win_lo, int32_t* win_rows,
                             int32_t* num_tiles, int32_t* maxima);
+/* Locality order of a graph's nodes (HOST pointers: a host copy of a CSR, either
+ * direction; the adjacency is symmetrised).  order[i] = the node placed at position i:
+ * reverse Cuthill-McKee, deterministic.  Relabelling a static station graph this way before
+ * batching (raincast_gnn.data.relabel_stations) narrows every tile's neighbour window (the
+ * reference's dataset order, utils/data.py:261-284, scatters k-NN neighbours over the whole
+ * graph).  Per-node results are unchanged: each node keeps its in/out edges in their
+ * original relative order. */
+int gine_graph_order_locality(const int32_t* rowptr, const int32_t* nbr, int64_t num_nodes,
+                              int32_t* order);
 int gine_mp_fwd_win(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                     const float* in_attr, const float* lin_w, const float* lin_b,
                     const float* eps, float* z, int64_t num_nodes, int32_t channels,

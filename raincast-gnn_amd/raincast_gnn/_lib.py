@@ -65,6 +65,7 @@ _SIGNATURES = {
     "gine_mp_bwd_side": [_c_void_p] * 11 + [_i64, _i32, _i32, _c_void_p, _i32, _i32]
                         + [_c_void_p] * 5,
     "gine_mp_bwd_finalize": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "gine_graph_order_locality": [_c_void_p, _c_void_p, _i64, _c_void_p],
     "gine_graph_plan_windows": [_c_void_p, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p,
                                 _c_void_p, _c_void_p, ctypes.POINTER(_i32), _c_void_p],
     "gine_mp_fwd_win": [_c_void_p] * 8 + [_i64, _i32, _i32, _plan_p, _c_void_p],

@@ -10,20 +10,25 @@ so it is built once per B and the SAME tensor object is returned for every batch
 size: the engine's graph cache (raincast_gnn/graph.py, keyed on tensor identity) then
 sorts it into its two CSRs once for the whole run instead of once per step.
 
-Node order, edge order and attributes are exactly PyG collation's (tests/test_batching.py
-compares with :func:`raincast_gnn.data.collate`).
+With ``relabel=False`` node order, edge order and attributes are exactly PyG collation's
+(tests/test_batching.py compares with :func:`raincast_gnn.data.collate`).  By default the
+stations are stored in the engine's locality order (:func:`raincast_gnn.data.station_order`,
+reverse Cuthill-McKee): every graph of a batch has its stations permuted the same way and
+the edge list relabelled with its edge order kept, so each node's result is the one the
+reference order gives (bit for bit through the message passing), stored at another row;
+``batch.extra["node_order"]`` maps the rows back (:func:`raincast_gnn.data.restore_node_order`).
 """
 from __future__ import annotations
 
 import torch
 
-from .data import GraphBatch
+from .data import GraphBatch, block_node_order, relabel_edges, station_order
 
 
 class DeviceDataset:
     """Samples of one station graph, stacked on ``device``."""
 
-    def __init__(self, samples: list[GraphBatch], device):
+    def __init__(self, samples: list[GraphBatch], device, relabel: bool = True):
         if not samples:
             raise ValueError("empty dataset")
         base = samples[0]
@@ -38,6 +43,14 @@ class DeviceDataset:
         self.y = torch.stack([s.y for s in samples]).to(self.device)
         self.edge_index = base.edge_index.to(self.device)
         self.edge_attr = base.edge_attr.to(self.device)
+        self.order = None   # station at each stored position (None: the dataset's order)
+        if relabel and self.num_stations > 1:
+            order = station_order(base.edge_index, self.num_stations).to(self.device)
+            self.order = order
+            self.x = self.x.index_select(1, order)
+            self.ensemble = self.ensemble.index_select(1, order)
+            self.y = self.y.index_select(1, order)
+            self.edge_index = relabel_edges(self.edge_index, order)
         self._blocks: dict[int, tuple] = {}
 
     def __len__(self) -> int:
@@ -52,13 +65,14 @@ class DeviceDataset:
         out.x = self.x.index_select(0, idx)
         out.ensemble = self.ensemble.index_select(0, idx)
         out.y = self.y.index_select(0, idx)
-        out.edge_index, out.edge_attr = self.edge_index, self.edge_attr
+        out.edge_index, out.edge_attr, out.order = self.edge_index, self.edge_attr, self.order
         out._blocks = self._blocks   # same station graph: share the per-size edge lists
         return out
 
     def block_graph(self, num_graphs: int):
-        """(edge_index, edge_attr, batch, ptr) of ``num_graphs`` copies of the station graph,
-        built once per size and returned as the same tensors afterwards."""
+        """(edge_index, edge_attr, batch, ptr, node_order) of ``num_graphs`` copies of the
+        station graph, built once per size and returned as the same tensors afterwards
+        (node_order: row map back to the collated order, None without relabelling)."""
         hit = self._blocks.get(num_graphs)
         if hit is None:
             n, E = self.num_stations, self.edge_index.size(1)
@@ -67,7 +81,8 @@ class DeviceDataset:
             ea = self.edge_attr.repeat(num_graphs, 1)
             batch = torch.arange(num_graphs, device=self.device).repeat_interleave(n)
             ptr = torch.arange(num_graphs + 1, device=self.device, dtype=torch.long) * n
-            hit = (ei.contiguous(), ea.contiguous(), batch, ptr)
+            rows = block_node_order(self.order, num_graphs) if self.order is not None else None
+            hit = (ei.contiguous(), ea.contiguous(), batch, ptr, rows)
             self._blocks[num_graphs] = hit
         return hit
 
@@ -75,14 +90,15 @@ class DeviceDataset:
         """The collated batch of samples ``indices`` (a device or host LongTensor)."""
         idx = indices.to(self.device, dtype=torch.long)
         B, n = idx.numel(), self.num_stations
-        ei, ea, batch, ptr = self.block_graph(B)
+        ei, ea, batch, ptr, rows = self.block_graph(B)
         F = self.x.size(-1)
+        extra = {} if rows is None else {"node_order": rows}
         return GraphBatch(
             x=self.x.index_select(0, idx).reshape(B * n, F),
             ensemble=self.ensemble.index_select(0, idx).reshape(B * n, *self.ensemble.shape[2:]),
             edge_index=ei, edge_attr=ea,
             y=self.y.index_select(0, idx).reshape(B * n),
-            batch=batch, ptr=ptr, num_graphs=B)
+            batch=batch, ptr=ptr, num_graphs=B, extra=extra)
 
 
 class DeviceLoader:

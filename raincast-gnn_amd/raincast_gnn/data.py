@@ -100,8 +100,9 @@ class GraphBatch:
 
     def to(self, device, non_blocking: bool = False) -> "GraphBatch":
         mv = lambda t: None if t is None else t.to(device, non_blocking=non_blocking)  # noqa: E731
+        extra = {k: mv(v) if isinstance(v, torch.Tensor) else v for k, v in self.extra.items()}
         return GraphBatch(mv(self.x), mv(self.ensemble), mv(self.edge_index), mv(self.edge_attr),
-                          mv(self.y), mv(self.batch), mv(self.ptr), self.num_graphs, dict(self.extra))
+                          mv(self.y), mv(self.batch), mv(self.ptr), self.num_graphs, extra)
 
 
 def collate(graphs: list[GraphBatch]) -> GraphBatch:
@@ -157,3 +158,85 @@ def synthetic_samples(num_stations: int, num_graphs: int, k: int = 10, seed: int
 def synthetic_batch(num_stations: int, num_graphs: int, k: int = 10, seed: int = 0,
                     **kw) -> GraphBatch:
     return collate(synthetic_samples(num_stations, num_graphs, k, seed, **kw))
+
+
+# -----------------------------------------------------------------------------------------
+# engine node order (station relabelling for neighbour locality)
+# -----------------------------------------------------------------------------------------
+def station_order(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
+    """Locality order of one station graph: ``order[i]`` = the station placed at position i
+    (reverse Cuthill-McKee over the symmetrised edge list, ``gine_graph_order_locality`` in
+    include/gine_hip.h; deterministic).  The reference's dataset order (utils/data.py:261-284)
+    scatters each station's k nearest neighbours over the whole index range; in this order
+    every edge stays within a short index band, so the window-staged message-passing tiles
+    (raincast_gnn.graph.plan_windows) stage a fraction of the graph instead of all of it."""
+    from . import _lib
+    n = int(num_nodes)
+    ei = edge_index.detach().to("cpu", torch.int64)
+    if ei.dim() != 2 or ei.size(0) != 2:
+        raise ValueError(f"edge_index must have shape [2, E], got {tuple(ei.shape)}")
+    if ei.numel() and (int(ei.min()) < 0 or int(ei.max()) >= n):
+        raise ValueError("edge_index holds node ids outside [0, num_nodes)")
+    src, dst = ei[0], ei[1]
+    rowptr = torch.zeros(n + 1, dtype=torch.int32)
+    rowptr[1:] = torch.cumsum(torch.bincount(dst, minlength=n), 0).to(torch.int32)
+    nbr = src[torch.argsort(dst, stable=True)].to(torch.int32).contiguous()
+    order = torch.empty(n, dtype=torch.int32)
+    _lib.call("gine_graph_order_locality", rowptr.data_ptr(), nbr.data_ptr() if nbr.numel() else None,
+              n, order.data_ptr())
+    return order.to(torch.int64)
+
+
+def inverse_order(order: torch.Tensor) -> torch.Tensor:
+    inv = torch.empty_like(order)
+    inv[order] = torch.arange(order.numel(), device=order.device, dtype=order.dtype)
+    return inv
+
+
+def block_node_order(order: torch.Tensor, num_graphs: int) -> torch.Tensor:
+    """Row map of a batch of ``num_graphs`` graphs sharing one station order: row r of the
+    relabelled batch is row ``block_node_order(...)[r]`` of the collated (reference) batch."""
+    n = order.numel()
+    offs = torch.arange(num_graphs, device=order.device, dtype=order.dtype) * n
+    return (order.view(1, -1) + offs.view(-1, 1)).reshape(-1)
+
+
+def relabel_edges(edge_index: torch.Tensor, order: torch.Tensor) -> torch.Tensor:
+    """Node ids of a block-diagonal edge list (graphs of ``order.numel()`` stations each)
+    mapped to the relabelled positions; the edge ORDER is kept, so every node's in- and
+    out-edges stay in their original relative order -- the order CPU ``scatter_add_`` and
+    ``index_add_`` accumulate in, hence bit-identical per-node z and dx."""
+    n = order.numel()
+    inv = inverse_order(order.to(edge_index.device))
+    return inv[edge_index % n] + (edge_index // n) * n
+
+
+def relabel_stations(batch: GraphBatch, order: torch.Tensor) -> GraphBatch:
+    """``batch`` (B graphs of one station set, collated graph-major) in the engine's node
+    order: the stations of every graph permuted by ``order`` and the edge list relabelled.
+    Graph membership (``batch``/``ptr``) is unchanged; ``extra["node_order"]`` maps rows back
+    (:func:`restore_node_order`).  Per-node model outputs are those of the reference order,
+    only stored at other rows; reductions over nodes (BatchNorm statistics, the loss mean,
+    parameter gradients) see the same terms in another order."""
+    n, B = order.numel(), batch.num_graphs
+    if batch.num_nodes != n * B:
+        raise ValueError(f"batch of {batch.num_nodes} nodes is not {B} graphs x {n} stations")
+    dev = batch.x.device
+    rows = block_node_order(order.to(dev), B)
+    extra = dict(batch.extra)
+    prev = extra.get("node_order")
+    extra["node_order"] = rows if prev is None else prev.to(dev)[rows]
+    return GraphBatch(
+        x=batch.x[rows], ensemble=batch.ensemble[rows],
+        edge_index=relabel_edges(batch.edge_index, order), edge_attr=batch.edge_attr,
+        y=batch.y[rows], batch=batch.batch, ptr=batch.ptr, num_graphs=B, extra=extra)
+
+
+def restore_node_order(t: torch.Tensor, batch: GraphBatch) -> torch.Tensor:
+    """Per-node rows of a relabelled batch's output back in the reference (collated) order."""
+    rows = batch.extra.get("node_order")
+    if rows is None:
+        return t
+    out = torch.empty_like(t)
+    out[rows.to(t.device)] = t
+    return out

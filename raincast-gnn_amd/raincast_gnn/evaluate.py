@@ -13,12 +13,16 @@ from typing import Iterable
 
 import torch
 
+from .data import restore_node_order
+
 
 @torch.no_grad()
 def predict_model(model: torch.nn.Module, batches: Iterable, device) -> torch.Tensor:
-    """eval.py:57-69: eval mode, one forward per batch, predictions concatenated on the CPU."""
+    """eval.py:57-69: eval mode, one forward per batch, predictions concatenated on the CPU
+    (rows in the collated order of each batch, whatever order the batch is stored in)."""
     model.eval()
-    out = [model(b.to(device)).cpu() for b in batches]
+    # batches in the engine's station order come back in the reference (collated) order
+    out = [restore_node_order(model(b.to(device)), b).cpu() for b in batches]
     return torch.cat(out, dim=0)
 
 

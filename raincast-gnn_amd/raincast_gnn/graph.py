@@ -28,6 +28,11 @@ WINDOW_ROW_BYTES = 64 * 1024
 # A window launch has tiles x slices workgroups; below this many the gather kernels (one
 # workgroup per 8 nodes) fill the chip better (measured: cfg1, 4 tiles, is slower staged).
 WINDOW_MIN_WORKGROUPS = 256
+# A plan whose windows together stage more than this many times the node table loses to
+# the gather kernels (measured r02_s11: cfg5's 10,000-station k=32 graph in locality order
+# plans 16-channel windows staging 10.8x the table, 186 us vs 118 us gathered; cfg2 in the
+# dataset order stages 4.0x and wins, 15.4 vs 18.1 us).
+WINDOW_MAX_STAGED = 6.0
 
 
 def window_settings() -> tuple[str, int]:
@@ -70,7 +75,7 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
                   max_nodes, max_edges, tb.data_ptr(), lo.data_ptr(), rows.data_ptr(),
                   ctypes.byref(nt), maxima.data_ptr())
         T = int(nt.value)
-        if T == 0:
+        if T == 0 or int(rows[:T].sum()) > WINDOW_MAX_STAGED * num_nodes:
             plans[cs] = None
             continue
         arrays = (tb[:T + 1].to(device), lo[:T].to(device), rows[:T].to(device))

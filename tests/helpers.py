@@ -102,7 +102,17 @@ def fro_rel(a: torch.Tensor, b: torch.Tensor) -> float:
     return (a - b).norm().item() / den if den else (a - b).norm().item()
 
 
-def check_training_step(params, batch, dev, tol=1e-5, seed=42, envelope_threads=None):
+def engine_order_batch(batch):
+    """``batch`` (B collated copies of one station graph) relabelled into the engine's
+    locality order (raincast_gnn.data.station_order / relabel_stations)."""
+    from raincast_gnn.data import relabel_stations, station_order
+    n = batch.num_nodes // batch.num_graphs
+    e1 = batch.edge_index.size(1) // batch.num_graphs   # graph 0's edges come first
+    return relabel_stations(batch, station_order(batch.edge_index[:, :e1], n))
+
+
+def check_training_step(params, batch, dev, tol=1e-5, seed=42, envelope_threads=None,
+                        relabel=False):
     """One training step (DeepSet + dim_red + GINE stack + head + PostProcess + loss +
     backward) of the engine's GNN on ``dev`` against the CPU oracle with the same weights.
 
@@ -124,6 +134,9 @@ def check_training_step(params, batch, dev, tol=1e-5, seed=42, envelope_threads=
     DESIGN.md 4).  There the bar is the reference's own envelope: for every parameter,
     ||gpu - fp64|| / ||fp64|| <= max(tol, 2 * the largest such error of the fp32 oracle over
     the thread counts ``envelope_threads``).
+    ``relabel``: the engine runs the batch in its locality order (engine_order_batch) and
+    its predictions are mapped back to the collated order; the oracle runs the reference
+    order.
     Returns the worst relative gradient error against the fp32 oracle."""
     from oracle import gine_cpu as O
     from raincast_gnn.models import GNN
@@ -135,9 +148,12 @@ def check_training_step(params, batch, dev, tol=1e-5, seed=42, envelope_threads=
     ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()},
                         strict=True)
     model = model.to(dev).train()
-    pred = model(batch.to(dev))
-    loss = model.loss_fn.crps(pred, batch.y.to(dev))
+    from raincast_gnn.data import restore_node_order
+    gb = engine_order_batch(batch) if relabel else batch
+    pred = model(gb.to(dev))
+    loss = model.loss_fn.crps(pred, gb.y.to(dev))
     loss.backward()
+    pred = restore_node_order(pred, gb)
     r32, pred32, loss32 = _oracle_step(ref, batch, torch.float32)
     r64, pred64, loss64 = _oracle_step(ref, batch, torch.float64, record=True)
     assert loss.dtype == loss32.dtype

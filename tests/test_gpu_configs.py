@@ -27,7 +27,7 @@ import copy
 import pytest
 import torch
 
-from helpers import check_training_step
+from helpers import check_training_step, engine_order_batch
 from raincast_gnn.data import synthetic_batch
 from raincast_gnn.params import BENCH_CONFIGS
 
@@ -36,14 +36,23 @@ DEV = torch.device("cuda:0")
 TOL = 1e-5
 
 
-@pytest.mark.parametrize("cfg,graphs", [(2, 32), (3, 4), (3, 9), (5, 1)],
-                         ids=["cfg2-full", "cfg3-b4-fused", "cfg3-b9-gather", "cfg5-b1"])
-def test_training_step_matches_oracle_at_config(cfg, graphs):
+@pytest.mark.parametrize("cfg,graphs,relabel",
+                         [(2, 32, False), (3, 4, False), (3, 9, False), (5, 1, False),
+                          (2, 32, True), (3, 9, True), (5, 1, True)],
+                         ids=["cfg2-full", "cfg3-b4-fused", "cfg3-b9-gather", "cfg5-b1",
+                              "cfg2-full-relabel", "cfg3-b9-relabel-window", "cfg5-b1-relabel"])
+def test_training_step_matches_oracle_at_config(cfg, graphs, relabel):
+    """relabel: the engine runs the batch in its station locality order (the order the
+    benchmark and the device loader use: narrow LDS windows, and at cfg3 a window plan where
+    the dataset order has none), predictions mapped back; the oracle runs the reference
+    order."""
     c = BENCH_CONFIGS[cfg]
     params = c.params()
     batch = synthetic_batch(c.num_stations, graphs, k=c.k, seed=100 + cfg)
-    worst = check_training_step(params, batch, DEV, TOL, envelope_threads=(1, 2, 4))
-    print(f"{c.name} x{graphs}: worst grad rel err vs fp32 oracle {worst:.2e}")
+    worst = check_training_step(params, batch, DEV, TOL, envelope_threads=(1, 2, 4),
+                                relabel=relabel)
+    print(f"{c.name} x{graphs} relabel={relabel}: worst grad rel err vs fp32 oracle "
+          f"{worst:.2e}")
 
 
 def _grads_after_step(model, batch):
@@ -84,7 +93,7 @@ def test_device_collation_on_gpu_matches_collate():
     from raincast_gnn.batching import DeviceDataset
     from raincast_gnn.data import collate, synthetic_samples
     samples = synthetic_samples(500, 12, k=10, seed=5)
-    ds = DeviceDataset(samples, DEV)
+    ds = DeviceDataset(samples, DEV, relabel=False)
     idx = torch.tensor([11, 3, 3, 0, 7, 9], device=DEV)
     got = ds.batch(idx)
     ref = collate([samples[i] for i in idx.tolist()])
@@ -102,3 +111,63 @@ def test_device_collation_on_gpu_matches_collate():
     m = gnn_from_params(EXPERIMENTS["24h_mixed"]).to(DEV).eval()
     with torch.no_grad():
         assert torch.equal(m(got), m(ref.to(DEV)))
+
+
+def test_relabelled_batch_gives_the_same_per_node_bits_in_eval():
+    """The station relabelling changes where a node's row is stored, not its value: in eval
+    mode (BatchNorm from running statistics, no reduction over nodes) every prediction of
+    the relabelled batch equals the collated batch's bit for bit once mapped back --
+    DeepSet, Linears and head are per node, and each node's message passing sums its edges
+    in the same (original) order."""
+    from raincast_gnn.batching import DeviceDataset
+    from raincast_gnn.data import collate, restore_node_order, synthetic_samples
+    from raincast_gnn.models import gnn_from_params
+    from raincast_gnn.params import EXPERIMENTS
+    samples = synthetic_samples(500, 12, k=10, seed=5)
+    ds = DeviceDataset(samples, DEV)            # default: engine (locality) order
+    assert ds.order is not None
+    idx = torch.tensor([11, 3, 3, 0, 7, 9], device=DEV)
+    got = ds.batch(idx)
+    ref = collate([samples[i] for i in idx.tolist()]).to(DEV)
+    assert torch.equal(restore_node_order(got.x, got), ref.x)
+    rows = got.extra["node_order"]
+    assert torch.equal(rows[got.edge_index], ref.edge_index)   # same edges, same order
+    torch.manual_seed(0)
+    m = gnn_from_params(EXPERIMENTS["24h_mixed"]).to(DEV)
+    with torch.no_grad():
+        m.train()
+        m(ref)                                   # non-trivial running statistics
+        m.eval()
+        assert torch.equal(restore_node_order(m(got), got), m(ref))
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 5])
+def test_relabelled_full_size_step_deterministic_and_close(cfg):
+    """The benchmark's batch (full size, engine order) against the same batch in the
+    reference order on the engine: both steps finite and deterministic; the loss and the
+    predictions equal within 1e-5 (only the order of node reductions differs)."""
+    from raincast_gnn.data import restore_node_order
+    from raincast_gnn.models import gnn_from_params
+    c = BENCH_CONFIGS[cfg]
+    torch.manual_seed(42)
+    base = gnn_from_params(c.params()).to(DEV).train()
+    batch = synthetic_batch(c.num_stations, c.graphs_per_gpu, k=c.k, seed=1000)
+    rb = engine_order_batch(batch).to(DEV)
+    batch = batch.to(DEV)
+
+    def run(b):
+        m = copy.deepcopy(base)
+        pred = m(b)
+        loss = m.loss_fn.crps(pred, b.y)
+        loss.backward()
+        torch.cuda.synchronize()
+        return (restore_node_order(pred.detach(), b), loss.detach(),
+                [p.grad.detach().clone() for p in m.parameters()])
+
+    p0, l0, g0 = run(rb)
+    p1, l1, g1 = run(rb)
+    assert torch.isfinite(l0) and all(torch.isfinite(g).all() for g in g0)
+    assert torch.equal(l0, l1) and all(torch.equal(a, b) for a, b in zip(g0, g1))
+    pr, lr, _ = run(batch)
+    assert abs(l0.item() - lr.item()) <= TOL * abs(lr.item())
+    assert (p0 - pr).abs().max().item() <= TOL * pr.abs().max().item()

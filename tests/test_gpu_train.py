@@ -3,8 +3,9 @@ engine against the same loop on the CPU oracle, and engine-level data parallelis
 
 * Two epochs (sanity forward, shuffled train batches with HIP-graph replays after the first
   two steps of each batch size, validation, best checkpoint) follow the oracle's loss
-  trajectory: per-epoch train and validation losses within 1e-5 relative (both run AdamW,
-  lr 1e-4, on the same batches in the same order).
+  trajectory: per-epoch train and validation losses against the fp64 oracle's within
+  1e-5 relative or twice the fp32 oracle's own drift from it (all run AdamW, lr 1e-4, on the
+  same batches in the same order).
 * The checkpoint is a reference state_dict: it loads into the oracle (strict) and gives the
   engine's validation loss.
 * Data parallelism: two ranks (gloo, both on cuda:0) running the engine; the all-reduced
@@ -41,6 +42,12 @@ class _Oracle(torch.nn.Module):
         self.loss_fn = type("L", (), {"crps": staticmethod(self.net.crps)})()
 
     def forward(self, data):
+        dt = self.net.dim_red.weight.dtype
+        if data.x.dtype != dt:   # the fp64 trajectory: inputs promoted like the weights
+            import copy as _copy
+            data = _copy.copy(data)
+            data.x, data.ensemble, data.edge_attr = (t.to(dt) for t in (
+                data.x, data.ensemble, data.edge_attr))
         return self.net(data)
 
 
@@ -57,6 +64,7 @@ def test_two_epochs_follow_oracle_trajectory(tmp_path):
     model = gnn_from_params(params)
     ref = _Oracle(params)
     ref.net.load_state_dict(model.state_dict(), strict=True)
+    init = {k: v.detach().clone() for k, v in model.state_dict().items()}
     model = model.to(DEV)
     opt = FlatAdamW(model.parameters(), lr=params["lr"])
     ropt = torch.optim.AdamW(ref.parameters(), lr=params["lr"])
@@ -68,9 +76,23 @@ def test_two_epochs_follow_oracle_trajectory(tmp_path):
     want = T.fit(ref, ropt, DeviceLoader(ctr, 4, seed=3), DeviceLoader(cva, 4, shuffle=False),
                  "cpu", 2, ckpt_dir=str(tmp_path / "cpu"), run_id="c",
                  example=ctr.batch(torch.tensor([0])))
+    # The trajectory's own conditioning: AdamW's first steps move every parameter by about
+    # lr * sign(g), so a gradient entry within rounding of zero -- which any change of
+    # summation order can flip -- moves its parameter by 2 lr either way, and two fp32 runs
+    # of the same loop drift apart by more than the one-step tolerance.  The bar is the
+    # reference restatement's own fp32 drift from the fp64 trajectory (x2), or 1e-5 if
+    # larger; the engine is compared with the fp64 trajectory.
+    ref64 = _Oracle(params).double()
+    ref64.net.load_state_dict({k: v.double() if v.is_floating_point() else v
+                               for k, v in init.items()}, strict=True)
+    want64 = T.fit(ref64, torch.optim.AdamW(ref64.parameters(), lr=params["lr"]),
+                   DeviceLoader(ctr, 4, seed=3), DeviceLoader(cva, 4, shuffle=False), "cpu", 2,
+                   ckpt_dir=str(tmp_path / "cpu64"), run_id="c64",
+                   example=ctr.batch(torch.tensor([0])))
     for key in ("train", "val"):
-        for a, b in zip(got["history"][key], want["history"][key]):
-            assert abs(a - b) <= TOL * abs(b), (key, a, b)
+        for a, b, c in zip(got["history"][key], want["history"][key], want64["history"][key]):
+            env = abs(b - c)
+            assert abs(a - c) <= max(TOL * abs(c), 2.0 * env), (key, a, b, c)
     # BatchNorm bookkeeping: sanity forward + every step, as the reference
     nbt = [int(b) for n, b in model.named_buffers() if n.endswith("num_batches_tracked")]
     rnbt = [int(b) for n, b in ref.net.named_buffers() if n.endswith("num_batches_tracked")]

@@ -35,7 +35,7 @@ for s in $STEPS; do
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 20 ;;
     bench5) run bench_cfg5 600 python bench.py --config 5 --steps 20 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-               python3 bench.py --steps 20 --warmup 5 --no-cpu ;;
+               python3 bench.py --steps 20 --warmup 5 --no-cpu --no-strong ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
