@@ -36,6 +36,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from raincast_gnn import functional as Fn  # noqa: E402
+from raincast_gnn import gradbuf  # noqa: E402
 from raincast_gnn.data import relabel_stations, synthetic_batch  # noqa: E402
 from raincast_gnn.data import station_order as station_order_of  # noqa: E402
 from raincast_gnn.distributed import FlatGradReducer, broadcast_parameters, env_rank  # noqa: E402
@@ -117,7 +118,7 @@ class Trainer:
         self.opt.zero_grad()            # set_to_none: kernels write grads into flat slices
         pred = self.model(self.batch)
         loss = self.model.loss_fn.crps(pred, self.batch.y)
-        loss.backward()
+        gradbuf.loss_backward(loss)      # (no seed-fill launch)
         self.opt.gather_grads()         # flat_grad complete before the all-reduce
         return loss
 

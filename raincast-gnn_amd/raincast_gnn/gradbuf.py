@@ -131,3 +131,22 @@ def mp_job(partials: torch.Tensor, rows: int, channels: int, eps_cols: int, dlw,
     j.rows, j.channels, j.eps_cols = int(rows), int(channels), int(eps_cols)
     j.w[0], j.w[1], j.w[2] = dlw.data_ptr(), dlb.data_ptr(), deps.data_ptr()
     return j
+
+
+_seeds: dict = {}  # (device, dtype) -> the constant 1 that seeds a scalar loss's backward
+
+
+def loss_backward(loss: torch.Tensor) -> None:
+    """``loss.backward()`` without its seed-fill launch: autograd uses a gradient tensor it
+    is given as is, so d loss / d loss = 1 comes from a cached device scalar instead of a
+    ``ones_like`` kernel per step (one launch fewer in the captured training step).  The
+    scalar is created outside graph capture (the eager warm-up steps); inside a capture
+    without one, the plain call runs."""
+    key = (loss.device, loss.dtype)
+    one = _seeds.get(key)
+    if one is None:
+        if loss.is_cuda and torch.cuda.is_current_stream_capturing():
+            loss.backward()
+            return
+        one = _seeds[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+    loss.backward(one)

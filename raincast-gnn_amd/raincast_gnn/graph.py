@@ -50,9 +50,11 @@ def window_settings() -> tuple[str, int]:
 
 
 def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device,
-                 max_nodes: int) -> dict:
+                 max_nodes: int, max_staged: float | None = WINDOW_MAX_STAGED) -> dict:
     """slice channels -> (WindowPlan, device arrays) or None, from a host copy of one CSR.
-    Blocks on the device (a D2H copy): call outside graph capture."""
+    ``max_staged`` rejects plans staging more than that many times the node table (None:
+    keep every plan, GINE_MP_WINDOW=all).  Blocks on the device (a D2H copy): call outside
+    graph capture."""
     plans = {}
     if num_nodes == 0:
         return plans
@@ -75,7 +77,7 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
                   max_nodes, max_edges, tb.data_ptr(), lo.data_ptr(), rows.data_ptr(),
                   ctypes.byref(nt), maxima.data_ptr())
         T = int(nt.value)
-        if T == 0 or int(rows[:T].sum()) > WINDOW_MAX_STAGED * num_nodes:
+        if T == 0 or (max_staged is not None and int(rows[:T].sum()) > max_staged * num_nodes):
             plans[cs] = None
             continue
         arrays = (tb[:T + 1].to(device), lo[:T].to(device), rows[:T].to(device))
@@ -146,11 +148,14 @@ class GineGraph:
         self._windows = {"in": {}, "out": {}}
         if mode == "off" or self.in_attr is None:
             return
+        # "all" forces the staged kernels wherever a plan exists (tests, experiments); "auto"
+        # keeps only plans that stage a bounded multiple of the table
+        staged = None if mode == "all" else WINDOW_MAX_STAGED
         if mode == "all":
             self._windows["in"] = plan_windows(self.in_rowptr, self.in_src, self.num_nodes,
-                                               self.device, max_nodes)
+                                               self.device, max_nodes, staged)
         self._windows["out"] = plan_windows(self.out_rowptr, self.out_dst, self.num_nodes,
-                                            self.device, max_nodes)
+                                            self.device, max_nodes, staged)
         self._windows["min_wg"] = 0 if mode == "all" else WINDOW_MIN_WORKGROUPS
 
     def window_plan(self, side: str, channels: int):

@@ -45,6 +45,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import gradbuf
 from .batching import DeviceDataset, DeviceLoader
 from .data import GraphBatch
 
@@ -107,7 +108,7 @@ class StepRunner:
     def _fwd_bwd(self, batch):
         self._zero()
         loss = self.model.loss_fn.crps(self.model(batch), batch.y)
-        loss.backward()
+        gradbuf.loss_backward(loss)
         if hasattr(self.opt, "gather_grads"):
             self.opt.gather_grads()   # the flat gradient buffer complete (all-reduce payload)
         return loss
