@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_fwd(
   for (int base = beg; base < end; base += L) {
     const int cnt = min(L, end - base);
     if (t < cnt) {
-      my_nbr[t] = nbr[base + t];
+      my_nbr[t] = (int32_t)((uint32_t)nbr[base + t] * rowb);  // row byte offset
       my_attr[t] = attr[base + t];
     }
     __builtin_amdgcn_wave_barrier();
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_fwd(
       float a[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t ro = (uint32_t)my_nbr[j + u] * rowb;
+        const uint32_t ro = (uint32_t)my_nbr[j + u];
         a[u] = my_attr[j + u];
 #pragma unroll
         for (int c = 0; c < C; ++c) r[u][c] = ld_f4v(xb, ro + qb[c]);
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kThreads) void k_mp_fwd(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int jj = min(j + u, cnt - 1);
-        const uint32_t ro = (uint32_t)my_nbr[jj] * rowb;
+        const uint32_t ro = (uint32_t)my_nbr[jj];
         a[u] = my_attr[jj];
 #pragma unroll
         for (int c = 0; c < C; ++c) r[u][c] = ld_f4v(xb, ro + qb[c]);
@@ -216,17 +216,36 @@ __global__ __launch_bounds__(kThreads, C == 1 ? 4 : 2) void k_mp_bwd(
     for (int base = beg; base < end; base += L) {
       const int cnt = min(L, end - base);
       if (t < cnt) {
-        my_nbr[t] = nbr[base + t];
+        my_nbr[t] = (int32_t)((uint32_t)nbr[base + t] * rowb);  // row byte offset
         my_attr[t] = attr[base + t];
       }
       __builtin_amdgcn_wave_barrier();
-      for (int j = 0; j < cnt; j += U) {
+      int j = 0;
+      // full batches of U neighbours: no per-edge test
+      for (; j + U <= cnt; j += U) {
+        f4v r[U][C];
+        float a[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t ro = (uint32_t)my_nbr[j + u];
+          a[u] = my_attr[j + u];
+#pragma unroll
+          for (int c = 0; c < C; ++c) r[u][c] = ld_f4v(dzb, ro + qb[c]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int c = 0; c < C; ++c)
+            bwd_edge<FMA>(acc[c], accw[c], r[u][c], a[u], h[c], w[c], b[c]);
+      }
+      // tail: loads clamped to the last neighbour (always issued), sums tested
+      if (j < cnt) {
         f4v r[U][C];
         float a[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int jj = min(j + u, cnt - 1);
-          const uint32_t ro = (uint32_t)my_nbr[jj] * rowb;
+          const uint32_t ro = (uint32_t)my_nbr[jj];
           a[u] = my_attr[jj];
 #pragma unroll
           for (int c = 0; c < C; ++c) r[u][c] = ld_f4v(dzb, ro + qb[c]);

@@ -21,7 +21,8 @@
 
 // Diagnostic switches (tools/wg_micro.hip only; 0 in the library): bit 0 skips the MFMA
 // chain, bit 1 replaces the operand loads by zeros, bit 2 skips the slab stores, bit 3
-// stamps s_memtime / s_memrealtime at body entry and exit into gine_wg_clock[block][4].
+// stamps s_memtime / s_memrealtime at body entry and exit into gine_wg_clock[block][4],
+// bit 4 replaces the chain's LDS operand reads by register values.
 #ifndef GINE_WG_VARIANT
 #define GINE_WG_VARIANT 0
 #endif
@@ -195,10 +196,17 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
 #pragma unroll
     for (int s = 0; s < kWgRows / 2; ++s) {
       if (s + 1 < kWgRows / 2) {
+        if constexpr ((GINE_WG_VARIANT & 16) != 0) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) an[j] = pa[(s + 1) * LDP + 32 * j];
+          for (int j = 0; j < NJ; ++j) an[j] = a[j] * 0.5f;
 #pragma unroll
-        for (int k = 0; k < NI; ++k) bn[k] = qb[(s + 1) * kWgLdQ + 32 * k];
+          for (int k = 0; k < NI; ++k) bn[k] = b[k] * 0.5f;
+        } else {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) an[j] = pa[(s + 1) * LDP + 32 * j];
+#pragma unroll
+          for (int k = 0; k < NI; ++k) bn[k] = qb[(s + 1) * kWgLdQ + 32 * k];
+        }
       }
       if (s % SP == 0 && s / SP < NITEMS) load_item(s / SP, n1);
       if constexpr ((GINE_WG_VARIANT & 1) == 0) {

@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--morton", action="store_true", help="Z-order station numbering")
+    ap.add_argument("--rcm", action="store_true",
+                    help="stations in the engine's locality order (reverse Cuthill-McKee, "
+                         "raincast_gnn.data.station_order), as bench.py runs them")
     ap.add_argument("--slice", type=int, default=0, help="force a window slice width")
     ap.add_argument("--eager", action="store_true", help="no graphs (for rocprofv3 --pmc)")
     args = ap.parse_args()
@@ -89,6 +92,9 @@ def main():
     for c in (int(v) for v in args.configs.split(",")):
         n, k, B = CONFIGS[c]
         ei, ea, N = (morton_batch_graph if args.morton else knn_batch_graph)(n, k, B, seed=0)
+        if args.rcm:
+            from raincast_gnn.data import relabel_edges, station_order
+            ei = relabel_edges(ei, station_order(ei[:, :ei.size(1) // B], n))
         E = ei.size(1)
         ei, ea = ei.to(dev), ea.to(dev)
         x = torch.randn(N, D, device=dev)
