@@ -13,8 +13,10 @@
 // (guaranteed: a workgroup sum of 2^52 or more is not added, see below, and grids are
 // <= 2048 workgroups); the resolution is 2^-64 absolute, so a column sum of 1e-10 (tiny
 // gradients in the backward) keeps ~31 significant bits.
-// Non-finite sums follow IEEE/ATen: a NaN, +Inf or -Inf workgroup sum is counted in its
-// own word (single copy; rare) instead of being converted, and the consumer rebuilds the
+// Non-finite sums follow IEEE/ATen: a NaN, +Inf or -Inf workgroup sum is counted (one
+// count word per column, single copy, rare: three 21-bit fields, nan | +inf << 21 |
+// -inf << 42 -- the per-step difference of the word is exact mod 2^64 whatever the running
+// total, and a step adds at most 2048 per field) instead of being converted, and the consumer rebuilds the
 // column total as NaN (a NaN, or both infinities), +Inf or -Inf -- so mean / var / alpha
 // come out non-finite exactly where ATen's batch_norm does.  A finite workgroup sum of
 // magnitude >= 2^52 (an activation column far beyond fp32 BatchNorm's useful range) is
@@ -26,21 +28,26 @@
 // statistics for that step instead of silently mixing steps.
 // Layout of acc (int64), W = 2 * D words per quantity (sum | sum of squares, or in the
 // backward sum dbn | sum dbn * xhat):
-//   [replica: 8][hi | mid | lo: W]   [count: nan | +inf | -inf: W]
-//   [snapshot: 2][hi | mid | lo | nan | +inf | -inf: W]   phase   consumed[2]
+//   [replica: R][hi | mid | lo: W]   [count: W]
+//   [snapshot: 2][hi | mid | lo | count: W]   phase   consumed[2]
 #pragma once
 
 #include "gine_common.hpp"
 
 namespace gine {
 
-// Workgroups of one XCD (blockIdx % 8 under round-robin dispatch) add into their own
-// replica: same-address atomics serialise at the memory side, and 256 workgroups on one
-// copy cost ~4 us at the end of the producer; 8 replicas make 32-deep chains.  The consumer
-// sums the replicas' integers (exact) before the one conversion to double.
-constexpr int kBnAccReplicas = 8;
+// Workgroups add into replica blockIdx % R: same-address atomics serialise at the memory
+// side (256 workgroups on one copy cost ~4 us at the end of the producer), while every
+// consumer workgroup reads every replica.  Measured on the cfg2 step (r02_s21, A/B twice):
+// R = 2 / 4 / 8 / 16 -> 0.579 / 0.572 / 0.586 / 0.605 ms.  The consumer sums the replicas'
+// integers (exact) before the one conversion to double.
+#ifndef GINE_BNACC_REPLICAS
+#define GINE_BNACC_REPLICAS 4
+#endif
+constexpr int kBnAccReplicas = GINE_BNACC_REPLICAS;
 constexpr int kBnAccWords = 3;   // hi, mid, lo
-constexpr int kBnAccCounts = 3;  // nan, +inf, -inf
+constexpr int kBnAccCounts = 1;  // nan | +inf << 21 | -inf << 42
+constexpr int kBnAccCountBits = 21;
 constexpr int kBnAccSnap = kBnAccWords + kBnAccCounts;
 
 __host__ __device__ constexpr int64_t bnacc_words(int D) {
@@ -70,8 +77,8 @@ __device__ __forceinline__ void bnacc_add(long long* acc, int W, int c, double v
                            __HIP_MEMORY_SCOPE_AGENT);
   } else {  // NaN, +-Inf, or out of range (counted as NaN)
     const int k = (v == __builtin_inf()) ? 1 : (v == -__builtin_inf()) ? 2 : 0;
-    __hip_atomic_fetch_add(bnacc_counts(acc, W) + k * W + c, 1ll, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(bnacc_counts(acc, W) + c, 1ll << (kBnAccCountBits * k),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (blockIdx.x == 0 && c == 0) {  // one producer launch = one phase (read by the consumer)
     long long* ph = bnacc_phase(acc, W);
@@ -114,11 +121,14 @@ __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool
 #pragma unroll
     for (int k = 0; k < kBnAccSnap; ++k) cur[k * W + t] = (long long)cur_v[k];
   }
-  const bool nan = d[3] != 0 || (d[4] != 0 && d[5] != 0) || ph - consumed != 1;
+  const unsigned long long fm = (1ull << kBnAccCountBits) - 1, cnt_d = (unsigned long long)d[3];
+  const bool n_nan = (cnt_d & fm) != 0, n_pinf = ((cnt_d >> kBnAccCountBits) & fm) != 0,
+             n_ninf = ((cnt_d >> (2 * kBnAccCountBits)) & fm) != 0;
+  const bool nan = n_nan || (n_pinf && n_ninf) || ph - consumed != 1;
   double v;
   if (nan) v = __builtin_nan("");
-  else if (d[4] != 0) v = __builtin_inf();
-  else if (d[5] != 0) v = -__builtin_inf();
+  else if (n_pinf) v = __builtin_inf();
+  else if (n_ninf) v = -__builtin_inf();
   else
     v = ((double)d[2] * 5.421010862427522e-20 + (double)d[1] * 2.3283064365386963e-10) +
         (double)d[0];  // lo * 2^-64 + mid * 2^-32 + hi, smallest first

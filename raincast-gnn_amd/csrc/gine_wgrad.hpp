@@ -38,7 +38,10 @@ typedef float wg_floatx16 __attribute__((ext_vector_type(16)));
 constexpr int kWgRows = 64;                   // rows per staged sub-tile
 constexpr int kWgTI = 128;                    // i-columns per workgroup tile
 constexpr int kWgLdQ = kWgTI + 4;             // padded LDS rows (floats)
-constexpr int kWgTargetBlocks = 256;          // one workgroup per CU
+#ifndef GINE_WG_TARGET_BLOCKS
+#define GINE_WG_TARGET_BLOCKS 256
+#endif
+constexpr int kWgTargetBlocks = GINE_WG_TARGET_BLOCKS;  // one workgroup per CU
 constexpr int kWgMinSubtiles = 2;             // per chunk
 #ifndef GINE_WG_WAVES64
 #define GINE_WG_WAVES64 8

@@ -30,6 +30,11 @@ def _words(D):
     return w.value
 
 
+def _replicas(D):
+    """Replica count of the accumulator layout (gine_bnacc.hpp): words = (3R + 9) 2D + 3."""
+    return ((_words(D) - 3) // (2 * D) - 9) // 3
+
+
 def _conv(D, seed):
     torch.manual_seed(seed)
     mlp = torch.nn.Sequential(torch.nn.Linear(D, D), torch.nn.BatchNorm1d(D), torch.nn.ReLU(),
@@ -131,11 +136,12 @@ def test_fused_forward_acc_equals_unfused(n, max_deg):
     # the totals are the column sums of a1 and a1^2
     a64 = a10.double()
     W = 2 * D
-    rep = acc0[:8 * 3 * W].view(8, 3, W).sum(0)   # replicas: [hi | mid | lo] x (sum | sumsq)
+    R = _replicas(D)
+    rep = acc0[:R * 3 * W].view(R, 3, W).sum(0)   # replicas: [hi | mid | lo] x (sum | sumsq)
     tot = (rep[0].double() + rep[1].double() * 2.0**-32 + rep[2].double() * 2.0**-64).view(2, D)
     torch.testing.assert_close(tot[0], a64.sum(0), rtol=1e-12, atol=1e-9)
     torch.testing.assert_close(tot[1], (a64 * a64).sum(0), rtol=1e-12, atol=1e-9)
-    assert int(acc0[8 * 3 * W:-3].abs().sum()) == 0       # no non-finite counts, no snapshot
+    assert int(acc0[R * 3 * W:-3].abs().sum()) == 0       # no non-finite counts, no snapshot
     assert int(acc0[-3]) == 1 and int(acc0[-2:].abs().sum()) == 0
 
 
@@ -144,7 +150,8 @@ def test_bn_acc_entry_points_validate():
     a = torch.zeros(64, 64, device=DEV)
     words = ctypes.c_int64(0)
     assert _lib.load().gine_bn_acc_words(64, ctypes.byref(words)) == 0
-    assert words.value == 78 * 64 + 3
+    # [R replicas x 3 words | 1 packed count word | 2 snapshots x 4 words] x 2D + 3
+    assert words.value == (3 * _replicas(64) + 1 + 8) * 128 + 3 and _replicas(64) == 4
     acc = torch.zeros(words.value, dtype=torch.int64, device=DEV)
     save = torch.empty(4, 64, device=DEV)
     w = torch.zeros(64, 64, device=DEV)
