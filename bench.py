@@ -378,7 +378,7 @@ def sec8d_launch_work(name: str, w: dict) -> dict:
     }.get(name, {})
 
 
-def roofline_for(kernels: dict, layers: int, work: dict):
+def roofline_for(kernels: dict, layers: int, work: dict, config: str = "cfg2"):
     """The dominant kernel of the step (largest time per step among the per-layer kernels
     the training step launches) against SURVEY.md 8(d)'s roofline: its ideal time is
     max(8(d) bytes / 8 TB/s, 8(d) flops / 157.3 TFLOP/s fp32 MFMA), frac = ideal / measured
@@ -389,10 +389,10 @@ def roofline_for(kernels: dict, layers: int, work: dict):
         step += ["gine_mlp_bwd1", "gine_mp_bwd_mlp_wgrad"]
     timed = [k for k in step if k in kernels]
     dominant = max(timed, key=lambda k: kernels[k]["us"])
-    return roof_of(dominant, kernels[dominant], layers, work)
+    return roof_of(dominant, kernels[dominant], layers, work, config)
 
 
-def roof_of(name: str, rec: dict, layers: int, work: dict) -> dict:
+def roof_of(name: str, rec: dict, layers: int, work: dict, config: str = "cfg2") -> dict:
     wl = sec8d_launch_work(name, work)
     b, f = wl.get("bytes", 0), wl.get("flops", 0)
     t_hbm = b / (HBM_PEAK_GBS * 1e9)
@@ -409,7 +409,7 @@ def roof_of(name: str, rec: dict, layers: int, work: dict) -> dict:
     roof["alg_flops_per_launch"] = f
     roof["avg_us"] = rec["us"]
     roof["launches_per_step"] = layers
-    t = pmc_traffic(name)
+    t = pmc_traffic(name, config)
     roof["traffic"] = t["bytes"] if t else None
     roof["traffic_source"] = t["source"] if t else None
     return roof
@@ -425,13 +425,13 @@ def roofline_step(work: dict, layers: int, ms_per_step: float) -> dict:
             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
-def roofline_mp(kernels: dict, layers: int, work: dict):
+def roofline_mp(kernels: dict, layers: int, work: dict, config: str = "cfg2"):
     """The message-passing kernels (the north-star gather / segmented-scatter path) alone
     against HBM, with the measured copy ceiling beside the 8 TB/s spec."""
     out = {}
     for name in ("gine_mp_fwd", "gine_mp_fwd_win", "gine_mp_bwd"):
         if name in kernels:
-            out[name] = roof_of(name, kernels[name], layers, work)
+            out[name] = roof_of(name, kernels[name], layers, work, config)
     return out or None
 
 
@@ -469,11 +469,12 @@ PMC_KERNELS = {
 }
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, config: str = "cfg2"):
     """HBM bytes per call of entry point ``kernel`` from the committed rocprofv3 PMC summary
     (profiles/*pmc_traffic.json: per-kernel (2 x FETCH_SIZE + WRITE_SIZE) bytes per launch,
     the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md), summed over the kernels the
-    call launches; None when no summary covers them."""
+    call launches; None when no summary of THIS configuration covers them (a summary names
+    its configuration in "_config"; untagged ones were taken on the default cfg2 run)."""
     names = PMC_KERNELS.get(kernel)
     if not names:
         return None
@@ -483,6 +484,8 @@ def pmc_traffic(kernel: str):
             with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
+            continue
+        if d.get("_config", "cfg2") != config:
             continue
         hits = [next((v for k, v in d.items() if k.startswith(n)), None) for n in names]
         if all(h is not None for h in hits):
@@ -653,8 +656,8 @@ def main():
     result = None
     if rank == 0:
         work = sec8d_work(tr.batch.num_nodes, E_rank, tr.params["gnn_hidden"])
-        roof = roofline_for(kernels, layers, work)
-        roof_mp = roofline_mp(kernels, layers, work)
+        roof = roofline_for(kernels, layers, work, cfg.name)
+        roof_mp = roofline_mp(kernels, layers, work, cfg.name)
         if roof_mp is not None:
             copy_gbs = copy_ceiling_gbps(device)
             for r in roof_mp.values():

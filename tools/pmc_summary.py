@@ -21,6 +21,7 @@ def main():
     ap.add_argument("files", nargs="+")
     ap.add_argument("--traffic-json")
     ap.add_argument("--filter", default="gine::")
+    ap.add_argument("--config", default="cfg2", help="bench configuration the counters ran on")
     a = ap.parse_args()
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in a.files:
@@ -38,6 +39,7 @@ def main():
         if "FETCH_SIZE" in row and "WRITE_SIZE" in row:
             traffic[k] = round((2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024)
     if a.traffic_json:
+        traffic["_config"] = a.config
         json.dump(traffic, open(a.traffic_json, "w"), indent=1, sort_keys=True)
 
 
