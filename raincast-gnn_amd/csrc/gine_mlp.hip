@@ -361,12 +361,319 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
   RG_FLUSH();
 }
 
+// ----------------------------------------------------------------------------------------
+// Software-pipelined row-tile GEMM: the same arithmetic as rowgemm_body (same MFMA chains,
+// same epilogue rounding -> identical outputs), with the per-tile work that is not matrix
+// work moved INTO the next tile's MFMA chain.  One wave per SIMD issues a 64-cycle
+// v_mfma_f32_32x32x2_f32 every 64 cycles; the matrix pipe runs asynchronously, so the gaps
+// between MFMA issues hold other instructions for free.  Per 32-row tile k the chain of
+// tile k carries, in fixed slots of its 16 four-MFMA steps:
+//   step 0      the accumulator of tile k-1 -> the LDS output tile (transpose)
+//   steps 1-2   staging of tile k+1 (prologue transform) into the other A buffer
+//   step 3      the raw loads of tile k+2 (in flight for a whole chain)
+//   step 4      barrier (every wave's tile k-1 rows are in LDS)
+//   steps 5-11  the epilogue of tile k-1: bias / BN statistics / residual / ReLU mask,
+//               16-byte global stores
+//   step 13     the epilogue operands of tile k (consumed one chain later)
+// so a workgroup's tiles cost one MFMA chain each, plus one staging and one epilogue for
+// the whole range, instead of (staging + chain + epilogue) per tile.  Loads are never
+// conditional (clamped to the last tile: a branch around a load drains the memory queue).
+// LDS: A buffers [2][32][D+4], output tile [32][D+4] (aliasing the W^T staging area).
+template <int D>
+constexpr int rowgemm_pipe_lds_floats(bool wl) {
+  return (wl && D * (D + 4) > 3 * kRowTile * (D + 4)) ? D * (D + 4) : 3 * kRowTile * (D + 4);
+}
+
+template <int D, int PRO, int EPI, bool BT, bool WL = false, class Hook = NoHook>
+__device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const ProArgs& pa,
+                                             const EpiArgs& ea, int64_t N, int num_tiles,
+                                             float* __restrict__ s_lds, int vb, int vgrid,
+                                             const Hook& hook = Hook{}) {
+  constexpr int NT = 2 * D;
+  constexpr int KS = D / 2;
+  constexpr int LD = D + 4;
+  constexpr int D4 = D / 4;
+  constexpr int ITEMS = kRowTile * D4 / NT;
+  constexpr int RSTEP = NT / D4;
+  constexpr int NQ = KS / 4;  // four-MFMA steps per chain
+  constexpr bool IS_OUT = (EPI == EPI_OUT) || (EPI == EPI_OUT_RELU) || (EPI == EPI_OUT_RES);
+  constexpr bool EPI_LOAD = (EPI == EPI_DBN) || (EPI == EPI_OUT_RES);
+  static_assert(NQ >= 8, "the pipeline slots need at least 8 steps (D >= 64)");
+  // slots: item i of the epilogue at step Q_EPI0 + i * (Q_EPLOAD - Q_EPI0) / ITEMS
+  constexpr int Q_STAGE0 = 1, Q_STAGE1 = 2, Q_LOAD = 3, Q_SYNC = 4, Q_EPI0 = 5;
+  constexpr int Q_EPLOAD = NQ - 2;
+  constexpr int EPI_SLOTS = Q_EPLOAD - Q_EPI0;
+
+  // A buffer b at s_lds + b * kRowTile * LD (arithmetic, not a pointer table: a runtime
+  // index into a table of pointers loses the LDS address space -> flat loads)
+  float* sO = s_lds + 2 * kRowTile * LD;
+
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int col = wave * 32 + c32;
+  const int q_me = threadIdx.x % D4, r_me = threadIdx.x / D4;
+
+  float bf[KS];
+  constexpr int WCH = D * D4 / NT;
+  float4 wtmp[WL ? WCH : 1];
+  if constexpr (WL) {
+    const float4* w4 = reinterpret_cast<const float4*>(W);
+#pragma unroll
+    for (int j = 0; j < WCH; ++j) wtmp[j] = w4[threadIdx.x + NT * j];
+  } else if constexpr (BT) {
+    const float4* wr = reinterpret_cast<const float4*>(W + (size_t)col * D + h * KS);
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const float4 v = wr[q];
+      bf[4 * q] = v.x;
+      bf[4 * q + 1] = v.y;
+      bf[4 * q + 2] = v.z;
+      bf[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bf[s] = W[(size_t)(h * KS + s) * D + col];
+  }
+  constexpr bool kHook = !std::is_same<Hook, NoHook>::value;
+  ColConst kc;
+  if constexpr (!kHook) kc = col_const<PRO>(pa, D, q_me);
+
+  float4 bias4 = f4_zero();
+  if constexpr (EPI == EPI_A1STATS || IS_OUT)
+    bias4 = *reinterpret_cast<const float4*>(ea.bias + 4 * q_me);
+  float4 al4 = f4_zero(), sh4 = f4_zero(), mu4 = f4_zero(), is4 = f4_zero();
+  if constexpr (EPI == EPI_DBN) {
+    const BnView b = bn_view(ea.bn, D);
+    al4 = *reinterpret_cast<const float4*>(b.alpha + 4 * q_me);
+    sh4 = *reinterpret_cast<const float4*>(b.shift + 4 * q_me);
+    mu4 = *reinterpret_cast<const float4*>(b.mean + 4 * q_me);
+    is4 = *reinterpret_cast<const float4*>(b.invstd + 4 * q_me);
+  }
+  double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
+
+  const TileRange tr = xcd_tile_range(num_tiles, vb, vgrid);
+  const int count = tr.first < tr.end ? (tr.end - tr.first + tr.step - 1) / tr.step : 0;
+  auto tile_of = [&](int i) { return tr.first + min(i, count - 1) * tr.step; };
+
+  auto load_tile = [&](int tile, RawItem (&raw)[ITEMS]) {
+    const int64_t n0 = (int64_t)tile * kRowTile;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      const int64_t n = n0 + r_me + i * RSTEP;
+      raw[i] = raw_load<PRO>(pa, D, n < N ? n : N - 1, q_me);
+    }
+  };
+  auto load_ep = [&](int tile, float4 (&ep)[ITEMS]) {
+    if constexpr (EPI_LOAD) {
+      const int64_t n0 = (int64_t)tile * kRowTile;
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        int64_t n = n0 + r_me + i * RSTEP;
+        n = n < N ? n : N - 1;
+        const float* src = EPI == EPI_DBN ? ea.a1 : ea.resid;
+        ep[i] = *reinterpret_cast<const float4*>(src + n * D + 4 * q_me);
+      }
+    }
+  };
+  auto stage_item = [&](int tile, const RawItem& raw, int i, float* dst) {
+    const int r = r_me + i * RSTEP;
+    float4 v = transform<PRO>(pa, raw, kc);
+    if ((int64_t)tile * kRowTile + r >= N) v = f4_zero();
+    *reinterpret_cast<float4*>(&dst[r * LD + 4 * q_me]) = v;
+  };
+  auto acc_to_lds = [&](const floatx16& acc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sO[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + col] = acc[r];
+  };
+  // epilogue of one item (rows r_me + i*RSTEP of tile `tile`), from the LDS output tile
+  auto epi_item = [&](int tile, int i, const float4 (&ep)[ITEMS]) {
+    const int r = r_me + i * RSTEP;
+    const int64_t n = (int64_t)tile * kRowTile + r;
+    const float4 v = *reinterpret_cast<const float4*>(&sO[r * LD + 4 * q_me]);
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+    if (n >= N) return;
+    const int64_t off = n * D + 4 * q_me;
+    float o4[4];
+    if constexpr (EPI == EPI_A1STATS) {
+      const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o4[k] = vv[k] + bb[k];
+        st1[k] += (double)o4[k];
+        st2[k] += (double)o4[k] * (double)o4[k];
+      }
+    } else if constexpr (IS_OUT) {
+      const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
+      if constexpr (EPI == EPI_OUT_RES) {
+        const float xr[4] = {ep[i].x, ep[i].y, ep[i].z, ep[i].w};
+        unsigned char mk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float o = vv[k] + bb[k];
+          o4[k] = xr[k] + relu_nan(o);
+          mk[k] = (o > 0.f) ? 1 : 0;
+        }
+        *reinterpret_cast<uchar4*>(ea.mask_out + off) = make_uchar4(mk[0], mk[1], mk[2], mk[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float o = vv[k] + bb[k];
+          o4[k] = (EPI == EPI_OUT_RELU) ? relu_nan(o) : o;
+        }
+      }
+    } else if constexpr (EPI == EPI_DBN) {
+      const float a1[4] = {ep[i].x, ep[i].y, ep[i].z, ep[i].w};
+      const float al[4] = {al4.x, al4.y, al4.z, al4.w}, sh[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+      const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float bn = bn_apply(a1[k], al[k], sh[k]);
+        o4[k] = (bn > 0.f) ? vv[k] : 0.f;
+        const double xhat = (double)((a1[k] - mu[k]) * is[k]);
+        st1[k] += (double)o4[k];
+        st2[k] += (double)o4[k] * xhat;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o4[k] = vv[k];
+    }
+    *reinterpret_cast<float4*>(ea.out + off) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+  };
+
+  RawItem raw[ITEMS];
+  float4 ep_prev[ITEMS], ep_cur[ITEMS];
+  floatx16 accp = zero16();
+  if (count > 0) {
+    load_tile(tile_of(0), raw);
+    if constexpr (WL) {
+#pragma unroll
+      for (int j = 0; j < WCH; ++j) {
+        const int idx = threadIdx.x + NT * j;
+        *reinterpret_cast<float4*>(&s_lds[(idx / D4) * LD + 4 * (idx % D4)]) = wtmp[j];
+      }
+      __syncthreads();
+      const float* wr = &s_lds[col * LD + h * KS];
+#pragma unroll
+      for (int q = 0; q < KS / 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(&wr[4 * q]);
+        bf[4 * q] = v.x;
+        bf[4 * q + 1] = v.y;
+        bf[4 * q + 2] = v.z;
+        bf[4 * q + 3] = v.w;
+      }
+    }
+    if constexpr (kHook) {
+      hook();
+      kc = col_const<PRO>(pa, D, q_me);
+    }
+    __syncthreads();  // W^T fragment reads (WL) are done before the A buffers overwrite them
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) stage_item(tile_of(0), raw[i], i, s_lds);
+    load_tile(tile_of(1), raw);
+    __syncthreads();  // tile 0 staged
+
+    // tile k's chain (A = sA[k & 1]) carrying the pipeline slots; EPI_ON: the epilogue of
+    // tile k-1 (every iteration but the first)
+    auto chain = [&](int k, auto epi_on) -> floatx16 {
+      constexpr bool EPI_ON = decltype(epi_on)::value;
+      const float* arow = s_lds + (k & 1) * (kRowTile * LD) + c32 * LD + h * KS;
+      float* snext = s_lds + ((k + 1) & 1) * (kRowTile * LD);
+      const int tprev = tile_of(k - 1), tnext = tile_of(k + 1);
+      floatx16 acc = zero16();
+      // each step's A fragment is read one step ahead (the step boundaries are scheduling
+      // barriers: a read issued in the same step would expose the LDS latency every step)
+      float4 a4 = *reinterpret_cast<const float4*>(&arow[0]);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const float4 an =
+            *reinterpret_cast<const float4*>(&arow[4 * (q + 1 < NQ ? q + 1 : q)]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+        if (q == 0 && EPI_ON) acc_to_lds(accp);
+        if (q == Q_STAGE0) {
+#pragma unroll
+          for (int i = 0; i < ITEMS / 2; ++i) stage_item(tnext, raw[i], i, snext);
+        }
+        if (q == Q_STAGE1) {
+#pragma unroll
+          for (int i = ITEMS / 2; i < ITEMS; ++i) stage_item(tnext, raw[i], i, snext);
+        }
+        if (q == Q_LOAD) load_tile(tile_of(k + 2), raw);
+        if (q == Q_SYNC && EPI_ON) __syncthreads();
+        if (EPI_ON) {
+#pragma unroll
+          for (int i = 0; i < ITEMS; ++i)
+            if (q == Q_EPI0 + i * EPI_SLOTS / ITEMS) epi_item(tprev, i, ep_prev);
+        }
+        if (q == Q_EPLOAD) load_ep(tile_of(k), ep_cur);  // tile k's operands, for next chain
+        __builtin_amdgcn_sched_barrier(0);
+        a4 = an;
+      }
+      return acc;
+    };
+
+    auto rotate_ep = [&]() {
+      if constexpr (EPI_LOAD) {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) ep_prev[i] = ep_cur[i];
+      }
+    };
+    // peeled first chain: no previous tile to finish
+    accp = chain(0, std::false_type{});
+    rotate_ep();
+    for (int k = 1; k < count; ++k) {
+      __syncthreads();  // tile k staged; the output tile and the other A buffer are free
+      accp = chain(k, std::true_type{});
+      rotate_ep();
+    }
+    // the last tile's epilogue
+    __syncthreads();
+    acc_to_lds(accp);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) epi_item(tile_of(count - 1), i, ep_prev);
+  } else if constexpr (kHook) {
+    hook();  // (no tiles: the hook still runs its workgroup-0 duties)
+  }
+
+  if constexpr (EPI == EPI_A1STATS || EPI == EPI_DBN) {
+    __syncthreads();
+    double* sr = reinterpret_cast<double*>(s_lds);
+    static_assert(2 * RSTEP * D * 8 <= kRowTile * LD * 4, "partials fit in the tile");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sr[(0 * RSTEP + r_me) * D + 4 * q_me + k] = st1[k];
+      sr[(1 * RSTEP + r_me) * D + 4 * q_me + k] = st2[k];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * D; c += NT) {
+      const int which = c / D, cc = c % D;
+      double t = 0.0;
+#pragma unroll
+      for (int g = 0; g < RSTEP; ++g) t += sr[(which * RSTEP + g) * D + cc];
+      if (ea.partials) ea.partials[(size_t)vb * 2 * D + c] = t;
+      if (ea.bnacc) bnacc_add(ea.bnacc, 2 * D, c, t);
+    }
+  }
+}
+
+#ifndef GINE_ROWGEMM_PIPE
+#define GINE_ROWGEMM_PIPE 1
+#endif
+
 template <int D, int PRO, int EPI, bool BT>
 __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, ProArgs pa,
                                                    EpiArgs ea, int64_t N, int num_tiles) {
   constexpr bool WL = BT && D <= 128;  // W^T staged through LDS (fits: 128*132*4 B)
-  __shared__ __attribute__((aligned(16))) float s_x[(WL ? D : kRowTile) * (D + 4)];
-  rowgemm_body<D, PRO, EPI, BT, WL>(W, pa, ea, N, num_tiles, s_x, blockIdx.x, gridDim.x);
+  if constexpr (GINE_ROWGEMM_PIPE && D >= 64) {
+    __shared__ __attribute__((aligned(16))) float s_x[rowgemm_pipe_lds_floats<D>(WL)];
+    rowgemm_pipe<D, PRO, EPI, BT, WL>(W, pa, ea, N, num_tiles, s_x, blockIdx.x, gridDim.x);
+  } else {
+    __shared__ __attribute__((aligned(16))) float s_x[(WL ? D : kRowTile) * (D + 4)];
+    rowgemm_body<D, PRO, EPI, BT, WL>(W, pa, ea, N, num_tiles, s_x, blockIdx.x, gridDim.x);
+  }
 }
 
 // Persistent grid.  One workgroup per CU while each has at most 4 tiles; past that two
@@ -431,7 +738,9 @@ __global__ __launch_bounds__(2 * D) void k_fwd2_bnacc(const float* __restrict__ 
                                                       long long* acc, int64_t N,
                                                       int num_tiles) {
   constexpr bool WL = D <= 128;
-  __shared__ __attribute__((aligned(16))) float s_x[(WL ? D : kRowTile) * (D + 4)];
+  constexpr bool PIPE = GINE_ROWGEMM_PIPE && D >= 64;
+  __shared__ __attribute__((aligned(16)))
+  float s_x[PIPE ? rowgemm_pipe_lds_floats<D>(WL) : (WL ? D : kRowTile) * (D + 4)];
   __shared__ __attribute__((aligned(16))) float s_bn[4 * D];
   __shared__ double s_tot[2 * D];
   auto finish = [=]() {  // by value: a reference to a kernel argument puts it in scratch
@@ -449,8 +758,12 @@ __global__ __launch_bounds__(2 * D) void k_fwd2_bnacc(const float* __restrict__ 
   };
   ProArgs p2 = pa;
   p2.bn = s_bn;
-  rowgemm_body<D, PRO_BNRELU, EPI, true, WL>(W, p2, ea, N, num_tiles, s_x, blockIdx.x,
-                                             gridDim.x, finish);
+  if constexpr (PIPE)
+    rowgemm_pipe<D, PRO_BNRELU, EPI, true, WL>(W, p2, ea, N, num_tiles, s_x, blockIdx.x,
+                                               gridDim.x, finish);
+  else
+    rowgemm_body<D, PRO_BNRELU, EPI, true, WL>(W, p2, ea, N, num_tiles, s_x, blockIdx.x,
+                                               gridDim.x, finish);
 }
 
 // dz = da1 W1 with the BatchNorm backward finish in its prologue (training): the totals
@@ -462,7 +775,9 @@ __global__ __launch_bounds__(2 * D) void k_bwd1_bnacc(const float* __restrict__ 
                                                       float* dgamma, float* dbeta, float* coef,
                                                       long long* acc, int64_t N,
                                                       int num_tiles) {
-  __shared__ __attribute__((aligned(16))) float s_x[kRowTile * (D + 4)];
+  constexpr bool PIPE = GINE_ROWGEMM_PIPE && D >= 64;
+  __shared__ __attribute__((aligned(16)))
+  float s_x[PIPE ? rowgemm_pipe_lds_floats<D>(false) : kRowTile * (D + 4)];
   __shared__ __attribute__((aligned(16))) float s_coef[3 * D];
   __shared__ double s_tot[2 * D];
   const float* bn_save = pa.bn;
@@ -492,8 +807,12 @@ __global__ __launch_bounds__(2 * D) void k_bwd1_bnacc(const float* __restrict__ 
   };
   ProArgs p2 = pa;
   p2.coef = s_coef;
-  rowgemm_body<D, PRO_DA1, EPI_PLAIN, false, false>(W, p2, ea, N, num_tiles, s_x, blockIdx.x,
-                                                    gridDim.x, finish);
+  if constexpr (PIPE)
+    rowgemm_pipe<D, PRO_DA1, EPI_PLAIN, false, false>(W, p2, ea, N, num_tiles, s_x,
+                                                      blockIdx.x, gridDim.x, finish);
+  else
+    rowgemm_body<D, PRO_DA1, EPI_PLAIN, false, false>(W, p2, ea, N, num_tiles, s_x,
+                                                      blockIdx.x, gridDim.x, finish);
 }
 
 template <int EPI>
