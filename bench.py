@@ -133,7 +133,11 @@ class Trainer:
         there is a collective) and AdamW.  If the collective cannot be captured (or
         ``allreduce="split"``), fwd+bwd and AdamW are two graphs with the all-reduce
         launched between them."""
-        if not self.collective or self.allreduce == "graph":
+        # only RCCL ("nccl") collectives can be captured; gloo (CPU rehearsals) always runs
+        # between two graphs -- a failed capture attempt would leave the stream invalidated
+        in_graph = self.allreduce == "graph" and (
+            not self.collective or dist.get_backend() == "nccl")
+        if not self.collective or in_graph:
             try:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):

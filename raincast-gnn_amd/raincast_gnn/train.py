@@ -91,7 +91,8 @@ class StepRunner:
     ``optimizer`` is a :class:`raincast_gnn.optim.FlatAdamW` (one kernel over the flat
     buffer) or any torch optimizer (``capturable=True`` for graph capture).  ``reducer`` is a
     :class:`raincast_gnn.distributed.FlatGradReducer` over the same gradients (data
-    parallelism); its all-reduce runs between the fwd+bwd graph and the optimizer graph.
+    parallelism); with RCCL its all-reduce is captured in the step graph, with other backends
+    it runs between the fwd+bwd graph and the optimizer graph.
     """
 
     def __init__(self, model, optimizer, graphed: bool = True, warmup: int = 2,
@@ -152,11 +153,18 @@ class StepRunner:
         static = GraphBatch(batch.x.clone(), batch.ensemble.clone(), batch.edge_index,
                             batch.edge_attr, batch.y.clone(), batch.batch, batch.ptr,
                             batch.num_graphs)
-        split = self.reducer is not None and _world() > 1
+        collective = self.reducer is not None and _world() > 1
+        # RCCL's all-reduce is captured inside the step graph (between the backward and the
+        # optimizer); other backends (gloo rehearsals) cannot be captured: two graphs with
+        # the all-reduce launched between them
+        in_graph = collective and dist.get_backend() == "nccl"
+        split = collective and not in_graph
         torch.cuda.synchronize()
         g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
             loss = self._fwd_bwd(static)
+            if in_graph:
+                self._reduce()
             if not split:
                 self.opt.step()
         g_opt = None
