@@ -17,7 +17,7 @@ import ctypes
 
 import torch
 
-from . import _lib, gradbuf, sidework
+from . import _lib, gradbuf
 from .gradbuf import grad_out
 
 HIDDEN = (64, 128)
@@ -89,12 +89,10 @@ class _ChainFn(torch.autograd.Function):
                       ctypes.byref(job))
             gradbuf.defer(job, dev, (slab,))
             return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
-        # ... while the four weight gradients run beside it on the side stream
-        sidework.launch(dev, lambda sh: _lib.call(
-            "gine_chain_wgrad", P(dh0), P(x), P(r), P(s), P(u), P(e), P(de), P(dt), P(ds),
-            P(slab), P(g[0]), P(g[1]), members, P(g[2]), P(g[3]), P(g[4]), P(g[5]), P(g[6]),
-            P(g[7]), N, D, F, sh), keep_alive=(dh0, x, r, s, u, e, de, dt, ds, slab),
-            params=p)
+        # ... else the four weight gradients reduced in the same call
+        _lib.call("gine_chain_wgrad", P(dh0), P(x), P(r), P(s), P(u), P(e), P(de), P(dt),
+                  P(ds), P(slab), P(g[0]), P(g[1]), members, P(g[2]), P(g[3]), P(g[4]),
+                  P(g[5]), P(g[6]), P(g[7]), N, D, F, _lib.stream_handle(dev))
         return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
 
 

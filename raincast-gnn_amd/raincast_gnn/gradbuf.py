@@ -111,8 +111,6 @@ def flush() -> None:
     with _pending_lock:
         items = list(_pending)
         _pending.clear()
-    from . import sidework  # slabs written on a side stream: wait for them first
-    sidework.wait_all()
     by_stream: dict = {}
     for job, stream, keep in items:
         by_stream.setdefault(stream, []).append(job)

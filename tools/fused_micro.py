@@ -24,12 +24,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,2,3")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--rcm", action="store_true", help="stations in the locality order")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     D = 128
     for c in (int(v) for v in args.configs.split(",")):
         n, k, b = CONFIGS[c]
         ei, ea, N = knn_batch_graph(n, k, b, seed=0)
+        if args.rcm:
+            from raincast_gnn.data import relabel_edges, station_order
+            ei = relabel_edges(ei, station_order(ei[:, :ei.size(1) // b], n))
         g = GineGraph(ei.to(dev), ea.to(dev), N)
         x = torch.randn(N, D, device=dev)
         lw, lb = torch.randn(D, device=dev), torch.randn(D, device=dev)
