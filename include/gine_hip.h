@@ -493,6 +493,41 @@ int gine_chain_wgrad(const float* dh0, const float* x, const float* r, const flo
                      float* dbdr, int64_t num_nodes, int32_t hidden, int32_t in_features,
                      void* stream);
 
+/* Folded chain (the default path of raincast_gnn.chain): rho[2] and dim_red have no
+ * nonlinearity between them, so h0 = [x | u] W'^T + b' with W' = [Wdr_x | Wdr_e Wr1],
+ * b' = Wdr_e br1 + bdr, and e / de are never formed.
+ * gine_chain_fwd_folded writes s, u, h0 and W' [D][F+D] | b' [D] | W'^T [F+D][D] into
+ *   wfold [2*D*(F+D) + D] (saved for the backward; folded from the current weights by every
+ *   call).
+ * gine_chain_bwd_folded: dt = (dh0 Wc) * 1[u > 0] (Wc = W'[:, F:]), ds = dt Wr0, dr = ds Wp2.
+ * gine_chain_wgrad_folded: one engine launch for G = dh0^T [x | u] | g = sum_n dh0 (into
+ *   gfold [D*(F+D) + D]), dWr0 | dbr0 and dWp2 | dbp2 (dbp2 scaled by bias_scale); slab of
+ *   gine_chain_bwd_slab_floats() floats.  gfold = dwr0 = dwp2 = NULL leaves the slab for
+ *   gine_grad_finalize_batch (job from gine_chain_wgrad_folded_grad_job).
+ * gine_chain_unfold_grads, after the reduction: dWdr = [G_x | G_u Wr1^T + g br1^T],
+ *   dbdr = g, dWr1 = Wdr_e^T G_u, dbr1 = Wdr_e^T g (fp32 MFMA; bias outputs may be NULL).
+ * Replaces the same reference modules as gine_chain_fwd / gine_chain_bwd. */
+int gine_chain_fwd_folded(const float* r, const float* x, const float* wp2, const float* bp2,
+                          float bias_scale, const float* wr0, const float* br0,
+                          const float* wr1, const float* br1, const float* wdr,
+                          const float* bdr, float* wfold, float* s, float* u, float* h0,
+                          int64_t num_nodes, int32_t hidden, int32_t in_features, void* stream);
+int gine_chain_bwd_folded(const float* dh0, const float* u, const float* wp2, const float* wr0,
+                          const float* wfold, float* dt, float* ds, float* dr,
+                          int64_t num_nodes, int32_t hidden, int32_t in_features, void* stream);
+int gine_chain_wgrad_folded(const float* dh0, const float* x, const float* r, const float* s,
+                            const float* u, const float* dt, const float* ds, float* slab,
+                            float* gfold, float* dwr0, float* dbr0, float* dwp2, float* dbp2,
+                            float bias_scale, int64_t num_nodes, int32_t hidden,
+                            int32_t in_features, void* stream);
+int gine_chain_wgrad_folded_grad_job(int64_t num_nodes, int32_t hidden, int32_t in_features,
+                                     const float* slab, float bias_scale, float* gfold,
+                                     float* dwr0, float* dbr0, float* dwp2, float* dbp2,
+                                     gine_grad_job* job);
+int gine_chain_unfold_grads(const float* gfold, const float* wr1, const float* br1,
+                            const float* wdr, float* dwdr, float* dbdr, float* dwr1,
+                            float* dbr1, int32_t hidden, int32_t in_features, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,20 +34,26 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kRowTile = 32;
 
-enum ChainKind { CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3 };
+// F2F / B1F: the one-stage kernels of the folded chain (rho[2] folded into dim_red, see
+// gine_chain_fwd_folded): F2F h0 = [x | u] W'^T + b', B1F dt = (dh0 Wc) * 1[u > 0].
+enum ChainKind { CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3, CH_F2F = 4, CH_B1F = 5 };
 
 struct ChainArgs {
-  const float* in;   // stage-1 A rows [N, D]: r | u | dh0 | dt
-  const float* x;    // F2: node features [N, F]
-  const float* aux;  // B1: u (ReLU mask of rho[1])
-  const float* w1;   // stage-1 weight
+  const float* in;   // stage-1 A rows [N, D]: r | u | dh0 | dt | u (F2F) | dh0 (B1F)
+  const float* x;    // F2 / F2F: node features [N, F]
+  const float* aux;  // B1 / B1F: u (ReLU mask of rho[1])
+  const float* w1;   // stage-1 weight (B1F: W')
   const float* b1;   // stage-1 bias (forward)
-  const float* w2;   // stage-2 weight
-  const float* b2;   // stage-2 bias (forward)
+  const float* w2;   // stage-2 weight (F2F: W')
+  const float* b2;   // stage-2 bias (forward; F2F: b')
   float* out1;       // stage-1 output [N, D]: s | e | de | ds
   float* out2;       // stage-2 output [N, D]: u | h0 | dt | dr
   float bias1_scale; // F1: M (phi[2]'s bias summed over members)
   int F;             // F2 / B1: dim_red's x width
+  // F1 of the folded chain: W' = [Wdr_x | Wdr_e Wr1] and b' = Wdr_e br1 + bdr into wfold
+  // ([D][F + D] then [D]) once the tiles are done (NULL: not folded)
+  const float *fw_r1, *fb_r1, *fw_dr, *fb_dr;
+  float* wfold;
 };
 
 __device__ __forceinline__ floatx16 zero16() {
@@ -106,12 +112,25 @@ __device__ __forceinline__ void frag_dimred(float (&bf)[(FP + D) / 2], const flo
   }
 }
 
+// The same from W^T [F + D][D] (the folded chain's W'^T): lanes read consecutive columns.
+template <int FP, int D>
+__device__ __forceinline__ void frag_dimred_t(float (&bf)[(FP + D) / 2], const float* WT, int F,
+                                              int col, int h) {
+  constexpr int KS = (FP + D) / 2;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = h * KS + s;
+    const int c = k < F ? k : (k < FP ? 0 : k - FP + F);
+    const float v = WT[(size_t)c * D + col];
+    bf[s] = (k >= F && k < FP) ? 0.f : v;
+  }
+}
+
 // Per-XCD contiguous tile ranges (as k_rowgemm).
 struct TileRange {
   int first, end, step;
 };
-__device__ __forceinline__ TileRange tile_range(int num_tiles) {
-  const int nb = gridDim.x;
+__device__ __forceinline__ TileRange tile_range(int num_tiles, int nb) {
   const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
   const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
   const int span = (num_tiles + kNumXcd - 1) / kNumXcd;
@@ -119,14 +138,142 @@ __device__ __forceinline__ TileRange tile_range(int num_tiles) {
   return TileRange{b + pos, min(num_tiles, b + span), here};
 }
 
+// v = sum_j sA[r][j] * svec[j] for the 32 rows staged in sA (row stride D + 4): 2D/32
+// threads per row, 16 products each, then a shuffle tree; every thread of row
+// threadIdx.x / (2D/32) returns that row's total.
+template <int D>
+__device__ __forceinline__ float rows_dot(const float* sA, const float* svec) {
+  constexpr int TPR = 2 * D / 32, LDA = D + 4, J = D / TPR;
+  const int r = threadIdx.x / TPR, p = threadIdx.x % TPR;
+  float v = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) v = fmaf(sA[r * LDA + p * J + j], svec[p * J + j], v);
+#pragma unroll
+  for (int o = TPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, TPR);
+  return v;
+}
+
+// A [32 x 32] tile of a small D x D product, contraction split over the D/32 waves of a
+// 2D-thread workgroup: wave w contracts k in [32w, 32w + 32) (lane half h: 16 of them) of
+// the 32 A rows staged in sA against its B fragment bf[s] = B[32w + 16h + s][c32]; the
+// partial tiles go to sR ([D/32][32 x 33], rows padded for transposed reads), to be summed by
+// ksplit_sum after a barrier.
+// 16 MFMAs per wave instead of a 64-long chain: these tiles are latency-bound.
+constexpr int kSR = 32 * 33;  // floats of one wave's partial tile in sR
+template <int D>
+__device__ __forceinline__ void ksplit_tile(const float* sA, const float (&bf)[16], float* sR,
+                                            int c32, int h) {
+  constexpr int LDA = D + 4;
+  const int w = threadIdx.x / kWave;
+  floatx16 acc = zero16();
+  const float* arow = sA + c32 * LDA + w * 32 + h * 16;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+    sR[w * kSR + rr * 33 + c32] = acc[r];
+  }
+}
+// element (row, col) of the tile (waves summed in order)
+template <int D>
+__device__ __forceinline__ float ksplit_sum(const float* sR, int row, int col) {
+  float v = sR[row * 33 + col];
+#pragma unroll
+  for (int w = 1; w < D / 32; ++w) v += sR[w * kSR + row * 33 + col];
+  return v;
+}
+
+// One [32 x 32] tile (rows k0, columns c0 of Wc) of W' = [Wdr_x | Wc], Wc = Wdr_e Wr1, and
+// (c0 = 0) the x columns and b' = Wdr_e br1 + bdr of its rows: the folded chain's dim_red
+// weight, written as W' [D][F+D], b' [D] and W'^T [F+D][D] (the forward kernel's B
+// fragments read W'^T along rows, coalesced).  Run by the fold workgroups of F1.
+template <int D>
+__device__ void fold_tile(const ChainArgs& a, int ft, float* sA, float* sR, int c32, int h) {
+  constexpr int NT = 2 * D, LDA = D + 4, T = D / 32;
+  const int F = a.F, LW = a.F + D;
+  const int k0 = 32 * (ft / T), c0 = 32 * (ft % T);
+  const int w = threadIdx.x / kWave;
+  __shared__ float svec[D];
+  float bf[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) bf[s] = a.fw_r1[(size_t)(w * 32 + h * 16 + s) * D + c0 + c32];
+  // every load of the staging issued before the first wait (unrolled, constant counts)
+  constexpr int SI = 32 * D / NT, XI = 32 * 64 / NT;
+  float st[SI], xv[XI];
+#pragma unroll
+  for (int i = 0; i < SI; ++i) {
+    const int idx = threadIdx.x + i * NT, r = idx / D, j = idx % D;
+    st[i] = a.fw_dr[(size_t)(k0 + r) * LW + F + j];
+  }
+  if (c0 == 0) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int idx = min(threadIdx.x + i * NT, 32 * F - 1), r = idx / F, c = idx % F;
+      xv[i] = a.fw_dr[(size_t)(k0 + r) * LW + c];
+    }
+  }
+  const float bv = threadIdx.x < D ? a.fb_r1[threadIdx.x] : 0.f;
+  __syncthreads();  // every wave is done with sA / sB
+#pragma unroll
+  for (int i = 0; i < SI; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    sA[(idx / D) * LDA + idx % D] = st[i];
+  }
+  float* wt = a.wfold + (size_t)D * LW + D;  // W'^T
+  if (c0 == 0) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int idx = threadIdx.x + i * NT;
+      if (idx < 32 * F) a.wfold[(size_t)(k0 + idx / F) * LW + idx % F] = xv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {  // x columns transposed: row r fastest
+      const int idx = threadIdx.x + i * NT, r = idx % 32, c = idx / 32;
+      if (idx < 32 * F) wt[(size_t)c * D + k0 + r] = a.fw_dr[(size_t)(k0 + r) * LW + c];
+    }
+  }
+  if (threadIdx.x < D) svec[threadIdx.x] = bv;
+  __syncthreads();
+  ksplit_tile<D>(sA, bf, sR, c32, h);
+  if (c0 == 0) {
+    const float v = rows_dot<D>(sA, svec);  // (Wdr_e br1)[k0 + r]
+    constexpr int TPR = NT / 32;
+    if (threadIdx.x % TPR == 0) {
+      const int r = threadIdx.x / TPR;
+      a.wfold[(size_t)D * LW + k0 + r] = v + a.fb_dr[k0 + r];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int o = threadIdx.x + i * NT;
+    a.wfold[(size_t)(k0 + o / 32) * LW + F + c0 + o % 32] = ksplit_sum<D>(sR, o / 32, o % 32);
+    wt[(size_t)(F + c0 + o / 32) * D + k0 + o % 32] = ksplit_sum<D>(sR, o % 32, o / 32);
+  }
+}
+
+// F1 of the folded chain launches (D/32)^2 workgroups more than its chain grid: block
+// chain_blocks + t folds tile t of W' beside the chain tiles (they fit on the CUs next to
+// the one chain workgroup per CU).
+template <int D>
+constexpr int kFoldBlocks = (D / 32) * (D / 32);
+
 template <int D, int FP, int KIND>
 __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num_tiles) {
   constexpr int NT = 2 * D;
   constexpr int D4 = D / 4;
   constexpr int LDA = D + 4;
-  constexpr int K2 = KIND == CH_F2 ? FP + D : D;    // stage-2 contraction length
+  constexpr bool kDimRed = KIND == CH_F2 || KIND == CH_F2F;
+  constexpr int K2 = kDimRed ? FP + D : D;          // stage-2 contraction length
   constexpr int LDB = K2 + 4;
-  constexpr int BOFF = KIND == CH_F2 ? FP : 0;      // stage-1 output column offset in sB
+  constexpr int BOFF = kDimRed ? FP : 0;            // stage-1 output column offset in sB
   constexpr int ITEMS = kRowTile * D4 / NT;         // 4
   constexpr int RSTEP = NT / D4;                    // 8
   constexpr int XITEMS = (kRowTile * FP + NT - 1) / NT;
@@ -137,28 +284,38 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
   const int q_me = threadIdx.x % D4, r_me = threadIdx.x / D4;
+  int nb = gridDim.x;  // chain workgroups
+  if constexpr (KIND == CH_F1) {
+    if (a.wfold != nullptr) {
+      nb -= kFoldBlocks<D>;
+      if ((int)blockIdx.x >= nb) {
+        fold_tile<D>(a, blockIdx.x - nb, sA, sB, c32, h);
+        return;
+      }
+    }
+  }
 
-  // both stages' weight fragments, once per workgroup
+  // both stages' weight fragments, once per workgroup (F2F: stage 2 only, B1F: stage 1)
   float bf1[D / 2], bf2[K2 / 2];
   if constexpr (KIND == CH_F1 || KIND == CH_F2) {
     frag_t<D>(bf1, a.w1, D, col, h);
-  } else if constexpr (KIND == CH_B1) {
-    frag_n<D>(bf1, a.w1, a.F + D, a.F, col, h);     // dim_red weight, e columns
-  } else {
+  } else if constexpr (KIND == CH_B1 || KIND == CH_B1F) {
+    frag_n<D>(bf1, a.w1, a.F + D, a.F, col, h);     // dim_red (B1F: W') weight, e columns
+  } else if constexpr (KIND == CH_B2) {
     frag_n<D>(bf1, a.w1, D, 0, col, h);
   }
   if constexpr (KIND == CH_F1) {
     frag_t<D>(bf2, a.w2, D, col, h);
   } else if constexpr (KIND == CH_F2) {
     frag_dimred<FP, D>(bf2, a.w2, a.F, col, h);
-  } else {
+  } else if constexpr (KIND == CH_F2F) {
+    frag_dimred_t<FP, D>(bf2, a.w2, a.F, col, h);  // w2 = W'^T
+  } else if constexpr (KIND != CH_B1F) {
     frag_n<D>(bf2, a.w2, D, 0, col, h);
   }
   float bias1 = 0.f, bias2 = 0.f;
-  if constexpr (KIND == CH_F1 || KIND == CH_F2) {
-    bias1 = a.b1[col] * a.bias1_scale;
-    bias2 = a.b2[col];
-  }
+  if constexpr (KIND == CH_F1 || KIND == CH_F2) bias1 = a.b1[col] * a.bias1_scale;
+  if constexpr (KIND == CH_F1 || kDimRed) bias2 = a.b2[col];
 
   auto load_tile = [&](int tile, float4 (&raw)[ITEMS], float (&xr)[XITEMS]) {
     const int64_t n0 = (int64_t)tile * kRowTile;
@@ -168,7 +325,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       n = n < N ? n : N - 1;  // clamped: always issued
       raw[i] = reinterpret_cast<const float4*>(a.in + n * D)[q_me];
     }
-    if constexpr (KIND == CH_F2) {
+    if constexpr (kDimRed) {
 #pragma unroll
       for (int i = 0; i < XITEMS; ++i) {
         const int idx = threadIdx.x + i * NT;      // over [32][FP]
@@ -182,7 +339,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     }
   };
 
-  const TileRange tr = tile_range(num_tiles);
+  const TileRange tr = tile_range(num_tiles, nb);
   float4 raw[ITEMS];
   float xr[XITEMS];
   if (tr.first < tr.end) load_tile(tr.first, raw, xr);
@@ -193,9 +350,10 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     for (int i = 0; i < ITEMS; ++i) {
       const int r = r_me + i * RSTEP;
       const float4 v = (n0 + r < N) ? raw[i] : f4_zero();
-      *reinterpret_cast<float4*>(&sA[r * LDA + 4 * q_me]) = v;
+      float* dst = KIND == CH_F2F ? &sB[r * LDB + BOFF + 4 * q_me] : &sA[r * LDA + 4 * q_me];
+      *reinterpret_cast<float4*>(dst) = v;
     }
-    if constexpr (KIND == CH_F2) {
+    if constexpr (kDimRed) {
 #pragma unroll
       for (int i = 0; i < XITEMS; ++i) {
         const int idx = threadIdx.x + i * NT;
@@ -205,7 +363,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     __syncthreads();
     if (tile + tr.step < tr.end) load_tile(tile + tr.step, raw, xr);  // next tile in flight
     float ep[16];
-    if constexpr (KIND == CH_B1) {  // ReLU mask operand of stage 2, in flight too
+    if constexpr (KIND == CH_B1 || KIND == CH_B1F) {  // ReLU mask operand, in flight too
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -214,17 +372,29 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       }
     }
 
-    // stage 1
-    floatx16 acc = tile_mma<D>(sA, LDA, bf1, c32, h);
+    floatx16 acc;
+    if constexpr (KIND == CH_B1F) {  // the one stage: dt = (dh0 Wc) * 1[u > 0]
+      acc = tile_mma<D>(sA, LDA, bf1, c32, h);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int64_t n = n0 + rr;
-      const float v = acc[r] + bias1;
-      sB[rr * LDB + BOFF + col] = v;
-      if (n < N) a.out1[n * D + col] = v;
+      for (int r = 0; r < 16; ++r) {
+        const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = ep[r] > 0.f ? acc[r] : 0.f;
+        if (n < N) a.out2[n * D + col] = v;
+      }
+      continue;
     }
-    __syncthreads();
+    if constexpr (KIND != CH_F2F) {  // stage 1
+      acc = tile_mma<D>(sA, LDA, bf1, c32, h);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t n = n0 + rr;
+        const float v = acc[r] + bias1;
+        sB[rr * LDB + BOFF + col] = v;
+        if (n < N) a.out1[n * D + col] = v;
+      }
+      __syncthreads();
+    }
 
     // stage 2
     acc = tile_mma<K2>(sB, LDB, bf2, c32, h);
@@ -254,56 +424,59 @@ inline int chain_grid(int64_t N) {
 template <int D, int FP, int KIND>
 int launch_chain(const ChainArgs& a, int64_t N, hipStream_t s) {
   const int tiles = (int)ceil_div(N, kRowTile);
-  hipLaunchKernelGGL((k_chain<D, FP, KIND>), dim3(chain_grid(N)), dim3(2 * D), 0, s, a, N,
-                     tiles);
+  const int fold = (KIND == CH_F1 && a.wfold != nullptr) ? kFoldBlocks<D> : 0;
+  hipLaunchKernelGGL((k_chain<D, FP, KIND>), dim3(chain_grid(N) + fold), dim3(2 * D), 0, s, a,
+                     N, tiles);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
 
 // ----------------------------------------------------------------------------------------
-// weight gradients of the four Linears, one engine launch (Z = 4)
-//   z = 0: dWdr [D x (F+D)] = dh0^T [x | e]     z = 1: dWr1 = de^T u
-//   z = 2: dWr0 = dt^T s                         z = 3: dWp2 = ds^T r
+// weight gradients, one engine launch
+//   NZ = 4 (unfolded):  z = 0: dWdr [D x (F+D)] = dh0^T [x | e]   z = 1: dWr1 = de^T u
+//                       z = 2: dWr0 = dt^T s                       z = 3: dWp2 = ds^T r
+//   NZ = 3 (folded):    z = 0: G = dh0^T [x | u]   z = 1: dWr0 = dt^T s   z = 2: dWp2 = ds^T r
+//                       (dWdr / dWr1 follow from G in gine_chain_unfold_grads)
 // ----------------------------------------------------------------------------------------
+template <int NZ>
 struct ChainWgradSrc {
-  static constexpr int kZ = 4;
-  const float *dh0, *de, *dt, *ds;  // P
-  const float *x, *e, *u, *s, *r;   // Q
+  static constexpr int kZ = NZ;
+  const float* p[4];  // P rows [N, D] of product z
+  const float* q[4];  // Q rows [N, D] of product z (z = 0: the D columns after x)
+  const float* x;
   int D, F;
   struct Raw {
     float4 v;
   };
   struct Col {
-    float keep[4];  // Q of z = 0: 1 for the columns inside [x | e], 0 for the padding
+    float keep[4];  // Q of z = 0: 1 for the columns inside [x | .], 0 for the padding
   };
   template <int Z> __device__ int i_dim(int) const { return Z == 0 ? F + D : D; }
   template <int Z> __device__ Col p_col(int) const { return Col{{1.f, 1.f, 1.f, 1.f}}; }
-  template <int Z> __device__ Col q_col(int q) const {
+  template <int Z> __device__ Col q_col(int q4) const {
     Col c{{1.f, 1.f, 1.f, 1.f}};
     if constexpr (Z == 0) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) c.keep[j] = 4 * q + j < F + D ? 1.f : 0.f;
+      for (int j = 0; j < 4; ++j) c.keep[j] = 4 * q4 + j < F + D ? 1.f : 0.f;
     }
     return c;
   }
-  template <int Z> __device__ Raw p_load(int64_t n, int q) const {
-    const float* p = Z == 0 ? dh0 : (Z == 1 ? de : (Z == 2 ? dt : ds));
-    return Raw{reinterpret_cast<const float4*>(p + n * D)[q]};
+  template <int Z> __device__ Raw p_load(int64_t n, int q4) const {
+    return Raw{reinterpret_cast<const float4*>(p[Z] + n * D)[q4]};
   }
-  template <int Z> __device__ Raw q_load(int64_t n, int q) const {
-    if constexpr (Z == 0) {  // [x | e]: F + D columns, x rows are not float4-aligned
+  template <int Z> __device__ Raw q_load(int64_t n, int q4) const {
+    if constexpr (Z == 0) {  // [x | q0]: F + D columns, x rows are not float4-aligned
       const int I = F + D;
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = min(4 * q + j, I - 1);
-        const float* src = c < F ? x + n * F + c : e + n * D + (c - F);
+        const int c = min(4 * q4 + j, I - 1);
+        const float* src = c < F ? x + n * F + c : q[0] + n * D + (c - F);
         v[j] = *src;  // raw: the padding is zeroed in q_xform, when the tile is staged
       }
       return Raw{make_float4(v[0], v[1], v[2], v[3])};
     } else {
-      const float* p = Z == 1 ? u : (Z == 2 ? s : r);
-      return Raw{reinterpret_cast<const float4*>(p + n * D)[q]};
+      return Raw{reinterpret_cast<const float4*>(q[Z] + n * D)[q4]};
     }
   }
   template <int Z> __device__ float4 p_xform(const Raw& r, const Col&) const { return r.v; }
@@ -316,28 +489,28 @@ struct ChainWgradSrc {
 };
 
 struct ChainWgradOut {
-  float* w[4];  // dWdr, dWr1, dWr0, dWp2 (product order)
+  float* w[4];  // product order of ChainWgradSrc
   float* b[4];
-  int D, F;
-  float bias_scale;  // phi[2]'s bias enters M times
+  int D, F, nz;
+  float bias_scale;  // phi[2]'s bias (the last product) enters M times
   __device__ void operator()(int z, int64_t e, double v) const {
     const int64_t I = z == 0 ? F + D : D;
     const int64_t ws = (int64_t)D * I;
     if (e < ws) {
       w[z][e] = (float)v;
     } else if (e < ws + D && b[z] != nullptr) {
-      b[z][e - ws] = (float)(z == 3 ? v * (double)bias_scale : v);
+      b[z][e - ws] = (float)(z == nz - 1 ? v * (double)bias_scale : v);
     }
   }
 };
 
-// output tiles: dim_red's [D x (F+D)] plus three [D x D]
-inline int chain_wgrad_tiles(int D, int F) {
+// output tiles: dim_red's [D x (F+D)] plus nz - 1 [D x D]
+inline int chain_wgrad_tiles(int D, int F, int nz) {
   const int to = (int)ceil_div(D, 64);
-  return to * (int)ceil_div(F + D, kWgTI) + 3 * to * (int)ceil_div(D, kWgTI);
+  return to * (int)ceil_div(F + D, kWgTI) + (nz - 1) * to * (int)ceil_div(D, kWgTI);
 }
-inline WgPlan chain_wgrad_plan(int64_t N, int D, int F) {
-  return wg_plan(N, D, F + D, 4, 64, chain_wgrad_tiles(D, F));
+inline WgPlan chain_wgrad_plan(int64_t N, int D, int F, int nz) {
+  return wg_plan(N, D, F + D, nz, 64, chain_wgrad_tiles(D, F, nz));
 }
 
 inline bool chain_dims_ok(int D, int F) { return (D == 64 || D == 128) && F >= 1 && F <= 64; }
@@ -385,9 +558,11 @@ extern "C" int gine_chain_bwd_slab_floats(int64_t num_nodes, int32_t hidden,
                                           int32_t in_features, size_t* floats) {
   if (!floats || num_nodes < 0) return GINE_ERR_INVALID;
   if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
-  const WgPlan p = chain_wgrad_plan(num_nodes, hidden, in_features);
+  // enough for either chain (4 products unfolded, 3 folded)
+  const WgPlan p4 = chain_wgrad_plan(num_nodes, hidden, in_features, 4);
+  const WgPlan p3 = chain_wgrad_plan(num_nodes, hidden, in_features, 3);
   const size_t per = (size_t)hidden * (hidden + in_features) + hidden;
-  *floats = 4 * (size_t)p.chunks * per;
+  *floats = std::max(4 * (size_t)p4.chunks, 3 * (size_t)p3.chunks) * per;
   return GINE_OK;
 }
 
@@ -437,18 +612,42 @@ extern "C" int gine_chain_wgrad(const float* dh0, const float* x, const float* r
   hipStream_t st = as_stream(stream);
   const int D = hidden, F = in_features;
   int rc;
-  const WgPlan p = chain_wgrad_plan(num_nodes, D, F);
+  const WgPlan p = chain_wgrad_plan(num_nodes, D, F, 4);
   const size_t per = (size_t)D * (D + F) + D;
-  const ChainWgradSrc src{dh0, de, dt, ds, x, e, u, s, r, D, F};
-  rc = launch_wgrad_engine<64>(src, num_nodes, D, D + F, chain_wgrad_tiles(D, F), p,
+  const ChainWgradSrc<4> src{{dh0, de, dt, ds}, {e, u, s, r}, x, D, F};
+  rc = launch_wgrad_engine<64>(src, num_nodes, D, D + F, chain_wgrad_tiles(D, F, 4), p,
                                 per * p.chunks, per, slab, st);
   if (rc != GINE_OK) return rc;
   if (!reduce) return GINE_OK;
   return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 4,
                          ChainWgradOut{{dwdr, dwr1, dwr0, dwp2}, {dbdr, dbr1, dbr0, dbp2}, D,
-                                       F, bias_scale},
+                                       F, 4, bias_scale},
                          st);
 }
+
+namespace {
+// the slab job of either chain; w / b in product order
+void chain_slab_job(int64_t N, int D, int F, int nz, const float* slab, float bias_scale,
+                    float* const* w, float* const* b, gine_grad_job* job) {
+  const WgPlan p = chain_wgrad_plan(N, D, F, nz);
+  const int64_t per = (int64_t)D * (D + F) + D;
+  *job = gine_grad_job{};
+  job->kind = GINE_GRAD_JOB_SLAB;
+  job->src = slab;
+  job->rows = p.chunks;
+  job->cstride = per;
+  job->zstride = per * p.chunks;
+  job->nz = nz;
+  for (int z = 0; z < nz; ++z) {
+    const int64_t ws = (int64_t)D * (z == 0 ? F + D : D);
+    job->per[z] = ws + D;
+    job->wsize[z] = ws;
+    job->w[z] = w[z];
+    job->b[z] = b[z];
+    job->bscale[z] = z == nz - 1 ? bias_scale : 1.0f;
+  }
+}
+}  // namespace
 
 extern "C" int gine_chain_wgrad_grad_job(int64_t num_nodes, int32_t hidden, int32_t in_features,
                                          const float* slab, float bias_scale, float* dwp2,
@@ -458,25 +657,221 @@ extern "C" int gine_chain_wgrad_grad_job(int64_t num_nodes, int32_t hidden, int3
   if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
   if (num_nodes <= 0 || !slab || !dwp2 || !dwr0 || !dwr1 || !dwdr || !job)
     return GINE_ERR_INVALID;
-  const int64_t D = hidden, F = in_features;
-  const WgPlan p = chain_wgrad_plan(num_nodes, hidden, in_features);
-  const int64_t per = D * (D + F) + D;
-  *job = gine_grad_job{};
-  job->kind = GINE_GRAD_JOB_SLAB;
-  job->src = slab;
-  job->rows = p.chunks;
-  job->cstride = per;
-  job->zstride = per * p.chunks;
-  job->nz = 4;
-  float* w[4] = {dwdr, dwr1, dwr0, dwp2};  // product order of ChainWgradSrc
+  float* w[4] = {dwdr, dwr1, dwr0, dwp2};  // product order of ChainWgradSrc<4>
   float* b[4] = {dbdr, dbr1, dbr0, dbp2};
-  for (int z = 0; z < 4; ++z) {
-    const int64_t ws = D * (z == 0 ? F + D : D);
-    job->per[z] = ws + D;
-    job->wsize[z] = ws;
-    job->w[z] = w[z];
-    job->b[z] = b[z];
-    job->bscale[z] = z == 3 ? bias_scale : 1.0f;
+  chain_slab_job(num_nodes, hidden, in_features, 4, slab, bias_scale, w, b, job);
+  return GINE_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Folded chain.  rho[2] is followed by dim_red with no nonlinearity between them, so
+//   h0 = [x | u Wr1^T + br1] Wdr^T + bdr = [x | u] W'^T + b',
+//   W' = [Wdr_x | Wc], Wc = Wdr_e Wr1, b' = Wdr_e br1 + bdr,
+// and the backward needs neither e nor de: dt = (dh0 Wc) * 1[u > 0], and with
+// G = dh0^T [x | u] and g = sum_n dh0 (one engine product instead of two):
+//   dWdr = [G_x | G_u Wr1^T + g br1^T], dbdr = g, dWr1 = Wdr_e^T G_u, dbr1 = Wdr_e^T g.
+// One GEMM fewer forward, one fewer input-gradient GEMM and one fewer weight-gradient
+// product backward; W' is folded by the first chain kernel's workgroups after their tiles,
+// G is unfolded by one small launch (2 (D/32)^2 workgroups) after the slab reduction.
+// ---------------------------------------------------------------------------------------
+namespace gine {
+namespace {
+
+// 2 (D/32)^2 workgroups, one [32 x 32] tile each (ksplit_tile): tiles of dWdr's e columns,
+// G_u Wr1^T + g br1^T (G_u rows staged, B = Wr1^T read along Wr1's rows), then tiles of
+// dWr1 = Wdr_e^T G_u (Wdr_e columns staged as rows, B = G_u); the x columns and dbdr (resp.
+// dbr1) by the tiles of column 0.
+template <int D>
+__global__ __launch_bounds__(2 * D) void k_chain_unfold(const float* __restrict__ gf,
+                                                        const float* __restrict__ wr1,
+                                                        const float* __restrict__ br1,
+                                                        const float* __restrict__ wdr,
+                                                        float* __restrict__ dwdr,
+                                                        float* __restrict__ dbdr,
+                                                        float* __restrict__ dwr1,
+                                                        float* __restrict__ dbr1, int F) {
+  constexpr int NT = 2 * D, LDA = D + 4, T = D / 32, TT = T * T;
+  constexpr int SI = 32 * D / NT, XI = 32 * 64 / NT;
+  __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
+  __shared__ float sR[T * kSR];
+  __shared__ float svec[D];
+  const int LW = F + D;
+  const float* g = gf + (size_t)D * LW;
+  const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const bool e_cols = (int)blockIdx.x < TT;
+  const int t = e_cols ? (int)blockIdx.x : (int)blockIdx.x - TT;
+  const int r0 = 32 * (t / T), c0 = 32 * (t % T);
+  float bf[16], st[SI];
+  if (e_cols) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) bf[s] = wr1[(size_t)(c0 + c32) * D + w * 32 + h * 16 + s];
+#pragma unroll
+    for (int i = 0; i < SI; ++i) {
+      const int idx = threadIdx.x + i * NT;
+      st[i] = gf[(size_t)(r0 + idx / D) * LW + F + idx % D];
+    }
+    if (c0 == 0) {
+      float xv[XI];
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        const int idx = min(threadIdx.x + i * NT, 32 * F - 1);
+        xv[i] = gf[(size_t)(r0 + idx / F) * LW + idx % F];
+      }
+#pragma unroll
+      for (int i = 0; i < XI; ++i) {
+        const int idx = threadIdx.x + i * NT;
+        if (idx < 32 * F) dwdr[(size_t)(r0 + idx / F) * LW + idx % F] = xv[i];
+      }
+      if (threadIdx.x < 32 && dbdr != nullptr) dbdr[r0 + threadIdx.x] = g[r0 + threadIdx.x];
+    }
+#pragma unroll
+    for (int i = 0; i < SI; ++i) {
+      const int idx = threadIdx.x + i * NT;
+      sA[(idx / D) * LDA + idx % D] = st[i];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      bf[s] = gf[(size_t)(w * 32 + h * 16 + s) * LW + F + c0 + c32];  // G_u[k][c0 + c32]
+#pragma unroll
+    for (int i = 0; i < SI; ++i) {
+      const int idx = threadIdx.x + i * NT;
+      st[i] = wdr[(size_t)(idx / 32) * LW + F + r0 + idx % 32];
+    }
+    const float gv = threadIdx.x < D ? g[threadIdx.x] : 0.f;
+#pragma unroll
+    for (int i = 0; i < SI; ++i) {
+      const int idx = threadIdx.x + i * NT;
+      sA[(idx % 32) * LDA + idx / 32] = st[i];
+    }
+    if (threadIdx.x < D) svec[threadIdx.x] = gv;
   }
+  __syncthreads();
+  ksplit_tile<D>(sA, bf, sR, c32, h);
+  if (!e_cols && c0 == 0) {
+    const float v = rows_dot<D>(sA, svec);  // (Wdr_e^T g)[r0 + r]
+    constexpr int TPR = NT / 32;
+    if (threadIdx.x % TPR == 0 && dbr1 != nullptr) dbr1[r0 + threadIdx.x / TPR] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int o = threadIdx.x + i * NT, rr = o / 32, cc = o % 32;
+    const float v = ksplit_sum<D>(sR, rr, cc);
+    if (e_cols)
+      dwdr[(size_t)(r0 + rr) * LW + F + c0 + cc] = fmaf(g[r0 + rr], br1[c0 + cc], v);
+    else
+      dwr1[(size_t)(r0 + rr) * D + c0 + cc] = v;
+  }
+}
+
+}  // namespace
+}  // namespace gine
+
+extern "C" int gine_chain_fwd_folded(const float* r, const float* x, const float* wp2,
+                                     const float* bp2, float bias_scale, const float* wr0,
+                                     const float* br0, const float* wr1, const float* br1,
+                                     const float* wdr, const float* bdr, float* wfold, float* s,
+                                     float* u, float* h0, int64_t num_nodes, int32_t hidden,
+                                     int32_t in_features, void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes < 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (num_nodes == 0) return GINE_OK;
+  if (!r || !x || !wp2 || !bp2 || !wr0 || !br0 || !wr1 || !br1 || !wdr || !bdr || !wfold ||
+      !s || !u || !h0)
+    return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  const int D = hidden, F = in_features;
+  const float* bfold = wfold + (size_t)D * (F + D);
+  const float* wfold_t = bfold + D;
+  const ChainArgs f1{r,  nullptr, nullptr, wp2, bp2, wr0, br0, s,
+                     u,  bias_scale, F,    wr1, br1, wdr, bdr, wfold};
+  const ChainArgs f2{u, x, nullptr, nullptr, nullptr, wfold_t, bfold, nullptr, h0, 1.f, F};
+  int rc = GINE_OK;
+#define CALL_F(DD, FF)                                                  \
+  rc = launch_chain<DD, FF, CH_F1>(f1, num_nodes, st);                  \
+  if (rc == GINE_OK) rc = launch_chain<DD, FF, CH_F2F>(f2, num_nodes, st)
+  GINE_CHAIN_DISPATCH(D, F, CALL_F);
+#undef CALL_F
+  return rc;
+}
+
+extern "C" int gine_chain_bwd_folded(const float* dh0, const float* u, const float* wp2,
+                                     const float* wr0, const float* wfold, float* dt, float* ds,
+                                     float* dr, int64_t num_nodes, int32_t hidden,
+                                     int32_t in_features, void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (!dh0 || !u || !wp2 || !wr0 || !wfold || !dt || !ds || !dr) return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  const int F = in_features;
+  const ChainArgs b1{dh0, nullptr, u, wfold, nullptr, nullptr, nullptr, nullptr, dt, 1.f, F};
+  const ChainArgs b2{dt, nullptr, nullptr, wr0, nullptr, wp2, nullptr, ds, dr, 1.f, F};
+  int rc = GINE_OK;
+#define CALL_B(DD, FF)                                                  \
+  rc = launch_chain<DD, FF, CH_B1F>(b1, num_nodes, st);                 \
+  if (rc == GINE_OK) rc = launch_chain<DD, FF, CH_B2>(b2, num_nodes, st)
+  GINE_CHAIN_DISPATCH(hidden, F, CALL_B);
+#undef CALL_B
+  return rc;
+}
+
+extern "C" int gine_chain_wgrad_folded(const float* dh0, const float* x, const float* r,
+                                       const float* s, const float* u, const float* dt,
+                                       const float* ds, float* slab, float* gfold, float* dwr0,
+                                       float* dbr0, float* dwp2, float* dbp2, float bias_scale,
+                                       int64_t num_nodes, int32_t hidden, int32_t in_features,
+                                       void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0) return GINE_ERR_INVALID;
+  if (!dh0 || !x || !r || !s || !u || !dt || !ds || !slab) return GINE_ERR_INVALID;
+  // gfold, dwr0, dwp2 all NULL: the slab is left for gine_grad_finalize_batch
+  const bool reduce = gfold || dwr0 || dwp2;
+  if (reduce && (!gfold || !dwr0 || !dwp2)) return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  const int D = hidden, F = in_features;
+  const WgPlan p = chain_wgrad_plan(num_nodes, D, F, 3);
+  const size_t per = (size_t)D * (D + F) + D;
+  const ChainWgradSrc<3> src{{dh0, dt, ds, nullptr}, {u, s, r, nullptr}, x, D, F};
+  int rc = launch_wgrad_engine<64>(src, num_nodes, D, D + F, chain_wgrad_tiles(D, F, 3), p,
+                                   per * p.chunks, per, slab, st);
+  if (rc != GINE_OK || !reduce) return rc;
+  return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 3,
+                         ChainWgradOut{{gfold, dwr0, dwp2, nullptr},
+                                       {gfold + (size_t)D * (F + D), dbr0, dbp2, nullptr}, D,
+                                       F, 3, bias_scale},
+                         st);
+}
+
+extern "C" int gine_chain_wgrad_folded_grad_job(int64_t num_nodes, int32_t hidden,
+                                                int32_t in_features, const float* slab,
+                                                float bias_scale, float* gfold, float* dwr0,
+                                                float* dbr0, float* dwp2, float* dbp2,
+                                                gine_grad_job* job) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !slab || !gfold || !dwr0 || !dwp2 || !job) return GINE_ERR_INVALID;
+  float* w[3] = {gfold, dwr0, dwp2};  // product order of ChainWgradSrc<3>
+  float* b[3] = {gfold + (size_t)hidden * (hidden + in_features), dbr0, dbp2};
+  chain_slab_job(num_nodes, hidden, in_features, 3, slab, bias_scale, w, b, job);
+  return GINE_OK;
+}
+
+extern "C" int gine_chain_unfold_grads(const float* gfold, const float* wr1, const float* br1,
+                                       const float* wdr, float* dwdr, float* dbdr, float* dwr1,
+                                       float* dbr1, int32_t hidden, int32_t in_features,
+                                       void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (!gfold || !wr1 || !br1 || !wdr || !dwdr || !dwr1) return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  if (hidden == 64)
+    hipLaunchKernelGGL((k_chain_unfold<64>), dim3(2 * 4), dim3(128), 0, st, gfold, wr1, br1,
+                       wdr, dwdr, dbdr, dwr1, dbr1, in_features);
+  else
+    hipLaunchKernelGGL((k_chain_unfold<128>), dim3(2 * 16), dim3(256), 0, st, gfold, wr1, br1,
+                       wdr, dwdr, dbdr, dwr1, dbr1, in_features);
+  GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

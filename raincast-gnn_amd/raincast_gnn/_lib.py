@@ -125,6 +125,13 @@ _SIGNATURES = {
     "gine_chain_bwd_slab_floats": [_i64, _i32, _i32, ctypes.POINTER(_size)],
     "gine_chain_bwd": [_c_void_p] * 17 + [_f32] + [_c_void_p] * 6 + [_i64, _i32, _i32,
                                                                        _c_void_p],
+    "gine_chain_fwd_folded": [_c_void_p] * 4 + [_f32] + [_c_void_p] * 10 + [_i64, _i32, _i32,
+                                                                              _c_void_p],
+    "gine_chain_bwd_folded": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
+    "gine_chain_wgrad_folded": [_c_void_p] * 13 + [_f32, _i64, _i32, _i32, _c_void_p],
+    "gine_chain_wgrad_folded_grad_job": [_i64, _i32, _i32, _c_void_p, _f32] + [_c_void_p] * 5
+                                        + [_job_p],
+    "gine_chain_unfold_grads": [_c_void_p] * 8 + [_i32, _i32, _c_void_p],
 }
 
 EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)

@@ -6,14 +6,21 @@ dense Linears and a ReLU on [N, D] rows::
 
     s = phi[2](r) (bias x M)  ->  u = relu(rho[0](s))  ->  e = rho[2](u)  ->  h0 = dim_red([x | e])
 
-``gine_chain_fwd`` runs them as two 2-stage row-chain kernels and ``gine_chain_bwd`` the
-backward (two chain kernels, one weight-gradient launch for all four Linears, one
-reduction) -- csrc/gine_chain.hip.  Modules, parameters and state_dict keys are the
-reference's; this is only the execution of ``GNN.forward``'s first half.
+By default the chain runs FOLDED (``gine_chain_fwd_folded``): rho[2] and dim_red have no
+nonlinearity between them, so ``h0 = [x | u] W'^T + b'`` with ``W' = [Wdr_x | Wdr_e Wr1]``
+folded from the current weights inside the first kernel; the backward needs one
+input-gradient GEMM and one weight-gradient product fewer, and dWr1 / dWdr_e are unfolded
+from ``G = dh0^T u`` after the slab reduction (profiles/r02_s38_chain_fold_ab_*: cfg2
+0.575 -> 0.560 ms per step, cfg3 3.26 -> 2.97).  RAINCAST_CHAIN_FOLD=0 runs the unfolded
+chain: ``gine_chain_fwd`` as two 2-stage row-chain kernels and ``gine_chain_bwd`` (two chain
+kernels, one weight-gradient launch for all four Linears, one reduction) -- csrc/
+gine_chain.hip.  Modules, parameters and state_dict keys are the reference's; this is only
+the execution of ``GNN.forward``'s first half.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -96,8 +103,86 @@ class _ChainFn(torch.autograd.Function):
         return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
 
 
+class _ChainFoldedFn(torch.autograd.Function):
+    """The folded chain (gine_chain_fwd_folded, include/gine_hip.h): rho[2] and dim_red have
+    no nonlinearity between them, so ``h0 = [x | u] W'^T + b'`` with ``W' = [Wdr_x | Wdr_e
+    Wr1]`` -- the embedding ``e`` and its gradient are never formed, and dWr1 / dWdr_e come
+    from the one product ``G = dh0^T u``.  Same parameters and gradients as :class:`_ChainFn`
+    (the rounding of sums differs, within the fp32 tolerance of the oracle tests)."""
+
+    @staticmethod
+    def forward(ctx, r, x, wp2, bp2, wr0, br0, wr1, br1, wdr, bdr, members):
+        r = r.contiguous()
+        x = x.contiguous()
+        N, D = r.shape
+        F = x.size(1)
+        dev = r.device
+        ws = [t.detach().contiguous() for t in (wp2, bp2, wr0, br0, wr1, br1, wdr, bdr)]
+        s, u, h0 = (torch.empty(N, D, dtype=torch.float32, device=dev) for _ in range(3))
+        wfold = torch.empty(2 * D * (F + D) + D, dtype=torch.float32, device=dev)
+        P = _lib.ptr
+        _lib.call("gine_chain_fwd_folded", P(r), P(x), P(ws[0]), P(ws[1]), float(members),
+                  P(ws[2]), P(ws[3]), P(ws[4]), P(ws[5]), P(ws[6]), P(ws[7]), P(wfold), P(s),
+                  P(u), P(h0), N, D, F, _lib.stream_handle(dev))
+        ctx.save_for_backward(r, x, s, u, wfold, ws[0], ws[2], ws[4], ws[5], ws[6])
+        ctx.params = (wp2, bp2, wr0, br0, wr1, br1, wdr, bdr)
+        ctx.members = float(members)
+        return h0
+
+    @staticmethod
+    def backward(ctx, dh0):
+        r, x, s, u, wfold, wp2, wr0, wr1, br1, wdr = ctx.saved_tensors
+        N, D = r.shape
+        F = x.size(1)
+        dev = r.device
+        dh0 = dh0.contiguous()
+        dt, ds, dr = (torch.empty(N, D, dtype=torch.float32, device=dev) for _ in range(3))
+        floats = ctypes.c_size_t(0)
+        _lib.call("gine_chain_bwd_slab_floats", N, D, F, ctypes.byref(floats))
+        slab = torch.empty(floats.value, dtype=torch.float32, device=dev)
+        gfold = torch.empty(D * (F + D) + D, dtype=torch.float32, device=dev)
+        p = ctx.params
+        g = [grad_out(p[0], (D, D), dev), grad_out(p[1], (D,), dev),
+             grad_out(p[2], (D, D), dev), grad_out(p[3], (D,), dev),
+             grad_out(p[4], (D, D), dev), grad_out(p[5], (D,), dev),
+             grad_out(p[6], (D, F + D), dev), grad_out(p[7], (D,), dev)]
+        P = _lib.ptr
+        stream = _lib.stream_handle(dev)
+        _lib.call("gine_chain_bwd_folded", P(dh0), P(u), P(wp2), P(wr0), P(wfold), P(dt), P(ds),
+                  P(dr), N, D, F, stream)
+        members = ctx.members
+
+        # raw pointers only: a reference to a gradient tensor held past this function would
+        # stop autograd adopting it as param.grad (it copies a shared tensor)
+        ptrs = (P(gfold), P(wr1), P(br1), P(wdr), P(g[6]), P(g[7]), P(g[4]), P(g[5]))
+
+        def unfold(st):
+            _lib.call("gine_chain_unfold_grads", *ptrs, D, F, st)
+
+        if gradbuf.deferrable(*g):
+            # the engine leaves its slab; the end-of-backward batch reduces it into
+            # G | dWr0 | dWp2, then unfolds G into dWdr / dWr1
+            _lib.call("gine_chain_wgrad_folded", P(dh0), P(x), P(r), P(s), P(u), P(dt), P(ds),
+                      P(slab), None, None, None, None, None, members, N, D, F, stream)
+            job = _lib.GradJob()
+            _lib.call("gine_chain_wgrad_folded_grad_job", N, D, F, P(slab), members, P(gfold),
+                      P(g[2]), P(g[3]), P(g[0]), P(g[1]), ctypes.byref(job))
+            gradbuf.defer(job, dev, (slab, gfold, wr1, br1, wdr), post=unfold)
+        else:
+            _lib.call("gine_chain_wgrad_folded", P(dh0), P(x), P(r), P(s), P(u), P(dt), P(ds),
+                      P(slab), P(gfold), P(g[2]), P(g[3]), P(g[0]), P(g[1]), members, N, D, F,
+                      stream)
+            unfold(stream)
+        return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
+
+
+# RAINCAST_CHAIN_FOLD=0: the unfolded chain (four GEMM stages forward, e materialised)
+FOLD = os.environ.get("RAINCAST_CHAIN_FOLD", "1") != "0"
+
+
 def chain(r: torch.Tensor, x: torch.Tensor, lins, members: int) -> torch.Tensor:
     """``dim_red(cat([x, rho(phi[2](r) summed over members)]))`` on the fused kernels."""
     p2, r0, r1, dr = lins
-    return _ChainFn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight, r1.bias,
-                          dr.weight, dr.bias, members)
+    fn = _ChainFoldedFn if FOLD else _ChainFn
+    return fn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight, r1.bias,
+                    dr.weight, dr.bias, members)

@@ -96,30 +96,38 @@ def deferrable(*outs) -> bool:
     return torch._C._current_graph_task_id() != -1
 
 
-def defer(job: "_lib.GradJob", device: torch.device, keep_alive=()) -> None:
-    """Queue ``job`` (its buffers kept alive) for the end-of-backward batch launch."""
+def defer(job: "_lib.GradJob", device: torch.device, keep_alive=(), post=None) -> None:
+    """Queue ``job`` (its buffers kept alive) for the end-of-backward batch launch.
+    ``post(stream)``, if given, is called after the batch launches of that stream (work that
+    reads the job's reduced outputs, e.g. gine_chain_unfold_grads)."""
     stream = _lib.stream_handle(device)
     with _pending_lock:
         first = not _pending
-        _pending.append((job, stream, tuple(keep_alive)))
+        _pending.append((job, stream, tuple(keep_alive), post))
     if first:
         torch.autograd.Variable._execution_engine.queue_callback(flush)
 
 
 def flush() -> None:
-    """Run every queued reduction (one launch per stream and per GRAD_MAX_JOBS jobs)."""
+    """Run every queued reduction (one launch per stream and per GRAD_MAX_JOBS jobs), then
+    the queued post steps."""
     with _pending_lock:
         items = list(_pending)
         _pending.clear()
     by_stream: dict = {}
-    for job, stream, keep in items:
-        by_stream.setdefault(stream, []).append(job)
-    for stream, jobs in by_stream.items():
+    for job, stream, keep, post in items:
+        by_stream.setdefault(stream, ([], []))
+        by_stream[stream][0].append(job)
+        if post is not None:
+            by_stream[stream][1].append(post)
+    for stream, (jobs, posts) in by_stream.items():
         for i in range(0, len(jobs), _lib.GRAD_MAX_JOBS):
             part = jobs[i:i + _lib.GRAD_MAX_JOBS]
             arr = (_lib.GradJob * len(part))(*part)
             _lib.call("gine_grad_finalize_batch", arr, len(part), stream)
-    # the buffers in ``items`` are released here, after their consumer is enqueued
+        for post in posts:
+            post(stream)
+    # the buffers in ``items`` are released here, after their consumers are enqueued
 
 
 def mp_job(partials: torch.Tensor, rows: int, channels: int, eps_cols: int, dlw, dlb, deps):

@@ -1,7 +1,8 @@
 """Fused dense chain (csrc/gine_chain.hip): phi[2] (member-summed) -> rho -> dim_red of
 models/gnn.py:48-68,112-113,132-135, forward and backward, against the same composition
 of torch Linears in fp64.  All eight parameter gradients, dr (-> DeepSet backward) and h0
-are checked at max-norm relative 1e-5 (fp32 MFMA accumulation over <= 16,000 rows)."""
+are checked at max-norm relative 1e-5 (fp32 MFMA accumulation over <= 16,000 rows), for
+the folded chain (the default: rho[2] folded into dim_red) and the unfolded one."""
 import pytest
 import torch
 
@@ -34,9 +35,15 @@ def _ref(r, x, lins, M):
     return h0, [t for pair in (p2, r0, r1, dr) for t in pair]
 
 
+@pytest.fixture(params=[True, False], ids=["folded", "unfolded"])
+def fold(request, monkeypatch):
+    monkeypatch.setattr(fused_chain, "FOLD", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("N,D,F,M", [(1, 128, 35, 11), (33, 128, 35, 11), (16000, 128, 35, 11),
                                      (1000, 64, 35, 51), (257, 128, 64, 3), (70, 64, 8, 1)])
-def test_chain_matches_torch_fp64(N, D, F, M):
+def test_chain_matches_torch_fp64(N, D, F, M, fold):
     lins = _lins(D, F, N + D + F)
     g = torch.Generator().manual_seed(N)
     r = (torch.randn(N, D, generator=g) * 3).to(DEV).requires_grad_()
@@ -56,7 +63,7 @@ def test_chain_matches_torch_fp64(N, D, F, M):
         assert _rel(a, b.grad) <= TOL, (name, _rel(a, b.grad))
 
 
-def test_chain_deterministic():
+def test_chain_deterministic(fold):
     lins = _lins(128, 35, 5)
     r = torch.randn(5000, 128, device=DEV, requires_grad=True)
     x = torch.randn(5000, 35, device=DEV)
@@ -108,6 +115,72 @@ def test_chain_bwd_intermediates(N, D, F):
     assert _rel(dr, dr64) <= TOL, "dr"
     xe = torch.cat([d(x), d(e)], 1)
     for name, got, ref in (("dWp2", g[0], ds64.T @ d(r)), ("dbp2", g[1], ds64.sum(0)),
+                           ("dWr0", g[2], dt64.T @ d(s)), ("dbr0", g[3], dt64.sum(0)),
+                           ("dWr1", g[4], de64.T @ d(u)), ("dbr1", g[5], de64.sum(0)),
+                           ("dWdr", g[6], d(dh0).T @ xe), ("dbdr", g[7], d(dh0).sum(0))):
+        assert _rel(got, ref) <= TOL, (name, _rel(got, ref))
+
+
+@pytest.mark.parametrize("N,D,F", [(33, 128, 35), (300, 64, 35), (2000, 128, 64)])
+def test_chain_folded_intermediates(N, D, F):
+    """The folded chain's pieces (C ABI) against fp64 torch: W' | b' from the forward, dt /
+    ds / dr, the engine's G | g and the weight gradients unfolded from it."""
+    import ctypes
+
+    from raincast_gnn import _lib
+    torch.manual_seed(2)
+    f = lambda *s: torch.randn(*s, device=DEV)  # noqa: E731
+    r, x = f(N, D), f(N, F)
+    wp2, wr0, wr1, wdr = f(D, D) / 10, f(D, D) / 10, f(D, D) / 10, f(D, F + D) / 10
+    bp2, br0, br1, bdr = f(D), f(D), f(D), f(D)
+    s, u, h0 = (torch.empty(N, D, device=DEV) for _ in range(3))
+    wfold = torch.full((2 * D * (F + D) + D,), float("nan"), device=DEV)
+    P = _lib.ptr
+    st = _lib.stream_handle(DEV)
+    _lib.call("gine_chain_fwd_folded", P(r), P(x), P(wp2), P(bp2), 7.0, P(wr0), P(br0), P(wr1),
+              P(br1), P(wdr), P(bdr), P(wfold), P(s), P(u), P(h0), N, D, F, st)
+    d = lambda t: t.double()  # noqa: E731
+    s64 = d(r) @ d(wp2).T + 7.0 * d(bp2)
+    u64 = torch.relu(d(s) @ d(wr0).T + d(br0))
+    e64 = d(u) @ d(wr1).T + d(br1)
+    h64 = torch.cat([d(x), e64], 1) @ d(wdr).T + d(bdr)
+    wc64 = d(wdr)[:, F:] @ d(wr1)
+    torch.cuda.synchronize()
+    W = wfold[:D * (F + D)].view(D, F + D)
+    assert torch.equal(W[:, :F], wdr[:, :F])
+    assert _rel(W[:, F:], wc64) <= TOL
+    assert _rel(wfold[D * (F + D):D * (F + D) + D], d(wdr)[:, F:] @ d(br1) + d(bdr)) <= TOL
+    assert torch.equal(wfold[D * (F + D) + D:].view(F + D, D), W.T)
+    assert _rel(s, s64) <= TOL and _rel(u, u64) <= TOL and _rel(h0, h64) <= TOL
+
+    dh0 = f(N, D)
+    dt, ds, dr = (torch.empty(N, D, device=DEV) for _ in range(3))
+    _lib.call("gine_chain_bwd_folded", P(dh0), P(u), P(wp2), P(wr0), P(wfold), P(dt), P(ds),
+              P(dr), N, D, F, st)
+    fl = ctypes.c_size_t(0)
+    _lib.call("gine_chain_bwd_slab_floats", N, D, F, ctypes.byref(fl))
+    slab = torch.empty(fl.value, device=DEV)
+    gfold = torch.empty(D * (F + D) + D, device=DEV)
+    g = [torch.full((D, D), 5.0, device=DEV), torch.empty(D, device=DEV),
+         torch.full((D, D), 5.0, device=DEV), torch.empty(D, device=DEV),
+         torch.full((D, D), 5.0, device=DEV), torch.empty(D, device=DEV),
+         torch.full((D, F + D), 5.0, device=DEV), torch.empty(D, device=DEV)]
+    _lib.call("gine_chain_wgrad_folded", P(dh0), P(x), P(r), P(s), P(u), P(dt), P(ds), P(slab),
+              P(gfold), P(g[2]), P(g[3]), P(g[0]), P(g[1]), 7.0, N, D, F, st)
+    _lib.call("gine_chain_unfold_grads", P(gfold), P(wr1), P(br1), P(wdr), P(g[6]), P(g[7]),
+              P(g[4]), P(g[5]), D, F, st)
+    torch.cuda.synchronize()
+    de64 = d(dh0) @ d(wdr)[:, F:]
+    dt64 = (de64 @ d(wr1)) * (u > 0).double()
+    ds64 = dt64 @ d(wr0)
+    dr64 = ds64 @ d(wp2)
+    assert _rel(dt, dt64) <= TOL, "dt"
+    assert _rel(ds, ds64) <= TOL, "ds"
+    assert _rel(dr, dr64) <= TOL, "dr"
+    e_in = d(u) @ d(wr1).T + d(br1)  # e of the saved u
+    xe = torch.cat([d(x), e_in], 1)
+    assert _rel(gfold[:D * (F + D)].view(D, F + D), d(dh0).T @ torch.cat([d(x), d(u)], 1)) <= TOL
+    for name, got, ref in (("dWp2", g[0], ds64.T @ d(r)), ("dbp2", g[1], 7.0 * ds64.sum(0)),
                            ("dWr0", g[2], dt64.T @ d(s)), ("dbr0", g[3], dt64.sum(0)),
                            ("dWr1", g[4], de64.T @ d(u)), ("dbr1", g[5], de64.sum(0)),
                            ("dWdr", g[6], d(dh0).T @ xe), ("dbdr", g[7], d(dh0).sum(0))):
