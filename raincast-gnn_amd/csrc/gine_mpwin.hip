@@ -28,9 +28,15 @@ namespace {
 constexpr int kWinThreads = 512;
 constexpr int kWinWaves = kWinThreads / kWave;
 constexpr int kWinMaxSlices = 8;    // column slices per tile (= finalize columns per block)
-constexpr int kWinUnroll = 6;       // neighbour rows in flight per lane (LDS reads)
+#ifndef GINE_WIN_UNROLL  // tuning experiments
+#define GINE_WIN_UNROLL 6
+#endif
+#ifndef GINE_WIN_ROW_BYTES
+#define GINE_WIN_ROW_BYTES (64 * 1024)
+#endif
+constexpr int kWinUnroll = GINE_WIN_UNROLL;  // neighbour rows in flight per lane (LDS reads)
 constexpr int kWinTileNodes = 128;  // planner cap on nodes per tile
-constexpr int kWinRowBytes = 64 * 1024;
+constexpr int kWinRowBytes = GINE_WIN_ROW_BYTES;
 // every thread's share of a tile's global loads, issued in one batch (bounds by construction:
 // window slice <= kWinRowBytes, tile edges <= kWinEdgeLoads * kWinThreads)
 constexpr int kWinRowLoads = kWinRowBytes / 16 / kWinThreads;  // float4 per thread
@@ -193,8 +199,13 @@ struct WinEngine {
 };
 constexpr size_t kWinEngineLds = sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
 
+// GINE_WIN_ENG_OCC (tuning experiments): workgroups per CU the combined launch is compiled
+// for (register budget); the plan's LDS must allow as many.
+#ifndef GINE_WIN_ENG_OCC
+#define GINE_WIN_ENG_OCC 2
+#endif
 template <int CS, bool FMA, bool ENG = false, int PDO = PRO_PLAIN>
-__global__ __launch_bounds__(kWinThreads, 2) void k_mp_bwd_win(
+__global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_bwd_win(
     const float4* __restrict__ dz4, const float4* __restrict__ x4,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ nbr,
     const float* __restrict__ attr, const float4* __restrict__ lw4,

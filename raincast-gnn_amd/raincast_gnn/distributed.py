@@ -41,8 +41,9 @@ class FlatGradReducer:
         dev = self.params[0].device
         total = sum(p.numel() for p in self.params)
         self.group = group
-        if flat is not None:  # gradients already live in this buffer (e.g. FlatAdamW's)
-            if flat.numel() != total:
+        if flat is not None:  # gradients already live in this buffer (e.g. FlatAdamW's,
+            # whose parameter slices are aligned: it may hold zero gaps between them)
+            if flat.numel() < total:
                 raise ValueError("flat gradient buffer does not match the parameters")
             self.flat = flat
             return

@@ -22,7 +22,9 @@ from . import _lib
 # Window-staged message passing (gine_graph_plan_windows / gine_mp_*_win): channel-slice
 # widths tried, the LDS bytes a window slice may take, and the tile size in nodes.
 WINDOW_SLICES = (32, 16, 8)
-WINDOW_ROW_BYTES = 64 * 1024
+WINDOW_ROW_BYTES = int(os.environ.get("GINE_MP_WINDOW_ROW_BYTES", 64 * 1024))
+# LDS a window workgroup may take (tuning experiments lower it to fit more workgroups per CU)
+WINDOW_LDS_BUDGET = int(os.environ.get("GINE_MP_WINDOW_LDS_BYTES", _lib.WINDOW_LDS_BYTES))
 
 
 # A window launch has tiles x slices workgroups; below this many the gather kernels (one
@@ -67,7 +69,7 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
         slices = (int(pref),)
     for cs in slices:
         max_rows = WINDOW_ROW_BYTES // (cs * 4)
-        max_edges = (_lib.WINDOW_LDS_BYTES - max_rows * cs * 4 - (max_nodes + 1) * 4) // 8
+        max_edges = (WINDOW_LDS_BUDGET - max_rows * cs * 4 - (max_nodes + 1) * 4) // 8
         tb = torch.empty(num_nodes + 1, **i32)
         lo = torch.empty(num_nodes, **i32)
         rows = torch.empty(num_nodes, **i32)

@@ -15,6 +15,8 @@ from . import _lib, gradbuf
 
 
 class FlatAdamW:
+    ALIGN = 64  # floats: parameter offsets in the flat buffers
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
@@ -25,20 +27,24 @@ class FlatAdamW:
             raise TypeError("FlatAdamW needs fp32 parameters on one device")
         self.lr, self.betas, self.eps, self.weight_decay = float(lr), betas, float(eps), \
             float(weight_decay)
-        n = sum(p.numel() for p in self.params)
+        # every parameter starts on a 256-byte boundary (the kernels' weight fragment loads
+        # use 16-byte vectors when a weight is aligned); the gaps stay zero in all four flat
+        # buffers, which AdamW leaves at zero
         self._offsets = []
-        self.flat_param = torch.empty(n, dtype=torch.float32, device=dev)
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
         off = 0
+        for p in self.params:
+            self._offsets.append(off)
+            off = -(-(off + p.numel()) // self.ALIGN) * self.ALIGN
+        n = off
+        self.flat_param = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
         with torch.no_grad():
-            for p in self.params:
+            for p, off in zip(self.params, self._offsets):
                 k = p.numel()
                 view = self.flat_param[off:off + k].view_as(p)
                 view.copy_(p)
                 p.data = view
                 gradbuf.register(p, self.flat_grad, off)
-                self._offsets.append(off)
-                off += k
         self.exp_avg = torch.zeros_like(self.flat_param)
         self.exp_avg_sq = torch.zeros_like(self.flat_param)
         # [count, ticket]: gine_adamw_step bumps the count in its last workgroup

@@ -134,7 +134,7 @@ def _dp_worker(rank, world, port, out_dir):
     runner._fwd_bwd(batch)
     red.all_reduce_()
     torch.cuda.synchronize()
-    torch.save({"flat": opt.flat_grad.cpu(), "start": start,
+    torch.save({"flat": opt.flat_grad.cpu(), "start": start, "offsets": list(opt._offsets),
                 "names": [n for n, _ in model.named_parameters()]},
                os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
@@ -167,15 +167,19 @@ def test_engine_data_parallel_gradient_is_mean_of_shards(tmp_path):
             ref.loss_fn.crps(ref(b), b.y).backward()
             grads.append(torch.cat([p.grad.reshape(-1) for p in ref.net.parameters()]))
         means[dt] = torch.stack(grads).mean(0)
-    off = 0
+    off = 0  # into the packed oracle gradient; FlatAdamW's slices are aligned (gaps zero)
     names = res[0]["names"]
     shapes = [p.shape for p in _Oracle(params).net.parameters()]
-    for name, shp in zip(names, shapes):
+    for name, shp, foff in zip(names, shapes, res[0]["offsets"]):
         n = int(torch.Size(shp).numel())
         sl = slice(off, off + n)
         off += n
         if name.endswith(".eps") or name.endswith(".nn.0.bias"):
             continue  # conditioning-scaled / analytically-zero: covered in test_gpu_parity
-        assert_close_tiebreak(res[0]["flat"][sl], means[torch.float32][sl],
+        assert_close_tiebreak(res[0]["flat"][foff:foff + n], means[torch.float32][sl],
                               means[torch.float64][sl], TOL, name)
-    assert off == res[0]["flat"].numel()
+    assert off == means[torch.float32].numel()
+    covered = torch.zeros(res[0]["flat"].numel(), dtype=torch.bool)
+    for shp, foff in zip(shapes, res[0]["offsets"]):
+        covered[foff:foff + int(torch.Size(shp).numel())] = True
+    assert not res[0]["flat"][~covered].any()  # the alignment gaps hold no gradient
