@@ -36,7 +36,9 @@ constexpr int kRowTile = 32;
 
 // F2F / B1F: the one-stage kernels of the folded chain (rho[2] folded into dim_red, see
 // gine_chain_fwd_folded): F2F h0 = [x | u] W'^T + b', B1F dt = (dh0 Wc) * 1[u > 0].
-enum ChainKind { CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3, CH_F2F = 4, CH_B1F = 5 };
+// B3: the folded chain's whole input-gradient backward in one launch (B1F's stage, then B2's
+// two: dt -> ds -> dr, each stage's output the next one's A tile in LDS).
+enum ChainKind { CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3, CH_F2F = 4, CH_B1F = 5, CH_B3 = 6 };
 
 struct ChainArgs {
   const float* in;   // stage-1 A rows [N, D]: r | u | dh0 | dt | u (F2F) | dh0 (B1F)
@@ -54,6 +56,8 @@ struct ChainArgs {
   // ([D][F + D] then [D]) once the tiles are done (NULL: not folded)
   const float *fw_r1, *fb_r1, *fw_dr, *fb_dr;
   float* wfold;
+  const float* w3;  // B3: stage-3 weight (Wp2)
+  float* out3;      // B3: stage-3 output (dr)
 };
 
 __device__ __forceinline__ floatx16 zero16() {
@@ -327,8 +331,8 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     }
   } else if constexpr (KIND == CH_F2) {
     frag_t<D>(bf1, a.w1, D, col, h);
-  } else if constexpr (KIND == CH_B1 || KIND == CH_B1F) {
-    frag_n<D>(bf1, a.w1, a.F + D, a.F, col, h);     // dim_red (B1F: W') weight, e columns
+  } else if constexpr (KIND == CH_B1 || KIND == CH_B1F || KIND == CH_B3) {
+    frag_n<D>(bf1, a.w1, a.F + D, a.F, col, h);     // dim_red (B1F / B3: W') weight, e columns
   } else if constexpr (KIND == CH_B2) {
     frag_n<D>(bf1, a.w1, D, 0, col, h);
   }
@@ -336,9 +340,11 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     frag_dimred<FP, D>(bf2, a.w2, a.F, col, h);
   } else if constexpr (KIND == CH_F2F) {
     frag_dimred_t<FP, D>(bf2, a.w2, a.F, col, h);  // w2 = W'^T
-  } else if constexpr (KIND == CH_B1 || KIND == CH_B2) {
+  } else if constexpr (KIND == CH_B1 || KIND == CH_B2 || KIND == CH_B3) {
     frag_n<D>(bf2, a.w2, D, 0, col, h);
   }
+  float bf3[KIND == CH_B3 ? D / 2 : 1];
+  if constexpr (KIND == CH_B3) frag_n<D>(bf3, a.w3, D, 0, col, h);
   float bias1 = 0.f, bias2 = 0.f;
   if constexpr (KIND == CH_F1 || KIND == CH_F2) bias1 = a.b1[col] * a.bias1_scale;
   if constexpr (KIND == CH_F1 || kDimRed) bias2 = a.b2[col];
@@ -389,7 +395,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     __syncthreads();
     if (tile + tr.step < tr.end) load_tile(tile + tr.step, raw, xr);  // next tile in flight
     float ep[16];
-    if constexpr (KIND == CH_B1 || KIND == CH_B1F) {  // ReLU mask operand, in flight too
+    if constexpr (KIND == CH_B1 || KIND == CH_B1F || KIND == CH_B3) {  // ReLU mask, in flight
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -415,7 +421,8 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       for (int r = 0; r < 16; ++r) {
         const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t n = n0 + rr;
-        const float v = acc[r] + bias1;
+        float v = acc[r] + bias1;
+        if constexpr (KIND == CH_B3) v = ep[r] > 0.f ? acc[r] : 0.f;  // dt = du * 1[u > 0]
         sB[rr * LDB + BOFF + col] = v;
         if (n < N) a.out1[n * D + col] = v;
       }
@@ -431,7 +438,17 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       float v = acc[r] + bias2;
       if constexpr (KIND == CH_F1) v = relu_nan(v);              // u = relu(rho[0](s))
       if constexpr (KIND == CH_B1) v = ep[r] > 0.f ? v : 0.f;   // dt = du * 1[u > 0]
+      if constexpr (KIND == CH_B3) sA[rr * LDA + col] = v;      // stage 3's A tile
       if (n < N) a.out2[n * D + col] = v;
+    }
+    if constexpr (KIND == CH_B3) {  // stage 3: dr = ds Wp2 (sA: every wave is past stage 1)
+      __syncthreads();
+      acc = tile_mma<D>(sA, LDA, bf3, c32, h);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (n < N) a.out3[n * D + col] = acc[r];
+      }
     }
   }
 }
@@ -445,6 +462,15 @@ inline int chain_grid(int64_t N) {
   }();
   const int64_t tiles = ceil_div(N, kRowTile);
   return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cap));
+}
+
+// GINE_CHAIN_B3=0 (A/B experiments): the folded backward as two launches (B1F, B2)
+inline bool chain_b3() {
+  static const bool on = [] {
+    const char* e = getenv("GINE_CHAIN_B3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 template <int D, int FP, int KIND>
@@ -834,9 +860,18 @@ extern "C" int gine_chain_bwd_folded(const float* dh0, const float* u, const flo
   if (!dh0 || !u || !wp2 || !wr0 || !wfold || !dt || !ds || !dr) return GINE_ERR_INVALID;
   hipStream_t st = as_stream(stream);
   const int F = in_features;
+  int rc = GINE_OK;
+  if (chain_b3()) {  // one launch: dt -> ds -> dr
+    ChainArgs b{dh0, nullptr, u, wfold, nullptr, wr0, nullptr, dt, ds, 1.f, F};
+    b.w3 = wp2;
+    b.out3 = dr;
+#define CALL_B(DD, FF) rc = launch_chain<DD, FF, CH_B3>(b, num_nodes, st)
+    GINE_CHAIN_DISPATCH(hidden, F, CALL_B);
+#undef CALL_B
+    return rc;
+  }
   const ChainArgs b1{dh0, nullptr, u, wfold, nullptr, nullptr, nullptr, nullptr, dt, 1.f, F};
   const ChainArgs b2{dt, nullptr, nullptr, wr0, nullptr, wp2, nullptr, ds, dr, 1.f, F};
-  int rc = GINE_OK;
 #define CALL_B(DD, FF)                                                  \
   rc = launch_chain<DD, FF, CH_B1F>(b1, num_nodes, st);                 \
   if (rc == GINE_OK) rc = launch_chain<DD, FF, CH_B2>(b2, num_nodes, st)
