@@ -137,11 +137,20 @@ typedef struct gine_window_plan {
   int32_t num_tiles;
   int32_t slice_channels;
   int32_t max_rows, max_edges, max_nodes;
+  const int16_t* slot;       /* device [num_nodes] or NULL: gine_graph_plan_window_slots */
 } gine_window_plan;
 int gine_graph_plan_windows(const int32_t* rowptr, const int32_t* nbr, int64_t num_nodes,
                             int32_t max_rows, int32_t max_nodes, int32_t max_edges,
                             int32_t* tile_begin, int32_t* win_lo, int32_t* win_rows,
                             int32_t* num_tiles, int32_t* maxima);
+/* Work order inside the tiles of a backward (out-CSR) window plan (HOST pointers):
+ * slot[tile_begin[t] + s] = the tile-local node a workgroup processes at position s.  A
+ * lane group takes positions g and g + 64 one after the other; the order pairs each tile's
+ * nodes by out-degree (heaviest with lightest, ties by index), so the groups of a wave run
+ * chains of similar length.  Per-node results are unchanged (each node's edges are still
+ * summed in their own order). */
+int gine_graph_plan_window_slots(const int32_t* rowptr, const int32_t* tile_begin,
+                                 int32_t num_tiles, int16_t* slot);
 /* Locality order of a graph's nodes (HOST pointers: a host copy of a CSR, either
  * direction; the adjacency is symmetrised).  order[i] = the node placed at position i:
  * reverse Cuthill-McKee, deterministic.  Relabelling a static station graph this way before

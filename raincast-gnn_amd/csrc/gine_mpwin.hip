@@ -20,7 +20,9 @@
 #include "gine_mlpsrc.hpp"
 #include "gine_reduce.hpp"
 
+#include <algorithm>
 #include <climits>
+#include <vector>
 
 namespace gine {
 namespace {
@@ -42,11 +44,25 @@ constexpr int kWinRowBytes = GINE_WIN_ROW_BYTES;
 constexpr int kWinRowLoads = kWinRowBytes / 16 / kWinThreads;  // float4 per thread
 constexpr int kWinEdgeLoads = 4;
 
+#ifdef GINE_WIN_PROFILE
+// Debug build only (make winprof): s_memtime at the phase boundaries of the window backward,
+// per workgroup: [block][8] (entry, loads issued, staged, edges done, reduced, end).
+__device__ long long g_win_prof[4096][8];
+#define WIN_MARK(i)                                                                   \
+  do {                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                        \
+      g_win_prof[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memtime();           \
+  } while (0)
+#else
+#define WIN_MARK(i) do {} while (0)
+#endif
+
 struct WinPlan {
   const int32_t* tile_begin;  // [T + 1]
   const int32_t* win_lo;      // [T]
   const int32_t* win_rows;    // [T]
   int max_rows, max_edges, max_nodes;
+  const int16_t* slot;        // [N] or null: tile-local node at each work position
 };
 
 // Dynamic LDS: window [max_rows][Q] float4 | nbr [max_edges] | attr [max_edges] | rp [nodes+1]
@@ -234,6 +250,7 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
       job.run(blockIdx.x - eb, reinterpret_cast<double(*)[kSlabQuads * 4 + 1]>(s_dyn));
     return;
   }
+  WIN_MARK(0);
   const WinLds lds(s_dyn, plan, Q);
   const int lb = xcd_remap(blockIdx.x - eb - job.nblocks, gridDim.x - eb - job.nblocks);
   const int tile = lb / S, slice = lb % S, col4 = slice * Q;
@@ -244,10 +261,17 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
   const char* dzb = reinterpret_cast<const char*>(dz4);
   const char* rb = reinterpret_cast<const char*>(dres4 != nullptr ? dres4 : dz4);
   const uint32_t rowb = (uint32_t)D4 * 16u, tb = (uint32_t)(col4 + t) * 16u;
+  // work position g + p*G -> tile-local node (the plan's degree-balanced order, if any)
+  int dn[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int d = min(g + p * G, nodes - 1);
+    dn[p] = plan.slot != nullptr ? (int)plan.slot[n0 + d] : d;
+  }
   f4v h[P], gs[P], rs[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    const uint32_t off = (uint32_t)(n0 + min(g + p * G, nodes - 1)) * rowb + tb;
+    const uint32_t off = (uint32_t)(n0 + dn[p]) * rowb + tb;
     h[p] = ld_f4v(xb, off);
     gs[p] = ld_f4v(dzb, off);
     rs[p] = ld_f4v(rb, off);
@@ -256,16 +280,18 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
   const f4v b = ld_f4v(reinterpret_cast<const char*>(lb4), tb);
   const float ope = 1.0f + eps[0];
   const bool add_self = (flags & GINE_MP_BWD_SELF) != 0;
+  WIN_MARK(1);
   stage_tile<Q>(dz4, D4, col4, rowptr, nbr, attr, n0, nodes, lo, plan.win_rows[tile], lds);
   __syncthreads();
+  WIN_MARK(2);
   const char* wb = reinterpret_cast<const char*>(lds.win) + t * 16;
 
   double pw[4] = {0.0, 0.0, 0.0, 0.0}, pb[4] = {0.0, 0.0, 0.0, 0.0};
   double pe = 0.0;
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    const int d = g + p * G;
-    if (d >= nodes) break;
+    if (g + p * G >= nodes) break;
+    const int d = dn[p];
     const int eb = lds.rp[d], ee = lds.rp[d + 1];
     f4v acc = f4v_zero(), accw = f4v_zero();
     int j = eb;
@@ -308,6 +334,10 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
           ((double)gs[p].z * (double)h[p].z + (double)gs[p].w * (double)h[p].w);
   }
 
+#ifdef GINE_WIN_PROFILE
+  __syncthreads();
+#endif
+  WIN_MARK(3);
   // Fixed-order block reduction: the G destination groups of a wave by butterfly over the
   // lane bits above Q, then the waves in order through LDS (the window is dead by now).
 #pragma unroll
@@ -332,6 +362,7 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
   }
   if (lane == 0) s_red[wave * (2 * CS + 1) + 2 * CS] = pe;
   __syncthreads();
+  WIN_MARK(4);
   const int D = D4 * 4;
   double* out = partials + (size_t)tile * 3 * D;
   for (int i = threadIdx.x; i <= 2 * CS; i += kWinThreads) {
@@ -342,6 +373,7 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
     else if (i < 2 * CS) out[D + slice * CS + (i - CS)] = v;
     else out[2 * D + slice] = v;
   }
+  WIN_MARK(5);
 }
 
 // Finish: blocks b < nb-1 own kWinMaxSlices of the 2D columns [dW_e | db_e]; the last one
@@ -388,7 +420,7 @@ bool valid_plan(const gine_window_plan* p, int64_t num_nodes, int32_t channels) 
 
 WinPlan device_plan(const gine_window_plan* p) {
   return WinPlan{p->tile_begin, p->win_lo, p->win_rows, p->max_rows, p->max_edges,
-                 p->max_nodes};
+                 p->max_nodes, p->slot};
 }
 
 // Raise the kernel's dynamic-LDS ceiling once per instantiation (thread-safe static init).
@@ -547,6 +579,28 @@ extern "C" int gine_graph_plan_windows(const int32_t* rowptr, const int32_t* nbr
   return GINE_OK;
 }
 
+extern "C" int gine_graph_plan_window_slots(const int32_t* rowptr, const int32_t* tile_begin,
+                                            int32_t num_tiles, int16_t* slot) {
+  if (!rowptr || !tile_begin || !slot || num_tiles < 0) return GINE_ERR_INVALID;
+  constexpr int G = kWinThreads / 8;  // lane groups of the 32-channel backward
+  std::vector<int> idx;
+  for (int t = 0; t < num_tiles; ++t) {
+    const int n0 = tile_begin[t], n = tile_begin[t + 1] - n0;
+    if (n < 0 || n > kWinTileNodes) return GINE_ERR_INVALID;
+    idx.resize(n);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) {
+      return rowptr[n0 + a + 1] - rowptr[n0 + a] > rowptr[n0 + b + 1] - rowptr[n0 + b];
+    });
+    // positions [0, G): the heaviest nodes; position G + g: the (g+1)-th lightest, so the
+    // lane group that runs the heaviest node runs the lightest second
+    const int first = n < G ? n : G;
+    for (int s = 0; s < first; ++s) slot[n0 + s] = (int16_t)idx[s];
+    for (int g = 0; G + g < n; ++g) slot[n0 + G + g] = (int16_t)idx[n - 1 - g];
+  }
+  return GINE_OK;
+}
+
 extern "C" int gine_mp_fwd_win(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                                const float* in_attr, const float* lin_w, const float* lin_b,
                                const float* eps, float* z, int64_t num_nodes, int32_t channels,
@@ -659,3 +713,10 @@ extern "C" int gine_mp_bwd_win_finalize(const double* partials, int32_t num_tile
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
+
+#ifdef GINE_WIN_PROFILE
+extern "C" int gine_debug_win_prof(long long* out) {  // [4096][8] host buffer
+  GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_prof), sizeof(g_win_prof)));
+  return GINE_OK;
+}
+#endif

@@ -35,7 +35,7 @@ class WindowPlan(ctypes.Structure):
     """``gine_window_plan`` (include/gine_hip.h): device tile arrays + LDS sizing."""
     _fields_ = [("tile_begin", _c_void_p), ("win_lo", _c_void_p), ("win_rows", _c_void_p),
                 ("num_tiles", _i32), ("slice_channels", _i32), ("max_rows", _i32),
-                ("max_edges", _i32), ("max_nodes", _i32)]
+                ("max_edges", _i32), ("max_nodes", _i32), ("slot", _c_void_p)]
 
 
 _plan_p = ctypes.POINTER(WindowPlan)
@@ -125,6 +125,7 @@ _SIGNATURES = {
     "gine_chain_bwd_slab_floats": [_i64, _i32, _i32, ctypes.POINTER(_size)],
     "gine_chain_bwd": [_c_void_p] * 17 + [_f32] + [_c_void_p] * 6 + [_i64, _i32, _i32,
                                                                        _c_void_p],
+    "gine_graph_plan_window_slots": [_c_void_p, _c_void_p, _i32, _c_void_p],
     "gine_chain_fwd_folded": [_c_void_p] * 4 + [_f32] + [_c_void_p] * 10 + [_i64, _i32, _i32,
                                                                               _c_void_p],
     "gine_chain_bwd_folded": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],

@@ -52,11 +52,13 @@ def window_settings() -> tuple[str, int]:
 
 
 def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device,
-                 max_nodes: int, max_staged: float | None = WINDOW_MAX_STAGED) -> dict:
+                 max_nodes: int, max_staged: float | None = WINDOW_MAX_STAGED,
+                 slots: bool = False) -> dict:
     """slice channels -> (WindowPlan, device arrays) or None, from a host copy of one CSR.
     ``max_staged`` rejects plans staging more than that many times the node table (None:
-    keep every plan, GINE_MP_WINDOW=all).  Blocks on the device (a D2H copy): call outside
-    graph capture."""
+    keep every plan, GINE_MP_WINDOW=all).  ``slots``: add the degree-balanced work order of
+    the backward (gine_graph_plan_window_slots; GINE_MP_WINDOW_SLOTS=0 leaves it out).
+    Blocks on the device (a D2H copy): call outside graph capture."""
     plans = {}
     if num_nodes == 0:
         return plans
@@ -86,6 +88,12 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
         m = [int(v) for v in maxima]
         plan = _lib.WindowPlan(arrays[0].data_ptr(), arrays[1].data_ptr(), arrays[2].data_ptr(),
                                T, cs, m[0], m[1], max(m[2], 1))
+        if slots and os.environ.get("GINE_MP_WINDOW_SLOTS", "1") != "0":
+            slot = torch.empty(num_nodes, dtype=torch.int16)
+            _lib.call("gine_graph_plan_window_slots", rp.data_ptr(), tb.data_ptr(), T,
+                      slot.data_ptr())
+            arrays = arrays + (slot.to(device),)
+            plan.slot = arrays[3].data_ptr()
         plans[cs] = (plan, arrays)
     return plans
 
@@ -157,7 +165,7 @@ class GineGraph:
             self._windows["in"] = plan_windows(self.in_rowptr, self.in_src, self.num_nodes,
                                                self.device, max_nodes, staged)
         self._windows["out"] = plan_windows(self.out_rowptr, self.out_dst, self.num_nodes,
-                                            self.device, max_nodes, staged)
+                                            self.device, max_nodes, staged, slots=True)
         self._windows["min_wg"] = 0 if mode == "all" else WINDOW_MIN_WORKGROUPS
 
     def window_plan(self, side: str, channels: int):

@@ -119,3 +119,34 @@ def test_window_entry_points_validate_on_host():
     assert lib.gine_mp_fwd_win(*([None] * 8), 100, 128, 0, ctypes.byref(plan_), None) == 1
     assert lib.gine_mp_bwd_win_finalize(None, 4, 128, 32, None, None, None, None) == 1
     assert lib.gine_mp_bwd_win_finalize(good, 4, 128, 48, good, good, good, None) == 1
+
+
+@pytest.mark.parametrize("max_nodes", [128, 100, 40])
+def test_plan_window_slots_balance_degrees(max_nodes):
+    """gine_graph_plan_window_slots: per tile a permutation of its nodes; positions [0, 64)
+    hold the heaviest nodes, position 64 + g the (g+1)-th lightest, so the lane group that
+    runs the heaviest node runs the lightest one second."""
+    ei, ea, n = knn_batch_graph(500, 10, 3, seed=1)
+    rowptr, nbr = csr(ei, n, 0)
+    T, tb, lo, rows, mx = plan(rowptr, nbr, n, 512, max_nodes, 1900)
+    slot = np.full(n, -1, np.int16)
+    _lib.call("gine_graph_plan_window_slots", rowptr.ctypes.data, tb.ctypes.data, T,
+              slot.ctypes.data)
+    deg = np.diff(rowptr)
+    for t in range(T):
+        n0, m = tb[t], tb[t + 1] - tb[t]
+        s = slot[n0:n0 + m].astype(np.int64)
+        assert sorted(s.tolist()) == list(range(m))          # a permutation of the tile
+        d = deg[n0 + s]
+        first = min(m, 64)
+        assert np.all(np.diff(d[:first]) <= 0)                # heaviest first
+        if m > 64:
+            assert np.all(np.diff(d[64:]) >= 0)               # then lightest first
+            assert d[:first].min() >= d[64:].max()
+            pair = d[:m - 64] + d[64:]
+            naive = deg[n0:n0 + m - 64] + deg[n0 + 64:n0 + m]
+            assert pair.max() <= naive.max()
+    bad = np.array([0, 200], np.int32)                        # a tile wider than 128 nodes
+    with pytest.raises(_lib.GineError):
+        _lib.call("gine_graph_plan_window_slots", np.zeros(201, np.int32).ctypes.data,
+                  bad.ctypes.data, 1, np.zeros(200, np.int16).ctypes.data)
