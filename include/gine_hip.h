@@ -138,6 +138,7 @@ typedef struct gine_window_plan {
   int32_t slice_channels;
   int32_t max_rows, max_edges, max_nodes;
   const int16_t* slot;       /* device [num_nodes] or NULL: gine_graph_plan_window_slots */
+  const int32_t* edge_begin; /* device [num_tiles + 1] or NULL: rowptr[tile_begin[t]] */
 } gine_window_plan;
 int gine_graph_plan_windows(const int32_t* rowptr, const int32_t* nbr, int64_t num_nodes,
                             int32_t max_rows, int32_t max_nodes, int32_t max_edges,

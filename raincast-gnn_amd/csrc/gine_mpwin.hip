@@ -63,6 +63,7 @@ struct WinPlan {
   const int32_t* win_rows;    // [T]
   int max_rows, max_edges, max_nodes;
   const int16_t* slot;        // [N] or null: tile-local node at each work position
+  const int32_t* edge_begin;  // [T + 1] or null: rowptr at the tile starts
 };
 
 // Dynamic LDS: window [max_rows][Q] float4 | nbr [max_edges] | attr [max_edges] | rp [nodes+1]
@@ -86,45 +87,71 @@ struct WinLds {
 
 // One tile's staging: every global load of the window slice, the CSR segment and the row
 // pointers is issued before the first LDS store, so the tile pays one memory latency.
+// The tile's global loads, held in registers until stage_store: window rows, the edge list
+// (from e0 / ne: the plan's edge offsets, or rowptr) and the local rowptr.
+struct StageRegs {
+  float4 v[kWinRowLoads];
+  int32_t nb[kWinEdgeLoads];
+  float at[kWinEdgeLoads];
+  int rp, e0, ne;
+};
+template <int Q>
+__device__ __forceinline__ void stage_load(StageRegs& r, const float4* __restrict__ tab4, int D4,
+                                           int col4, const int32_t* __restrict__ rowptr,
+                                           const int32_t* __restrict__ nbr,
+                                           const float* __restrict__ attr, int n0, int nodes,
+                                           int lo, int rows, int e0, int ne) {
+  const int tid = threadIdx.x;
+  const int n = rows * Q;
+#pragma unroll
+  for (int k = 0; k < kWinRowLoads; ++k) {
+    const int i = min(tid + k * kWinThreads, max(n - 1, 0));
+    r.v[k] = n > 0 ? tab4[(int64_t)(lo + i / Q) * D4 + col4 + i % Q] : f4_zero();
+  }
+  r.rp = rowptr[n0 + min(tid, nodes)];
+  r.e0 = e0;
+  r.ne = ne;
+#pragma unroll
+  for (int k = 0; k < kWinEdgeLoads; ++k) {
+    const int i = min(tid + k * kWinThreads, max(ne - 1, 0));
+    r.nb[k] = ne > 0 ? nbr[e0 + i] : 0;
+    r.at[k] = ne > 0 ? attr[e0 + i] : 0.f;
+  }
+}
+template <int Q>
+__device__ __forceinline__ void stage_store(const StageRegs& r, int nodes, int lo, int rows,
+                                            const WinLds& lds) {
+  const int tid = threadIdx.x;
+  const int n = rows * Q;
+#pragma unroll
+  for (int k = 0; k < kWinRowLoads; ++k) {
+    const int i = tid + k * kWinThreads;
+    if (i < n) lds.win[i] = r.v[k];
+  }
+  if (tid <= nodes) lds.rp[tid] = r.rp - r.e0;
+#pragma unroll
+  for (int k = 0; k < kWinEdgeLoads; ++k) {
+    const int i = tid + k * kWinThreads;
+    if (i < r.ne) {
+      lds.nbr[i] = (r.nb[k] - lo) * Q * 16;
+      lds.attr[i] = r.at[k];
+    }
+  }
+}
+// Stage tile t's window slice, edge list and local rowptr into LDS.  Every global load of
+// the tile is issued before the first LDS store, so the tile pays the edge list's
+// dependent latency (rowptr -> edges) once.
 template <int Q>
 __device__ __forceinline__ void stage_tile(const float4* __restrict__ tab4, int D4, int col4,
                                            const int32_t* __restrict__ rowptr,
                                            const int32_t* __restrict__ nbr,
                                            const float* __restrict__ attr, int n0, int nodes,
                                            int lo, int rows, const WinLds& lds) {
-  const int tid = threadIdx.x;
-  const int n = rows * Q;
-  float4 v[kWinRowLoads];
-#pragma unroll
-  for (int k = 0; k < kWinRowLoads; ++k) {
-    const int i = min(tid + k * kWinThreads, max(n - 1, 0));
-    v[k] = n > 0 ? tab4[(int64_t)(lo + i / Q) * D4 + col4 + i % Q] : f4_zero();
-  }
   const int e0 = rowptr[n0];
   const int ne = rowptr[n0 + nodes] - e0;
-  const int rp = rowptr[n0 + min(tid, nodes)];
-  int32_t nb[kWinEdgeLoads];
-  float at[kWinEdgeLoads];
-#pragma unroll
-  for (int k = 0; k < kWinEdgeLoads; ++k) {
-    const int i = min(tid + k * kWinThreads, max(ne - 1, 0));
-    nb[k] = ne > 0 ? nbr[e0 + i] : 0;
-    at[k] = ne > 0 ? attr[e0 + i] : 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < kWinRowLoads; ++k) {
-    const int i = tid + k * kWinThreads;
-    if (i < n) lds.win[i] = v[k];
-  }
-  if (tid <= nodes) lds.rp[tid] = rp - e0;
-#pragma unroll
-  for (int k = 0; k < kWinEdgeLoads; ++k) {
-    const int i = tid + k * kWinThreads;
-    if (i < ne) {
-      lds.nbr[i] = (nb[k] - lo) * Q * 16;
-      lds.attr[i] = at[k];
-    }
-  }
+  StageRegs r;
+  stage_load<Q>(r, tab4, D4, col4, rowptr, nbr, attr, n0, nodes, lo, rows, e0, ne);
+  stage_store<Q>(r, nodes, lo, rows, lds);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -261,6 +288,14 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
   const char* dzb = reinterpret_cast<const char*>(dz4);
   const char* rb = reinterpret_cast<const char*>(dres4 != nullptr ? dres4 : dz4);
   const uint32_t rowb = (uint32_t)D4 * 16u, tb = (uint32_t)(col4 + t) * 16u;
+  // The tile's staging loads first (the edge range from the plan: no dependent rowptr read),
+  // then the work order, then this thread's own rows: the staging pays about one memory
+  // latency after the plan's, and the own rows arrive under the LDS stores and barrier.
+  const int e0 = plan.edge_begin != nullptr ? plan.edge_begin[tile] : rowptr[n0];
+  const int ne = (plan.edge_begin != nullptr ? plan.edge_begin[tile + 1] : rowptr[n0 + nodes]) - e0;
+  StageRegs sr;
+  stage_load<Q>(sr, dz4, D4, col4, rowptr, nbr, attr, n0, nodes, lo, plan.win_rows[tile], e0,
+                ne);
   // work position g + p*G -> tile-local node (the plan's degree-balanced order, if any)
   int dn[P];
 #pragma unroll
@@ -268,6 +303,7 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
     const int d = min(g + p * G, nodes - 1);
     dn[p] = plan.slot != nullptr ? (int)plan.slot[n0 + d] : d;
   }
+  stage_store<Q>(sr, nodes, lo, plan.win_rows[tile], lds);
   f4v h[P], gs[P], rs[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
@@ -281,7 +317,6 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
   const float ope = 1.0f + eps[0];
   const bool add_self = (flags & GINE_MP_BWD_SELF) != 0;
   WIN_MARK(1);
-  stage_tile<Q>(dz4, D4, col4, rowptr, nbr, attr, n0, nodes, lo, plan.win_rows[tile], lds);
   __syncthreads();
   WIN_MARK(2);
   const char* wb = reinterpret_cast<const char*>(lds.win) + t * 16;
@@ -420,7 +455,7 @@ bool valid_plan(const gine_window_plan* p, int64_t num_nodes, int32_t channels) 
 
 WinPlan device_plan(const gine_window_plan* p) {
   return WinPlan{p->tile_begin, p->win_lo, p->win_rows, p->max_rows, p->max_edges,
-                 p->max_nodes, p->slot};
+                 p->max_nodes, p->slot, p->edge_begin};
 }
 
 // Raise the kernel's dynamic-LDS ceiling once per instantiation (thread-safe static init).

@@ -35,7 +35,8 @@ class WindowPlan(ctypes.Structure):
     """``gine_window_plan`` (include/gine_hip.h): device tile arrays + LDS sizing."""
     _fields_ = [("tile_begin", _c_void_p), ("win_lo", _c_void_p), ("win_rows", _c_void_p),
                 ("num_tiles", _i32), ("slice_channels", _i32), ("max_rows", _i32),
-                ("max_edges", _i32), ("max_nodes", _i32), ("slot", _c_void_p)]
+                ("max_edges", _i32), ("max_nodes", _i32), ("slot", _c_void_p),
+                ("edge_begin", _c_void_p)]
 
 
 _plan_p = ctypes.POINTER(WindowPlan)

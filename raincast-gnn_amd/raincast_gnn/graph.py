@@ -84,16 +84,19 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
         if T == 0 or (max_staged is not None and int(rows[:T].sum()) > max_staged * num_nodes):
             plans[cs] = None
             continue
-        arrays = (tb[:T + 1].to(device), lo[:T].to(device), rows[:T].to(device))
+        edge_begin = rp[tb[:T + 1].long()].to(torch.int32)  # rowptr at the tile starts
+        arrays = (tb[:T + 1].to(device), lo[:T].to(device), rows[:T].to(device),
+                  edge_begin.to(device))
         m = [int(v) for v in maxima]
         plan = _lib.WindowPlan(arrays[0].data_ptr(), arrays[1].data_ptr(), arrays[2].data_ptr(),
                                T, cs, m[0], m[1], max(m[2], 1))
+        plan.edge_begin = arrays[3].data_ptr()
         if slots and os.environ.get("GINE_MP_WINDOW_SLOTS", "1") != "0":
             slot = torch.empty(num_nodes, dtype=torch.int16)
             _lib.call("gine_graph_plan_window_slots", rp.data_ptr(), tb.data_ptr(), T,
                       slot.data_ptr())
             arrays = arrays + (slot.to(device),)
-            plan.slot = arrays[3].data_ptr()
+            plan.slot = arrays[4].data_ptr()
         plans[cs] = (plan, arrays)
     return plans
 
