@@ -244,6 +244,46 @@ constexpr size_t kWinEngineLds = sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
 
 // GINE_WIN_ENG_OCC (tuning experiments): workgroups per CU the combined launch is compiled
 // for (register budget); the plan's LDS must allow as many.
+// Cross-lane double sums for the block reduction of the window backward, without the LDS
+// round trip of ds_bpermute: DPP within a row of 16 lanes, v_permlane16/32_swap across rows.
+// Each returns, in every lane, the same-order sum of the two lanes it pairs (so all lanes
+// agree bit for bit).
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov_d(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xf, 0xf,
+                                                            false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL,
+                                                            0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// lanes i and i^8 (same row of 16): DPP row_ror:8
+__device__ __forceinline__ double sum_x8(double v) { return v + dpp_mov_d<0x128>(v); }
+// lanes i and i^1 / i^2: DPP quad_perm [1,0,3,2] / [2,3,0,1]; the two quads of an 8-lane
+// half row: DPP row_half_mirror
+__device__ __forceinline__ double sum_x1(double v) { return v + dpp_mov_d<0xB1>(v); }
+__device__ __forceinline__ double sum_x2(double v) { return v + dpp_mov_d<0x4E>(v); }
+__device__ __forceinline__ double sum_x4(double v) { return v + dpp_mov_d<0x141>(v); }
+// row pairs (lanes i and i^16) / wave halves (i and i^32): even + odd in every lane
+__device__ __forceinline__ double sum_x16(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto a = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32),
+                                                  false, false);
+  const double even = __builtin_bit_cast(double, ((uint64_t)b[0] << 32) | (uint32_t)a[0]);
+  const double odd = __builtin_bit_cast(double, ((uint64_t)b[1] << 32) | (uint32_t)a[1]);
+  return even + odd;
+}
+__device__ __forceinline__ double sum_x32(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32),
+                                                  false, false);
+  const double low = __builtin_bit_cast(double, ((uint64_t)b[0] << 32) | (uint32_t)a[0]);
+  const double high = __builtin_bit_cast(double, ((uint64_t)b[1] << 32) | (uint32_t)a[1]);
+  return low + high;
+}
+
 #ifndef GINE_WIN_ENG_OCC
 #define GINE_WIN_ENG_OCC 2
 #endif
@@ -373,18 +413,27 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
   __syncthreads();
 #endif
   WIN_MARK(3);
-  // Fixed-order block reduction: the G destination groups of a wave by butterfly over the
+  // Fixed-order block reduction: the G destination groups of a wave by a butterfly over the
   // lane bits above Q, then the waves in order through LDS (the window is dead by now).
-#pragma unroll
-  for (int m = Q; m < kWave; m <<= 1) {
+  if constexpr (Q == 8) {  // the 32-channel slice: DPP / permlane swaps, no LDS round trips
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      pw[k] += shfl_xor_d(pw[k], m);
-      pb[k] += shfl_xor_d(pb[k], m);
+      pw[k] = sum_x32(sum_x16(sum_x8(pw[k])));
+      pb[k] = sum_x32(sum_x16(sum_x8(pb[k])));
     }
-  }
+    pe = sum_x4(sum_x2(sum_x1(sum_x32(sum_x16(sum_x8(pe))))));
+  } else {
 #pragma unroll
-  for (int m = 1; m < kWave; m <<= 1) pe += shfl_xor_d(pe, m);
+    for (int m = Q; m < kWave; m <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        pw[k] += shfl_xor_d(pw[k], m);
+        pb[k] += shfl_xor_d(pb[k], m);
+      }
+    }
+#pragma unroll
+    for (int m = 1; m < kWave; m <<= 1) pe += shfl_xor_d(pe, m);
+  }
   __syncthreads();
   double* s_red = reinterpret_cast<double*>(s_dyn);  // [kWinWaves][2 * CS + 1]
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
