@@ -12,6 +12,11 @@
 
 namespace gine {
 
+// Chunk loads in flight per thread: 8 covers the engines' <= 64 chunks (8 groups) in one
+// batch (r02_s58: gradient batch 15.1 -> 13.6 us at cfg2; 4 took two memory round trips).
+#ifndef GINE_SLAB_UNROLL
+#define GINE_SLAB_UNROLL 8
+#endif
 constexpr int kSlabQuads = 32;   // float4 quads per workgroup
 constexpr int kSlabGroups = 8;   // interleaved chunk groups per workgroup
 
@@ -28,7 +33,7 @@ __device__ __forceinline__ void slab_sum_block(const float* __restrict__ slab, i
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (e0 < per) {
     if constexpr (VEC) {
-#pragma unroll 4
+#pragma unroll GINE_SLAB_UNROLL
       for (int c = g; c < chunks; c += kSlabGroups) {
         const float4 v = *reinterpret_cast<const float4*>(base + (size_t)c * cstride + e0);
         a0 += (double)v.x;
