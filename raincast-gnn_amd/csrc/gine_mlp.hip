@@ -396,6 +396,10 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
   constexpr int ITEMS = kRowTile * D4 / NT;
   constexpr int RSTEP = NT / D4;
   constexpr int NQ = KS / 4;  // four-MFMA steps per chain
+  // rgprof build: 0 start, 1 tile 0 staged (prologue done), 2 first chain done, 3 each later
+  // chain done, 4 last epilogue done, 5 statistics written
+  RG_DECL;
+  RG_MARK(0);
   constexpr bool IS_OUT = (EPI == EPI_OUT) || (EPI == EPI_OUT_RELU) || (EPI == EPI_OUT_RES);
   constexpr bool EPI_LOAD = (EPI == EPI_DBN) || (EPI == EPI_OUT_RES);
   static_assert(NQ >= 8, "the pipeline slots need at least 8 steps (D >= 64)");
@@ -571,6 +575,7 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
     for (int i = 0; i < ITEMS; ++i) stage_item(tile_of(0), raw[i], i, s_lds);
     load_tile(tile_of(1), raw);
     __syncthreads();  // tile 0 staged
+    RG_MARK(1);
 
     // tile k's chain (A = sA[k & 1]) carrying the pipeline slots; EPI_ON: the epilogue of
     // tile k-1 (every iteration but the first)
@@ -623,10 +628,12 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
     // peeled first chain: no previous tile to finish
     accp = chain(0, std::false_type{});
     rotate_ep();
+    RG_MARK(2);
     for (int k = 1; k < count; ++k) {
       __syncthreads();  // tile k staged; the output tile and the other A buffer are free
       accp = chain(k, std::true_type{});
       rotate_ep();
+      RG_MARK(3);
     }
     // the last tile's epilogue
     __syncthreads();
@@ -634,6 +641,7 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) epi_item(tile_of(count - 1), i, ep_prev);
+    RG_MARK(4);
   } else if constexpr (kHook) {
     hook();  // (no tiles: the hook still runs its workgroup-0 duties)
   }
@@ -657,6 +665,8 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
       if (ea.bnacc) bnacc_add(ea.bnacc, 2 * D, c, t);
     }
   }
+  RG_MARK(5);
+  RG_FLUSH();
 }
 
 #ifndef GINE_ROWGEMM_PIPE
