@@ -439,6 +439,14 @@ int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32_t hidden, 
 int gine_deepset_fwd(const float* ens, const float* w1, const float* b1, float* r,
                      uint16_t* mask, int64_t num_nodes, int32_t members, int32_t in_features,
                      int32_t hidden, void* stream);
+/* gine_deepset_fwd plus the dense chain's folded dim_red weight (W' | b' | W'^T of
+ * gine_chain_fwd_folded, hidden in {64, 128}, x_features <= 64) into wfold, computed by
+ * extra workgroups of the same launch for gine_chain_fwd_folded3. */
+int gine_deepset_fwd_fold(const float* ens, const float* w1, const float* b1, float* r,
+                          uint16_t* mask, int64_t num_nodes, int32_t members,
+                          int32_t in_features, int32_t hidden, const float* wr1,
+                          const float* br1, const float* wdr, const float* bdr, float* wfold,
+                          int32_t x_features, void* stream);
 int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t* num_partials);
 int gine_deepset_bwd(const float* ens, const uint16_t* mask, const float* dr, float* slab,
                      float* dw1, float* db1, int64_t num_nodes, int32_t members,
@@ -522,6 +530,12 @@ int gine_chain_fwd_folded(const float* r, const float* x, const float* wp2, cons
                           const float* wr1, const float* br1, const float* wdr,
                           const float* bdr, float* wfold, float* s, float* u, float* h0,
                           int64_t num_nodes, int32_t hidden, int32_t in_features, void* stream);
+/* The folded forward in ONE launch (s -> u -> h0), W' | b' | W'^T already in wfold (folded
+ * by gine_deepset_fwd_fold in the launch before). */
+int gine_chain_fwd_folded3(const float* r, const float* x, const float* wp2, const float* bp2,
+                           float bias_scale, const float* wr0, const float* br0,
+                           const float* wfold, float* s, float* u, float* h0, int64_t num_nodes,
+                           int32_t hidden, int32_t in_features, void* stream);
 int gine_chain_bwd_folded(const float* dh0, const float* u, const float* wp2, const float* wr0,
                           const float* wfold, float* dt, float* ds, float* dr,
                           int64_t num_nodes, int32_t hidden, int32_t in_features, void* stream);

@@ -23,6 +23,7 @@
 #include "gine_common.hpp"
 #include "gine_slab.hpp"
 #include "gine_wgrad.hpp"
+#include "gine_chainfold.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -38,7 +39,11 @@ constexpr int kRowTile = 32;
 // gine_chain_fwd_folded): F2F h0 = [x | u] W'^T + b', B1F dt = (dh0 Wc) * 1[u > 0].
 // B3: the folded chain's whole input-gradient backward in one launch (B1F's stage, then B2's
 // two: dt -> ds -> dr, each stage's output the next one's A tile in LDS).
-enum ChainKind { CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3, CH_F2F = 4, CH_B1F = 5, CH_B3 = 6 };
+// F3: the folded chain's whole forward in one launch (s -> u -> h0 = [x | u] W'^T + b',
+// with W' folded beforehand by gine_deepset_fwd_fold).
+enum ChainKind {
+  CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3, CH_F2F = 4, CH_B1F = 5, CH_B3 = 6, CH_F3 = 7
+};
 
 struct ChainArgs {
   const float* in;   // stage-1 A rows [N, D]: r | u | dh0 | dt | u (F2F) | dh0 (B1F)
@@ -56,8 +61,9 @@ struct ChainArgs {
   // ([D][F + D] then [D]) once the tiles are done (NULL: not folded)
   const float *fw_r1, *fb_r1, *fw_dr, *fb_dr;
   float* wfold;
-  const float* w3;  // B3: stage-3 weight (Wp2)
-  float* out3;      // B3: stage-3 output (dr)
+  const float* w3;  // B3: stage-3 weight (Wp2); F3: W'^T
+  float* out3;      // B3: stage-3 output (dr); F3: h0
+  const float* b3;  // F3: b'
 };
 
 __device__ __forceinline__ floatx16 zero16() {
@@ -160,133 +166,6 @@ __device__ __forceinline__ TileRange tile_range(int num_tiles, int nb) {
   return TileRange{b + pos, min(num_tiles, b + span), here};
 }
 
-// v = sum_j sA[r][j] * svec[j] for the 32 rows staged in sA (row stride D + 4): 2D/32
-// threads per row, 16 products each, then a shuffle tree; every thread of row
-// threadIdx.x / (2D/32) returns that row's total.
-template <int D>
-__device__ __forceinline__ float rows_dot(const float* sA, const float* svec) {
-  constexpr int TPR = 2 * D / 32, LDA = D + 4, J = D / TPR;
-  const int r = threadIdx.x / TPR, p = threadIdx.x % TPR;
-  float v = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) v = fmaf(sA[r * LDA + p * J + j], svec[p * J + j], v);
-#pragma unroll
-  for (int o = TPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, TPR);
-  return v;
-}
-
-// A [32 x 32] tile of a small D x D product, contraction split over the D/32 waves of a
-// 2D-thread workgroup: wave w contracts k in [32w, 32w + 32) (lane half h: 16 of them) of
-// the 32 A rows staged in sA against its B fragment bf[s] = B[32w + 16h + s][c32]; the
-// partial tiles go to sR ([D/32][32 x 33], rows padded for transposed reads), to be summed by
-// ksplit_sum after a barrier.
-// 16 MFMAs per wave instead of a 64-long chain: these tiles are latency-bound.
-constexpr int kSR = 32 * 33;  // floats of one wave's partial tile in sR
-template <int D>
-__device__ __forceinline__ void ksplit_tile(const float* sA, const float (&bf)[16], float* sR,
-                                            int c32, int h) {
-  constexpr int LDA = D + 4;
-  const int w = threadIdx.x / kWave;
-  floatx16 acc = zero16();
-  const float* arow = sA + c32 * LDA + w * 32 + h * 16;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-    sR[w * kSR + rr * 33 + c32] = acc[r];
-  }
-}
-// element (row, col) of the tile (waves summed in order)
-template <int D>
-__device__ __forceinline__ float ksplit_sum(const float* sR, int row, int col) {
-  float v = sR[row * 33 + col];
-#pragma unroll
-  for (int w = 1; w < D / 32; ++w) v += sR[w * kSR + row * 33 + col];
-  return v;
-}
-
-// One [32 x 32] tile (rows k0, columns c0 of Wc) of W' = [Wdr_x | Wc], Wc = Wdr_e Wr1, and
-// (c0 = 0) the x columns and b' = Wdr_e br1 + bdr of its rows: the folded chain's dim_red
-// weight, written as W' [D][F+D], b' [D] and W'^T [F+D][D] (the forward kernel's B
-// fragments read W'^T along rows, coalesced).  Run by the fold workgroups of F1.
-template <int D>
-__device__ void fold_tile(const ChainArgs& a, int ft, float* sA, float* sR, int c32, int h) {
-  constexpr int NT = 2 * D, LDA = D + 4, T = D / 32;
-  const int F = a.F, LW = a.F + D;
-  const int k0 = 32 * (ft / T), c0 = 32 * (ft % T);
-  const int w = threadIdx.x / kWave;
-  __shared__ float svec[D];
-  float bf[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) bf[s] = a.fw_r1[(size_t)(w * 32 + h * 16 + s) * D + c0 + c32];
-  // every load of the staging issued before the first wait (unrolled, constant counts)
-  constexpr int SI = 32 * D / NT, XI = 32 * 64 / NT;
-  float st[SI], xv[XI];
-#pragma unroll
-  for (int i = 0; i < SI; ++i) {
-    const int idx = threadIdx.x + i * NT, r = idx / D, j = idx % D;
-    st[i] = a.fw_dr[(size_t)(k0 + r) * LW + F + j];
-  }
-  if (c0 == 0) {
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int idx = min(threadIdx.x + i * NT, 32 * F - 1), r = idx / F, c = idx % F;
-      xv[i] = a.fw_dr[(size_t)(k0 + r) * LW + c];
-    }
-  }
-  const float bv = threadIdx.x < D ? a.fb_r1[threadIdx.x] : 0.f;
-  __syncthreads();  // every wave is done with sA / sB
-#pragma unroll
-  for (int i = 0; i < SI; ++i) {
-    const int idx = threadIdx.x + i * NT;
-    sA[(idx / D) * LDA + idx % D] = st[i];
-  }
-  float* wt = a.wfold + (size_t)D * LW + D;  // W'^T
-  if (c0 == 0) {
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int idx = threadIdx.x + i * NT;
-      if (idx < 32 * F) a.wfold[(size_t)(k0 + idx / F) * LW + idx % F] = xv[i];
-    }
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {  // x columns transposed: row r fastest
-      const int idx = threadIdx.x + i * NT, r = idx % 32, c = idx / 32;
-      if (idx < 32 * F) wt[(size_t)c * D + k0 + r] = a.fw_dr[(size_t)(k0 + r) * LW + c];
-    }
-  }
-  if (threadIdx.x < D) svec[threadIdx.x] = bv;
-  __syncthreads();
-  ksplit_tile<D>(sA, bf, sR, c32, h);
-  if (c0 == 0) {
-    const float v = rows_dot<D>(sA, svec);  // (Wdr_e br1)[k0 + r]
-    constexpr int TPR = NT / 32;
-    if (threadIdx.x % TPR == 0) {
-      const int r = threadIdx.x / TPR;
-      a.wfold[(size_t)D * LW + k0 + r] = v + a.fb_dr[k0 + r];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 1024 / NT; ++i) {
-    const int o = threadIdx.x + i * NT;
-    a.wfold[(size_t)(k0 + o / 32) * LW + F + c0 + o % 32] = ksplit_sum<D>(sR, o / 32, o % 32);
-    wt[(size_t)(F + c0 + o / 32) * D + k0 + o % 32] = ksplit_sum<D>(sR, o % 32, o / 32);
-  }
-}
-
-// F1 of the folded chain launches (D/32)^2 workgroups more than its chain grid: block
-// chain_blocks + t folds tile t of W' beside the chain tiles (they fit on the CUs next to
-// the one chain workgroup per CU).
-template <int D>
-constexpr int kFoldBlocks = (D / 32) * (D / 32);
-
 template <int D, int FP, int KIND>
 __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num_tiles) {
   constexpr int NT = 2 * D;
@@ -299,8 +178,12 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   constexpr int ITEMS = kRowTile * D4 / NT;         // 4
   constexpr int RSTEP = NT / D4;                    // 8
   constexpr int XITEMS = (kRowTile * FP + NT - 1) / NT;
+  constexpr bool kF3 = KIND == CH_F3;
+  constexpr bool kX = kDimRed || kF3;               // stages x rows
+  constexpr int LDC = FP + D + 4;                   // F3: stage-3 A tile [x | u]
   __shared__ __attribute__((aligned(16))) float sA[kRowTile * LDA];
   __shared__ __attribute__((aligned(16))) float sB[kRowTile * LDB];
+  __shared__ __attribute__((aligned(16))) float sC[kF3 ? kRowTile * LDC : 4];
 
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
@@ -311,7 +194,8 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     if (a.wfold != nullptr) {
       nb -= kFoldBlocks<D>;
       if ((int)blockIdx.x >= nb) {
-        fold_tile<D>(a, blockIdx.x - nb, sA, sB, c32, h);
+        fold_tile<D>(FoldArgs{a.fw_r1, a.fb_r1, a.fw_dr, a.fb_dr, a.wfold, a.F},
+                     blockIdx.x - nb, sA, sB, c32, h);
         return;
       }
     }
@@ -321,7 +205,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   float bf1[D / 2], bf2[K2 / 2];
   const bool w16 =
       ((reinterpret_cast<uintptr_t>(a.w1) | reinterpret_cast<uintptr_t>(a.w2)) & 15) == 0;
-  if constexpr (KIND == CH_F1) {
+  if constexpr (KIND == CH_F1 || kF3) {
     if (w16) {
       frag_t4<D>(bf1, a.w1, D, col, h);
       frag_t4<D>(bf2, a.w2, D, col, h);
@@ -343,11 +227,13 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   } else if constexpr (KIND == CH_B1 || KIND == CH_B2 || KIND == CH_B3) {
     frag_n<D>(bf2, a.w2, D, 0, col, h);
   }
-  float bf3[KIND == CH_B3 ? D / 2 : 1];
+  float bf3[KIND == CH_B3 ? D / 2 : (kF3 ? (FP + D) / 2 : 1)];
   if constexpr (KIND == CH_B3) frag_n<D>(bf3, a.w3, D, 0, col, h);
-  float bias1 = 0.f, bias2 = 0.f;
-  if constexpr (KIND == CH_F1 || KIND == CH_F2) bias1 = a.b1[col] * a.bias1_scale;
-  if constexpr (KIND == CH_F1 || kDimRed) bias2 = a.b2[col];
+  if constexpr (kF3) frag_dimred_t<FP, D>(bf3, a.w3, a.F, col, h);  // w3 = W'^T
+  float bias1 = 0.f, bias2 = 0.f, bias3 = 0.f;
+  if constexpr (KIND == CH_F1 || KIND == CH_F2 || kF3) bias1 = a.b1[col] * a.bias1_scale;
+  if constexpr (KIND == CH_F1 || kDimRed || kF3) bias2 = a.b2[col];
+  if constexpr (kF3) bias3 = a.b3[col];
 
   auto load_tile = [&](int tile, float4 (&raw)[ITEMS], float (&xr)[XITEMS]) {
     const int64_t n0 = (int64_t)tile * kRowTile;
@@ -357,7 +243,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       n = n < N ? n : N - 1;  // clamped: always issued
       raw[i] = reinterpret_cast<const float4*>(a.in + n * D)[q_me];
     }
-    if constexpr (kDimRed) {
+    if constexpr (kX) {
 #pragma unroll
       for (int i = 0; i < XITEMS; ++i) {
         const int idx = threadIdx.x + i * NT;      // over [32][FP]
@@ -385,11 +271,13 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       float* dst = KIND == CH_F2F ? &sB[r * LDB + BOFF + 4 * q_me] : &sA[r * LDA + 4 * q_me];
       *reinterpret_cast<float4*>(dst) = v;
     }
-    if constexpr (kDimRed) {
+    if constexpr (kX) {
+      float* sx = kF3 ? sC : sB;
+      constexpr int LDX = kF3 ? LDC : LDB;
 #pragma unroll
       for (int i = 0; i < XITEMS; ++i) {
         const int idx = threadIdx.x + i * NT;
-        if (idx < kRowTile * FP) sB[(idx / FP) * LDB + idx % FP] = idx % FP < a.F ? xr[i] : 0.f;
+        if (idx < kRowTile * FP) sx[(idx / FP) * LDX + idx % FP] = idx % FP < a.F ? xr[i] : 0.f;
       }
     }
     __syncthreads();
@@ -436,10 +324,20 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
       const int64_t n = n0 + rr;
       float v = acc[r] + bias2;
-      if constexpr (KIND == CH_F1) v = relu_nan(v);              // u = relu(rho[0](s))
+      if constexpr (KIND == CH_F1 || kF3) v = relu_nan(v);      // u = relu(rho[0](s))
+      if constexpr (kF3) sC[rr * LDC + FP + col] = v;           // stage 3's A tile
       if constexpr (KIND == CH_B1) v = ep[r] > 0.f ? v : 0.f;   // dt = du * 1[u > 0]
       if constexpr (KIND == CH_B3) sA[rr * LDA + col] = v;      // stage 3's A tile
       if (n < N) a.out2[n * D + col] = v;
+    }
+    if constexpr (kF3) {  // stage 3: h0 = [x | u] W'^T + b'
+      __syncthreads();
+      acc = tile_mma<FP + D>(sC, LDC, bf3, c32, h);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (n < N) a.out3[n * D + col] = acc[r] + bias3;
+      }
     }
     if constexpr (KIND == CH_B3) {  // stage 3: dr = ds Wp2 (sA: every wave is past stage 1)
       __syncthreads();
@@ -845,6 +743,31 @@ extern "C" int gine_chain_fwd_folded(const float* r, const float* x, const float
 #define CALL_F(DD, FF)                                                  \
   rc = launch_chain<DD, FF, CH_F1>(f1, num_nodes, st);                  \
   if (rc == GINE_OK) rc = launch_chain<DD, FF, CH_F2F>(f2, num_nodes, st)
+  GINE_CHAIN_DISPATCH(D, F, CALL_F);
+#undef CALL_F
+  return rc;
+}
+
+extern "C" int gine_chain_fwd_folded3(const float* r, const float* x, const float* wp2,
+                                      const float* bp2, float bias_scale, const float* wr0,
+                                      const float* br0, const float* wfold, float* s, float* u,
+                                      float* h0, int64_t num_nodes, int32_t hidden,
+                                      int32_t in_features, void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes < 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (num_nodes == 0) return GINE_OK;
+  if (!r || !x || !wp2 || !bp2 || !wr0 || !br0 || !wfold || !s || !u || !h0)
+    return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  const int D = hidden, F = in_features;
+  const float* bfold = wfold + (size_t)D * (F + D);
+  ChainArgs f{r, x, nullptr, wp2, bp2, wr0, br0, s, u, bias_scale, F};
+  f.w3 = bfold + D;  // W'^T
+  f.b3 = bfold;
+  f.out3 = h0;
+  int rc = GINE_OK;
+#define CALL_F(DD, FF) rc = launch_chain<DD, FF, CH_F3>(f, num_nodes, st)
   GINE_CHAIN_DISPATCH(D, F, CALL_F);
 #undef CALL_F
   return rc;

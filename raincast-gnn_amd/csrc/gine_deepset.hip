@@ -18,6 +18,7 @@
 //    half's 16 registers are 16 distinct k of a 32x32x2 A fragment under a k-permutation
 //    that B -- read from the staged ens rows 16h+q -- follows too).
 #include "gine_common.hpp"
+#include "gine_chainfold.hpp"
 
 #include <algorithm>
 
@@ -162,8 +163,7 @@ __device__ __forceinline__ void load_b(const float* __restrict__ w1, int col, in
 // its workgroups with stride = that number.
 struct Groups {
   int first, step, end;
-  __device__ __forceinline__ explicit Groups(int num_groups) {
-    const int nb = gridDim.x;
+  __device__ __forceinline__ Groups(int num_groups, int nb) {  // nb: the walking workgroups
     const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
     const int q = nb / kNumXcd, rm = nb % kNumXcd;
     const int here = q + (xcd < rm ? 1 : 0);
@@ -257,14 +257,28 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
 // memory operations in flight and the next tiles' loads stay in flight under the MFMAs
 // (a conditional store there made it drain the whole queue -- s_waitcnt vmcnt(0) -- every
 // tile).
-template <int H, int KP, bool MASK>
+// FOLD (gine_deepset_fwd_fold): the last kFoldBlocks<H> workgroups fold the dense chain's
+// dim_red weight (gine_chainfold.hpp) beside the member sums, for the chain's one-launch
+// forward that follows.
+template <int H, int KP, bool MASK, bool FOLD = false>
 __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__ ens,
                                                        const float* __restrict__ w1,
                                                        const float* __restrict__ b1,
                                                        float* __restrict__ r,
                                                        uint16_t* __restrict__ mask_out,
                                                        int64_t N, int M, int F,
-                                                       int num_groups) {
+                                                       int num_groups, FoldArgs fold) {
+  int nbw = gridDim.x;  // workgroups walking the groups
+  if constexpr (FOLD) {
+    nbw -= kFoldBlocks<H>;
+    if ((int)blockIdx.x >= nbw) {
+      __shared__ __attribute__((aligned(16))) float s_fold[32 * (H + 4) + (H / 32) * kSR];
+      const int lane = threadIdx.x % kWave;
+      fold_tile<H>(fold, blockIdx.x - nbw, s_fold, s_fold + 32 * (H + 4), lane & 31,
+                   lane >> 5);
+      return;
+    }
+  }
   constexpr int NT = 2 * H;
   constexpr int LD = KP + 4;
   __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
@@ -280,7 +294,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
 
   Stager<NT, KP> st;
   st.init(F, M);
-  const Groups gr(num_groups);
+  const Groups gr(num_groups, nbw);
   // uniform walk state: node (0..15 within each half's 16) and rows left in it
   int node = 0, rem = M;
   float run = 0.f;
@@ -351,7 +365,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
 
   Stager<NT, KP> st;
   st.init(F, M);
-  const Groups gr(num_groups);
+  const Groups gr(num_groups, gridDim.x);
   const float* my_dr = s_dr + 16 * h * H + col;  // this lane: node j of its half at j*H
   int node = 0, rem = M;
   walk_tiles(gr, M, st, ens, N * M, F, s_e[0], s_e[1], mask,
@@ -520,7 +534,7 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD_M(H_, KP_, MK_)                                                            \
   hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, MK_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, b1, \
-                     r, mask, num_nodes, members, in_features, groups)
+                     r, mask, num_nodes, members, in_features, groups, FoldArgs{})
 #define LAUNCH_FWD(H_, KP_)                     \
   do {                                          \
     if (mask) LAUNCH_FWD_M(H_, KP_, true);      \
@@ -599,3 +613,40 @@ extern "C" int gine_debug_ds_prof(long long* out, int* n) {
   return GINE_OK;
 }
 #endif
+
+extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const float* b1,
+                                     float* r, uint16_t* mask, int64_t num_nodes,
+                                     int32_t members, int32_t in_features, int32_t hidden,
+                                     const float* wr1, const float* br1, const float* wdr,
+                                     const float* bdr, float* wfold, int32_t x_features,
+                                     void* stream) {
+  const int KP = pad_fwd(in_features);
+  if ((hidden != 64 && hidden != 128) || KP < 0 || in_features <= 0) return GINE_ERR_DIM;
+  if (x_features < 1 || x_features > 64) return GINE_ERR_DIM;
+  if (num_nodes < 0 || members <= 0) return GINE_ERR_INVALID;
+  if (!wr1 || !br1 || !wdr || !bdr || !wfold) return GINE_ERR_INVALID;
+  if (num_nodes > 0 && (!ens || !w1 || !b1 || !r)) return GINE_ERR_INVALID;
+  if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  const int groups = (int)ceil_div(num_nodes > 0 ? num_nodes : 1, kNodes);
+  const int walk = num_nodes > 0 ? std::min(groups, 1024) : 0;
+  const FoldArgs fold{wr1, br1, wdr, bdr, wfold, x_features};
+  hipStream_t s = as_stream(stream);
+#define LAUNCH_FWD_F(H_, KP_, MK_)                                                            \
+  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, MK_, true>), dim3(walk + kFoldBlocks<H_>),       \
+                     dim3(2 * H_), 0, s, ens, w1, b1, r, mask, num_nodes, members, in_features, \
+                     groups, fold)
+#define LAUNCH_FWD(H_, KP_)                     \
+  do {                                          \
+    if (mask) LAUNCH_FWD_F(H_, KP_, true);      \
+    else LAUNCH_FWD_F(H_, KP_, false);          \
+  } while (0)
+  if (hidden == 64) {
+    DS_FWD_KP(64, KP, LAUNCH_FWD);
+  } else {
+    DS_FWD_KP(128, KP, LAUNCH_FWD);
+  }
+#undef LAUNCH_FWD
+#undef LAUNCH_FWD_F
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

@@ -130,6 +130,10 @@ _SIGNATURES = {
     "gine_chain_fwd_folded": [_c_void_p] * 4 + [_f32] + [_c_void_p] * 10 + [_i64, _i32, _i32,
                                                                               _c_void_p],
     "gine_chain_bwd_folded": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
+    "gine_chain_fwd_folded3": [_c_void_p] * 4 + [_f32] + [_c_void_p] * 6 + [_i64, _i32, _i32,
+                                                                             _c_void_p],
+    "gine_deepset_fwd_fold": [_c_void_p] * 5 + [_i64, _i32, _i32, _i32] + [_c_void_p] * 5
+                             + [_i32, _c_void_p],
     "gine_chain_wgrad_folded": [_c_void_p] * 13 + [_f32, _i64, _i32, _i32, _c_void_p],
     "gine_chain_wgrad_folded_grad_job": [_i64, _i32, _i32, _c_void_p, _f32] + [_c_void_p] * 5
                                         + [_job_p],

@@ -32,11 +32,15 @@ MAX_FEATURES = 64
 
 
 def fusable(r: torch.Tensor, x: torch.Tensor, lins) -> bool:
+    return r.is_cuda and r.dtype == torch.float32 and fusable_dims(r.size(1), x, lins)
+
+
+def fusable_dims(D: int, x: torch.Tensor, lins) -> bool:
+    """The chain's conditions on everything but r (r [N, D] fp32 on the device)."""
     p2, r0, r1, dr = lins
-    D = r.size(1)
     F = x.size(1)
     shapes = ((p2, D, D), (r0, D, D), (r1, D, D), (dr, F + D, D))
-    return (r.is_cuda and x.is_cuda and r.dtype == torch.float32 and x.dtype == torch.float32
+    return (x.is_cuda and x.dtype == torch.float32
             and D in HIDDEN and 0 < F <= MAX_FEATURES and not x.requires_grad
             and all(isinstance(m, torch.nn.Linear) and m.bias is not None
                     and m.weight.dtype == torch.float32 and m.in_features == i
@@ -111,7 +115,7 @@ class _ChainFoldedFn(torch.autograd.Function):
     (the rounding of sums differs, within the fp32 tolerance of the oracle tests)."""
 
     @staticmethod
-    def forward(ctx, r, x, wp2, bp2, wr0, br0, wr1, br1, wdr, bdr, members):
+    def forward(ctx, r, x, wp2, bp2, wr0, br0, wr1, br1, wdr, bdr, members, wfold=None):
         r = r.contiguous()
         x = x.contiguous()
         N, D = r.shape
@@ -119,11 +123,16 @@ class _ChainFoldedFn(torch.autograd.Function):
         dev = r.device
         ws = [t.detach().contiguous() for t in (wp2, bp2, wr0, br0, wr1, br1, wdr, bdr)]
         s, u, h0 = (torch.empty(N, D, dtype=torch.float32, device=dev) for _ in range(3))
-        wfold = torch.empty(2 * D * (F + D) + D, dtype=torch.float32, device=dev)
         P = _lib.ptr
-        _lib.call("gine_chain_fwd_folded", P(r), P(x), P(ws[0]), P(ws[1]), float(members),
-                  P(ws[2]), P(ws[3]), P(ws[4]), P(ws[5]), P(ws[6]), P(ws[7]), P(wfold), P(s),
-                  P(u), P(h0), N, D, F, _lib.stream_handle(dev))
+        if wfold is not None:  # folded by the DeepSet launch: the whole forward in one launch
+            _lib.call("gine_chain_fwd_folded3", P(r), P(x), P(ws[0]), P(ws[1]), float(members),
+                      P(ws[2]), P(ws[3]), P(wfold), P(s), P(u), P(h0), N, D, F,
+                      _lib.stream_handle(dev))
+        else:
+            wfold = torch.empty(2 * D * (F + D) + D, dtype=torch.float32, device=dev)
+            _lib.call("gine_chain_fwd_folded", P(r), P(x), P(ws[0]), P(ws[1]), float(members),
+                      P(ws[2]), P(ws[3]), P(ws[4]), P(ws[5]), P(ws[6]), P(ws[7]), P(wfold),
+                      P(s), P(u), P(h0), N, D, F, _lib.stream_handle(dev))
         ctx.save_for_backward(r, x, s, u, wfold, ws[0], ws[2], ws[4], ws[5], ws[6])
         ctx.params = (wp2, bp2, wr0, br0, wr1, br1, wdr, bdr)
         ctx.members = float(members)
@@ -173,16 +182,27 @@ class _ChainFoldedFn(torch.autograd.Function):
                       P(slab), P(gfold), P(g[2]), P(g[3]), P(g[0]), P(g[1]), members, N, D, F,
                       stream)
             unfold(stream)
-        return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None)
+        return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None, None)
 
 
 # RAINCAST_CHAIN_FOLD=0: the unfolded chain (four GEMM stages forward, e materialised)
 FOLD = os.environ.get("RAINCAST_CHAIN_FOLD", "1") != "0"
 
 
-def chain(r: torch.Tensor, x: torch.Tensor, lins, members: int) -> torch.Tensor:
-    """``dim_red(cat([x, rho(phi[2](r) summed over members)]))`` on the fused kernels."""
+# RAINCAST_CHAIN_F3=0: the folded forward as two launches (W' folded by the first).  The
+# one-launch form (three stages, one workgroup per CU) wins while a CU walks a few tiles
+# (cfg2, 16,000 nodes: 0.5442 -> 0.5405 ms per step) and loses at many (cfg3, 128,000:
+# 2.922 -> 2.937, profiles/r02_s67_*), so it is used up to F3_MAX_NODES rows.
+F3 = os.environ.get("RAINCAST_CHAIN_F3", "1") != "0"
+F3_MAX_NODES = 32768
+
+
+def chain(r: torch.Tensor, x: torch.Tensor, lins, members: int, wfold=None) -> torch.Tensor:
+    """``dim_red(cat([x, rho(phi[2](r) summed over members)]))`` on the fused kernels;
+    ``wfold`` = the folded dim_red weight from gine_deepset_fwd_fold (folded chain only)."""
     p2, r0, r1, dr = lins
-    fn = _ChainFoldedFn if FOLD else _ChainFn
-    return fn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight, r1.bias,
-                    dr.weight, dr.bias, members)
+    if FOLD:
+        return _ChainFoldedFn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight,
+                                    r1.bias, dr.weight, dr.bias, members, wfold)
+    return _ChainFn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight, r1.bias,
+                          dr.weight, dr.bias, members)

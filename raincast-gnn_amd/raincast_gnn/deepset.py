@@ -34,7 +34,10 @@ def fusable(ens: torch.Tensor, weight: torch.Tensor, bias) -> bool:
 
 class _PhiSumFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ens, weight, bias):
+    def forward(ctx, ens, weight, bias, fold=None):
+        """``fold`` = (rho[2] weight, rho[2] bias, dim_red weight, dim_red bias): the same
+        launch also folds the dense chain's dim_red weight (gine_deepset_fwd_fold) and the
+        function returns (r, wfold), wfold not differentiable."""
         ens = ens.contiguous()
         weight, bias = weight.contiguous(), bias.contiguous()
         N, M, Fdim = ens.shape
@@ -45,15 +48,25 @@ class _PhiSumFn(torch.autograd.Function):
             nbytes = ctypes.c_size_t(0)
             _lib.call("gine_deepset_mask_bytes", N, M, H, ctypes.byref(nbytes))
             mask = torch.empty(nbytes.value, dtype=torch.uint8, device=ens.device)
-        _lib.call("gine_deepset_fwd", _lib.ptr(ens), _lib.ptr(weight), _lib.ptr(bias),
-                  _lib.ptr(r), _lib.ptr(mask), N, M, Fdim, H, _lib.stream_handle(ens.device))
         ctx.save_for_backward(ens, mask)
         ctx.params = (weight, bias)
         ctx.hidden = H
-        return r
+        stream = _lib.stream_handle(ens.device)
+        if fold is None:
+            _lib.call("gine_deepset_fwd", _lib.ptr(ens), _lib.ptr(weight), _lib.ptr(bias),
+                      _lib.ptr(r), _lib.ptr(mask), N, M, Fdim, H, stream)
+            return r
+        wr1, br1, wdr, bdr = (t.detach().contiguous() for t in fold)
+        F = wdr.size(1) - H
+        wfold = torch.empty(2 * H * (F + H) + H, dtype=torch.float32, device=ens.device)
+        _lib.call("gine_deepset_fwd_fold", _lib.ptr(ens), _lib.ptr(weight), _lib.ptr(bias),
+                  _lib.ptr(r), _lib.ptr(mask), N, M, Fdim, H, _lib.ptr(wr1), _lib.ptr(br1),
+                  _lib.ptr(wdr), _lib.ptr(bdr), _lib.ptr(wfold), F, stream)
+        ctx.mark_non_differentiable(wfold)
+        return r, wfold
 
     @staticmethod
-    def backward(ctx, dr):
+    def backward(ctx, dr, *unused):
         ens, mask = ctx.saved_tensors
         N, M, Fdim = ens.shape
         H = ctx.hidden
@@ -73,9 +86,14 @@ class _PhiSumFn(torch.autograd.Function):
             _lib.call("gine_deepset_bwd_grad_job", N, Fdim, H, _lib.ptr(slab), _lib.ptr(dw),
                       _lib.ptr(db), ctypes.byref(job))
             gradbuf.defer(job, dr.device, (slab,))
-        return None, dw, db
+        return None, dw, db, None
 
 
-def phi_sum(ens: torch.Tensor, lin1: torch.nn.Linear) -> torch.Tensor:
-    """``relu(lin1(ens)).sum(dim=1)`` for ens [N, M, F] on the fused kernels."""
-    return _PhiSumFn.apply(ens, lin1.weight, lin1.bias)
+def phi_sum(ens: torch.Tensor, lin1: torch.nn.Linear, fold=None):
+    """``relu(lin1(ens)).sum(dim=1)`` for ens [N, M, F] on the fused kernels; with
+    ``fold`` = (rho[2], dim_red) Linears, (r, wfold) for the one-launch folded chain."""
+    if fold is None:
+        return _PhiSumFn.apply(ens, lin1.weight, lin1.bias)
+    r1, dr = fold
+    return _PhiSumFn.apply(ens, lin1.weight, lin1.bias,
+                           (r1.weight, r1.bias, dr.weight, dr.bias))

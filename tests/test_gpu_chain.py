@@ -185,3 +185,32 @@ def test_chain_folded_intermediates(N, D, F):
                            ("dWr1", g[4], de64.T @ d(u)), ("dbr1", g[5], de64.sum(0)),
                            ("dWdr", g[6], d(dh0).T @ xe), ("dbdr", g[7], d(dh0).sum(0))):
         assert _rel(got, ref) <= TOL, (name, _rel(got, ref))
+
+
+@pytest.mark.parametrize("N,D,F", [(2000, 128, 35), (33, 64, 20), (16000, 128, 64)])
+def test_chain_one_launch_forward_matches_two_launch(N, D, F):
+    """The folded forward in one launch (W' folded by the DeepSet launch,
+    gine_deepset_fwd_fold + gine_chain_fwd_folded3) equals the two-launch form bit for bit,
+    forward and backward."""
+    from raincast_gnn import deepset
+    torch.manual_seed(N + D)
+    M, Fe = 11, 36
+    ens = torch.randn(N, M, Fe, device=DEV)
+    lin1 = torch.nn.Linear(Fe, D).to(DEV)
+    lins = _lins(D, F, N)
+    x = torch.randn(N, F, device=DEV)
+    outs = []
+    for one in (False, True):
+        for m in lins + (lin1,):
+            m.zero_grad(set_to_none=True)
+        if one:
+            r, wfold = deepset.phi_sum(ens, lin1, fold=(lins[2], lins[3]))
+            h0 = fused_chain.chain(r, x, lins, M, wfold=wfold)
+        else:
+            r = deepset.phi_sum(ens, lin1)
+            h0 = fused_chain.chain(r, x, lins, M)
+        h0.backward(torch.ones_like(h0))
+        outs.append([h0.detach()] + [p.grad.clone() for m in lins + (lin1,)
+                                     for p in (m.weight, m.bias)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
