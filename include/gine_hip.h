@@ -405,6 +405,13 @@ int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t 
                   double* loss_out, double* count_out, uint32_t* ticket, void* stream);
 int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
                   int64_t num_nodes, int32_t kind, float* grad_pred, void* stream);
+/* gine_crps_fwd that also writes grad_unit = (float)(dpred / count_in[0]), the gradient for
+ * gloss = 1 exactly as gine_crps_bwd would round it, given the count of non-NaN targets
+ * up front (count_in: device double) -- a backward seeded with 1 then needs no launch. */
+int gine_crps_fwd_grad(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
+                       double u, double xi, double c, double t, double* dpred, double* partials,
+                       double* loss_out, double* count_out, uint32_t* ticket,
+                       const double* count_in, float* grad_unit, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * Weight/bias gradient of a plain Linear y = x W^T + b over many rows (the DeepSet,

@@ -214,7 +214,9 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
                                                    double* __restrict__ partials,
                                                    double* __restrict__ loss_out,
                                                    double* __restrict__ count_out,
-                                                   unsigned int* __restrict__ ticket) {
+                                                   unsigned int* __restrict__ ticket,
+                                                   const double* __restrict__ count_in,
+                                                   float* __restrict__ grad_unit) {
   constexpr int K = LossK<KIND>::value;
   __shared__ double s_sum[kThreads];
   __shared__ double s_cnt[kThreads];
@@ -248,6 +250,11 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) dpred[i * K + k] = g[k];
+    if (grad_unit != nullptr) {  // d loss / d pred for gloss = 1, as k_crps_bwd rounds it
+      const double cnt_all = count_in[0];
+#pragma unroll
+      for (int k = 0; k < K; ++k) grad_unit[i * K + k] = (float)(1.0 * g[k] / cnt_all);
+    }
   }
   s_sum[threadIdx.x] = val;
   s_cnt[threadIdx.x] = cnt;
@@ -324,18 +331,21 @@ extern "C" int gine_crps_num_partials(int64_t num_nodes, int32_t* num_partials) 
   return GINE_OK;
 }
 
-extern "C" int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
-                             double u, double xi, double c, double t, double* dpred,
-                             double* partials, double* loss_out, double* count_out,
-                             uint32_t* ticket, void* stream) {
+namespace {
+int crps_fwd_launch(const float* pred, const float* y, int64_t num_nodes, int32_t kind, double u,
+                    double xi, double c, double t, double* dpred, double* partials,
+                    double* loss_out, double* count_out, uint32_t* ticket,
+                    const double* count_in, float* grad_unit, void* stream) {
   if (num_nodes < 0 || !partials || !loss_out || !count_out || !ticket) return GINE_ERR_INVALID;
+  if ((count_in == nullptr) != (grad_unit == nullptr)) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!pred || !y || !dpred)) return GINE_ERR_INVALID;
   if (kind < GINE_LOSS_NORMAL || kind > GINE_LOSS_MIXED_U) return GINE_ERR_INVALID;
   hipStream_t s = as_stream(stream);
   const int64_t blocks = ceil_div(num_nodes, kThreads) > 0 ? ceil_div(num_nodes, kThreads) : 1;
 #define LAUNCH_CRPS(KIND_)                                                                  \
   hipLaunchKernelGGL(k_crps<KIND_>, dim3((unsigned)blocks), dim3(kThreads), 0, s, pred, y,  \
-                     num_nodes, u, xi, c, t, dpred, partials, loss_out, count_out, ticket)
+                     num_nodes, u, xi, c, t, dpred, partials, loss_out, count_out, ticket,   \
+                     count_in, grad_unit)
   switch (kind) {
     case GINE_LOSS_NORMAL: LAUNCH_CRPS(GINE_LOSS_NORMAL); break;
     case GINE_LOSS_MIXED_NORMAL: LAUNCH_CRPS(GINE_LOSS_MIXED_NORMAL); break;
@@ -345,6 +355,25 @@ extern "C" int gine_crps_fwd(const float* pred, const float* y, int64_t num_node
 #undef LAUNCH_CRPS
   GINE_LAUNCH_STATUS();
   return GINE_OK;
+}
+}  // namespace
+
+extern "C" int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
+                             double u, double xi, double c, double t, double* dpred,
+                             double* partials, double* loss_out, double* count_out,
+                             uint32_t* ticket, void* stream) {
+  return crps_fwd_launch(pred, y, num_nodes, kind, u, xi, c, t, dpred, partials, loss_out,
+                         count_out, ticket, nullptr, nullptr, stream);
+}
+
+extern "C" int gine_crps_fwd_grad(const float* pred, const float* y, int64_t num_nodes,
+                                  int32_t kind, double u, double xi, double c, double t,
+                                  double* dpred, double* partials, double* loss_out,
+                                  double* count_out, uint32_t* ticket, const double* count_in,
+                                  float* grad_unit, void* stream) {
+  if (!count_in || !grad_unit) return GINE_ERR_INVALID;
+  return crps_fwd_launch(pred, y, num_nodes, kind, u, xi, c, t, dpred, partials, loss_out,
+                         count_out, ticket, count_in, grad_unit, stream);
 }
 
 extern "C" int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,

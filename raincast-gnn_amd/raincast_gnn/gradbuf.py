@@ -156,3 +156,10 @@ def loss_backward(loss: torch.Tensor) -> None:
             return
         one = _seeds[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
     loss.backward(one)
+
+
+def is_unit_seed(g: torch.Tensor) -> bool:
+    """True when ``g`` is the cached constant 1 that :func:`loss_backward` seeds with (the
+    object autograd hands to the loss node unchanged)."""
+    one = _seeds.get((g.device, g.dtype))
+    return one is not None and g is one

@@ -19,11 +19,12 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, gradbuf
 
 _LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
 # NormalCRPS keeps 1/sqrt(pi) as an fp32 tensor (loss.py:343): same value as a Python float
@@ -85,11 +86,41 @@ def _masked_mean(values: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return total / m.sum().to(values.dtype)
 
 
+class _ValidCounts:
+    """Number of non-NaN targets of a ``y`` tensor as a device double, computed once per
+    distinct tensor (identity + version; the entry holds ``y`` so its memory is not reused
+    while cached) -- in a replayed training step ``y`` is the same tensor every step."""
+
+    def __init__(self, capacity: int = 8):
+        self.capacity = capacity
+        self._entries: dict = {}
+
+    def get(self, y: torch.Tensor) -> torch.Tensor:
+        key = (y.data_ptr(), y._version, tuple(y.shape), y.device)
+        hit = self._entries.get(key)
+        if hit is not None:
+            return hit[0]
+        cnt = (~torch.isnan(y)).sum().to(torch.float64).reshape(1)
+        self._entries[key] = (cnt, y)
+        while len(self._entries) > self.capacity:
+            self._entries.pop(next(iter(self._entries)))
+        return cnt
+
+
+_valid_counts = _ValidCounts()
+# RAINCAST_CRPS_UNIT_GRAD=0: the backward always runs gine_crps_bwd (A/B experiments)
+UNIT_GRAD = os.environ.get("RAINCAST_CRPS_UNIT_GRAD", "1") != "0"
+
+
 class _FusedCRPS(torch.autograd.Function):
-    """Reduced CRPS of ``pred [N, K]`` vs ``y [N]`` in one HIP pass (fp64 result)."""
+    """Reduced CRPS of ``pred [N, K]`` vs ``y [N]`` in one HIP pass (fp64 result).  When the
+    prediction needs a gradient, the pass also writes d loss / d pred for a unit seed
+    (gine_crps_fwd_grad): ``loss.backward()`` seeded with the cached 1 of
+    gradbuf.loss_backward then costs no launch (any other seed: gine_crps_bwd)."""
 
     @staticmethod
     def forward(ctx, pred, y, kind, u, xi, c, t):
+        needs = ctx.needs_input_grad[0]
         pred = pred.detach().float().contiguous()
         y = y.detach().float().contiguous()
         N, K = pred.shape
@@ -100,15 +131,26 @@ class _FusedCRPS(torch.autograd.Function):
         partials = torch.empty(n_part.value, 2, dtype=torch.float64, device=dev)
         loss = torch.empty((), dtype=torch.float64, device=dev)
         count = torch.empty(1, dtype=torch.float64, device=dev)
-        _lib.call("gine_crps_fwd", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c, t,
-                  _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss), _lib.ptr(count),
-                  _lib.ptr(_ticket(dev)), _lib.stream_handle(dev))
+        ctx.grad_unit = None
+        if needs and N > 0 and UNIT_GRAD:
+            count_in = _valid_counts.get(y)
+            ctx.grad_unit = torch.empty(N, K, dtype=torch.float32, device=dev)
+            _lib.call("gine_crps_fwd_grad", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c, t,
+                      _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss), _lib.ptr(count),
+                      _lib.ptr(_ticket(dev)), _lib.ptr(count_in), _lib.ptr(ctx.grad_unit),
+                      _lib.stream_handle(dev))
+        else:
+            _lib.call("gine_crps_fwd", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c, t,
+                      _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss), _lib.ptr(count),
+                      _lib.ptr(_ticket(dev)), _lib.stream_handle(dev))
         ctx.save_for_backward(dpred, count)
         ctx.kind = kind
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
+        if ctx.grad_unit is not None and gradbuf.is_unit_seed(gloss):
+            return ctx.grad_unit, None, None, None, None, None, None
         dpred, count = ctx.saved_tensors
         N = dpred.size(0)
         g = gloss.detach().to(torch.float64).reshape(1).contiguous()
