@@ -63,11 +63,15 @@ class _PhiSumFn(torch.autograd.Function):
                   _lib.ptr(r), _lib.ptr(mask), N, M, Fdim, H, _lib.ptr(wr1), _lib.ptr(br1),
                   _lib.ptr(wdr), _lib.ptr(bdr), _lib.ptr(wfold), F, stream)
         ctx.mark_non_differentiable(wfold)
+        # no zero-filled gradient for wfold in the backward (a fill launch per step)
+        ctx.set_materialize_grads(False)
         return r, wfold
 
     @staticmethod
     def backward(ctx, dr, *unused):
         ens, mask = ctx.saved_tensors
+        if dr is None:  # (grads are not materialised in the folding form)
+            return None, None, None, None
         N, M, Fdim = ens.shape
         H = ctx.hidden
         dr = dr.contiguous()
