@@ -163,8 +163,10 @@ __device__ __forceinline__ void load_b(const float* __restrict__ w1, int col, in
 // its workgroups with stride = that number.
 struct Groups {
   int first, step, end;
-  __device__ __forceinline__ Groups(int num_groups, int nb) {  // nb: the walking workgroups
-    const int xcd = blockIdx.x % kNumXcd, pos = blockIdx.x / kNumXcd;
+  // nb: the walking workgroups; b: this one's index among them (blockIdx.x unless other
+  // workgroups are dealt first -- a multiple of kNumXcd of them keeps the XCD of each)
+  __device__ __forceinline__ Groups(int num_groups, int nb, int b = (int)blockIdx.x) {
+    const int xcd = b % kNumXcd, pos = b / kNumXcd;
     const int q = nb / kNumXcd, rm = nb % kNumXcd;
     const int here = q + (xcd < rm ? 1 : 0);
     const int before = xcd * q + min(xcd, rm);  // workgroups on lower XCDs
@@ -257,9 +259,11 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
 // memory operations in flight and the next tiles' loads stay in flight under the MFMAs
 // (a conditional store there made it drain the whole queue -- s_waitcnt vmcnt(0) -- every
 // tile).
-// FOLD (gine_deepset_fwd_fold): the last kFoldBlocks<H> workgroups fold the dense chain's
+// FOLD (gine_deepset_fwd_fold): the first kFoldBlocks<H> workgroups fold the dense chain's
 // dim_red weight (gine_chainfold.hpp) beside the member sums, for the chain's one-launch
-// forward that follows.
+// forward that follows.  They are dealt first (so they never wait for a free slot behind the
+// walk) and share one LDS buffer with the walk's tiles (so the walk's occupancy is that of
+// the larger of the two, not of their sum).
 template <int H, int KP, bool MASK, bool FOLD = false>
 __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__ ens,
                                                        const float* __restrict__ w1,
@@ -268,21 +272,23 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
                                                        uint16_t* __restrict__ mask_out,
                                                        int64_t N, int M, int F,
                                                        int num_groups, FoldArgs fold) {
-  int nbw = gridDim.x;  // workgroups walking the groups
+  constexpr int NT = 2 * H;
+  constexpr int LD = KP + 4;
+  constexpr int kWalk = 2 * 32 * LD + kNodes * H;  // two staged tiles + the group's node sums
+  constexpr int kFold = FOLD ? 32 * (H + 4) + (H / 32) * kSR : 0;
+  __shared__ __attribute__((aligned(16))) float s_lds[kWalk > kFold ? kWalk : kFold];
+  int nbw = gridDim.x, bw = blockIdx.x;  // workgroups walking the groups, this one's index
   if constexpr (FOLD) {
     nbw -= kFoldBlocks<H>;
-    if ((int)blockIdx.x >= nbw) {
-      __shared__ __attribute__((aligned(16))) float s_fold[32 * (H + 4) + (H / 32) * kSR];
+    bw -= kFoldBlocks<H>;
+    if (bw < 0) {
       const int lane = threadIdx.x % kWave;
-      fold_tile<H>(fold, blockIdx.x - nbw, s_fold, s_fold + 32 * (H + 4), lane & 31,
-                   lane >> 5);
+      fold_tile<H>(fold, blockIdx.x, s_lds, s_lds + 32 * (H + 4), lane & 31, lane >> 5);
       return;
     }
   }
-  constexpr int NT = 2 * H;
-  constexpr int LD = KP + 4;
-  __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
-  __shared__ float s_r[kNodes * H];  // node sums of the current group
+  float(*s_e)[32 * LD] = reinterpret_cast<float(*)[32 * LD]>(s_lds);
+  float* s_r = s_lds + 2 * 32 * LD;  // node sums of the current group
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
@@ -294,7 +300,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
 
   Stager<NT, KP> st;
   st.init(F, M);
-  const Groups gr(num_groups, nbw);
+  const Groups gr(num_groups, nbw, bw);
   // uniform walk state: node (0..15 within each half's 16) and rows left in it
   int node = 0, rem = M;
   float run = 0.f;
