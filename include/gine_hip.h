@@ -412,6 +412,22 @@ int gine_crps_fwd_grad(const float* pred, const float* y, int64_t num_nodes, int
                        double u, double xi, double c, double t, double* dpred, double* partials,
                        double* loss_out, double* count_out, uint32_t* ticket,
                        const double* count_in, float* grad_unit, void* stream);
+/* gine_crps_fwd_grad that also runs the output head's backward for that unit seed (the head
+ * of gine_head_fwd: raw [N, K], its input h [N, channels], weight w [K, channels]): dh
+ * [N, channels] as gine_head_bwd writes it from grad_pred = grad_unit, and per-workgroup dW |
+ * db partials in head_slab (gine_crps_head_slab_floats() floats; gine_crps_head_grad_job
+ * describes them for gine_grad_finalize_batch).  One launch instead of three (crps, crps_bwd,
+ * head_bwd) for a training step's loss.backward() seeded with 1. */
+int gine_crps_head_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind,
+                               size_t* floats);
+int gine_crps_head_fwd_grad(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
+                            double u, double xi, double c, double t, double* dpred,
+                            double* partials, double* loss_out, double* count_out,
+                            uint32_t* ticket, const double* count_in, float* grad_unit,
+                            const float* raw, const float* h, const float* w, int32_t channels,
+                            float* dh, float* head_slab, void* stream);
+int gine_crps_head_grad_job(int64_t num_nodes, int32_t channels, int32_t kind,
+                            const float* head_slab, float* dw, float* db, gine_grad_job* job);
 
 /* ------------------------------------------------------------------------------------
  * Weight/bias gradient of a plain Linear y = x W^T + b over many rows (the DeepSet,

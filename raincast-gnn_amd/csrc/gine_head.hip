@@ -16,6 +16,7 @@
 // and db = sum d raw as fp32 per-workgroup partials in a slab, reduced in fixed order by
 // k_slab_sum (deterministic).
 #include "gine_common.hpp"
+#include "gine_headrow.hpp"
 #include "gine_slab.hpp"
 
 #include <algorithm>
@@ -23,57 +24,7 @@
 namespace gine {
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kRowsPerBlock = kThreads / 32;  // one node per half-wave
-constexpr int kMaxK = 5;
-constexpr int kMaxChunks = 2;                  // D <= 256: two float4 per lane
-constexpr int kHeadBlocks = 256;               // backward grid (partials = one slab row each)
-
-// Column roles of the K outputs for each loss (models/model_utils.py:80-111).
-enum Role { R_ID = 0, R_SOFTPLUS = 1, R_SIGMOID = 2, R_SIGMOID_U = 3 };
-
-__device__ __forceinline__ int role_of(int kind, int k) {
-  if (k == 0) return R_ID;                              // mu
-  if (k == 1 || k == 3) return R_SOFTPLUS;              // sigma, sigma_u
-  if (k == 2) return R_SIGMOID;                         // p
-  return kind == GINE_LOSS_MIXED_U ? R_SIGMOID_U : R_ID;  // u (learned threshold)
-}
-
-// torch.nn.functional.softplus(beta=1, threshold=20)
-__device__ __forceinline__ float softplus_f(float x) {
-  return x > 20.f ? x : log1pf(expf(x));
-}
-__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
-
-__device__ __forceinline__ float post(int role, float x) {
-  switch (role) {
-    case R_SOFTPLUS: return softplus_f(x) + 1e-6f;
-    case R_SIGMOID: return sigmoid_f(x);
-    case R_SIGMOID_U: return sigmoid_f(x) * 2.12f;
-    default: return x;
-  }
-}
-
-// d post / d x applied to g (ATen: softplus_backward z = exp(x), g*z/(z+1) below the
-// threshold; sigmoid_backward g*(1-s)*s from the output s)
-__device__ __forceinline__ float post_bwd(int role, float x, float g) {
-  switch (role) {
-    case R_SOFTPLUS: {
-      if (x > 20.f) return g;
-      const float z = expf(x);
-      return g * z / (z + 1.f);
-    }
-    case R_SIGMOID: {
-      const float s = sigmoid_f(x);
-      return g * (1.f - s) * s;
-    }
-    case R_SIGMOID_U: {
-      const float s = sigmoid_f(x);
-      return (g * 2.12f) * (1.f - s) * s;
-    }
-    default: return g;
-  }
-}
+using namespace head;
 
 template <int K>
 __global__ __launch_bounds__(kThreads) void k_head_fwd(const float* __restrict__ h,
@@ -129,77 +80,14 @@ __global__ __launch_bounds__(kThreads) void k_head_bwd(const float* __restrict__
                                                        float* __restrict__ slab, int64_t N,
                                                        int D, int kind) {
   __shared__ float s_part[kRowsPerBlock][kMaxK * 256 + kMaxK];
-  const int t = threadIdx.x & 31, hw = threadIdx.x / 32;
-  const int D4 = D / 4;
-  float4 aw[kMaxChunks][K];  // sum over this half-wave's nodes of d raw[k] * h[n, cols]
-  float ab[K];
+  bwd_rows<K, 8>(
+      [&](int64_t n, float (&g)[K]) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    ab[k] = 0.f;
-#pragma unroll
-    for (int c = 0; c < kMaxChunks; ++c) aw[c][k] = f4_zero();
-  }
-  float4 wk[kMaxChunks][K];
-#pragma unroll
-  for (int c = 0; c < kMaxChunks; ++c) {
-    const int q = min(t + 32 * c, D4 - 1);
-#pragma unroll
-    for (int k = 0; k < K; ++k) wk[c][k] = reinterpret_cast<const float4*>(w + (size_t)k * D)[q];
-  }
-  for (int64_t n = (int64_t)blockIdx.x * kRowsPerBlock + hw; n < N;
-       n += (int64_t)gridDim.x * kRowsPerBlock) {
-    float g[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      g[k] = post_bwd(role_of(kind, k), raw[n * K + k], gpred[n * K + k]);
-      ab[k] += g[k];
-    }
-#pragma unroll
-    for (int c = 0; c < kMaxChunks; ++c) {
-      const int q = t + 32 * c;
-      if (q < D4) {
-        const float4 x = reinterpret_cast<const float4*>(h + n * D)[q];
-        float4 o = f4_zero();
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          o.x = __builtin_fmaf(g[k], wk[c][k].x, o.x);
-          o.y = __builtin_fmaf(g[k], wk[c][k].y, o.y);
-          o.z = __builtin_fmaf(g[k], wk[c][k].z, o.z);
-          o.w = __builtin_fmaf(g[k], wk[c][k].w, o.w);
-          aw[c][k].x = __builtin_fmaf(g[k], x.x, aw[c][k].x);
-          aw[c][k].y = __builtin_fmaf(g[k], x.y, aw[c][k].y);
-          aw[c][k].z = __builtin_fmaf(g[k], x.z, aw[c][k].z);
-          aw[c][k].w = __builtin_fmaf(g[k], x.w, aw[c][k].w);
-        }
-        reinterpret_cast<float4*>(dh + n * D)[q] = o;
-      }
-    }
-  }
-  // workgroup partial: the 8 half-waves summed in fixed order (fp64) -> one slab row
-#pragma unroll
-  for (int c = 0; c < kMaxChunks; ++c) {
-    const int q = t + 32 * c;
-    if (q < D4) {
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        *reinterpret_cast<float4*>(&s_part[hw][k * D + 4 * q]) = aw[c][k];
-    }
-  }
-  if (t < K) {
-    float v = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) v = (t == k) ? ab[k] : v;
-    s_part[hw][K * D + t] = v;
-  }
-  __syncthreads();
-  const int per = K * D + K;
-  float* out = slab + (size_t)blockIdx.x * per;
-  for (int e = threadIdx.x; e < per; e += kThreads) {
-    double s = 0.0;
-#pragma unroll
-    for (int r = 0; r < kRowsPerBlock; ++r) s += (double)s_part[r][e];
-    out[e] = (float)s;
-  }
+        for (int k = 0; k < K; ++k)
+          g[k] = post_bwd(role_of(kind, k), raw[n * K + k], gpred[n * K + k]);
+      },
+      (int64_t)blockIdx.x * kRowsPerBlock, (int64_t)gridDim.x * kRowsPerBlock, N, h, w, dh,
+      slab + (size_t)blockIdx.x * (K * D + K), D, s_part);
 }
 
 struct HeadOut {

@@ -10,6 +10,7 @@
 //   MixedNormalCRPS loss.py:6-68      pred = [mu, sigma, p]
 //   MixedLoss       loss.py:71-272    pred = [mu, sigma, p, sigma_u] (+ u if grad_u)
 #include "gine_common.hpp"
+#include "gine_headrow.hpp"
 #include "gine_reduce.hpp"
 
 namespace gine {
@@ -19,6 +20,7 @@ constexpr double kInvSqrtPi = 0.56418958354775628695;   // 1/sqrt(pi)
 constexpr double kLogSqrt2Pi = 0.91893853320467274178;  // log(sqrt(2 pi))
 constexpr double kSqrt2 = 1.41421356237309504880;
 constexpr int kThreads = 256;
+constexpr int kHeadNodes = 64;  // nodes per workgroup of the pass that runs the head backward
 
 // ---------------------------------------------------------------------------------------
 // forward-mode dual numbers: value + gradient w.r.t. the K prediction columns
@@ -203,10 +205,25 @@ struct LossK {
                                : KIND == GINE_LOSS_MIXED ? 4 : 5;
 };
 
+// The output head's backward run by the CRPS pass for a unit loss seed (gine_crps_head_fwd_grad):
+// raw = the head's pre-PostProcess output, h / w its input and weight; dh and the dW | db
+// partial row of each workgroup (gine_headrow.hpp) are written beside grad_unit.
+struct HeadBwdArgs {
+  const float* raw;
+  const float* h;
+  const float* w;
+  float* dh;
+  float* slab;
+  int D;
+};
+
 // One thread per node.  Writes d crps_n / d pred_n (0 for NaN targets) and per-block
 // [sum crps, count] partials; the workgroup that finishes last (ticket) reduces the partials
-// into the loss -- no separate finalize launch.
-template <int KIND>
+// into the loss -- no separate finalize launch.  HEAD: kHeadNodes nodes per workgroup (the
+// CRPS evaluation is latency-bound: one busy wave per CU costs what four do), then the head
+// backward of those nodes from grad_unit, one batch of 8 rows per half-wave
+// (gine_headrow.hpp) -- with 256 nodes per workgroup each half-wave would walk 32 rows.
+template <int KIND, bool HEAD = false>
 __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pred,
                                                    const float* __restrict__ y, int64_t n,
                                                    double u_fixed, double xi, double c,
@@ -216,14 +233,27 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
                                                    double* __restrict__ count_out,
                                                    unsigned int* __restrict__ ticket,
                                                    const double* __restrict__ count_in,
-                                                   float* __restrict__ grad_unit) {
+                                                   float* __restrict__ grad_unit,
+                                                   HeadBwdArgs hb) {
   constexpr int K = LossK<KIND>::value;
+  static_assert(kThreads == head::kThreads, "one CRPS node per head-backward thread");
+  __shared__ float s_graw[HEAD ? kHeadNodes : 1][K];
+  __shared__ float s_part[HEAD ? head::kRowsPerBlock : 1][head::kMaxK * 256 + head::kMaxK];
   __shared__ double s_sum[kThreads];
   __shared__ double s_cnt[kThreads];
   __shared__ int s_last;
-  const int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+  constexpr int NPB = HEAD ? kHeadNodes : kThreads;
+  static_assert(kHeadNodes == 8 * head::kRowsPerBlock, "one batch of 8 rows per half-wave");
+  const int64_t i = blockIdx.x * (int64_t)NPB + threadIdx.x;
+  const int64_t first = blockIdx.x * (int64_t)NPB;
+  const int64_t n_blk = min<int64_t>(n, first + NPB);
+  head::HeadRows<K, HEAD ? 8 : 1> rows;
+  if constexpr (HEAD) {  // the head's weight and h rows arrive while the loss is evaluated
+    rows.init(hb.w, hb.D);
+    rows.load(first + threadIdx.x / 32, head::kRowsPerBlock, n_blk, hb.h, hb.D);
+  }
   double val = 0.0, cnt = 0.0;
-  if (i < n) {
+  if ((NPB == kThreads || (int)threadIdx.x < NPB) && i < n) {
     const float yf = y[i];
     double g[K];
 #pragma unroll
@@ -253,8 +283,23 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
     if (grad_unit != nullptr) {  // d loss / d pred for gloss = 1, as k_crps_bwd rounds it
       const double cnt_all = count_in[0];
 #pragma unroll
-      for (int k = 0; k < K; ++k) grad_unit[i * K + k] = (float)(1.0 * g[k] / cnt_all);
+      for (int k = 0; k < K; ++k) {
+        const float gu = (float)(1.0 * g[k] / cnt_all);
+        grad_unit[i * K + k] = gu;
+        if constexpr (HEAD)  // d raw, as k_head_bwd forms it from grad_pred
+          s_graw[threadIdx.x][k] =
+              head::post_bwd(head::role_of(KIND, k), hb.raw[i * K + k], gu);
+      }
     }
+  }
+  if constexpr (HEAD) {
+    __syncthreads();
+    rows.step([&](int64_t nd, float (&gr)[K]) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) gr[k] = s_graw[nd - first][k];
+              },
+              first + threadIdx.x / 32, head::kRowsPerBlock, n_blk, hb.dh, hb.D);
+    rows.flush(hb.slab + (size_t)blockIdx.x * (K * hb.D + K), hb.D, s_part);
   }
   s_sum[threadIdx.x] = val;
   s_cnt[threadIdx.x] = cnt;
@@ -326,7 +371,7 @@ using namespace gine;
 
 extern "C" int gine_crps_num_partials(int64_t num_nodes, int32_t* num_partials) {
   if (!num_partials || num_nodes < 0) return GINE_ERR_INVALID;
-  const int64_t p = ceil_div(num_nodes, kThreads);
+  const int64_t p = ceil_div(num_nodes, kHeadNodes);  // enough for either workgroup size
   *num_partials = (int32_t)(p > 0 ? p : 1);
   return GINE_OK;
 }
@@ -335,17 +380,24 @@ namespace {
 int crps_fwd_launch(const float* pred, const float* y, int64_t num_nodes, int32_t kind, double u,
                     double xi, double c, double t, double* dpred, double* partials,
                     double* loss_out, double* count_out, uint32_t* ticket,
-                    const double* count_in, float* grad_unit, void* stream) {
+                    const double* count_in, float* grad_unit, void* stream,
+                    const HeadBwdArgs* hb = nullptr) {
   if (num_nodes < 0 || !partials || !loss_out || !count_out || !ticket) return GINE_ERR_INVALID;
   if ((count_in == nullptr) != (grad_unit == nullptr)) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!pred || !y || !dpred)) return GINE_ERR_INVALID;
   if (kind < GINE_LOSS_NORMAL || kind > GINE_LOSS_MIXED_U) return GINE_ERR_INVALID;
   hipStream_t s = as_stream(stream);
-  const int64_t blocks = ceil_div(num_nodes, kThreads) > 0 ? ceil_div(num_nodes, kThreads) : 1;
-#define LAUNCH_CRPS(KIND_)                                                                  \
-  hipLaunchKernelGGL(k_crps<KIND_>, dim3((unsigned)blocks), dim3(kThreads), 0, s, pred, y,  \
-                     num_nodes, u, xi, c, t, dpred, partials, loss_out, count_out, ticket,   \
-                     count_in, grad_unit)
+  const int npb = hb ? kHeadNodes : kThreads;
+  const int64_t blocks = ceil_div(num_nodes, npb) > 0 ? ceil_div(num_nodes, npb) : 1;
+#define LAUNCH_CRPS_H(KIND_, H_)                                                               \
+  hipLaunchKernelGGL((k_crps<KIND_, H_>), dim3((unsigned)blocks), dim3(kThreads), 0, s, pred, y, \
+                     num_nodes, u, xi, c, t, dpred, partials, loss_out, count_out, ticket,      \
+                     count_in, grad_unit, hb ? *hb : HeadBwdArgs{})
+#define LAUNCH_CRPS(KIND_)                        \
+  do {                                            \
+    if (hb) LAUNCH_CRPS_H(KIND_, true);           \
+    else LAUNCH_CRPS_H(KIND_, false);             \
+  } while (0)
   switch (kind) {
     case GINE_LOSS_NORMAL: LAUNCH_CRPS(GINE_LOSS_NORMAL); break;
     case GINE_LOSS_MIXED_NORMAL: LAUNCH_CRPS(GINE_LOSS_MIXED_NORMAL); break;
@@ -353,6 +405,7 @@ int crps_fwd_launch(const float* pred, const float* y, int64_t num_nodes, int32_
     default: LAUNCH_CRPS(GINE_LOSS_MIXED_U); break;
   }
 #undef LAUNCH_CRPS
+#undef LAUNCH_CRPS_H
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
@@ -374,6 +427,68 @@ extern "C" int gine_crps_fwd_grad(const float* pred, const float* y, int64_t num
   if (!count_in || !grad_unit) return GINE_ERR_INVALID;
   return crps_fwd_launch(pred, y, num_nodes, kind, u, xi, c, t, dpred, partials, loss_out,
                          count_out, ticket, count_in, grad_unit, stream);
+}
+
+namespace {
+int loss_k(int kind) {
+  return kind == GINE_LOSS_NORMAL ? 2 : kind == GINE_LOSS_MIXED_NORMAL ? 3
+         : kind == GINE_LOSS_MIXED ? 4 : kind == GINE_LOSS_MIXED_U ? 5 : -1;
+}
+int64_t crps_head_blocks(int64_t num_nodes) {
+  const int64_t b = ceil_div(num_nodes, kHeadNodes);
+  return b > 0 ? b : 1;
+}
+}  // namespace
+
+extern "C" int gine_crps_head_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind,
+                                          size_t* floats) {
+  const int K = loss_k(kind);
+  if (K < 0 || num_nodes < 0 || !floats) return GINE_ERR_INVALID;
+  if (channels <= 0 || channels % 4 != 0 || channels > 32 * 4 * head::kMaxChunks)
+    return GINE_ERR_DIM;
+  *floats = (size_t)crps_head_blocks(num_nodes) * (size_t)(K * channels + K);
+  return GINE_OK;
+}
+
+extern "C" int gine_crps_head_fwd_grad(const float* pred, const float* y, int64_t num_nodes,
+                                       int32_t kind, double u, double xi, double c, double t,
+                                       double* dpred, double* partials, double* loss_out,
+                                       double* count_out, uint32_t* ticket,
+                                       const double* count_in, float* grad_unit,
+                                       const float* raw, const float* h, const float* w,
+                                       int32_t channels, float* dh, float* head_slab,
+                                       void* stream) {
+  size_t floats = 0;
+  const int rc = gine_crps_head_slab_floats(num_nodes, channels, kind, &floats);
+  if (rc != GINE_OK) return rc;
+  if (!count_in || !grad_unit || !head_slab || !w) return GINE_ERR_INVALID;
+  if (num_nodes > 0 && (!raw || !h || !dh)) return GINE_ERR_INVALID;
+  const HeadBwdArgs hb{raw, h, w, dh, head_slab, channels};
+  return crps_fwd_launch(pred, y, num_nodes, kind, u, xi, c, t, dpred, partials, loss_out,
+                         count_out, ticket, count_in, grad_unit, stream, &hb);
+}
+
+extern "C" int gine_crps_head_grad_job(int64_t num_nodes, int32_t channels, int32_t kind,
+                                       const float* head_slab, float* dw, float* db,
+                                       gine_grad_job* job) {
+  size_t floats = 0;
+  const int rc = gine_crps_head_slab_floats(num_nodes, channels, kind, &floats);
+  if (rc != GINE_OK) return rc;
+  if (!head_slab || !dw || !job) return GINE_ERR_INVALID;
+  const int K = loss_k(kind);
+  const int64_t per = (int64_t)K * channels + K;
+  *job = gine_grad_job{};
+  job->kind = GINE_GRAD_JOB_SLAB;
+  job->src = head_slab;
+  job->rows = (int32_t)crps_head_blocks(num_nodes);
+  job->cstride = per;
+  job->nz = 1;
+  job->per[0] = per;
+  job->wsize[0] = (int64_t)K * channels;
+  job->w[0] = dw;
+  job->b[0] = db;
+  job->bscale[0] = 1.0f;
+  return GINE_OK;
 }
 
 extern "C" int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,

@@ -111,6 +111,10 @@ _SIGNATURES = {
     "gine_crps_bwd": [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
     "gine_crps_fwd_grad": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64]
                           + [_c_void_p] * 8,
+    "gine_crps_head_slab_floats": [_i64, _i32, _i32, ctypes.POINTER(ctypes.c_size_t)],
+    "gine_crps_head_fwd_grad": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64]
+                               + [_c_void_p] * 10 + [_i32] + [_c_void_p] * 3,
+    "gine_crps_head_grad_job": [_i64, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _job_p],
     "gine_linear_wgrad_num_chunks": [_i64, _i32, _i32, ctypes.POINTER(_i32)],
     "gine_linear_wgrad": [_c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p,
                           _c_void_p, _f32, _c_void_p],

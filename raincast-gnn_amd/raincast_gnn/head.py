@@ -13,11 +13,34 @@ import ctypes
 
 import torch
 
+from torch.utils.weak import WeakIdKeyDictionary
+
 from . import _lib
 from . import gradbuf
 from .gradbuf import grad_out
 
 MAX_CHANNELS = 256
+
+
+class HeadRecord:
+    """What the CRPS pass needs to run this head's backward ahead of time (loss.py,
+    gine_crps_head_fwd_grad): the head's input, weight and pre-PostProcess output.  ``pre``
+    = (grad_unit, dh, slab) once it has: the backward then uses dh / slab if its incoming
+    gradient is that very grad_unit tensor (a unit-seeded loss.backward())."""
+
+    __slots__ = ("h", "w", "raw", "kind", "params", "pre")
+
+    def __init__(self, h, w, raw, kind, params):
+        self.h, self.w, self.raw, self.kind, self.params = h, w, raw, kind, params
+        self.pre = None
+
+
+_records = WeakIdKeyDictionary()  # pred tensor -> HeadRecord
+
+
+def record_of(pred: torch.Tensor) -> HeadRecord | None:
+    """The HeadRecord of a prediction returned by :func:`head` (None for any other tensor)."""
+    return _records.get(pred)
 
 
 def loss_kind(loss: str, grad_u) -> int | None:
@@ -55,6 +78,8 @@ class _HeadFn(torch.autograd.Function):
         ctx.save_for_backward(h, w, raw)
         ctx.kind = kind
         ctx.params = (weight, bias)
+        ctx.rec = HeadRecord(h, w, raw, kind, (weight, bias))
+        _records[pred] = ctx.rec
         return pred
 
     @staticmethod
@@ -63,6 +88,20 @@ class _HeadFn(torch.autograd.Function):
         N, D = h.shape
         K = w.size(0)
         dev = h.device
+        pre, ctx.rec.pre = ctx.rec.pre, None
+        if pre is not None and gpred is pre[0]:  # run by the CRPS pass (unit seed)
+            _, dh, slab = pre
+            dw = grad_out(ctx.params[0], (K, D), dev)
+            db = grad_out(ctx.params[1], (K,), dev)
+            job = _lib.GradJob()
+            _lib.call("gine_crps_head_grad_job", N, D, ctx.kind, _lib.ptr(slab), _lib.ptr(dw),
+                      _lib.ptr(db), ctypes.byref(job))
+            if gradbuf.deferrable(dw, db):
+                gradbuf.defer(job, dev, (slab,))
+            else:
+                arr = (_lib.GradJob * 1)(job)
+                _lib.call("gine_grad_finalize_batch", arr, 1, _lib.stream_handle(dev))
+            return dh, dw, db, None
         gpred = gpred.float().contiguous()
         floats = ctypes.c_size_t(0)
         _lib.call("gine_head_bwd_slab_floats", N, D, ctx.kind, ctypes.byref(floats))

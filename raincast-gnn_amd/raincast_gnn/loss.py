@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib, gradbuf
+from . import head as _head
 
 _LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
 # NormalCRPS keeps 1/sqrt(pi) as an fp32 tensor (loss.py:343): same value as a Python float
@@ -110,16 +111,21 @@ class _ValidCounts:
 _valid_counts = _ValidCounts()
 # RAINCAST_CRPS_UNIT_GRAD=0: the backward always runs gine_crps_bwd (A/B experiments)
 UNIT_GRAD = os.environ.get("RAINCAST_CRPS_UNIT_GRAD", "1") != "0"
+# RAINCAST_CRPS_HEAD=0: the head backward always runs as its own launch (gine_head_bwd)
+HEAD_BWD = os.environ.get("RAINCAST_CRPS_HEAD", "1") != "0"
 
 
 class _FusedCRPS(torch.autograd.Function):
     """Reduced CRPS of ``pred [N, K]`` vs ``y [N]`` in one HIP pass (fp64 result).  When the
     prediction needs a gradient, the pass also writes d loss / d pred for a unit seed
     (gine_crps_fwd_grad): ``loss.backward()`` seeded with the cached 1 of
-    gradbuf.loss_backward then costs no launch (any other seed: gine_crps_bwd)."""
+    gradbuf.loss_backward then costs no launch (any other seed: gine_crps_bwd).  ``rec``: the
+    HeadRecord of the fused head that produced ``pred``; the pass then also runs that head's
+    backward for the unit seed (gine_crps_head_fwd_grad), which the head's backward picks up
+    when it receives exactly this grad_unit tensor."""
 
     @staticmethod
-    def forward(ctx, pred, y, kind, u, xi, c, t):
+    def forward(ctx, pred, y, kind, u, xi, c, t, rec=None):
         needs = ctx.needs_input_grad[0]
         pred = pred.detach().float().contiguous()
         y = y.detach().float().contiguous()
@@ -135,10 +141,24 @@ class _FusedCRPS(torch.autograd.Function):
         if needs and N > 0 and UNIT_GRAD:
             count_in = _valid_counts.get(y)
             ctx.grad_unit = torch.empty(N, K, dtype=torch.float32, device=dev)
-            _lib.call("gine_crps_fwd_grad", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c, t,
-                      _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss), _lib.ptr(count),
-                      _lib.ptr(_ticket(dev)), _lib.ptr(count_in), _lib.ptr(ctx.grad_unit),
-                      _lib.stream_handle(dev))
+            if rec is not None:
+                D = rec.h.size(1)
+                floats = ctypes.c_size_t(0)
+                _lib.call("gine_crps_head_slab_floats", N, D, kind, ctypes.byref(floats))
+                slab = torch.empty(floats.value, dtype=torch.float32, device=dev)
+                dh = torch.empty_like(rec.h)
+                _lib.call("gine_crps_head_fwd_grad", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi,
+                          c, t, _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss),
+                          _lib.ptr(count), _lib.ptr(_ticket(dev)), _lib.ptr(count_in),
+                          _lib.ptr(ctx.grad_unit), _lib.ptr(rec.raw), _lib.ptr(rec.h),
+                          _lib.ptr(rec.w), D, _lib.ptr(dh), _lib.ptr(slab),
+                          _lib.stream_handle(dev))
+                rec.pre = (ctx.grad_unit, dh, slab)
+            else:
+                _lib.call("gine_crps_fwd_grad", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c,
+                          t, _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss),
+                          _lib.ptr(count), _lib.ptr(_ticket(dev)), _lib.ptr(count_in),
+                          _lib.ptr(ctx.grad_unit), _lib.stream_handle(dev))
         else:
             _lib.call("gine_crps_fwd", _lib.ptr(pred), _lib.ptr(y), N, kind, u, xi, c, t,
                       _lib.ptr(dpred), _lib.ptr(partials), _lib.ptr(loss), _lib.ptr(count),
@@ -150,20 +170,24 @@ class _FusedCRPS(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gloss):
         if ctx.grad_unit is not None and gradbuf.is_unit_seed(gloss):
-            return ctx.grad_unit, None, None, None, None, None, None
+            return ctx.grad_unit, None, None, None, None, None, None, None
         dpred, count = ctx.saved_tensors
         N = dpred.size(0)
         g = gloss.detach().to(torch.float64).reshape(1).contiguous()
         grad = torch.empty(dpred.shape, dtype=torch.float32, device=dpred.device)
         _lib.call("gine_crps_bwd", _lib.ptr(dpred), _lib.ptr(count), _lib.ptr(g), N, ctx.kind,
                   _lib.ptr(grad), _lib.stream_handle(dpred.device))
-        return grad, None, None, None, None, None, None
+        return grad, None, None, None, None, None, None, None
 
 
 def _fused(prediction, y, kind, u=0.0, xi=0.5, c=float(np.log(0.01)), t=5.0):
     if prediction.dim() != 2:
         raise ValueError("prediction must be [N, K]")
-    return _FusedCRPS.apply(prediction, y, kind, float(u), float(xi), float(c), float(t))
+    rec = _head.record_of(prediction) if HEAD_BWD else None
+    if rec is not None and (rec.kind != kind or rec.raw.shape != prediction.shape
+                            or not prediction.requires_grad):
+        rec = None
+    return _FusedCRPS.apply(prediction, y, kind, float(u), float(xi), float(c), float(t), rec)
 
 
 def _use_fused(prediction: torch.Tensor, reduce: bool = True) -> bool:

@@ -285,3 +285,40 @@ def test_mlp_weight_grads_in_mp_launch_small_graphs(graphs, stations, k, monkeyp
         if n.endswith("nn.0.weight") or n.endswith("nn.3.weight"):
             assert torch.equal(got, gref), n
         assert rel_err(got, gref) <= 1e-6, n
+
+
+@pytest.mark.parametrize("name,loss,grad_u", CASES)
+def test_head_backward_in_crps_pass_matches_separate_launch(name, loss, grad_u):
+    """gine_crps_head_fwd_grad: for a unit-seeded backward (gradbuf.loss_backward) the CRPS
+    pass also runs the head's backward.  dh and so every gradient below the head are
+    bit-identical to the separate gine_head_bwd launch (plain backward(), whose seed is not
+    the cached unit, so the head falls back to it); the head's own
+    dW / db differ only in the grouping of their fixed-order partial sums."""
+    from raincast_gnn import gradbuf, head
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.models import GNN
+    torch.manual_seed(3)
+    base = GNN(35, 128, 128, 2, loss=loss, grad_u=grad_u, u=1.71, xi=0.5)
+    batch = synthetic_batch(700, 2, k=10, seed=4).to(DEV)
+    batch.y[::7] = float("nan")  # masked targets: zero rows of d raw
+
+    def grads(unit):
+        m = copy.deepcopy(base).to(DEV)
+        pred = m(batch)
+        loss_v = m.loss_fn.crps(pred, batch.y)
+        rec = head.record_of(pred)
+        assert rec is not None and rec.pre is not None  # computed; used for the unit seed only
+        if unit:
+            gradbuf.loss_backward(loss_v)
+        else:
+            loss_v.backward()
+        return loss_v.item(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+
+    l_sep, g_sep = grads(False)
+    l_fus, g_fus = grads(True)
+    assert l_sep == l_fus
+    for n, g in g_sep.items():
+        if n.startswith("aggr."):
+            assert rel_err(g_fus[n], g) <= 1e-6, n
+        else:
+            assert torch.equal(g_fus[n], g), n
