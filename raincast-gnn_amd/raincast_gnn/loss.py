@@ -111,8 +111,12 @@ class _ValidCounts:
 _valid_counts = _ValidCounts()
 # RAINCAST_CRPS_UNIT_GRAD=0: the backward always runs gine_crps_bwd (A/B experiments)
 UNIT_GRAD = os.environ.get("RAINCAST_CRPS_UNIT_GRAD", "1") != "0"
-# RAINCAST_CRPS_HEAD=0: the head backward always runs as its own launch (gine_head_bwd)
+# RAINCAST_CRPS_HEAD=0: the head backward always runs as its own launch (gine_head_bwd).
+# The CRPS pass that runs it takes 64 nodes per workgroup: one round of workgroups up to
+# HEAD_BWD_MAX_NODES nodes (cfg2, 16,000: one launch fewer), several rounds of the fp64 loss
+# chain above (cfg3 / cfg5 lose), so it is used up to that size.
 HEAD_BWD = os.environ.get("RAINCAST_CRPS_HEAD", "1") != "0"
+HEAD_BWD_MAX_NODES = int(os.environ.get("RAINCAST_CRPS_HEAD_MAX_NODES", "32768"))
 
 
 class _FusedCRPS(torch.autograd.Function):
@@ -185,7 +189,8 @@ def _fused(prediction, y, kind, u=0.0, xi=0.5, c=float(np.log(0.01)), t=5.0):
         raise ValueError("prediction must be [N, K]")
     rec = _head.record_of(prediction) if HEAD_BWD else None
     if rec is not None and (rec.kind != kind or rec.raw.shape != prediction.shape
-                            or not prediction.requires_grad):
+                            or not prediction.requires_grad
+                            or prediction.size(0) > HEAD_BWD_MAX_NODES):
         rec = None
     return _FusedCRPS.apply(prediction, y, kind, float(u), float(xi), float(c), float(t), rec)
 
