@@ -371,8 +371,9 @@ int gine_mlp_bwd1_wgrad(const float* dy, const float* y, const uint8_t* mask, co
 /* ------------------------------------------------------------------------------------
  * AdamW over one flat fp32 parameter buffer (the optimizer of the benchmarked training
  * step, train.py:67-69 with torch.optim.AdamW, lr from params.json).  Bumps the device
- * step counter `step` (fp32 [2]: the count, then a ticket word that must start at 0 and is
- * left at 0) and updates param / exp_avg / exp_avg_sq in place with torch.optim.AdamW's
+ * step counter `step` (fp32 [288]: the count, a ticket word, and at floats 32 + 32 g
+ * (g < 8) the sub-tickets of a two-level ticket, one per 128-byte line; every ticket word
+ * must start at 0 and is left at 0) and updates param / exp_avg / exp_avg_sq in place with torch.optim.AdamW's
  * default (amsgrad=False) formulation.  One launch, graph-safe; the four buffers must be
  * 16-byte aligned (float4 accesses).
  * ---------------------------------------------------------------------------------- */

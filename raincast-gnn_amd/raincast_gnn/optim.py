@@ -47,8 +47,9 @@ class FlatAdamW:
                 gradbuf.register(p, self.flat_grad, off)
         self.exp_avg = torch.zeros_like(self.flat_param)
         self.exp_avg_sq = torch.zeros_like(self.flat_param)
-        # [count, ticket]: gine_adamw_step bumps the count in its last workgroup
-        self._step_state = torch.zeros(2, dtype=torch.float32, device=dev)
+        # [count, ticket, -, 8 sub-tickets at 32 + 32 g]: gine_adamw_step bumps the count in
+        # its last workgroup (two-level ticket, include/gine_hip.h)
+        self._step_state = torch.zeros(32 + 8 * 32, dtype=torch.float32, device=dev)
         self.step_count = self._step_state[:1]
 
     @property
