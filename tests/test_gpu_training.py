@@ -38,6 +38,30 @@ def test_flat_adamw_matches_torch_adamw():
     assert opt.step_count.item() == st["step"].item() == 6
 
 
+@pytest.mark.parametrize("numel", [64, 3 * 1024, 8 * 1024, 13 * 1024 - 40, 900_000])
+def test_flat_adamw_step_count_across_grid_sizes(numel):
+    """The step counter sits behind a two-level ticket (gine_adamw_step: 8 sub-tickets, then
+    the top word): grids of 1, 3, 8, 13 and the capped 512 workgroups (ragged groups) bump it
+    exactly once per step and leave every ticket word at 0, and the update follows torch."""
+    torch.manual_seed(1)
+    p = torch.nn.Parameter(torch.randn(numel, device=DEV))
+    q = torch.nn.Parameter(p.detach().clone())
+    opt = FlatAdamW([p], lr=1e-3, weight_decay=0.01)
+    opt_ref = torch.optim.AdamW([q], lr=1e-3, weight_decay=0.01, foreach=False)
+    for _ in range(5):
+        g = torch.randn(numel, device=DEV)
+        opt.zero_grad(set_to_none=False)
+        p.grad.copy_(g)
+        q.grad = g.clone()
+        opt.step()
+        opt_ref.step()
+    torch.cuda.synchronize()
+    assert opt.step_count.item() == 5
+    state = opt._step_state.view(torch.int32).cpu()
+    assert int(state[1:].abs().sum()) == 0      # top and sub-tickets re-armed
+    assert rel_err(p.detach(), q.detach()) <= 2e-6
+
+
 def test_deepset_restructure_matches_reference_form():
     torch.manual_seed(1)
     enc = DeepSetEncoder(35, 128, 128)
