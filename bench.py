@@ -80,6 +80,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm, the benchmark) | gloo (multi-rank rehearsal on "
                          "one GPU: ranks share the device)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: ranks over gloo build their shards and time the gradient "
+                         "all-reduce alone (launcher / rank / shard / JSON plumbing; no GPU "
+                         "step, no HIP call)")
     return ap.parse_args()
 
 
@@ -130,30 +134,33 @@ class Trainer:
 
     def capture(self):
         """The whole step as ONE HIP graph -- fwd + bwd, the RCCL gradient all-reduce (when
-        there is a collective) and AdamW.  If the collective cannot be captured (or
-        ``allreduce="split"``), fwd+bwd and AdamW are two graphs with the all-reduce
-        launched between them."""
-        # only RCCL ("nccl") collectives can be captured; gloo (CPU rehearsals) always runs
-        # between two graphs -- a failed capture attempt would leave the stream invalidated
-        in_graph = self.allreduce == "graph" and (
-            not self.collective or dist.get_backend() == "nccl")
-        if not self.collective or in_graph:
+        there is a collective) and AdamW -- or, with a gloo group or ``allreduce="split"``,
+        fwd+bwd and AdamW as two graphs with the all-reduce launched between them.
+
+        The form is decided here, before any capture starts: only RCCL ("nccl") collectives
+        are captured.  A capture that fails is fatal -- a failed capture leaves its stream
+        invalidated, so nothing may run on it afterwards (the 2-rank abort of commit
+        3462363); the error is printed and the process exits non-zero."""
+        in_graph = not self.collective or (
+            self.allreduce == "graph" and dist.get_backend() == "nccl")
+        if in_graph:
+            g = torch.cuda.CUDAGraph()
             try:
-                g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     self.loss = self.fwd_bwd()
                     if self.collective:
                         self.reducer.all_reduce_()
                     self.opt.step()
-                self.graph_fb, self.graph_opt = g, None
-                self.allreduce_in_graph = self.collective
-                assert self.opt.views_intact()
-                return
-            except Exception as e:  # noqa: BLE001 -- fall back to the split form
-                if not self.collective:
-                    raise
-                log(f"all-reduce capture failed ({type(e).__name__}: {e}); split graphs")
-                torch.cuda.synchronize(self.device)
+            except Exception as e:
+                log(f"FATAL: capture of the training step "
+                    f"{'with the RCCL all-reduce ' if self.collective else ''}failed "
+                    f"({type(e).__name__}: {e}); the capture stream is invalid, exiting "
+                    f"(run with --allreduce split to keep the collective out of the graph)")
+                raise SystemExit(3) from e
+            self.graph_fb, self.graph_opt = g, None
+            self.allreduce_in_graph = self.collective
+            assert self.opt.views_intact()
+            return
         self.graph_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph_fb):
             self.loss = self.fwd_bwd()
@@ -614,12 +621,153 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     return tr, elapsed, pct
 
 
+# -----------------------------------------------------------------------------------------
+# multi-rank launch: one process per GPU
+# -----------------------------------------------------------------------------------------
+LAUNCH_ENV = "RAINCAST_BENCH_LAUNCHED"
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(nranks: int, argv: list) -> int:
+    """``python bench.py --gpus N`` without a torchrun environment: start N fresh child
+    processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one per GPU)
+    and return the worst exit status.  The parent makes no HIP call -- it only waits:
+    children inherit stdout, and rank 0 prints the one JSON line.  When a child fails,
+    the others get a grace period to finish (or notice the broken group), then are
+    terminated by PID."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env[LAUNCH_ENV] = "1"
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    try:
+        deadline = None
+        while any(p.poll() is None for p in procs):
+            if deadline is None and any(p.returncode not in (None, 0) for p in procs):
+                deadline = time.monotonic() + 60.0
+                log("bench launcher: a rank failed; waiting 60 s for the others")
+            if deadline is not None and time.monotonic() > deadline:
+                stop()
+                for p in procs:
+                    try:
+                        p.wait(timeout=10)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                break
+            time.sleep(0.2)
+        for p in procs:
+            p.wait()
+    finally:
+        signal.signal(signal.SIGTERM, old)
+    rcs = [p.returncode for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log(f"bench launcher: rank exit codes {rcs}")
+        # a signal death (negative) counts as failure with the shell's 128+signal code
+        return max((128 - rc) if rc < 0 else rc for rc in bad)
+    return 0
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """CPU rehearsal of the N-rank bench: gloo group, per-rank synthetic shard of the
+    configuration, the step's gradient all-reduce (the flat fp32 buffer of the model) timed
+    between barriers, max over ranks, rank 0's JSON line.  No GPU work."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    if os.environ.get("RAINCAST_BENCH_DRY_FAIL_RANK") == str(rank):  # launcher test hook
+        raise SystemExit(7)
+    cfg = BENCH_CONFIGS[args.config]
+    graphs_per_rank = (cfg.graphs_per_gpu // world if args.config == 4 else cfg.graphs_per_gpu)
+    params = cfg.params()
+    torch.manual_seed(42)
+    model = gnn_from_params(params).train()
+    broadcast_parameters(model)
+    n_params = sum(p.numel() for p in model.parameters())
+    reducer = FlatGradReducer(model.parameters())
+    shard = synthetic_batch(cfg.num_stations, graphs_per_rank, k=cfg.k, seed=1000 + rank)
+    for _ in range(args.warmup):
+        reducer.all_reduce_()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        reducer.flat.fill_(float(rank + 1))
+        reducer.all_reduce_()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    expect = (world + 1) / 2.0  # mean over ranks of (rank + 1)
+    assert torch.allclose(reducer.flat, torch.full_like(reducer.flat, expect)), "all-reduce"
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        nodes = torch.tensor([shard.num_nodes], dtype=torch.int64)
+        dist.all_reduce(nodes)
+        nodes_total = int(nodes)
+    else:
+        nodes_total = shard.num_nodes
+    elapsed = float(t)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "dry run: gradient all-reduce only (no GPU step)",
+            "value": round(graphs_per_rank * world * args.steps / elapsed, 2),
+            "unit": "graphs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong" if args.config == 4 else "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic", "dry_run": True,
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "rccl_world_size": None, "launcher": os.environ.get(LAUNCH_ENV) == "1",
+            "config": {"workload": cfg.name, "global_batch": graphs_per_rank * world,
+                       "graphs_per_gpu": graphs_per_rank, "nodes_global": nodes_total,
+                       "allreduce_floats": reducer.numel, "parameters": n_params,
+                       "parallelism": f"dp{world}"}}), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, started before anything here touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank, local_rank, world = env_rank()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} rank(s) "
+                         f"(WORLD_SIZE); they must agree")
+    if args.dry_run:
+        return dry_run(args, rank, world)
     if world > 1 or args.force_allreduce:
         dist.init_process_group(args.dist_backend)
-    device = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and local_rank >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but only {ndev} GPU(s) "
+                         f"visible; RCCL needs one GPU per rank")
+    device = torch.device("cuda", local_rank % max(1, ndev))
     torch.cuda.set_device(device)
     cfg = BENCH_CONFIGS[args.config]
     if args.config == 4:  # global batch fixed -> strong scaling
@@ -677,6 +825,12 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (k-NN station graphs, random-init weights)",
+            "backend": dist.get_backend() if dist.is_initialized() else None,
+            "rccl_world_size": (dist.get_world_size() if dist.is_initialized()
+                                and dist.get_backend() == "nccl" else None),
+            "launcher": ("bench.py --gpus (one child process per GPU)"
+                         if os.environ.get(LAUNCH_ENV) == "1" else
+                         "torch.distributed.run" if world > 1 else "single process"),
             "config": {"workload": f"{cfg.name}: {cfg.experiment}, {graphs_global} graphs x "
                                    f"{cfg.num_stations} stations, k={cfg.k}, "
                                    f"{layers} GINE layers, D={tr.params['gnn_hidden']}",

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GINE_ABI_VERSION 1
+#define GINE_ABI_VERSION 2  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin */
 
 #define GINE_OK 0
 #define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
@@ -299,7 +299,8 @@ int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in
                      int32_t max_in_degree, int32_t flags, void* stream);
 
 /* BatchNorm statistics without a finish launch (training, momentum >= 0; csrc/gine_bnacc.hpp).
- * bn_acc: int64[gine_bn_acc_words(D) = 78D + 3], zeroed once by the caller at allocation,
+ * bn_acc: int64[gine_bn_acc_words(D)] (query it: the size follows the build-time replica count
+ * R = GINE_BNACC_REPLICAS, (3R + 1 + 2R) * 2D + 3 words), zeroed once by the caller at allocation,
  * then owned by the kernels (the sums only grow; each consumer differences them against a
  * snapshot the previous consumer left), so one buffer serves every step of one BatchNorm,
  * HIP-graph replays included.  Every producer launch must be followed by exactly one
@@ -380,6 +381,8 @@ int gine_mlp_bwd1_wgrad(const float* dy, const float* y, const uint8_t* mask, co
 int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                     float* step, int64_t n, float lr, float beta1, float beta2, float eps,
                     float weight_decay, void* stream);
+/* Length in floats of gine_adamw_step's `step` buffer (288 since ABI 2). */
+int gine_adamw_state_floats(int64_t* floats);
 
 /* ------------------------------------------------------------------------------------
  * Fused CRPS losses (models/loss.py) over the post-processed predictions pred [N, K]
@@ -395,6 +398,8 @@ int gine_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_
  * calls sharing a ticket must not overlap).  c = censoring point (log 0.01), t = sigmoid
  * temperature of grad_u, xi = GPD shape, u = fixed threshold.
  * gine_crps_bwd: grad_pred = gloss[0] * dpred / count (fp32).
+ * gine_count_valid: count[0] = number of non-NaN y (device double; one workgroup) -- the
+ * count_in of gine_crps_fwd_grad, recounted every step (inside a captured step too).
  * ---------------------------------------------------------------------------------- */
 #define GINE_LOSS_NORMAL 0
 #define GINE_LOSS_MIXED_NORMAL 1
@@ -406,6 +411,7 @@ int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t 
                   double* loss_out, double* count_out, uint32_t* ticket, void* stream);
 int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
                   int64_t num_nodes, int32_t kind, float* grad_pred, void* stream);
+int gine_count_valid(const float* y, int64_t num_nodes, double* count, void* stream);
 /* gine_crps_fwd that also writes grad_unit = (float)(dpred / count_in[0]), the gradient for
  * gloss = 1 exactly as gine_crps_bwd would round it, given the count of non-NaN targets
  * up front (count_in: device double) -- a backward seeded with 1 then needs no launch. */

@@ -354,6 +354,38 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
   }
 }
 
+// Number of non-NaN targets (the size of the reference's y[mask], loss.py:39-42, 234-239)
+// as a double, by ONE workgroup: the unit-seed gradient of the CRPS pass divides by it
+// before any workgroup of that pass could know the total.  Part of every step (a replayed
+// graph recounts whatever y holds now).  Integer count: exact and order-independent.
+constexpr int kCountThreads = 1024;
+__global__ __launch_bounds__(kCountThreads) void k_count_valid(const float* __restrict__ y,
+                                                               int64_t n,
+                                                               double* __restrict__ count) {
+  // scalar head up to a 16-byte boundary, float4 body, scalar tail
+  const int64_t head = min<int64_t>(n, (int64_t)((16 - ((uintptr_t)y & 15)) & 15) / 4);
+  const int64_t nv = (n - head) / 4;
+  const float4* yv = reinterpret_cast<const float4*>(y + head);
+  unsigned int c = 0;
+  const int t = threadIdx.x;
+  if (t < head) c += y[t] == y[t];
+#pragma unroll 8
+  for (int64_t i = t; i < nv; i += kCountThreads) {
+    const float4 v = yv[i];
+    c += (v.x == v.x) + (v.y == v.y) + (v.z == v.z) + (v.w == v.w);
+  }
+  for (int64_t i = head + 4 * nv + t; i < n; i += kCountThreads) c += y[i] == y[i];
+  __shared__ unsigned int s_c[kCountThreads / 64];
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((t & 63) == 0) s_c[t >> 6] = c;
+  __syncthreads();
+  if (t == 0) {
+    unsigned long long tot = 0;
+    for (int w = 0; w < kCountThreads / 64; ++w) tot += s_c[w];
+    count[0] = (double)tot;
+  }
+}
+
 // grad_pred = gloss * dpred / count
 __global__ __launch_bounds__(kThreads) void k_crps_bwd(const double* __restrict__ dpred,
                                                        const double* __restrict__ count,
@@ -488,6 +520,16 @@ extern "C" int gine_crps_head_grad_job(int64_t num_nodes, int32_t channels, int3
   job->w[0] = dw;
   job->b[0] = db;
   job->bscale[0] = 1.0f;
+  return GINE_OK;
+}
+
+extern "C" int gine_count_valid(const float* y, int64_t num_nodes, double* count,
+                                void* stream) {
+  if (num_nodes < 0 || !count || (num_nodes > 0 && !y)) return GINE_ERR_INVALID;
+  if (num_nodes > ((int64_t)1 << 32) - 1) return GINE_ERR_DIM;  // 32-bit per-thread counts
+  hipLaunchKernelGGL(k_count_valid, dim3(1), dim3(kCountThreads), 0, as_stream(stream), y,
+                     num_nodes, count);
+  GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
 

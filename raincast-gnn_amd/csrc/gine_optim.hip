@@ -11,18 +11,20 @@
 //   p  += -(lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
 // The step counter lives on the device, so the update is legal inside a captured HIP graph
 // and replays correctly: every workgroup uses step[0] + 1, and the workgroup that finishes
-// last (ticket in step[1]; by then every workgroup has read step[0]) stores the bump and
-// re-arms the ticket -- one launch per optimizer step.
+// last stores the bump -- one launch per optimizer step.  "Last" is found by a two-level
+// ticket: workgroup b draws from sub-ticket b % 8 (step[32 + 32 g], one 128-byte line each),
+// the last of each group draws from the top ticket (step[1]); every ticket word is re-armed
+// to 0 by its last drawer.  The step buffer is kAdamStateFloats = 288 floats
+// (gine_adamw_state_floats), all zero at allocation.
 #include "gine_common.hpp"
 
-#include <cstdlib>
-#include <cstring>
 
 namespace gine {
 namespace {
 
 constexpr int kAdamGroups = 8;     // sub-tickets (one per XCD's share of the grid)
 constexpr int kAdamSubBase = 32;   // floats: sub-ticket g at step[32 + 32 g]
+constexpr int kAdamStateFloats = kAdamSubBase + 32 * kAdamGroups;
 
 struct AdamW {
   float decay, neg_step_size, bc2_sqrt, w1, w2, beta2, eps;
@@ -42,7 +44,7 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
                                                float* __restrict__ m, float* __restrict__ v,
                                                float* __restrict__ step, int64_t n,
                                                float lr, float beta1, float beta2, float eps,
-                                               float weight_decay, bool flat_ticket) {
+                                               float weight_decay) {
   const float t_new = step[0] + 1.0f;
   const double t = (double)t_new;
   const AdamW op{(float)(1.0 - (double)lr * (double)weight_decay),
@@ -76,26 +78,19 @@ __global__ __launch_bounds__(256) void k_adamw(float* __restrict__ p, const floa
   __syncthreads();  // every thread of this workgroup has read step[0]
   if (threadIdx.x == 0) {
     unsigned int* ticket = reinterpret_cast<unsigned int*>(&step[1]);  // 0.0f == 0u
-    if (flat_ticket) {
-      if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+    // two-level ticket: same-word returning atomics serialise (~88 per us on one word,
+    // MI355X_MICROARCH.md "dequeue"), so 512 workgroups on one ticket cost ~6 us at the
+    // end of the launch; workgroup b draws from sub-ticket b % 8 (own 128-byte line),
+    // the last of each group from the top ticket (one word: 6.81 -> 5.46 us, r02_s84)
+    const unsigned int g = blockIdx.x % kAdamGroups;
+    const unsigned int groups = min(gridDim.x, (unsigned)kAdamGroups);
+    const unsigned int size = (gridDim.x - g + kAdamGroups - 1) / kAdamGroups;
+    unsigned int* sub = reinterpret_cast<unsigned int*>(step + kAdamSubBase) + 32 * g;
+    if (atomicAdd(sub, 1u) == size - 1) {
+      *sub = 0u;  // re-armed (the next launch is ordered after this one)
+      if (atomicAdd(ticket, 1u) == groups - 1) {
         step[0] = t_new;
         *ticket = 0u;
-      }
-    } else {
-      // two-level ticket: same-word returning atomics serialise (~88 per us on one word,
-      // MI355X_MICROARCH.md "dequeue"), so 512 workgroups on one ticket cost ~6 us at the
-      // end of the launch; workgroup b draws from sub-ticket b % 8 (own 128-byte line),
-      // the last of each group from the top ticket
-      const unsigned int g = blockIdx.x % kAdamGroups;
-      const unsigned int groups = min(gridDim.x, (unsigned)kAdamGroups);
-      const unsigned int size = (gridDim.x - g + kAdamGroups - 1) / kAdamGroups;
-      unsigned int* sub = reinterpret_cast<unsigned int*>(step + kAdamSubBase) + 32 * g;
-      if (atomicAdd(sub, 1u) == size - 1) {
-        *sub = 0u;  // re-armed (the next launch is ordered after this one)
-        if (atomicAdd(ticket, 1u) == groups - 1) {
-          step[0] = t_new;
-          *ticket = 0u;
-        }
       }
     }
   }
@@ -121,12 +116,14 @@ extern "C" int gine_adamw_step(float* param, const float* grad, float* exp_avg,
   if (n > 0 && (al & 15) != 0) return GINE_ERR_INVALID;
   int64_t blocks = ceil_div(n > 0 ? ceil_div(n, 4) : 1, 256);
   if (blocks > 512) blocks = 512;
-  static const bool flat_ticket = [] {  // experiment switch: one ticket word for the grid
-    const char* e = getenv("GINE_ADAMW_TICKET");
-    return e != nullptr && strcmp(e, "flat") == 0;
-  }();
   hipLaunchKernelGGL(k_adamw, dim3((unsigned)blocks), dim3(256), 0, s, param, grad, exp_avg,
-                     exp_avg_sq, step, n, lr, beta1, beta2, eps, weight_decay, flat_ticket);
+                     exp_avg_sq, step, n, lr, beta1, beta2, eps, weight_decay);
   GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_adamw_state_floats(int64_t* floats) {
+  if (!floats) return GINE_ERR_INVALID;
+  *floats = kAdamStateFloats;
   return GINE_OK;
 }

@@ -23,7 +23,7 @@ GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _c_void_p = ctypes.c_void_p
 _i32, _i64, _f32, _size = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
@@ -109,6 +109,8 @@ _SIGNATURES = {
     "gine_crps_fwd": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64, _c_void_p,
                       _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "gine_crps_bwd": [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
+    "gine_count_valid": [_c_void_p, _i64, _c_void_p, _c_void_p],
+    "gine_adamw_state_floats": [ctypes.POINTER(_i64)],
     "gine_crps_fwd_grad": [_c_void_p, _c_void_p, _i64, _i32, _f64, _f64, _f64, _f64]
                           + [_c_void_p] * 8,
     "gine_crps_head_slab_floats": [_i64, _i32, _i32, ctypes.POINTER(ctypes.c_size_t)],

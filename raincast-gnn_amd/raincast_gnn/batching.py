@@ -107,13 +107,19 @@ class DeviceLoader:
     (``torch.randperm``, as PyG's DataLoader's RandomSampler does), so the batch order is the
     same whatever the dataset's device.  With ``world > 1`` every rank walks the same global
     batches and yields its contiguous shard of graphs (:func:`~raincast_gnn.distributed.
-    shard_range`); a (short, last) batch with fewer graphs than ranks is skipped by all."""
+    shard_range`).  ``batch_size`` must then be a multiple of ``world``, so every full batch
+    gives every rank the same number of graphs and the equal-weight gradient average (DDP's
+    semantics) is the mean of equal shards; only a short last batch can split unevenly, and
+    one with fewer graphs than ranks is skipped by all."""
 
     def __init__(self, dataset: DeviceDataset, batch_size: int, shuffle: bool = True,
                  seed: int = 0, drop_last: bool = False, rank: int = 0, world: int = 1):
         self.dataset, self.batch_size = dataset, int(batch_size)
         self.shuffle, self.drop_last = shuffle, drop_last
         self.rank, self.world = int(rank), int(world)
+        if self.world > 1 and self.batch_size % self.world != 0:
+            raise ValueError(f"batch_size {self.batch_size} is not a multiple of the {self.world} "
+                             f"data-parallel ranks: shards would be unequal in every step")
         self._gen = torch.Generator()
         self._gen.manual_seed(seed)
 

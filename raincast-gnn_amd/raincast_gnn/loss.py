@@ -87,28 +87,16 @@ def _masked_mean(values: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return total / m.sum().to(values.dtype)
 
 
-class _ValidCounts:
-    """Number of non-NaN targets of a ``y`` tensor as a device double, computed once per
-    distinct tensor (identity + version; the entry holds ``y`` so its memory is not reused
-    while cached) -- in a replayed training step ``y`` is the same tensor every step."""
-
-    def __init__(self, capacity: int = 8):
-        self.capacity = capacity
-        self._entries: dict = {}
-
-    def get(self, y: torch.Tensor) -> torch.Tensor:
-        key = (y.data_ptr(), y._version, tuple(y.shape), y.device)
-        hit = self._entries.get(key)
-        if hit is not None:
-            return hit[0]
-        cnt = (~torch.isnan(y)).sum().to(torch.float64).reshape(1)
-        self._entries[key] = (cnt, y)
-        while len(self._entries) > self.capacity:
-            self._entries.pop(next(iter(self._entries)))
-        return cnt
+def _valid_count(y: torch.Tensor) -> torch.Tensor:
+    """Number of non-NaN targets of ``y`` as a device double (gine_count_valid: one small
+    launch).  Counted on every call -- inside a captured step too, so a replay whose ``y``
+    was refilled in place (``static_y.copy_(new)``) divides by the count of the new targets."""
+    cnt = torch.empty(1, dtype=torch.float64, device=y.device)
+    _lib.call("gine_count_valid", _lib.ptr(y), y.numel(), _lib.ptr(cnt),
+              _lib.stream_handle(y.device))
+    return cnt
 
 
-_valid_counts = _ValidCounts()
 # RAINCAST_CRPS_UNIT_GRAD=0: the backward always runs gine_crps_bwd (A/B experiments)
 UNIT_GRAD = os.environ.get("RAINCAST_CRPS_UNIT_GRAD", "1") != "0"
 # RAINCAST_CRPS_HEAD=0: the head backward always runs as its own launch (gine_head_bwd).
@@ -143,7 +131,7 @@ class _FusedCRPS(torch.autograd.Function):
         count = torch.empty(1, dtype=torch.float64, device=dev)
         ctx.grad_unit = None
         if needs and N > 0 and UNIT_GRAD:
-            count_in = _valid_counts.get(y)
+            count_in = _valid_count(y)
             ctx.grad_unit = torch.empty(N, K, dtype=torch.float32, device=dev)
             if rec is not None:
                 D = rec.h.size(1)

@@ -9,6 +9,8 @@ kernel (``gine_adamw_step``, include/gine_hip.h) that reproduces torch's AdamW a
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib, gradbuf
@@ -49,7 +51,9 @@ class FlatAdamW:
         self.exp_avg_sq = torch.zeros_like(self.flat_param)
         # [count, ticket, -, 8 sub-tickets at 32 + 32 g]: gine_adamw_step bumps the count in
         # its last workgroup (two-level ticket, include/gine_hip.h)
-        self._step_state = torch.zeros(32 + 8 * 32, dtype=torch.float32, device=dev)
+        floats = ctypes.c_int64(0)
+        _lib.call("gine_adamw_state_floats", ctypes.byref(floats))
+        self._step_state = torch.zeros(int(floats.value), dtype=torch.float32, device=dev)
         self.step_count = self._step_state[:1]
 
     @property

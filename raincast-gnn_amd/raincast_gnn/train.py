@@ -189,6 +189,10 @@ def train_one_epoch(model, loader, optimizer, device, logger=None, runner=None) 
     runner = runner or StepRunner(model, optimizer, graphed=False)
     losses = [runner(b.to(device) if b.x.device != torch.device(device) else b)
               for b in loader]
+    if not losses:
+        raise ValueError(
+            "the training loader yielded no batch (a data-parallel loader skips batches with "
+            "fewer graphs than ranks: use at least one graph per rank per batch)")
     total = 0.0
     for v in torch.stack(losses).double().cpu().tolist():  # train.py:72 order, one readback
         total += v
@@ -202,6 +206,8 @@ def evaluate(model, loader, device, logger=None) -> float:
     """train.py:76-91: eval mode (BatchNorm from running statistics), mean batch loss."""
     model.eval()
     losses = [model.loss_fn.crps(model(b.to(device)), b.to(device).y) for b in loader]
+    if not losses:
+        raise ValueError("the validation loader yielded no batch")
     total = 0.0
     for v in torch.stack(losses).double().cpu().tolist():
         total += v

@@ -64,3 +64,49 @@ def test_head_deterministic_and_model_uses_it():
         loss.backward()
         grads.append(torch.cat([model.aggr.weight.grad.reshape(-1), model.aggr.bias.grad]))
     assert torch.equal(grads[0], grads[1])
+
+
+def test_captured_step_recounts_valid_targets():
+    """The whole-network capture pattern: eager warm-up on ``static_y``, capture with the same
+    tensor, then ``static_y.copy_(new)`` with a different number of NaN targets before the
+    replay.  The replayed gradient must divide by the NEW count (the count is recomputed
+    inside the graph), i.e. equal the eager gradient on the new targets bit for bit."""
+    from raincast_gnn import gradbuf
+    from raincast_gnn.data import synthetic_batch
+    from raincast_gnn.models import GNN
+    from raincast_gnn.optim import FlatAdamW
+
+    torch.manual_seed(0)
+    model = GNN(35, 128, 128, 2, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5).to(DEV)
+    model.train()
+    opt = FlatAdamW(model.parameters(), lr=1e-4)
+    batch = synthetic_batch(60, 2, k=5, seed=1).to(DEV)
+    static_y = batch.y.clone()
+
+    def fwd_bwd():
+        opt.zero_grad()
+        loss = model.loss_fn.crps(model(batch), static_y)
+        gradbuf.loss_backward(loss)
+        opt.gather_grads()
+        return loss
+
+    side = torch.cuda.Stream(DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            fwd_bwd()
+    torch.cuda.current_stream(DEV).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        loss_g = fwd_bwd()
+    new_y = batch.y.clone()
+    new_y[::3] = float("nan")
+    assert int(torch.isnan(new_y).sum()) != int(torch.isnan(batch.y).sum())
+    static_y.copy_(new_y)
+    graph.replay()
+    torch.cuda.synchronize()
+    g_graph, l_graph = opt.flat_grad.clone(), loss_g.clone()
+    l_eager = fwd_bwd()
+    torch.cuda.synchronize()
+    assert torch.equal(l_graph, l_eager)
+    assert torch.equal(g_graph, opt.flat_grad), (g_graph - opt.flat_grad).abs().max()

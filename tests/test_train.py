@@ -78,3 +78,15 @@ def test_train_one_epoch_mean_matches_reference_loop():
         total += loss.item()
         n += 1
     assert got == total / n
+
+
+def test_data_parallel_loader_needs_equal_shards_and_a_batch():
+    import pytest
+    ds = DeviceDataset(synthetic_samples(20, 5, k=4, seed=0), "cpu")
+    with pytest.raises(ValueError, match="multiple"):
+        DeviceLoader(ds, 4, rank=0, world=3)        # 4 graphs over 3 ranks: 2/1/1 every step
+    # 8 ranks, batches of 8, 5 samples: the only batch has fewer graphs than ranks
+    loader = DeviceLoader(ds, 8, rank=0, world=8)
+    assert list(loader) == []
+    with pytest.raises(ValueError, match="no batch"):
+        T.train_one_epoch(_OracleModel(), loader, None, "cpu")
