@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(BENCH_CONFIGS))
+    ap.add_argument("--hidden", type=int, default=None,
+                    help="gnn_hidden override (the D=64 sweep of BASELINE.md:47 / the north "
+                         "star's 64-dim features); default: params.json's 128")
     ap.add_argument("--no-graph", action="store_true", help="eager steps (no HIP graph)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU-baseline sample")
@@ -69,8 +72,8 @@ def parse():
                          "default cfg2 run adds")
     ap.add_argument("--allreduce", choices=("graph", "split"), default="graph",
                     help="graph: the gradient all-reduce captured inside the step's HIP "
-                         "graph (falls back to split if capture fails); split: fwd+bwd "
-                         "graph, eager all-reduce, optimizer graph")
+                         "graph with RCCL (gloo always splits; a failed capture exits "
+                         "non-zero); split: fwd+bwd graph, eager all-reduce, optimizer graph")
     ap.add_argument("--station-order", choices=("locality", "dataset"), default="locality",
                     help="locality: the batch in the engine's station order (reverse "
                          "Cuthill-McKee, raincast_gnn.data.station_order -- the device "
@@ -80,6 +83,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm, the benchmark) | gloo (multi-rank rehearsal on "
                          "one GPU: ranks share the device)")
+    ap.add_argument("--dropin", action="store_true",
+                    help="time the drop-in path instead: the reference's model structure in "
+                         "torch with raincast_gnn's GINEConv, train.py's loop (batch.to(device) "
+                         "and loss.item() every step); 1 GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: ranks over gloo build their shards and time the gradient "
                          "all-reduce alone (launcher / rank / shard / JSON plumbing; no GPU "
@@ -697,7 +704,7 @@ def dry_run(args, rank: int, world: int) -> None:
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     if os.environ.get("RAINCAST_BENCH_DRY_FAIL_RANK") == str(rank):  # launcher test hook
         raise SystemExit(7)
-    cfg = BENCH_CONFIGS[args.config]
+    cfg = BENCH_CONFIGS[args.config].with_hidden(args.hidden)
     graphs_per_rank = (cfg.graphs_per_gpu // world if args.config == 4 else cfg.graphs_per_gpu)
     params = cfg.params()
     torch.manual_seed(42)
@@ -747,6 +754,83 @@ def dry_run(args, rank: int, world: int) -> None:
         dist.destroy_process_group()
 
 
+def dropin_bench(args, cfg, device) -> dict:
+    """The reference's own training loop (train.py:61-71) over the reference's model
+    structure with only GINEConv swapped (raincast_gnn.dropin.ReferenceStructGNN: torch
+    DeepSet / dim_red / ResGnn activations / aggr / PostProcess / CRPS, torch AdamW): every
+    step copies a host batch to the device (``batch.to(device)``: a fresh edge_index tensor
+    each step), runs forward, loss, backward, optimizer step and ``loss.item()``.  Host
+    batches are pre-collated (the DataLoader's collation is host work that this timing
+    leaves out).  The GINE share is the conv stack's forward + backward timed alone on the
+    same device inputs, also with a fresh edge_index tensor per step."""
+    from raincast_gnn.data import collate, synthetic_samples
+    from raincast_gnn.dropin import reference_struct_from_params
+    from raincast_gnn.graph import graph_cache
+    params = cfg.params()
+    graphs = cfg.graphs_per_gpu
+    torch.manual_seed(42)
+    model = reference_struct_from_params(params).to(device).train()
+    opt = torch.optim.AdamW(model.parameters(), lr=params["lr"])
+    samples = synthetic_samples(cfg.num_stations, 2 * graphs, k=cfg.k, seed=1000)
+    host = [collate(samples[:graphs]), collate(samples[graphs:])]
+
+    def step(i):
+        batch = host[i % 2].to(device)                      # train.py:62
+        preds = model(batch)                                # train.py:64
+        loss = model.loss_fn.crps(preds, batch.y)           # train.py:65
+        opt.zero_grad()                                     # train.py:67-69
+        loss.backward()
+        opt.step()
+        return loss.item()                                  # train.py:71
+
+    for i in range(max(args.warmup, 2)):
+        step(i)
+    torch.cuda.synchronize(device)
+    stats0 = dict(graph_cache.stats)
+    t0 = time.perf_counter()
+    total = 0.0
+    for i in range(args.steps):
+        total += step(i)
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    stats = {k: graph_cache.stats[k] - stats0[k] for k in stats0}
+
+    # the GINE stack alone (4 GINEConv + torch ReLU / residual), forward + backward
+    D = params["gnn_hidden"]
+    x0 = torch.randn(host[0].num_nodes, D, device=device, requires_grad=True)
+    gy = torch.randn(host[0].num_nodes, D, device=device)
+    ea_host = host[0].edge_attr
+
+    def gine_step(i):
+        ei = host[i % 2].edge_index.to(device)
+        out = model.conv(x0, ei, ea_host.to(device))
+        out.backward(gy)
+
+    for i in range(3):
+        gine_step(i)
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        gine_step(i)
+    torch.cuda.synchronize(device)
+    gine_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    ms = elapsed / args.steps * 1e3
+    return {"metric": "training graphs/s, drop-in path (models/gnn.py structure in torch, "
+                      "raincast_gnn GINEConv, train.py loop with batch.to(device) and "
+                      "loss.item() every step)",
+            "value": round(graphs * args.steps / elapsed, 2), "unit": "graphs/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (host batches)",
+            "config": {"workload": f"{cfg.name}-dropin: {graphs} graphs x {cfg.num_stations} "
+                                   f"stations, k={cfg.k}, {params['gnn_layers']} GINE layers, "
+                                   f"D={D}", "global_batch": graphs},
+            "gine_stack_ms_fwd_bwd": round(gine_ms, 4),
+            "gine_share_of_step": round(gine_ms / ms, 4),
+            "graph_cache_per_timed_steps": stats,
+            "mean_loss": total / args.steps}
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -769,7 +853,12 @@ def main():
                          f"visible; RCCL needs one GPU per rank")
     device = torch.device("cuda", local_rank % max(1, ndev))
     torch.cuda.set_device(device)
-    cfg = BENCH_CONFIGS[args.config]
+    cfg = BENCH_CONFIGS[args.config].with_hidden(args.hidden)
+    if args.dropin:
+        if world > 1:
+            raise SystemExit("--dropin measures the single-GPU drop-in path (--gpus 1)")
+        print(json.dumps(dropin_bench(args, cfg, device)), flush=True)
+        return
     if args.config == 4:  # global batch fixed -> strong scaling
         graphs_per_rank = cfg.graphs_per_gpu // world
         scaling = "strong"
@@ -791,7 +880,7 @@ def main():
     if args.config == 2 and not args.no_strong:
         # the same model at a fixed global batch of 256 graphs split over
         # the ranks (strong scaling), measured in the same run as the weak-scaling line
-        c4 = BENCH_CONFIGS[4]
+        c4 = BENCH_CONFIGS[4].with_hidden(args.hidden)
         g4 = c4.graphs_per_gpu // world
         tr4, el4, pct4 = measure(c4, g4, args, device, rank, world)
         strong = {"config": "cfg4", "global_batch": g4 * world, "graphs_per_gpu": g4,

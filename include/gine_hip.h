@@ -62,6 +62,17 @@ int gine_graph_build(const int64_t* edge_index, const float* edge_attr, int64_t 
                      int64_t num_edges, int32_t* in_rowptr, int32_t* in_src, float* in_attr,
                      int32_t* out_rowptr, int32_t* out_dst, float* out_attr, int32_t* d_error,
                      void* workspace, size_t workspace_bytes, void* stream);
+/* Content check for the graph cache: *differ = 1 when edge_index_a [2, E] (int64, 16-byte
+ * aligned) differs from edge_index_b or, if given, edge_attr_a [E] from edge_attr_b (bit
+ * patterns); *differ is zeroed by the caller and otherwise left alone.  Lets a caller that
+ * copies the same static graph to the device every step (train.py:62) reuse its CSRs and
+ * window plans instead of rebuilding them.  differ may be mapped host memory: */
+int gine_graph_same_edges(const int64_t* edge_index_a, const int64_t* edge_index_b,
+                          const float* edge_attr_a, const float* edge_attr_b, int64_t num_edges,
+                          int32_t* differ, void* stream);
+/* the device address of pinned (page-locked) host memory (hipHostGetDevicePointer); an error
+ * status when the memory is not mapped for the device. */
+int gine_host_device_ptr(void* host_ptr, void** device_ptr);
 
 /* ------------------------------------------------------------------------------------
  * Message passing forward.  Replaces GINEConv.forward up to (excluding) self.nn:
@@ -398,8 +409,10 @@ int gine_adamw_state_floats(int64_t* floats);
  * calls sharing a ticket must not overlap).  c = censoring point (log 0.01), t = sigmoid
  * temperature of grad_u, xi = GPD shape, u = fixed threshold.
  * gine_crps_bwd: grad_pred = gloss[0] * dpred / count (fp32).
- * gine_count_valid: count[0] = number of non-NaN y (device double; one workgroup) -- the
- * count_in of gine_crps_fwd_grad, recounted every step (inside a captured step too).
+ * gine_count_valid: the number of non-NaN y as GINE_COUNT_PARTS uint32 partial counts
+ * (count_parts; their sum is the count) -- the count_parts of gine_crps_fwd_grad, recounted
+ * every step (inside a captured step too).  gine_head_fwd_count writes the same partials
+ * beside the head forward, so a training step needs no launch for them.
  * ---------------------------------------------------------------------------------- */
 #define GINE_LOSS_NORMAL 0
 #define GINE_LOSS_MIXED_NORMAL 1
@@ -411,14 +424,16 @@ int gine_crps_fwd(const float* pred, const float* y, int64_t num_nodes, int32_t 
                   double* loss_out, double* count_out, uint32_t* ticket, void* stream);
 int gine_crps_bwd(const double* dpred, const double* count, const double* gloss,
                   int64_t num_nodes, int32_t kind, float* grad_pred, void* stream);
-int gine_count_valid(const float* y, int64_t num_nodes, double* count, void* stream);
-/* gine_crps_fwd that also writes grad_unit = (float)(dpred / count_in[0]), the gradient for
+#define GINE_COUNT_PARTS 64
+int gine_count_valid(const float* y, int64_t num_nodes, uint32_t* count_parts, void* stream);
+/* gine_crps_fwd that also writes grad_unit = (float)(dpred / count), the gradient for
  * gloss = 1 exactly as gine_crps_bwd would round it, given the count of non-NaN targets
- * up front (count_in: device double) -- a backward seeded with 1 then needs no launch. */
+ * up front (count_parts: GINE_COUNT_PARTS device uint32 partial counts of y, from
+ * gine_count_valid or gine_head_fwd_count) -- a backward seeded with 1 then needs no launch. */
 int gine_crps_fwd_grad(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
                        double u, double xi, double c, double t, double* dpred, double* partials,
                        double* loss_out, double* count_out, uint32_t* ticket,
-                       const double* count_in, float* grad_unit, void* stream);
+                       const uint32_t* count_parts, float* grad_unit, void* stream);
 /* gine_crps_fwd_grad that also runs the output head's backward for that unit seed (the head
  * of gine_head_fwd: raw [N, K], its input h [N, channels], weight w [K, channels]): dh
  * [N, channels] as gine_head_bwd writes it from grad_pred = grad_unit, and per-workgroup dW |
@@ -430,7 +445,7 @@ int gine_crps_head_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind
 int gine_crps_head_fwd_grad(const float* pred, const float* y, int64_t num_nodes, int32_t kind,
                             double u, double xi, double c, double t, double* dpred,
                             double* partials, double* loss_out, double* count_out,
-                            uint32_t* ticket, const double* count_in, float* grad_unit,
+                            uint32_t* ticket, const uint32_t* count_parts, float* grad_unit,
                             const float* raw, const float* h, const float* w, int32_t channels,
                             float* dh, float* head_slab, void* stream);
 int gine_crps_head_grad_job(int64_t num_nodes, int32_t channels, int32_t kind,
@@ -496,6 +511,11 @@ int gine_deepset_bwd(const float* ens, const uint16_t* mask, const float* dr, fl
  * ---------------------------------------------------------------------------------- */
 int gine_head_fwd(const float* h, const float* w, const float* b, float* raw, float* pred,
                   int64_t num_nodes, int32_t channels, int32_t kind, void* stream);
+/* gine_head_fwd that also counts the batch's non-NaN targets y [N] into count_parts
+ * (GINE_COUNT_PARTS uint32, as gine_count_valid) for the loss pass that follows. */
+int gine_head_fwd_count(const float* h, const float* w, const float* b, float* raw,
+                        float* pred, int64_t num_nodes, int32_t channels, int32_t kind,
+                        const float* y, uint32_t* count_parts, void* stream);
 int gine_head_bwd_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind,
                               size_t* floats);
 int gine_head_bwd(const float* grad_pred, const float* raw, const float* h, const float* w,

@@ -63,4 +63,24 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Non-NaN targets of y [n] as GINE_COUNT_PARTS uint32 partial counts (part p counts the
+// contiguous range p * ceil(n / P) ...), written by the workgroups of the calling launch:
+// workgroup b writes parts b, b + gridDim.x, ...  Blocks of exactly 256 threads.  Integer
+// counts: the consumer's sum is exact whatever the order (gine_crps_fwd_grad).
+__device__ __forceinline__ void count_valid_parts(const float* __restrict__ y, int64_t n,
+                                                  uint32_t* __restrict__ parts) {
+  __shared__ uint32_t s_w[4];
+  const int64_t chunk = (n + GINE_COUNT_PARTS - 1) / GINE_COUNT_PARTS;
+  for (int p = blockIdx.x; p < GINE_COUNT_PARTS; p += gridDim.x) {
+    const int64_t lo = (int64_t)p * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    uint32_t c = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) c += y[i] == y[i];
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    __syncthreads();  // s_w of the previous part has been read
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) parts[p] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  }
+}
+
 }  // namespace gine

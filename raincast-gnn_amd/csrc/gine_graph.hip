@@ -176,6 +176,70 @@ extern "C" int gine_graph_build(const int64_t* edge_index, const float* edge_att
 }
 
 // ---------------------------------------------------------------------------------------
+// Content check of a fresh edge list against a cached one (the drop-in path: train.py:62
+// copies the batch to the device every step, so edge_index is a new tensor each time while
+// its content -- the static station graph, block-diagonally collated -- is the same).  One
+// pass over both lists (16-byte loads); any difference stores 1 into *differ, which the
+// caller zeroed (concurrent stores of the same value: no atomics needed).  `differ` may be
+// host memory mapped into the device (gine_host_device_ptr), so the answer reaches the host
+// without a copy.  Attributes compare as bit patterns (what the CSRs store).
+// ---------------------------------------------------------------------------------------
+namespace gine {
+namespace {
+__global__ __launch_bounds__(256) void k_same_edges(const int4* __restrict__ a,
+                                                    const int4* __restrict__ b, int64_t n16,
+                                                    const int32_t* __restrict__ tail_a,
+                                                    const int32_t* __restrict__ tail_b,
+                                                    int64_t ntail, int32_t* differ) {
+  bool diff = false;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const int4 u = a[i], v = b[i];
+    diff |= (u.x != v.x) | (u.y != v.y) | (u.z != v.z) | (u.w != v.w);
+  }
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < ntail) diff |= tail_a[t] != tail_b[t];
+  if (diff) differ[0] = 1;
+}
+
+int launch_same(const void* a, const void* b, int64_t bytes, int32_t* differ, hipStream_t s) {
+  if (bytes == 0) return GINE_OK;
+  if (!a || !b) return GINE_ERR_INVALID;
+  if (((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) != 0)
+    return GINE_ERR_INVALID;
+  if (bytes % 4 != 0) return GINE_ERR_INVALID;
+  const int64_t n16 = bytes / 16, ntail = (bytes % 16) / 4;
+  const int32_t* ta = reinterpret_cast<const int32_t*>(static_cast<const char*>(a) + 16 * n16);
+  const int32_t* tb = reinterpret_cast<const int32_t*>(static_cast<const char*>(b) + 16 * n16);
+  int64_t blocks = ceil_div(n16 > 0 ? n16 : 1, 256 * 4);
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_same_edges, dim3((unsigned)blocks), dim3(256), 0, s,
+                     static_cast<const int4*>(a), static_cast<const int4*>(b), n16, ta, tb, ntail,
+                     differ);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+}  // namespace
+}  // namespace gine
+
+extern "C" int gine_graph_same_edges(const int64_t* edge_index_a, const int64_t* edge_index_b,
+                                     const float* edge_attr_a, const float* edge_attr_b,
+                                     int64_t num_edges, int32_t* differ, void* stream) {
+  if (num_edges < 0 || !differ) return GINE_ERR_INVALID;
+  if ((edge_attr_a == nullptr) != (edge_attr_b == nullptr)) return GINE_ERR_INVALID;
+  hipStream_t s = as_stream(stream);
+  int st = launch_same(edge_index_a, edge_index_b, 16 * num_edges, differ, s);
+  if (st != GINE_OK || edge_attr_a == nullptr) return st;
+  return launch_same(edge_attr_a, edge_attr_b, 4 * num_edges, differ, s);
+}
+
+extern "C" int gine_host_device_ptr(void* host_ptr, void** device_ptr) {
+  if (!host_ptr || !device_ptr) return GINE_ERR_INVALID;
+  GINE_RETURN_IF_HIP(hipHostGetDevicePointer(device_ptr, host_ptr, 0));
+  return GINE_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 // Station relabelling for neighbour locality (host side, once per static station graph).
 //
 // The window-staged message passing (gine_mpwin.hip) stages, per tile of consecutive

@@ -26,13 +26,17 @@ namespace {
 
 using namespace head;
 
-template <int K>
+template <int K, bool COUNT>
 __global__ __launch_bounds__(kThreads) void k_head_fwd(const float* __restrict__ h,
                                                        const float* __restrict__ w,
                                                        const float* __restrict__ b,
                                                        float* __restrict__ raw,
                                                        float* __restrict__ pred, int64_t N,
-                                                       int D, int kind) {
+                                                       int D, int kind,
+                                                       const float* __restrict__ y,
+                                                       uint32_t* __restrict__ count_parts) {
+  static_assert(kThreads == 256, "count_valid_parts takes 256-thread blocks");
+  if constexpr (COUNT) count_valid_parts(y, N, count_parts);
   const int t = threadIdx.x & 31;
   const int D4 = D / 4;
   for (int64_t n = (int64_t)blockIdx.x * kRowsPerBlock + threadIdx.x / 32; n < N;
@@ -121,19 +125,30 @@ inline int head_bwd_grid(int64_t N) {
 
 using namespace gine;
 
-extern "C" int gine_head_fwd(const float* h, const float* w, const float* b, float* raw,
-                             float* pred, int64_t num_nodes, int32_t channels, int32_t kind,
-                             void* stream) {
+namespace {
+int head_fwd(const float* h, const float* w, const float* b, float* raw, float* pred,
+             int64_t num_nodes, int32_t channels, int32_t kind, const float* y,
+             uint32_t* count_parts, void* stream) {
   const int K = k_of(kind);
   if (K < 0 || num_nodes < 0) return GINE_ERR_INVALID;
   if (!head_dim_ok(channels)) return GINE_ERR_DIM;
-  if (num_nodes == 0) return GINE_OK;
+  if (count_parts && num_nodes > 0 && !y) return GINE_ERR_INVALID;
+  if (num_nodes == 0) {
+    if (count_parts) return gine_count_valid(y, 0, count_parts, stream);
+    return GINE_OK;
+  }
   if (!h || !w || !b || !raw || !pred) return GINE_ERR_INVALID;
   const int grid = (int)std::min<int64_t>(2048, ceil_div(num_nodes, kRowsPerBlock));
   hipStream_t s = as_stream(stream);
-#define HEAD_FWD(KK)                                                                      \
-  hipLaunchKernelGGL(k_head_fwd<KK>, dim3(grid), dim3(kThreads), 0, s, h, w, b, raw, pred, \
-                     num_nodes, channels, kind)
+#define HEAD_FWD(KK)                                                                         \
+  do {                                                                                       \
+    if (count_parts)                                                                         \
+      hipLaunchKernelGGL((k_head_fwd<KK, true>), dim3(grid), dim3(kThreads), 0, s, h, w, b,  \
+                         raw, pred, num_nodes, channels, kind, y, count_parts);              \
+    else                                                                                     \
+      hipLaunchKernelGGL((k_head_fwd<KK, false>), dim3(grid), dim3(kThreads), 0, s, h, w, b, \
+                         raw, pred, num_nodes, channels, kind, nullptr, nullptr);            \
+  } while (0)
   switch (K) {
     case 2: HEAD_FWD(2); break;
     case 3: HEAD_FWD(3); break;
@@ -143,6 +158,21 @@ extern "C" int gine_head_fwd(const float* h, const float* w, const float* b, flo
 #undef HEAD_FWD
   GINE_LAUNCH_STATUS();
   return GINE_OK;
+}
+}  // namespace
+
+extern "C" int gine_head_fwd(const float* h, const float* w, const float* b, float* raw,
+                             float* pred, int64_t num_nodes, int32_t channels, int32_t kind,
+                             void* stream) {
+  return head_fwd(h, w, b, raw, pred, num_nodes, channels, kind, nullptr, nullptr, stream);
+}
+
+extern "C" int gine_head_fwd_count(const float* h, const float* w, const float* b, float* raw,
+                                   float* pred, int64_t num_nodes, int32_t channels,
+                                   int32_t kind, const float* y, uint32_t* count_parts,
+                                   void* stream) {
+  if (!count_parts) return GINE_ERR_INVALID;
+  return head_fwd(h, w, b, raw, pred, num_nodes, channels, kind, y, count_parts, stream);
 }
 
 extern "C" int gine_head_bwd_slab_floats(int64_t num_nodes, int32_t channels, int32_t kind,

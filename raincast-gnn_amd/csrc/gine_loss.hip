@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
                                                    double* __restrict__ loss_out,
                                                    double* __restrict__ count_out,
                                                    unsigned int* __restrict__ ticket,
-                                                   const double* __restrict__ count_in,
+                                                   const uint32_t* __restrict__ count_parts,
                                                    float* __restrict__ grad_unit,
                                                    HeadBwdArgs hb) {
   constexpr int K = LossK<KIND>::value;
@@ -242,7 +242,17 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
   __shared__ double s_sum[kThreads];
   __shared__ double s_cnt[kThreads];
   __shared__ int s_last;
+  __shared__ double s_count;
   constexpr int NPB = HEAD ? kHeadNodes : kThreads;
+  static_assert(GINE_COUNT_PARTS == kWave, "one partial count per lane of wave 0");
+  if (grad_unit != nullptr) {  // the count of valid targets: wave 0 sums the partials
+    if (threadIdx.x < kWave) {
+      uint32_t c = count_parts[threadIdx.x];
+      for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+      if (threadIdx.x == 0) s_count = (double)c;
+    }
+    __syncthreads();
+  }
   static_assert(kHeadNodes == 8 * head::kRowsPerBlock, "one batch of 8 rows per half-wave");
   const int64_t i = blockIdx.x * (int64_t)NPB + threadIdx.x;
   const int64_t first = blockIdx.x * (int64_t)NPB;
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
 #pragma unroll
     for (int k = 0; k < K; ++k) dpred[i * K + k] = g[k];
     if (grad_unit != nullptr) {  // d loss / d pred for gloss = 1, as k_crps_bwd rounds it
-      const double cnt_all = count_in[0];
+      const double cnt_all = s_count;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const float gu = (float)(1.0 * g[k] / cnt_all);
@@ -355,35 +365,13 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
 }
 
 // Number of non-NaN targets (the size of the reference's y[mask], loss.py:39-42, 234-239)
-// as a double, by ONE workgroup: the unit-seed gradient of the CRPS pass divides by it
-// before any workgroup of that pass could know the total.  Part of every step (a replayed
-// graph recounts whatever y holds now).  Integer count: exact and order-independent.
-constexpr int kCountThreads = 1024;
-__global__ __launch_bounds__(kCountThreads) void k_count_valid(const float* __restrict__ y,
-                                                               int64_t n,
-                                                               double* __restrict__ count) {
-  // scalar head up to a 16-byte boundary, float4 body, scalar tail
-  const int64_t head = min<int64_t>(n, (int64_t)((16 - ((uintptr_t)y & 15)) & 15) / 4);
-  const int64_t nv = (n - head) / 4;
-  const float4* yv = reinterpret_cast<const float4*>(y + head);
-  unsigned int c = 0;
-  const int t = threadIdx.x;
-  if (t < head) c += y[t] == y[t];
-#pragma unroll 8
-  for (int64_t i = t; i < nv; i += kCountThreads) {
-    const float4 v = yv[i];
-    c += (v.x == v.x) + (v.y == v.y) + (v.z == v.z) + (v.w == v.w);
-  }
-  for (int64_t i = head + 4 * nv + t; i < n; i += kCountThreads) c += y[i] == y[i];
-  __shared__ unsigned int s_c[kCountThreads / 64];
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
-  if ((t & 63) == 0) s_c[t >> 6] = c;
-  __syncthreads();
-  if (t == 0) {
-    unsigned long long tot = 0;
-    for (int w = 0; w < kCountThreads / 64; ++w) tot += s_c[w];
-    count[0] = (double)tot;
-  }
+// as GINE_COUNT_PARTS partial counts: the unit-seed gradient of the CRPS pass divides by
+// their sum before any workgroup of that pass could know the total.  Recounted every step
+// (a replayed graph counts whatever y holds now).  The training step gets the same partials
+// from the head forward (gine_head_fwd_count); this launch is the stand-alone form.
+__global__ __launch_bounds__(256) void k_count_valid(const float* __restrict__ y, int64_t n,
+                                                     uint32_t* __restrict__ parts) {
+  count_valid_parts(y, n, parts);
 }
 
 // grad_pred = gloss * dpred / count
@@ -412,10 +400,10 @@ namespace {
 int crps_fwd_launch(const float* pred, const float* y, int64_t num_nodes, int32_t kind, double u,
                     double xi, double c, double t, double* dpred, double* partials,
                     double* loss_out, double* count_out, uint32_t* ticket,
-                    const double* count_in, float* grad_unit, void* stream,
+                    const uint32_t* count_parts, float* grad_unit, void* stream,
                     const HeadBwdArgs* hb = nullptr) {
   if (num_nodes < 0 || !partials || !loss_out || !count_out || !ticket) return GINE_ERR_INVALID;
-  if ((count_in == nullptr) != (grad_unit == nullptr)) return GINE_ERR_INVALID;
+  if ((count_parts == nullptr) != (grad_unit == nullptr)) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!pred || !y || !dpred)) return GINE_ERR_INVALID;
   if (kind < GINE_LOSS_NORMAL || kind > GINE_LOSS_MIXED_U) return GINE_ERR_INVALID;
   hipStream_t s = as_stream(stream);
@@ -424,7 +412,7 @@ int crps_fwd_launch(const float* pred, const float* y, int64_t num_nodes, int32_
 #define LAUNCH_CRPS_H(KIND_, H_)                                                               \
   hipLaunchKernelGGL((k_crps<KIND_, H_>), dim3((unsigned)blocks), dim3(kThreads), 0, s, pred, y, \
                      num_nodes, u, xi, c, t, dpred, partials, loss_out, count_out, ticket,      \
-                     count_in, grad_unit, hb ? *hb : HeadBwdArgs{})
+                     count_parts, grad_unit, hb ? *hb : HeadBwdArgs{})
 #define LAUNCH_CRPS(KIND_)                        \
   do {                                            \
     if (hb) LAUNCH_CRPS_H(KIND_, true);           \
@@ -454,11 +442,11 @@ extern "C" int gine_crps_fwd(const float* pred, const float* y, int64_t num_node
 extern "C" int gine_crps_fwd_grad(const float* pred, const float* y, int64_t num_nodes,
                                   int32_t kind, double u, double xi, double c, double t,
                                   double* dpred, double* partials, double* loss_out,
-                                  double* count_out, uint32_t* ticket, const double* count_in,
-                                  float* grad_unit, void* stream) {
-  if (!count_in || !grad_unit) return GINE_ERR_INVALID;
+                                  double* count_out, uint32_t* ticket,
+                                  const uint32_t* count_parts, float* grad_unit, void* stream) {
+  if (!count_parts || !grad_unit) return GINE_ERR_INVALID;
   return crps_fwd_launch(pred, y, num_nodes, kind, u, xi, c, t, dpred, partials, loss_out,
-                         count_out, ticket, count_in, grad_unit, stream);
+                         count_out, ticket, count_parts, grad_unit, stream);
 }
 
 namespace {
@@ -486,18 +474,18 @@ extern "C" int gine_crps_head_fwd_grad(const float* pred, const float* y, int64_
                                        int32_t kind, double u, double xi, double c, double t,
                                        double* dpred, double* partials, double* loss_out,
                                        double* count_out, uint32_t* ticket,
-                                       const double* count_in, float* grad_unit,
+                                       const uint32_t* count_parts, float* grad_unit,
                                        const float* raw, const float* h, const float* w,
                                        int32_t channels, float* dh, float* head_slab,
                                        void* stream) {
   size_t floats = 0;
   const int rc = gine_crps_head_slab_floats(num_nodes, channels, kind, &floats);
   if (rc != GINE_OK) return rc;
-  if (!count_in || !grad_unit || !head_slab || !w) return GINE_ERR_INVALID;
+  if (!count_parts || !grad_unit || !head_slab || !w) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!raw || !h || !dh)) return GINE_ERR_INVALID;
   const HeadBwdArgs hb{raw, h, w, dh, head_slab, channels};
   return crps_fwd_launch(pred, y, num_nodes, kind, u, xi, c, t, dpred, partials, loss_out,
-                         count_out, ticket, count_in, grad_unit, stream, &hb);
+                         count_out, ticket, count_parts, grad_unit, stream, &hb);
 }
 
 extern "C" int gine_crps_head_grad_job(int64_t num_nodes, int32_t channels, int32_t kind,
@@ -523,12 +511,12 @@ extern "C" int gine_crps_head_grad_job(int64_t num_nodes, int32_t channels, int3
   return GINE_OK;
 }
 
-extern "C" int gine_count_valid(const float* y, int64_t num_nodes, double* count,
+extern "C" int gine_count_valid(const float* y, int64_t num_nodes, uint32_t* count_parts,
                                 void* stream) {
-  if (num_nodes < 0 || !count || (num_nodes > 0 && !y)) return GINE_ERR_INVALID;
-  if (num_nodes > ((int64_t)1 << 32) - 1) return GINE_ERR_DIM;  // 32-bit per-thread counts
-  hipLaunchKernelGGL(k_count_valid, dim3(1), dim3(kCountThreads), 0, as_stream(stream), y,
-                     num_nodes, count);
+  if (num_nodes < 0 || !count_parts || (num_nodes > 0 && !y)) return GINE_ERR_INVALID;
+  if (num_nodes > ((int64_t)1 << 32) - 1) return GINE_ERR_DIM;  // 32-bit counts
+  hipLaunchKernelGGL(k_count_valid, dim3(GINE_COUNT_PARTS), dim3(256), 0, as_stream(stream), y,
+                     num_nodes, count_parts);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

@@ -24,6 +24,7 @@ GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
 ABI_VERSION = 2
+COUNT_PARTS = 64  # GINE_COUNT_PARTS
 
 _c_void_p = ctypes.c_void_p
 _i32, _i64, _f32, _size = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
@@ -60,6 +61,8 @@ _SIGNATURES = {
     "gine_graph_workspace_bytes": [_i64, _i64, ctypes.POINTER(_size)],
     "gine_graph_build": [_c_void_p, _c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p,
                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size, _c_void_p],
+    "gine_graph_same_edges": [_c_void_p] * 4 + [_i64, _c_void_p, _c_void_p],
+    "gine_host_device_ptr": [_c_void_p, ctypes.POINTER(_c_void_p)],
     "gine_mp_fwd": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
     "gine_mp_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_mp_bwd": [_c_void_p] * 11 + [_i64, _i32, _i32, _c_void_p],
@@ -127,6 +130,7 @@ _SIGNATURES = {
     "gine_deepset_bwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                          _i64, _i32, _i32, _i32, _c_void_p],
     "gine_head_fwd": [_c_void_p] * 5 + [_i64, _i32, _i32, _c_void_p],
+    "gine_head_fwd_count": [_c_void_p] * 5 + [_i64, _i32, _i32] + [_c_void_p] * 3,
     "gine_head_bwd_slab_floats": [_i64, _i32, _i32, ctypes.POINTER(_size)],
     "gine_head_bwd": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
     "gine_chain_fwd": [_c_void_p] * 4 + [_f32] + [_c_void_p] * 10 + [_i64, _i32, _i32,

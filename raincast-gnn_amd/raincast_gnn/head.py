@@ -26,13 +26,23 @@ class HeadRecord:
     """What the CRPS pass needs to run this head's backward ahead of time (loss.py,
     gine_crps_head_fwd_grad): the head's input, weight and pre-PostProcess output.  ``pre``
     = (grad_unit, dh, slab) once it has: the backward then uses dh / slab if its incoming
-    gradient is that very grad_unit tensor (a unit-seeded loss.backward())."""
+    gradient is that very grad_unit tensor (a unit-seeded loss.backward()).  ``y`` /
+    ``count_parts``: the batch targets the forward was given and their non-NaN partial
+    counts (gine_head_fwd_count), which the loss uses when it is called with that ``y``."""
 
-    __slots__ = ("h", "w", "raw", "kind", "params", "pre")
+    __slots__ = ("h", "w", "raw", "kind", "params", "pre", "y", "y_version", "count_parts")
 
     def __init__(self, h, w, raw, kind, params):
         self.h, self.w, self.raw, self.kind, self.params = h, w, raw, kind, params
         self.pre = None
+        self.y = self.y_version = self.count_parts = None
+
+    def counts_for(self, y: torch.Tensor):
+        """The partial counts of ``y`` if this forward counted exactly that tensor, as it
+        is now (same object, no in-place change since), else None."""
+        if self.y is y and y._version == self.y_version:
+            return self.count_parts
+        return None
 
 
 _records = WeakIdKeyDictionary()  # pred tensor -> HeadRecord
@@ -66,19 +76,29 @@ def fusable(h: torch.Tensor, lin: torch.nn.Linear, kind) -> bool:
 
 class _HeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, weight, bias, kind):
+    def forward(ctx, h, weight, bias, kind, y=None):
         h = h.contiguous()
         w, b = weight.detach().contiguous(), bias.detach().contiguous()
         N, D = h.shape
         K = w.size(0)
         raw = torch.empty(N, K, dtype=torch.float32, device=h.device)
         pred = torch.empty(N, K, dtype=torch.float32, device=h.device)
-        _lib.call("gine_head_fwd", _lib.ptr(h), _lib.ptr(w), _lib.ptr(b), _lib.ptr(raw),
-                  _lib.ptr(pred), N, D, kind, _lib.stream_handle(h.device))
+        rec = HeadRecord(h, w, raw, kind, (weight, bias))
+        if (y is not None and y.is_cuda and y.device == h.device and y.dtype == torch.float32
+                and y.is_contiguous() and y.numel() == N):
+            # the loss's valid-target count, computed beside the head (no launch of its own)
+            parts = torch.empty(_lib.COUNT_PARTS, dtype=torch.int32, device=h.device)
+            _lib.call("gine_head_fwd_count", _lib.ptr(h), _lib.ptr(w), _lib.ptr(b),
+                      _lib.ptr(raw), _lib.ptr(pred), N, D, kind, _lib.ptr(y), _lib.ptr(parts),
+                      _lib.stream_handle(h.device))
+            rec.y, rec.y_version, rec.count_parts = y, y._version, parts
+        else:
+            _lib.call("gine_head_fwd", _lib.ptr(h), _lib.ptr(w), _lib.ptr(b), _lib.ptr(raw),
+                      _lib.ptr(pred), N, D, kind, _lib.stream_handle(h.device))
         ctx.save_for_backward(h, w, raw)
         ctx.kind = kind
         ctx.params = (weight, bias)
-        ctx.rec = HeadRecord(h, w, raw, kind, (weight, bias))
+        ctx.rec = rec
         _records[pred] = ctx.rec
         return pred
 
@@ -101,7 +121,7 @@ class _HeadFn(torch.autograd.Function):
             else:
                 arr = (_lib.GradJob * 1)(job)
                 _lib.call("gine_grad_finalize_batch", arr, 1, _lib.stream_handle(dev))
-            return dh, dw, db, None
+            return dh, dw, db, None, None
         gpred = gpred.float().contiguous()
         floats = ctypes.c_size_t(0)
         _lib.call("gine_head_bwd_slab_floats", N, D, ctx.kind, ctypes.byref(floats))
@@ -118,9 +138,11 @@ class _HeadFn(torch.autograd.Function):
             _lib.call("gine_head_bwd_grad_job", N, D, ctx.kind, _lib.ptr(slab), _lib.ptr(dw),
                       _lib.ptr(db), ctypes.byref(job))
             gradbuf.defer(job, dev, (slab,))
-        return dh, dw, db, None
+        return dh, dw, db, None, None
 
 
-def head(h: torch.Tensor, lin: torch.nn.Linear, kind: int) -> torch.Tensor:
-    """``PostProcess(lin(h))`` for the loss ``kind`` on the fused kernels."""
-    return _HeadFn.apply(h, lin.weight, lin.bias, kind)
+def head(h: torch.Tensor, lin: torch.nn.Linear, kind: int, y: torch.Tensor | None = None
+         ) -> torch.Tensor:
+    """``PostProcess(lin(h))`` for the loss ``kind`` on the fused kernels.  ``y``: the
+    batch targets, whose non-NaN count the launch also takes for the loss that follows."""
+    return _HeadFn.apply(h, lin.weight, lin.bias, kind, y)

@@ -87,14 +87,20 @@ def _masked_mean(values: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return total / m.sum().to(values.dtype)
 
 
-def _valid_count(y: torch.Tensor) -> torch.Tensor:
-    """Number of non-NaN targets of ``y`` as a device double (gine_count_valid: one small
-    launch).  Counted on every call -- inside a captured step too, so a replay whose ``y``
-    was refilled in place (``static_y.copy_(new)``) divides by the count of the new targets."""
-    cnt = torch.empty(1, dtype=torch.float64, device=y.device)
-    _lib.call("gine_count_valid", _lib.ptr(y), y.numel(), _lib.ptr(cnt),
+def _valid_count(y: torch.Tensor, rec=None, y_orig=None) -> torch.Tensor:
+    """Number of non-NaN targets of ``y`` as GINE_COUNT_PARTS device partial counts: the
+    ones the fused head forward took beside its launch when it was given this very ``y``
+    (models.GNN.forward passes ``data.y``), else one gine_count_valid launch.  Counted on
+    every step -- inside a captured step too, so a replay whose ``y`` was refilled in place
+    (``static_y.copy_(new)``) divides by the count of the new targets.  ``y_orig``: the
+    tensor the caller passed (``y`` may be its fp32 contiguous copy)."""
+    parts = rec.counts_for(y if y_orig is None else y_orig) if rec is not None else None
+    if parts is not None:
+        return parts
+    parts = torch.empty(_lib.COUNT_PARTS, dtype=torch.int32, device=y.device)
+    _lib.call("gine_count_valid", _lib.ptr(y), y.numel(), _lib.ptr(parts),
               _lib.stream_handle(y.device))
-    return cnt
+    return parts
 
 
 # RAINCAST_CRPS_UNIT_GRAD=0: the backward always runs gine_crps_bwd (A/B experiments)
@@ -117,9 +123,10 @@ class _FusedCRPS(torch.autograd.Function):
     when it receives exactly this grad_unit tensor."""
 
     @staticmethod
-    def forward(ctx, pred, y, kind, u, xi, c, t, rec=None):
+    def forward(ctx, pred, y, kind, u, xi, c, t, rec=None, count_rec=None):
         needs = ctx.needs_input_grad[0]
         pred = pred.detach().float().contiguous()
+        y_in = y
         y = y.detach().float().contiguous()
         N, K = pred.shape
         dev = pred.device
@@ -131,7 +138,7 @@ class _FusedCRPS(torch.autograd.Function):
         count = torch.empty(1, dtype=torch.float64, device=dev)
         ctx.grad_unit = None
         if needs and N > 0 and UNIT_GRAD:
-            count_in = _valid_count(y)
+            count_in = _valid_count(y, count_rec, y_in)
             ctx.grad_unit = torch.empty(N, K, dtype=torch.float32, device=dev)
             if rec is not None:
                 D = rec.h.size(1)
@@ -162,29 +169,31 @@ class _FusedCRPS(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gloss):
         if ctx.grad_unit is not None and gradbuf.is_unit_seed(gloss):
-            return ctx.grad_unit, None, None, None, None, None, None, None
+            return ctx.grad_unit, None, None, None, None, None, None, None, None
         dpred, count = ctx.saved_tensors
         N = dpred.size(0)
         g = gloss.detach().to(torch.float64).reshape(1).contiguous()
         grad = torch.empty(dpred.shape, dtype=torch.float32, device=dpred.device)
         _lib.call("gine_crps_bwd", _lib.ptr(dpred), _lib.ptr(count), _lib.ptr(g), N, ctx.kind,
                   _lib.ptr(grad), _lib.stream_handle(dpred.device))
-        return grad, None, None, None, None, None, None, None
+        return grad, None, None, None, None, None, None, None, None
 
 
 def _fused(prediction, y, kind, u=0.0, xi=0.5, c=float(np.log(0.01)), t=5.0):
     if prediction.dim() != 2:
         raise ValueError("prediction must be [N, K]")
-    rec = _head.record_of(prediction) if HEAD_BWD else None
+    count_rec = _head.record_of(prediction)
+    rec = count_rec if HEAD_BWD else None
     if rec is not None and (rec.kind != kind or rec.raw.shape != prediction.shape
                             or not prediction.requires_grad
                             or prediction.size(0) > HEAD_BWD_MAX_NODES):
         rec = None
-    return _FusedCRPS.apply(prediction, y, kind, float(u), float(xi), float(c), float(t), rec)
+    return _FusedCRPS.apply(prediction, y, kind, float(u), float(xi), float(c), float(t), rec,
+                            count_rec)
 
 
-def _use_fused(prediction: torch.Tensor, reduce: bool = True) -> bool:
-    return reduce and prediction.is_cuda
+def _use_fused(prediction: torch.Tensor, reduce: bool = True, fused: bool = True) -> bool:
+    return fused and reduce and prediction.is_cuda
 
 
 def _prepare(prediction: torch.Tensor, y: torch.Tensor, width: int):
@@ -197,10 +206,14 @@ def _prepare(prediction: torch.Tensor, y: torch.Tensor, width: int):
 
 
 class NormalCRPS(torch.nn.Module):
-    """models/loss.py:335-369."""
+    """models/loss.py:335-369.  ``fused`` (every loss class): False keeps the torch
+    formulation on a HIP device too (the drop-in model, raincast_gnn/dropin.py)."""
+
+    fused = True
 
     def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-        if _use_fused(prediction):  # the reference's NormalCRPS stays fp32 (loss.py:358-369)
+        # the reference's NormalCRPS stays fp32 (loss.py:358-369)
+        if _use_fused(prediction, True, self.fused):
             return _fused(prediction, y, _lib.LOSS_NORMAL).to(torch.float32)
         mask, (mu, sigma), y1 = _prepare(prediction, y, 2)
         z = (y1 - mu) / sigma
@@ -211,13 +224,15 @@ class NormalCRPS(torch.nn.Module):
 class MixedNormalCRPS(torch.nn.Module):
     """Censored normal with a point mass p at c, models/loss.py:6-68."""
 
+    fused = True
+
     def __init__(self, reduce: bool = True, c: float = np.log(0.01)):
         super().__init__()
         self.reduce = reduce
         self.c = c
 
     def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-        if _use_fused(prediction, self.reduce):
+        if _use_fused(prediction, self.reduce, self.fused):
             return _fused(prediction, y, _lib.LOSS_MIXED_NORMAL, c=float(self.c))
         mask, (mu, sigma, p), y1 = _prepare(prediction, y, 3)
         c = _consts.get(self.c, y.device)  # float64: np.float64 is a float
@@ -236,6 +251,8 @@ class MixedNormalCRPS(torch.nn.Module):
 
 class MixedLoss(torch.nn.Module):
     """Censored normal body + generalised Pareto tail above u, models/loss.py:71-272."""
+
+    fused = True
 
     def __init__(self, grad_u: bool, xi: float, u=None, reduce: bool = True, t: float = 5,
                  c=np.log(0.01)):
@@ -278,7 +295,7 @@ class MixedLoss(torch.nn.Module):
         return sigma * (u_t + t2 + t3 + t4 + t5)
 
     def crps(self, prediction: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-        if _use_fused(prediction, self.reduce):
+        if _use_fused(prediction, self.reduce, self.fused):
             # u / xi are fp32 tensors in the reference (torch.tensor([python float]))
             kind = _lib.LOSS_MIXED_U if self.grad_u else _lib.LOSS_MIXED
             u = 0.0 if self.grad_u else float(np.float32(self.u))

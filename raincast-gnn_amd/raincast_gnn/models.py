@@ -140,7 +140,8 @@ class GNN(nn.Module):
         h = self.conv(h, data.edge_index, data.edge_attr)
         kind = fused_head.loss_kind(self.postprocess.loss, self.postprocess.grad_u)
         if type(self.aggr) in (RowLinear, Linear) and fused_head.fusable(h, self.aggr, kind):
-            return fused_head.head(h, self.aggr, kind)   # aggr + PostProcess, one kernel
+            # aggr + PostProcess in one kernel, which also counts the loss's valid targets
+            return fused_head.head(h, self.aggr, kind, getattr(data, "y", None))
         return self.postprocess(self.aggr(h))
 
     def configure_optimizers(self):

@@ -9,7 +9,7 @@ BASELINE.json / SURVEY.md section 8.
 from __future__ import annotations
 
 import json
-from dataclasses import dataclass
+from dataclasses import dataclass, replace
 
 _COMMON = {"batch_size": 8, "gnn_hidden": 128, "gnn_layers": 4, "heads": 8, "lr": 0.0001,
            "max_dist": 100, "max_epochs": 20, "u": 1.71, "xi": 0.5}
@@ -44,12 +44,22 @@ class BenchConfig:
     graphs_per_gpu: int
     gnn_layers: int | None = None   # override of params.json
     note: str = ""
+    gnn_hidden: int | None = None   # override of params.json (the D=64 sweep, BASELINE.md:47)
 
     def params(self) -> dict:
         p = dict(EXPERIMENTS[self.experiment])
         if self.gnn_layers is not None:
             p["gnn_layers"] = self.gnn_layers
+        if self.gnn_hidden is not None:
+            p["gnn_hidden"] = self.gnn_hidden
         return p
+
+    def with_hidden(self, hidden: int | None) -> "BenchConfig":
+        """This configuration at hidden size ``hidden`` (None or params.json's own value:
+        unchanged); the name records the sweep point, e.g. ``cfg2-D64``."""
+        if hidden is None or hidden == EXPERIMENTS[self.experiment]["gnn_hidden"]:
+            return self
+        return replace(self, gnn_hidden=int(hidden), name=f"{self.name}-D{int(hidden)}")
 
 
 BENCH_CONFIGS = {

@@ -26,12 +26,20 @@ run() {  # run <name> <seconds> cmd...
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 660 python -u -m pytest tests -m gpu -q -rf --durations=15 --timeout 120 --timeout-method thread ;;
+    ntests) run pytest_new 300 python -u -m pytest ${NTESTS:-tests/test_gpu_dropin.py} -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     btests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/bounds/libgine_hip.so \
             run pytest_bounds 300 python -u -m pytest tests/test_gpu_bnacc.py tests/test_gpu_deepset.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     ktests) run pytest_k 600 python -u -m pytest tests -m gpu -q -rf -k "${KTESTS:-window}" --timeout 120 --timeout-method thread ;;
     smoke) run smoke 150 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    benchnc) run bench_nocpu 600 python bench.py --no-cpu ;;
     bench1) run bench_cfg1 600 python bench.py --config 1 ;;
+    bench64) run bench_cfg2_d64 600 python bench.py --hidden 64 ;;
+    dropin) run bench_dropin 600 python bench.py --dropin --steps 30 ;;
+    dropinprof) run rocprof_dropin 600 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+               -d "$OUT/prof_dropin" -o run -- python3 bench.py --dropin --steps 20 --warmup 5 ;;
+    prof64) run rocprof_d64 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof64" -o run -- \
+               python3 bench.py --hidden 64 --steps 20 --warmup 5 --no-cpu --no-strong ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 20 ;;
     bench5) run bench_cfg5 600 python bench.py --config 5 --steps 20 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
@@ -45,9 +53,8 @@ for s in $STEPS; do
                > "$OUT/pmc_summary.txt" 2>&1 ;;
     rgsweep) for g in 256 512 1024; do export GINE_ROWGEMM_BLOCKS=$g; run bench_rg$g 300 python bench.py --no-cpu --steps 30 ${VARARGS:-}; done; unset GINE_ROWGEMM_BLOCKS ;;
     mbsweep) for g in 512 1024 2048 4096; do export GINE_MPBWD_BLOCKS=$g; run bench_mb$g 300 python bench.py --no-cpu --steps 30; done; unset GINE_MPBWD_BLOCKS ;;
-    dist2) run bench_dist2_gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-               --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --dist-backend gloo \
-               --steps 10 --warmup 3 ;;
+    dist2) run bench_dist2_gloo 600 python bench.py --gpus 2 --dist-backend gloo --steps 10 \
+               --warmup 3 --no-cpu ;;
     rgprof) GINE_HIP_LIB=raincast-gnn_amd/csrc/build/dbg/libgine_hip_rgprof.so run rg_prof 300 python tools/rg_prof.py ;;
     var)   for v in raincast-gnn_amd/csrc/build/var/*/; do n=$(basename "$v")
              GINE_HIP_LIB=${v}libgine_hip.so run var_${n}_base 300 python bench.py --no-cpu --steps 30 ${VARARGS:-}
