@@ -256,7 +256,7 @@ def time_kernels(tr: Trainer, reps: int):
             (lambda: call("gine_mp_bwd", ptr(dz), ptr(x), ptr(g.out_rowptr), ptr(g.out_dst),
                           ptr(g.out_attr), ptr(lw), ptr(lb), ptr(ep), ptr(dz), ptr(dx),
                           ptr(mp_part), N, D, 1 | lin, S[0])),
-            {"bytes": 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D}),
+            {"bytes": 4 * (3 * N * D + 2 * E + N + 1)}),   # 8(d) B_b, as the roofline
         "gine_mlp_fwd1": (lambda: call("gine_mlp_fwd1", ptr(z), ptr(w1), ptr(b1), ptr(a1),
                                        ptr(partials), N, D, S[0]),
                           {"flops": 2 * N * D * D, "bytes": 8 * N * D}),
@@ -470,13 +470,15 @@ def copy_ceiling_gbps(device, nbytes=1 << 30, reps=10):
 
 
 # entry point -> the kernels one call launches (names as in the rocprofv3 PMC summary; D=128,
-# the residual epilogue of layers >= 1)
+# the residual epilogue of layers >= 1).  A tuple lists alternatives: the first kernel the
+# summary holds is the one the configuration ran (gine_mp_bwd: the window kernel where the
+# graph has a plan, the gather kernel otherwise -- cfg5).
 PMC_KERNELS = {
     "gine_mp_fwd": ["gine::k_mp_fwd<32, 1, "],
     "gine_mp_fwd_mlp1": ["gine::k_mp_fwd_mlp1<"],
     # (the GPU box's host rounds the edge Linear mul-then-add: FMA = false)
     "gine_mp_bwd_mlp_wgrad": ["gine::k_mp_bwd_win<32, false, true, 5>"],
-    "gine_mp_bwd": ["gine::k_mp_bwd_win<32, "],
+    "gine_mp_bwd": [("gine::k_mp_bwd_win<32, ", "gine::k_mp_bwd<32, 1, ")],
     "gine_mlp_fwd1": ["gine::k_rowgemm<128, 0, 0, true>"],
     "gine_mlp_fwd2": ["gine::k_rowgemm<128, 1, 5, true>"],
     "gine_mlp_bwd2": ["gine::k_rowgemm<128, 5, 2, false>"],
@@ -505,7 +507,8 @@ def pmc_traffic(kernel: str, config: str = "cfg2"):
             continue
         if d.get("_config", "cfg2") != config:
             continue
-        hits = [next((v for k, v in d.items() if k.startswith(n)), None) for n in names]
+        hits = [next((v for alt in (n if isinstance(n, tuple) else (n,))
+                      for k, v in d.items() if k.startswith(alt)), None) for n in names]
         if all(h is not None for h in hits):
             return {"bytes": int(sum(hits)), "source": os.path.basename(path)}
     return None

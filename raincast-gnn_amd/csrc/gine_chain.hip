@@ -26,7 +26,6 @@
 #include "gine_chainfold.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace gine {
 namespace {
@@ -352,23 +351,10 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
 }
 
 // Persistent grid, one workgroup per CU (two per CU measured slower at cfg2: 0.614 vs
-// 0.589 ms per step).  GINE_CHAIN_BLOCKS (tuning experiments only) overrides the cap.
+// 0.589 ms per step).
 inline int chain_grid(int64_t N) {
-  static const int cap = [] {
-    const char* e = getenv("GINE_CHAIN_BLOCKS");
-    return e && atoi(e) > 0 ? atoi(e) : kNumCu;
-  }();
   const int64_t tiles = ceil_div(N, kRowTile);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cap));
-}
-
-// GINE_CHAIN_B3=0 (A/B experiments): the folded backward as two launches (B1F, B2)
-inline bool chain_b3() {
-  static const bool on = [] {
-    const char* e = getenv("GINE_CHAIN_B3");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, kNumCu));
 }
 
 template <int D, int FP, int KIND>
@@ -784,20 +770,11 @@ extern "C" int gine_chain_bwd_folded(const float* dh0, const float* u, const flo
   hipStream_t st = as_stream(stream);
   const int F = in_features;
   int rc = GINE_OK;
-  if (chain_b3()) {  // one launch: dt -> ds -> dr
-    ChainArgs b{dh0, nullptr, u, wfold, nullptr, wr0, nullptr, dt, ds, 1.f, F};
-    b.w3 = wp2;
-    b.out3 = dr;
+  // one launch: dt -> ds -> dr (two launches, B1F + B2, measured slower: r02_s43)
+  ChainArgs b{dh0, nullptr, u, wfold, nullptr, wr0, nullptr, dt, ds, 1.f, F};
+  b.w3 = wp2;
+  b.out3 = dr;
 #define CALL_B(DD, FF) rc = launch_chain<DD, FF, CH_B3>(b, num_nodes, st)
-    GINE_CHAIN_DISPATCH(hidden, F, CALL_B);
-#undef CALL_B
-    return rc;
-  }
-  const ChainArgs b1{dh0, nullptr, u, wfold, nullptr, nullptr, nullptr, nullptr, dt, 1.f, F};
-  const ChainArgs b2{dt, nullptr, nullptr, wr0, nullptr, wp2, nullptr, ds, dr, 1.f, F};
-#define CALL_B(DD, FF)                                                  \
-  rc = launch_chain<DD, FF, CH_B1F>(b1, num_nodes, st);                 \
-  if (rc == GINE_OK) rc = launch_chain<DD, FF, CH_B2>(b2, num_nodes, st)
   GINE_CHAIN_DISPATCH(hidden, F, CALL_B);
 #undef CALL_B
   return rc;

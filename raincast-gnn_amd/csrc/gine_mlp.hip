@@ -29,7 +29,6 @@
 
 #include <algorithm>
 #include <type_traits>
-#include <cstdlib>
 
 namespace gine {
 namespace {
@@ -689,14 +688,9 @@ __global__ __launch_bounds__(2 * D) void k_rowgemm(const float* __restrict__ W, 
 // Persistent grid.  One workgroup per CU while each has at most 4 tiles; past that two
 // per CU, so one workgroup's epilogue and staging run beside the other's MFMA chain (cfg3,
 // 4,000 tiles: 48 -> 44 us fwd1, 65 -> 54 us bwd2; at cfg2, 500 tiles, the second
-// workgroup's weight staging costs more than the overlap gains).  GINE_ROWGEMM_BLOCKS
-// (tuning experiments only) overrides the cap.
+// workgroup's weight staging costs more than the overlap gains; 512 / 1024 workgroups at
+// cfg2 measured no better, r02_s61).
 inline int rowgemm_cap(int D, int64_t tiles) {
-  static const int env = [] {
-    const char* e = getenv("GINE_ROWGEMM_BLOCKS");
-    return e ? atoi(e) : 0;
-  }();
-  if (env > 0) return std::min(env, 2048);  // gine_bnacc.hpp range bound
   const int per_cu = (D == 128 && tiles > 4 * kNumCu) ? 2 : 1;
   return std::max(kNumCu * per_cu, 1024 / (D / 32));
 }

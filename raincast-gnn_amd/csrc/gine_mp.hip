@@ -20,7 +20,6 @@
 #include "gine_reduce.hpp"
 #include "gine_slab.hpp"
 
-#include <cstdlib>
 
 namespace gine {
 namespace {
@@ -379,14 +378,8 @@ inline bool pick_shape(int D, Shape* s) {
 
 inline int nodes_per_block(const Shape& s) { return kWaves * (kWave / s.L); }
 
-// Persistent grid cap (GINE_MPBWD_BLOCKS overrides it, for tuning experiments only).
-inline int64_t max_bwd_blocks() {
-  static const int env = [] {
-    const char* e = getenv("GINE_MPBWD_BLOCKS");
-    return e ? atoi(e) : 0;
-  }();
-  return env > 0 ? env : 1024;
-}
+// Persistent grid cap (512 - 4096 measured within noise at cfg2).
+inline int64_t max_bwd_blocks() { return 1024; }
 
 inline int bwd_grid(int64_t N, const Shape& s) {
   const int64_t tiles = ceil_div(N, nodes_per_block(s));

@@ -508,16 +508,6 @@ WinPlan device_plan(const gine_window_plan* p) {
 }
 
 // Raise the kernel's dynamic-LDS ceiling once per instantiation (thread-safe static init).
-// GINE_WIN_EXTRA_LDS (occupancy experiments only): bytes added to the backward window
-// launches' dynamic LDS, so fewer workgroups fit per CU
-inline size_t win_extra_lds() {
-  static const size_t v = [] {
-    const char* e = getenv("GINE_WIN_EXTRA_LDS");
-    const long x = e ? atol(e) : 0;
-    return (size_t)(x > 0 && x <= 80 * 1024 ? x : 0);
-  }();
-  return v;
-}
 
 template <auto K>
 int set_lds_limit() {
@@ -567,7 +557,6 @@ int mp_bwd_win_launch(const float* dz, const float* x, const int32_t* out_rowptr
     smem = smem > kWinEngineLds ? smem : kWinEngineLds;
   }
   if (smem > GINE_WINDOW_LDS_BYTES) return GINE_ERR_INVALID;
-  smem += win_extra_lds();
   const unsigned grid =
       (unsigned)(plan->num_tiles * S + job.nblocks + (eng ? eng->nblocks : 0));
   const WinPlan wp = device_plan(plan);

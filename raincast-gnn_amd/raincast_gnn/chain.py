@@ -11,7 +11,7 @@ nonlinearity between them, so ``h0 = [x | u] W'^T + b'`` with ``W' = [Wdr_x | Wd
 folded from the current weights inside the first kernel; the backward needs one
 input-gradient GEMM and one weight-gradient product fewer, and dWr1 / dWdr_e are unfolded
 from ``G = dh0^T u`` after the slab reduction (profiles/r02_s38_chain_fold_ab_*: cfg2
-0.575 -> 0.560 ms per step, cfg3 3.26 -> 2.97).  RAINCAST_CHAIN_FOLD=0 runs the unfolded
+0.575 -> 0.560 ms per step, cfg3 3.26 -> 2.97).  ``FOLD = False`` runs the unfolded
 chain: ``gine_chain_fwd`` as two 2-stage row-chain kernels and ``gine_chain_bwd`` (two chain
 kernels, one weight-gradient launch for all four Linears, one reduction) -- csrc/
 gine_chain.hip.  Modules, parameters and state_dict keys are the reference's; this is only
@@ -20,7 +20,6 @@ the execution of ``GNN.forward``'s first half.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -185,15 +184,15 @@ class _ChainFoldedFn(torch.autograd.Function):
         return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None, None)
 
 
-# RAINCAST_CHAIN_FOLD=0: the unfolded chain (four GEMM stages forward, e materialised)
-FOLD = os.environ.get("RAINCAST_CHAIN_FOLD", "1") != "0"
+# False: the unfolded chain (four GEMM stages forward, e materialised); measured slower
+# (cfg2 0.5749 vs 0.5595 ms per step, r02_s38), kept for the tests that compare the two
+FOLD = True
 
 
-# RAINCAST_CHAIN_F3=0: the folded forward as two launches (W' folded by the first).  The
-# one-launch form (three stages, one workgroup per CU) wins while a CU walks a few tiles
+# False: the folded forward as two launches (W' folded by the first).  The one-launch form (three stages, one workgroup per CU) wins while a CU walks a few tiles
 # (cfg2, 16,000 nodes: 0.5442 -> 0.5405 ms per step) and loses at many (cfg3, 128,000:
 # 2.922 -> 2.937, profiles/r02_s67_*), so it is used up to F3_MAX_NODES rows.
-F3 = os.environ.get("RAINCAST_CHAIN_F3", "1") != "0"
+F3 = True
 F3_MAX_NODES = 32768
 
 

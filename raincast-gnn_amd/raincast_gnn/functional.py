@@ -22,7 +22,7 @@ import warnings
 
 import torch
 
-from . import _lib
+from . import _lib, options
 from ._lib import call, ptr
 from . import gradbuf
 from .gradbuf import grad_out
@@ -212,9 +212,9 @@ FUSED_MAX_NODES = 2 * 256 * 32
 
 def fused_forward_ok(graph, N: int, D: int) -> bool:
     """gine_mp_fwd_mlp1 applies: D = 128, edge attributes, every in-degree within
-    GINE_MP_FUSED_MAX_DEGREE, N <= FUSED_MAX_NODES, no forward window plan.
-    GINE_MP_FUSED=0 turns it off, =all lifts the size limit (tests, experiments)."""
-    mode = os.environ.get("GINE_MP_FUSED", "1")
+    GINE_MP_FUSED_MAX_DEGREE, N <= FUSED_MAX_NODES, no forward window plan
+    (options.MP_FUSED: "0" turns it off, "all" lifts the size limit)."""
+    mode = options.MP_FUSED
     if mode == "0" or (N > FUSED_MAX_NODES and mode != "all"):
         return False
     deg = graph.max_in_degree
@@ -224,8 +224,8 @@ def fused_forward_ok(graph, N: int, D: int) -> bool:
 
 def engine_in_mp_ok(graph, D: int) -> bool:
     """gine_mp_bwd_win_mlp_wgrad applies: D = 128 and a 32-channel window plan for the
-    backward.  GINE_MLP_WGRAD_IN_MP=0 keeps the engine in the dz launch."""
-    if os.environ.get("GINE_MLP_WGRAD_IN_MP", "1") == "0" or D != 128:
+    backward (options.ENGINE_IN_MP = False keeps the engine in the dz launch)."""
+    if not options.ENGINE_IN_MP or D != 128:
         return False
     plan = graph.window_plan("out", D)
     return plan is not None and plan.slice_channels == 32
@@ -237,9 +237,9 @@ _BN_ACC = weakref.WeakKeyDictionary()
 def bn_accumulator(bn: "BnConfig", D: int, dev, kind: str = "fwd") -> "torch.Tensor | None":
     """The int64 fixed-point accumulator of gine_mlp_fwd2_bn for this BatchNorm (one per
     module and device, zeroed at allocation, then owned by the kernels), or None when the
-    finish launch is needed: eval mode, momentum=None, or GINE_BN_ACC=0."""
+    finish launch is needed: eval mode, momentum=None, or options.BN_ACC = False."""
     if (not bn.use_batch_stats or bn.momentum < 0 or bn.module is None
-            or os.environ.get("GINE_BN_ACC", "1") == "0"):
+            or not options.BN_ACC):
         return None
     per_dev = _BN_ACC.setdefault(bn.module, {})
     acc = per_dev.get((dev, kind))
@@ -341,9 +341,8 @@ class GineLayer(torch.autograd.Function):
                               lw, lb, ep, w1c, w2c, g)
         ctx.graph, ctx.epilogue = graph, epilogue
         ctx.use_batch_stats = bn.use_batch_stats
-        # backward form (GINE_BN_ACC_BWD=0 turns it off); allocated here, outside backward
-        ctx.bn_acc_bwd = (bn_accumulator(bn, D, dev, "bwd")
-                          if os.environ.get("GINE_BN_ACC_BWD", "1") != "0" else None)
+        # backward form (options.BN_ACC_BWD); allocated here, outside backward
+        ctx.bn_acc_bwd = bn_accumulator(bn, D, dev, "bwd") if options.BN_ACC_BWD else None
         ctx.params = (lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2)
         ctx.shapes = (lin_w.shape, gamma is not None)
         return y

@@ -13,7 +13,6 @@ using the buffer that every ``param.grad`` really is its slice and copies it in 
 """
 from __future__ import annotations
 
-import os
 import threading
 import weakref
 
@@ -79,9 +78,10 @@ def grad_out(param: torch.Tensor | None, shape=None, device=None) -> torch.Tenso
 # pass and run as ONE launch when the pass ends (an autograd final callback, so
 # ``param.grad`` is complete when ``backward()`` returns and before any accumulation).  Only
 # outputs that are flat-buffer slices adopted as ``param.grad`` qualify: autograd then
-# never reads them during the pass.  RAINCAST_BATCH_GRAD_FINISH=0 turns it off.
+# never reads them during the pass.  (BATCH_ENABLED = False: one finish launch per
+# reduction, the form the tests compare the batch with.)
 
-BATCH_ENABLED = os.environ.get("RAINCAST_BATCH_GRAD_FINISH", "1") != "0"
+BATCH_ENABLED = True
 _pending: list = []
 _pending_lock = threading.Lock()
 

@@ -12,19 +12,19 @@ training run the same ``edge_index`` tensor (or a handful of them) recurs every 
 from __future__ import annotations
 
 import ctypes
-import os
 from collections import OrderedDict
 
 import torch
 
-from . import _lib
+from . import _lib, options
 
 # Window-staged message passing (gine_graph_plan_windows / gine_mp_*_win): channel-slice
 # widths tried, the LDS bytes a window slice may take, and the tile size in nodes.
 WINDOW_SLICES = (32, 16, 8)
-WINDOW_ROW_BYTES = int(os.environ.get("GINE_MP_WINDOW_ROW_BYTES", 64 * 1024))
-# LDS a window workgroup may take (tuning experiments lower it to fit more workgroups per CU)
-WINDOW_LDS_BUDGET = int(os.environ.get("GINE_MP_WINDOW_LDS_BYTES", _lib.WINDOW_LDS_BYTES))
+WINDOW_ROW_BYTES = 64 * 1024
+# LDS a window workgroup may take (a smaller budget for three workgroups per CU spilled:
+# r02_s40)
+WINDOW_LDS_BUDGET = _lib.WINDOW_LDS_BYTES
 
 
 # A window launch has tiles x slices workgroups; below this many the gather kernels (one
@@ -38,17 +38,17 @@ WINDOW_MAX_STAGED = 6.0
 
 
 def window_settings() -> tuple[str, int]:
-    """(mode, max nodes per tile).  GINE_MP_WINDOW: "auto" (default) stages the backward
-    only -- measured faster than the gather kernel at cfg2, while the staged forward is
-    not --, "all" stages both directions, "0" uses the gather kernels everywhere."""
-    mode = os.environ.get("GINE_MP_WINDOW", "auto").lower()
+    """(mode, max nodes per tile).  options.MP_WINDOW: "auto" (default) stages the
+    backward only -- measured faster than the gather kernel at cfg2, while the staged
+    forward is not --, "all" stages both directions, "0" uses the gather kernels."""
+    mode = str(options.MP_WINDOW).lower()
     if mode in ("0", "off", "false", "none"):
         mode = "off"
     elif mode in ("1", "all", "on"):
         mode = "all"
     elif mode != "auto":
-        raise ValueError(f"GINE_MP_WINDOW={mode!r}: expected auto, all or 0")
-    return mode, int(os.environ.get("GINE_MP_WINDOW_NODES", "128"))
+        raise ValueError(f"options.MP_WINDOW={mode!r}: expected auto, all or 0")
+    return mode, int(options.WINDOW_NODES)
 
 
 def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device,
@@ -56,8 +56,8 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
                  slots: bool = False) -> dict:
     """slice channels -> (WindowPlan, device arrays) or None, from a host copy of one CSR.
     ``max_staged`` rejects plans staging more than that many times the node table (None:
-    keep every plan, GINE_MP_WINDOW=all).  ``slots``: add the degree-balanced work order of
-    the backward (gine_graph_plan_window_slots; GINE_MP_WINDOW_SLOTS=0 leaves it out).
+    keep every plan, MP_WINDOW "all").  ``slots``: add the degree-balanced work order of
+    the backward (gine_graph_plan_window_slots).
     Blocks on the device (a D2H copy): call outside graph capture."""
     plans = {}
     if num_nodes == 0:
@@ -65,11 +65,7 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
     rp = rowptr.cpu()
     nb = nbr.cpu()
     i32 = dict(dtype=torch.int32)
-    slices = WINDOW_SLICES
-    pref = os.environ.get("GINE_MP_WINDOW_SLICE")  # tuning experiments: force one width
-    if pref:
-        slices = (int(pref),)
-    for cs in slices:
+    for cs in WINDOW_SLICES:
         max_rows = WINDOW_ROW_BYTES // (cs * 4)
         max_edges = (WINDOW_LDS_BUDGET - max_rows * cs * 4 - (max_nodes + 1) * 4) // 8
         tb = torch.empty(num_nodes + 1, **i32)
@@ -91,7 +87,7 @@ def plan_windows(rowptr: torch.Tensor, nbr: torch.Tensor, num_nodes: int, device
         plan = _lib.WindowPlan(arrays[0].data_ptr(), arrays[1].data_ptr(), arrays[2].data_ptr(),
                                T, cs, m[0], m[1], max(m[2], 1))
         plan.edge_begin = arrays[3].data_ptr()
-        if slots and os.environ.get("GINE_MP_WINDOW_SLOTS", "1") != "0":
+        if slots:
             slot = torch.empty(num_nodes, dtype=torch.int16)
             _lib.call("gine_graph_plan_window_slots", rp.data_ptr(), tb.data_ptr(), T,
                       slot.data_ptr())

@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -103,14 +102,12 @@ def _valid_count(y: torch.Tensor, rec=None, y_orig=None) -> torch.Tensor:
     return parts
 
 
-# RAINCAST_CRPS_UNIT_GRAD=0: the backward always runs gine_crps_bwd (A/B experiments)
-UNIT_GRAD = os.environ.get("RAINCAST_CRPS_UNIT_GRAD", "1") != "0"
-# RAINCAST_CRPS_HEAD=0: the head backward always runs as its own launch (gine_head_bwd).
-# The CRPS pass that runs it takes 64 nodes per workgroup: one round of workgroups up to
+# The head backward of a unit-seeded loss runs inside the CRPS pass (gine_crps_head_fwd_grad;
+# otherwise gine_head_bwd, its own launch).  The CRPS pass that runs it takes 64 nodes per workgroup: one round of workgroups up to
 # HEAD_BWD_MAX_NODES nodes (cfg2, 16,000: one launch fewer), several rounds of the fp64 loss
 # chain above (cfg3 / cfg5 lose), so it is used up to that size.
-HEAD_BWD = os.environ.get("RAINCAST_CRPS_HEAD", "1") != "0"
-HEAD_BWD_MAX_NODES = int(os.environ.get("RAINCAST_CRPS_HEAD_MAX_NODES", "32768"))
+HEAD_BWD = True
+HEAD_BWD_MAX_NODES = 32768
 
 
 class _FusedCRPS(torch.autograd.Function):
@@ -137,7 +134,7 @@ class _FusedCRPS(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float64, device=dev)
         count = torch.empty(1, dtype=torch.float64, device=dev)
         ctx.grad_unit = None
-        if needs and N > 0 and UNIT_GRAD:
+        if needs and N > 0:
             count_in = _valid_count(y, count_rec, y_in)
             ctx.grad_unit = torch.empty(N, K, dtype=torch.float32, device=dev)
             if rec is not None:

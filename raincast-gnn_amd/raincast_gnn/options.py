@@ -1,0 +1,28 @@
+"""Engine path selection.
+
+Every value here is the measured-best default of the path it selects; the alternatives stay
+reachable because the engine needs them elsewhere (a shape the default cannot take: eval
+mode, graphs without a window plan, more than 16,384 nodes, in-degree above 32) and because
+the parity tests compare the paths with each other (tests set these attributes with
+``monkeypatch.setattr``).  Nothing reads the environment: the product path has no tuning
+switches.
+
+MP_FUSED     "1": gine_mp_fwd_mlp1 (gather + Linear1 + BN statistics in one launch) where it
+             applies (functional.fused_forward_ok); "0": never; "all": lift its size limit.
+MP_WINDOW    "auto": LDS-window message-passing backward where a plan exists and the launch
+             fills the chip; "all": every plan, both directions; "0": gather kernels only.
+WINDOW_NODES nodes per window tile.
+ENGINE_IN_MP True: the node-MLP weight-gradient engine runs inside the window backward
+             launch (gine_mp_bwd_win_mlp_wgrad); False: beside the dz GEMM.
+BN_ACC       True: BatchNorm statistics through the fixed-point accumulator (no finish
+             launch) in training mode; False: fp64 partials + finish launch.
+BN_ACC_BWD   the same for the BatchNorm backward sums.
+"""
+from __future__ import annotations
+
+MP_FUSED = "1"
+MP_WINDOW = "auto"
+WINDOW_NODES = 128
+ENGINE_IN_MP = True
+BN_ACC = True
+BN_ACC_BWD = True

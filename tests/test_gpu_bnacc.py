@@ -1,7 +1,7 @@
 """GPU: BatchNorm statistics summed by fixed-point integer atomics and finished inside the
 second node-MLP GEMM (gine_mlp_fwd1_acc / gine_mp_fwd_mlp1_acc + gine_mlp_fwd2_bn,
 csrc/gine_bnacc.hpp) against the finish-launch path (partials -> gine_bn_fwd_finalize ->
-gine_mlp_fwd2).  The layer uses it by default in training mode (GINE_BN_ACC=0 turns it
+gine_mlp_fwd2).  The layer uses it by default in training mode (options.BN_ACC = False turns it
 off), so test_gpu_parity.py's test_gine_layer_fused also checks it against the oracle.
 
 Tolerance: the fixed-point sums round each workgroup's fp64 partial to 2^-64, so mean and
@@ -14,6 +14,8 @@ import os
 import numpy as np
 import pytest
 import torch
+
+from raincast_gnn import options
 
 from helpers import knn_batch_graph
 from raincast_gnn import GINEConv, _lib, functional as Fn
@@ -64,9 +66,9 @@ def test_bn_acc_matches_finish_launch(D, epilogue, monkeypatch):
     state = {k: v.clone() for k, v in conv.state_dict().items()}
     x = torch.randn(n, D, device=DEV) * 2 + 0.5
     eid, ead = ei.to(DEV), ea.to(DEV)
-    monkeypatch.setenv("GINE_BN_ACC", "0")
+    monkeypatch.setattr(options, "BN_ACC", False)
     ref = _run(conv, state, x, eid, ead, 3, epilogue)
-    monkeypatch.setenv("GINE_BN_ACC", "1")
+    monkeypatch.setattr(options, "BN_ACC", True)
     got = _run(conv, state, x, eid, ead, 3, epilogue)
     for a, b in zip(got[0], ref[0]):   # three steps: each consumer differences against the snapshot of the last
         assert ((a - b).abs() <= TOL * (1 + b.abs())).all()
@@ -79,7 +81,7 @@ def test_bn_acc_matches_finish_launch(D, epilogue, monkeypatch):
 
 
 def test_bn_acc_deterministic(monkeypatch):
-    monkeypatch.setenv("GINE_BN_ACC", "1")
+    monkeypatch.setattr(options, "BN_ACC", True)
     ei, ea, n = knn_batch_graph(2000, 16, 4, seed=7)
     conv = _conv(128, seed=3)
     state = {k: v.clone() for k, v in conv.state_dict().items()}
@@ -93,7 +95,7 @@ def test_bn_acc_deterministic(monkeypatch):
 
 
 def test_bn_acc_eval_and_momentum_none_use_finish_launch(monkeypatch):
-    monkeypatch.setenv("GINE_BN_ACC", "1")
+    monkeypatch.setattr(options, "BN_ACC", True)
     conv = _conv(64, seed=1)
     bn = Fn.BnConfig(conv.nn[1])
     assert Fn.bn_accumulator(bn, 64, DEV) is not None
@@ -169,8 +171,8 @@ def test_bn_acc_entry_points_validate():
 def test_bn_acc_backward_matches_finish_launch(epilogue, monkeypatch):
     """gine_mlp_bwd2_acc + gine_mlp_bwd1_bn (taken with the window-plan backward, D = 128)
     against gine_mlp_bwd2 + gine_bn_bwd_finalize + gine_mlp_bwd1, over two steps."""
-    monkeypatch.setenv("GINE_MP_WINDOW", "all")
-    monkeypatch.setenv("GINE_BN_ACC_BWD", "1")
+    monkeypatch.setattr(options, "MP_WINDOW", "all")
+    monkeypatch.setattr(options, "BN_ACC_BWD", True)
     ei, ea, n = knn_batch_graph(500, 10, 4, seed=11)
     conv = _conv(128, seed=5)
     state = {k: v.clone() for k, v in conv.state_dict().items()}
@@ -180,7 +182,7 @@ def test_bn_acc_backward_matches_finish_launch(epilogue, monkeypatch):
     fn = {"none": "forward", "relu": "forward_relu", "residual": "forward_residual_relu"}
     grads = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("GINE_BN_ACC", mode)
+        monkeypatch.setattr(options, "BN_ACC", mode == "1")
         conv.load_state_dict(state)
         out = []
         for _ in range(2):
@@ -323,7 +325,7 @@ def test_bn_acc_pairing_break_gives_nan_then_recovers():
 def test_bn_acc_backward_small_gradients(monkeypatch):
     """Gradients of order 1e-10 (the ADVICE case): the backward accumulator's 2^-64
     resolution keeps them within 1e-5 (max-norm relative) of the fp64-partials path."""
-    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    monkeypatch.setattr(options, "MP_WINDOW", "all")
     ei, ea, n = knn_batch_graph(500, 10, 4, seed=12)
     conv = _conv(128, seed=6)
     state = {k: v.clone() for k, v in conv.state_dict().items()}
@@ -332,7 +334,7 @@ def test_bn_acc_backward_small_gradients(monkeypatch):
     dy = torch.randn(n, 128, device=DEV) * 1e-10
     grads = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("GINE_BN_ACC_BWD", mode)
+        monkeypatch.setattr(options, "BN_ACC_BWD", mode == "1")
         conv.load_state_dict(state)
         conv.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)

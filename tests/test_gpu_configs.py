@@ -29,6 +29,8 @@ import copy
 import pytest
 import torch
 
+from raincast_gnn import options
+
 from helpers import check_training_step, engine_order_batch
 from raincast_gnn.data import synthetic_batch
 from raincast_gnn.params import BENCH_CONFIGS
@@ -75,7 +77,7 @@ def test_full_size_step_deterministic_and_fused_equal(cfg, monkeypatch):
     assert batch.num_nodes == c.num_stations * c.graphs_per_gpu
 
     def run(mode):
-        monkeypatch.setenv("GINE_MP_FUSED", mode)
+        monkeypatch.setattr(options, "MP_FUSED", mode)
         return _grads_after_step(copy.deepcopy(base), batch)
 
     l0, g0 = run("1")       # what the training step runs at this size

@@ -13,6 +13,8 @@ import numpy as np
 import pytest
 import torch
 
+from raincast_gnn import options
+
 from raincast_gnn import _lib, functional as Fn
 from raincast_gnn.graph import GineGraph
 
@@ -46,7 +48,7 @@ CASES = [(s, n, d) for s, (n, d) in enumerate(
 @pytest.mark.parametrize("seed,n,max_deg", CASES)
 @pytest.mark.parametrize("flag", [0, _lib.GINE_MP_LIN_MULADD], ids=["fma", "muladd"])
 def test_fused_forward_fuzz(seed, n, max_deg, flag, monkeypatch):
-    monkeypatch.setenv("GINE_MP_FUSED", "all")
+    monkeypatch.setattr(options, "MP_FUSED", "all")
     ei, ea = _graph(1000 + seed, n, max_deg)
     g = GineGraph(ei.to(DEV), ea.to(DEV), n)
     torch.manual_seed(seed)
@@ -75,7 +77,7 @@ def test_fused_forward_fuzz(seed, n, max_deg, flag, monkeypatch):
 @pytest.mark.parametrize("seed,n,max_deg", [c for c in CASES if c[1] >= 33])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_combined_backward_fuzz(seed, n, max_deg, epi, monkeypatch):
-    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    monkeypatch.setattr(options, "MP_WINDOW", "all")
     ei, ea = _graph(2000 + seed, n, max_deg, local=150)
     g = GineGraph(ei.to(DEV), ea.to(DEV), n)
     plan = g.window_plan("out", D)

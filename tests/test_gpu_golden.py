@@ -12,6 +12,8 @@ import numpy as np
 import pytest
 import torch
 
+from raincast_gnn import options
+
 from conftest import GOLDEN
 from helpers import rel_err
 from raincast_gnn import GINEConv, _lib, functional as Fn
@@ -32,7 +34,7 @@ def t(key):
 @pytest.mark.parametrize("window", ["0", "all"])
 @pytest.mark.parametrize("name", CASES)
 def test_mp_matches_golden(name, window, monkeypatch):
-    monkeypatch.setenv("GINE_MP_WINDOW", window)
+    monkeypatch.setattr(options, "MP_WINDOW", window)
     p = f"mp/{name}/"
     x = t(p + "x").to(DEV)
     ei, ea = t(p + "edge_index"), t(p + "edge_attr")

@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 import torch
 
+from raincast_gnn import options
+
 from helpers import (assert_close_tiebreak, check_training_step, knn_batch_graph, random_graph,
                      rel_err, special_graphs)
 from oracle import gine_cpu as O
@@ -128,10 +130,10 @@ def test_mp_window_path_matches_gather_and_oracle(case, D, tile_nodes, monkeypat
     """LDS-staged window kernels (gine_mp_*_win) vs the gather kernels and the oracle:
     z and dx bit-identical, the parameter reductions at fp32 tolerance."""
     _, ei, ea, n = case
-    monkeypatch.setenv("GINE_MP_WINDOW_NODES", str(tile_nodes))
-    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    monkeypatch.setattr(options, "WINDOW_NODES", str(tile_nodes))
+    monkeypatch.setattr(options, "MP_WINDOW", "all")
     gw = GineGraph(ei.to(DEV), ea.to(DEV), n)
-    monkeypatch.setenv("GINE_MP_WINDOW", "0")
+    monkeypatch.setattr(options, "MP_WINDOW", "0")
     gg = GineGraph(ei.to(DEV), ea.to(DEV), n)
     assert gg.window_plan("in", D) is None and gg.window_plan("out", D) is None
     plan_in, plan_out = gw.window_plan("in", D), gw.window_plan("out", D)
@@ -174,9 +176,7 @@ def test_mp_window_path_matches_gather_and_oracle(case, D, tile_nodes, monkeypat
 
 def test_mp_window_auto_policy(monkeypatch):
     """Default mode: the backward is staged when the launch has >= 256 workgroups, the
-    forward keeps the gather kernel; GINE_MP_WINDOW=0 disables staging."""
-    monkeypatch.delenv("GINE_MP_WINDOW", raising=False)
-    monkeypatch.delenv("GINE_MP_WINDOW_NODES", raising=False)
+    forward keeps the gather kernel; options.MP_WINDOW "0" disables staging."""
     ei, ea, n = knn_batch_graph(500, 10, 32, seed=0)
     g = GineGraph(ei.to(DEV), ea.to(DEV), n)
     assert g.window_plan("in", 128) is None
@@ -185,10 +185,10 @@ def test_mp_window_auto_policy(monkeypatch):
     ei1, ea1, n1 = knn_batch_graph(500, 10, 1, seed=0)
     g1 = GineGraph(ei1.to(DEV), ea1.to(DEV), n1)
     assert g1.window_plan("out", 128) is None      # 4 tiles x 4 slices: too few
-    monkeypatch.setenv("GINE_MP_WINDOW", "0")
+    monkeypatch.setattr(options, "MP_WINDOW", "0")
     g0 = GineGraph(ei.to(DEV), ea.to(DEV), n)
     assert g0.window_plan("out", 128) is None
-    monkeypatch.setenv("GINE_MP_WINDOW", "bogus")
+    monkeypatch.setattr(options, "MP_WINDOW", "bogus")
     with pytest.raises(ValueError):
         GineGraph(ei.to(DEV), ea.to(DEV), n)
 
@@ -481,7 +481,7 @@ def _fused_cases():
 def test_mp_fwd_mlp1_fused_matches_unfused(case, rounding, monkeypatch):
     """One-launch gather + Linear1 + BN partials == gine_mp_fwd then gine_mlp_fwd1, bit for
     bit (z, a1 and every partial row); above the degree limit it refuses."""
-    monkeypatch.setenv("GINE_MP_FUSED", "all")
+    monkeypatch.setattr(options, "MP_FUSED", "all")
     _, ei, ea, n = case
     D = 128
     g = GineGraph(ei.to(DEV), ea.to(DEV), n)
@@ -540,7 +540,7 @@ def test_layer_fused_forward_equals_unfused(monkeypatch):
     assert n <= Fn.FUSED_MAX_NODES
     outs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("GINE_MP_FUSED", flag)
+        monkeypatch.setattr(options, "MP_FUSED", flag)
         torch.manual_seed(0)
         net = ResGnn(128, 128, 2, 128).to(DEV).train()
         x = torch.randn(n, 128, device=DEV, requires_grad=True)

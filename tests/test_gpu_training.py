@@ -5,6 +5,8 @@ import copy
 import pytest
 import torch
 
+from raincast_gnn import options
+
 from helpers import rel_err
 from oracle import gine_cpu as O
 from raincast_gnn.models import DeepSetEncoder
@@ -269,7 +271,7 @@ def test_mlp_weight_grads_in_message_passing_launch(monkeypatch):
     batch = synthetic_batch(500, 32, k=10, seed=5).to(DEV)   # window backward active
     grads = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("GINE_MLP_WGRAD_IN_MP", flag)
+        monkeypatch.setattr(options, "ENGINE_IN_MP", flag == "1")
         m = copy.deepcopy(base).to(DEV)
         opt = FlatAdamW(m.parameters(), lr=1e-3)
         opt.zero_grad()
@@ -285,17 +287,17 @@ def test_mlp_weight_grads_in_message_passing_launch(monkeypatch):
 @pytest.mark.parametrize("graphs,stations,k", [(1, 64, 4), (3, 500, 10), (2, 37, 36)])
 def test_mlp_weight_grads_in_mp_launch_small_graphs(graphs, stations, k, monkeypatch):
     """The combined launch at sizes where the engine has few row chunks and the window plan
-    is forced (GINE_MP_WINDOW=all): same gradients as the engine beside the dz GEMM."""
+    is forced (options.MP_WINDOW "all"): same gradients as the engine beside the dz GEMM."""
     from raincast_gnn import functional as Fn
     from raincast_gnn.data import synthetic_batch
     from raincast_gnn.models import GNN
-    monkeypatch.setenv("GINE_MP_WINDOW", "all")
+    monkeypatch.setattr(options, "MP_WINDOW", "all")
     torch.manual_seed(graphs + stations)
     base = GNN(35, 128, 128, 2, loss="MixedLoss", grad_u="False", u=1.71, xi=0.5)
     batch = synthetic_batch(stations, graphs, k=k, seed=6).to(DEV)
     grads = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("GINE_MLP_WGRAD_IN_MP", flag)
+        monkeypatch.setattr(options, "ENGINE_IN_MP", flag == "1")
         m = copy.deepcopy(base).to(DEV)
         opt = FlatAdamW(m.parameters(), lr=1e-3)
         opt.zero_grad()
