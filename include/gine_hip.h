@@ -189,7 +189,7 @@ int gine_mp_bwd_win_side(const float* dz, const float* x, const int32_t* out_row
                          int32_t mlp_channels, float* dw1, float* db1, float* dw2, float* db2,
                          void* stream);
 /* gine_mp_bwd_win + the node-MLP weight-gradient engine of the same GINE layer in ONE launch
- * (D = 128, slice_channels = 32): extra workgroups write the fp32 slab
+ * (D = 64 or 128, slice_channels = 32): extra workgroups write the fp32 slab
  * [2][gine_mlp_wgrad_num_chunks][D*D + D] exactly as gine_mlp_wgrad does with NULL outputs
  * (operands dy, y, mask, a1, bn_save, dbn, coef, z, epilogue as for gine_mlp_wgrad), while
  * the window workgroups run the message-passing backward; the slab is then reduced by

@@ -239,6 +239,7 @@ struct WinEngine {
   int64_t N;
   size_t zstride, cstride;
   int nblocks, tiles, rows_per_chunk;
+  int D;  // node-MLP width (64 or 128): the engine's O = I
 };
 constexpr size_t kWinEngineLds = sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
 
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
       float* sP = reinterpret_cast<float*>(s_dyn);
       float* sQ = sP + kWgRows * (64 + 4);
       const int e = xcd_remap(blockIdx.x, eng.nblocks);
-      wgrad_block<MlpWgradSrc<PDO>, 64, 8>(eng.src, eng.N, 128, 128, e / eng.tiles,
+      wgrad_block<MlpWgradSrc<PDO>, 64, 8>(eng.src, eng.N, eng.D, eng.D, e / eng.tiles,
                                            e % eng.tiles, eng.rows_per_chunk, eng.zstride,
                                            eng.cstride, eng.slab, sP, sQ);
       return;
@@ -551,8 +552,9 @@ int mp_bwd_win_launch(const float* dz, const float* x, const int32_t* out_rowptr
   const size_t jobb = job.nblocks > 0 ? sizeof(double) * kSlabGroups * (kSlabQuads * 4 + 1) : 0;
   smem = smem > red ? smem : red;
   smem = smem > jobb ? smem : jobb;
-  if (eng) {  // the engine: D = 128, 32-channel slices, no slab side job in the same launch
-    if (channels != 128 || cs != 32 || job.nblocks != 0 || eng->nblocks <= 0)
+  if (eng) {  // the engine: D = 64 / 128, 32-channel slices, no slab side job in the launch
+    if ((channels != 128 && channels != 64) || eng->D != channels || cs != 32 ||
+        job.nblocks != 0 || eng->nblocks <= 0)
       return GINE_ERR_INVALID;
     smem = smem > kWinEngineLds ? smem : kWinEngineLds;
   }
@@ -746,7 +748,7 @@ extern "C" int gine_mp_bwd_win_mlp_wgrad(
   if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
-  if (channels != 128) return GINE_ERR_DIM;
+  if (channels != 128 && channels != 64) return GINE_ERR_DIM;
   static_assert(kMlpWgTO == 64, "the fused engine runs 64-row output tiles");
   const int D = channels;
   const WgPlan p = wg_plan(num_nodes, D, D, 2, kMlpWgTO);  // = gine_mlp_wgrad's plan
@@ -760,7 +762,7 @@ extern "C" int gine_mp_bwd_win_mlp_wgrad(
 #define MP_ENG(PD)                                                                           \
   do {                                                                                       \
     const WinEngine<PD> e{MlpWgradSrc<PD>{p_do, q_r, p_da1, q_z, D}, slab, num_nodes,        \
-                          per * p.chunks, per, p.chunks * tiles, tiles, p.rows_per_chunk};   \
+                          per * p.chunks, per, p.chunks * tiles, tiles, p.rows_per_chunk, D};\
     return mp_bwd_win_launch<PD>(dz, x, out_rowptr, out_dst, out_attr, lin_w, lin_b, eps,    \
                                  dres, dx, partials, num_nodes, channels, flags, plan, none,  \
                                  &e, stream);                                                \

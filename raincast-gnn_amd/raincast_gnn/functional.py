@@ -223,9 +223,9 @@ def fused_forward_ok(graph, N: int, D: int) -> bool:
 
 
 def engine_in_mp_ok(graph, D: int) -> bool:
-    """gine_mp_bwd_win_mlp_wgrad applies: D = 128 and a 32-channel window plan for the
-    backward (options.ENGINE_IN_MP = False keeps the engine in the dz launch)."""
-    if not options.ENGINE_IN_MP or D != 128:
+    """gine_mp_bwd_win_mlp_wgrad applies: D = 64 or 128 and a 32-channel window plan for
+    the backward (options.ENGINE_IN_MP = False keeps the engine in the dz launch)."""
+    if not options.ENGINE_IN_MP or D not in (64, 128):
         return False
     plan = graph.window_plan("out", D)
     return plan is not None and plan.slice_channels == 32

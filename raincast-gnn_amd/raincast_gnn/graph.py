@@ -29,7 +29,8 @@ WINDOW_LDS_BUDGET = _lib.WINDOW_LDS_BYTES
 
 # A window launch has tiles x slices workgroups; below this many the gather kernels (one
 # workgroup per 8 nodes) fill the chip better (measured: cfg1, 4 tiles, is slower staged).
-WINDOW_MIN_WORKGROUPS = 256
+# (The D = 64 sweep point, 125 tiles x 2 slices of 32 channels, is above it.)
+WINDOW_MIN_WORKGROUPS = 200
 # A plan whose windows together stage more than this many times the node table loses to
 # the gather kernels (measured r02_s11: cfg5's 10,000-station k=32 graph in locality order
 # plans 16-channel windows staging 10.8x the table, 186 us vs 118 us gathered; cfg2 in the

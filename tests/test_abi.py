@@ -104,4 +104,5 @@ def test_fused_entry_points_validate_without_device():
     assert g(*args, 2, None) == 1                                          # empty plan
     assert g(*([p] * 11 + [100, 128, 1, ctypes.byref(plan)] + [None] + [p] * 8), 2, None) == 1
     assert g(*args, 7, None) == 1                                          # bad epilogue
-    assert g(*([p] * 11 + [100, 64, 1, ctypes.byref(plan)] + [p] * 9), 2, None) == 2
+    assert g(*([p] * 11 + [100, 32, 1, ctypes.byref(plan)] + [p] * 9), 2, None) == 2  # D 32
+    assert g(*([p] * 11 + [100, 64, 1, ctypes.byref(plan)] + [p] * 9), 2, None) == 1  # D 64

@@ -59,6 +59,32 @@ def test_training_step_matches_oracle_at_config(cfg, graphs, relabel):
           f"{worst:.2e}")
 
 
+@pytest.mark.parametrize("relabel", [False, True], ids=["dataset-order", "relabel"])
+def test_training_step_matches_oracle_at_cfg2_d64(relabel):
+    """The D = 64 sweep point of the 24h_mixed benchmark (BASELINE.md:47, the north star's
+    64-dim features) at full size: 32 x 500 stations, gnn_hidden = 64.  In the locality
+    order the window backward carries the node-MLP weight-gradient engine (32-channel
+    slices: 2 per tile) and the BatchNorm backward sums go through the accumulator."""
+    c = BENCH_CONFIGS[2].with_hidden(64)
+    params = c.params()
+    assert params["gnn_hidden"] == 64
+    batch = synthetic_batch(c.num_stations, c.graphs_per_gpu, k=c.k, seed=102)
+    worst = check_training_step(params, batch, DEV, TOL, envelope_threads=(1, 2, 4),
+                                relabel=relabel)
+    print(f"{c.name} relabel={relabel}: worst grad rel err vs fp32 oracle {worst:.2e}")
+
+
+def test_cfg2_d64_uses_the_combined_backward():
+    from raincast_gnn import functional as Fn
+    from raincast_gnn.graph import GineGraph
+    c = BENCH_CONFIGS[2]
+    b = engine_order_batch(synthetic_batch(c.num_stations, c.graphs_per_gpu, k=c.k, seed=1))
+    g = GineGraph(b.edge_index.to(DEV), b.edge_attr.to(DEV), b.num_nodes)
+    plan = g.window_plan("out", 64)
+    assert plan is not None and plan.slice_channels == 32
+    assert Fn.engine_in_mp_ok(g, 64)
+
+
 def _grads_after_step(model, batch):
     model.zero_grad(set_to_none=True)
     loss = model.loss_fn.crps(model(batch), batch.y)
@@ -145,14 +171,15 @@ def test_relabelled_batch_gives_the_same_per_node_bits_in_eval():
         assert torch.equal(restore_node_order(m(got), got), m(ref))
 
 
-@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
-def test_relabelled_full_size_step_deterministic_and_close(cfg):
+@pytest.mark.parametrize("cfg,hidden", [(2, None), (2, 64), (3, None), (4, None), (5, None)],
+                         ids=["cfg2", "cfg2-D64", "cfg3", "cfg4", "cfg5"])
+def test_relabelled_full_size_step_deterministic_and_close(cfg, hidden):
     """The benchmark's batch (full size, engine order) against the same batch in the
     reference order on the engine: both steps finite and deterministic; the loss and the
     predictions equal within 1e-5 (only the order of node reductions differs)."""
     from raincast_gnn.data import restore_node_order
     from raincast_gnn.models import gnn_from_params
-    c = BENCH_CONFIGS[cfg]
+    c = BENCH_CONFIGS[cfg].with_hidden(hidden)
     torch.manual_seed(42)
     base = gnn_from_params(c.params()).to(DEV).train()
     batch = synthetic_batch(c.num_stations, c.graphs_per_gpu, k=c.k, seed=1000)
