@@ -18,6 +18,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from raincast_gnn import functional as Fn  # noqa: E402
+from raincast_gnn import graph as G, options  # noqa: E402
 from raincast_gnn.graph import GineGraph  # noqa: E402
 from helpers import knn_batch_graph  # noqa: E402
 
@@ -103,14 +104,14 @@ def main():
         lw, lb = torch.randn(D, device=dev), torch.randn(D, device=dev)
         eps = torch.tensor([0.1], device=dev)
         bf = 4 * (2 * N * D + 2 * E + N + 1)
-        bb = 4 * (3 * N * D + 2 * E + N + 1) + 4 * N * D
+        bb = 4 * (3 * N * D + 2 * E + N + 1)   # SURVEY 8(d) B_b
         variants = [("gather", "0", 128)] + [(f"win{t}", "all", t)
-                                             for t in (int(v) for v in args.tiles.split(","))]
+                                             for t in (int(v) for v in args.tiles.split(",") if v)]
         for name, on, tiles in variants:
-            os.environ["GINE_MP_WINDOW"] = on
-            os.environ["GINE_MP_WINDOW_NODES"] = str(tiles)
+            options.MP_WINDOW = on
+            options.WINDOW_NODES = tiles
             if args.slice:
-                os.environ["GINE_MP_WINDOW_SLICE"] = str(args.slice)
+                G.WINDOW_SLICES = (args.slice,)
             g = GineGraph(ei, ea, N)
             plan = g.window_plan("in", D)
             if on == "all" and plan is None:
