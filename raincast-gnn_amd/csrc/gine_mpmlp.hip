@@ -169,10 +169,16 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
 #pragma unroll
     for (int q = 0; q < (GINE_FUSED_DBG == 2 ? 1 : kKS / 4); ++q) {
       const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
+      if constexpr (GINE_BF16_PROBE) {
+        if (q % 2 == 1)
+          acc = probe6(a4, make_float4(bf[4 * q], bf[4 * q + 1], bf[4 * q + 2], bf[4 * q + 3]),
+                       acc);
+      } else {
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+      }
     }
     // this wave's 32x32 block -> row-major through its own LDS tile
 #pragma unroll
