@@ -72,11 +72,12 @@ def parse():
                          "default cfg2 run adds")
     ap.add_argument("--allreduce", choices=("graph", "split"), default="split",
                     help="split (default): fwd+bwd graph, the RCCL all-reduce launched "
-                         "between it and the optimizer graph -- the step stays GPU-bound "
-                         "(0.5 ms of device work against tens of us of host launches), so "
-                         "this costs nothing measurable and keeps multi-rank runs off the "
-                         "collective-capture path; graph: the all-reduce captured inside the "
-                         "step's HIP graph (RCCL only; a failed capture exits non-zero)")
+                         "between it and the optimizer graph -- keeps multi-rank runs off "
+                         "the collective-capture path, which has never run with more than "
+                         "one rank; costs the two cross-stream hops of an eager collective "
+                         "(0.548 vs 0.534 ms per cfg2 step at world 1, profiles/r03_s08); "
+                         "graph: the all-reduce captured inside the step's HIP graph (RCCL "
+                         "only; a failed capture exits non-zero)")
     ap.add_argument("--station-order", choices=("locality", "dataset"), default="locality",
                     help="locality: the batch in the engine's station order (reverse "
                          "Cuthill-McKee, raincast_gnn.data.station_order -- the device "
