@@ -44,12 +44,28 @@ import torch.nn.functional as F
 # ---------------------------------------------------------------------------------------
 
 
-def gine_aggregate(x, edge_index, edge_attr, lin_w, lin_b, eps):
+def tie_relu(v, decide=None):
+    """relu(v); with ``decide`` = (on, band, log): where |v| <= band * max|v| -- a decision
+    within fp32 rounding of zero, which any fp32 implementation may take either way -- the
+    boolean ``on`` (another implementation's decision) is taken instead of v > 0, and the
+    number of decisions that differ from v > 0 is appended to ``log``.  The tie-break
+    oracle of tests/helpers.check_training_step: the exact gradient on the engine's side
+    of each such tie."""
+    if decide is None:
+        return v.relu()
+    on, band, log = decide
+    amb = v.abs() <= band * v.abs().max()
+    keep = torch.where(amb, on.to(v.device), v > 0)
+    log.append(int((keep != (v > 0)).sum()))
+    return v * keep.to(v.dtype)
+
+
+def gine_aggregate(x, edge_index, edge_attr, lin_w, lin_b, eps, decide=None):
     """z = scatter_add(relu(x[src] + lin(a)), dst) + (1 + eps) * x  (PyG op sequence)."""
     src, dst = edge_index[0], edge_index[1]
     x_j = x.index_select(0, src)
     e = F.linear(edge_attr.reshape(-1, lin_w.size(1)), lin_w, lin_b)
-    m = (x_j + e).relu()
+    m = tie_relu(x_j + e, decide)
     agg = x.new_zeros(x.size(0), m.size(1)).scatter_add_(0, dst.view(-1, 1).expand_as(m), m)
     return agg + (1 + eps) * x
 
@@ -97,16 +113,25 @@ class OracleGINEConv(nn.Module):
         self.eps.data.fill_(eps)
 
     record = None  # tests may set a list: (x, d z) pairs are appended during backward
+    decide = None  # tests may set {"msg" | "bn" | "res": (on, band, log)} (see tie_relu)
+
+    def _decide(self, key):
+        return None if self.decide is None else self.decide.get(key)
 
     def aggregate(self, x, edge_index, edge_attr):
-        z = gine_aggregate(x, edge_index, edge_attr, self.lin.weight, self.lin.bias, self.eps)
+        z = gine_aggregate(x, edge_index, edge_attr, self.lin.weight, self.lin.bias, self.eps,
+                           self._decide("msg"))
         if self.record is not None and z.requires_grad:
             xd = x.detach()
             z.register_hook(lambda g: self.record.append((xd, g.detach())))
         return z
 
     def forward(self, x, edge_index, edge_attr):
-        return self.nn(self.aggregate(x, edge_index, edge_attr))
+        z = self.aggregate(x, edge_index, edge_attr)
+        if self._decide("bn") is None:
+            return self.nn(z)
+        l1, bn, _, l2 = self.nn
+        return l2(tie_relu(bn(l1(z)), self._decide("bn")))
 
 
 class OracleResGnn(nn.Module):
@@ -128,7 +153,7 @@ class OracleResGnn(nn.Module):
         x = x.to(dt)
         edge_attr = edge_attr.to(dt)
         for i, conv in enumerate(self.convolutions):
-            h = self.relu(conv(x, edge_index, edge_attr))
+            h = tie_relu(conv(x, edge_index, edge_attr), conv._decide("res"))
             x = h if i == 0 else x + h
         return x
 

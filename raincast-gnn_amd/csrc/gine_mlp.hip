@@ -26,6 +26,7 @@
 #include "gine_wgrad.hpp"
 #include "gine_mlpsrc.hpp"
 #include "gine_bnacc.hpp"
+#include "gine_bf16x3.hpp"
 
 #include <algorithm>
 #include <type_traits>
@@ -121,6 +122,15 @@ __device__ __forceinline__ TileRange xcd_tile_range(int num_tiles, int vb, int n
 // ----------------------------------------------------------------------------------------
 // One persistent workgroup (virtual index vb of vgrid) of the row-tile GEMM; s_x: LDS of
 // kRowTile * (D + 4) floats.
+// The fp32 re-do of a non-finite tile (gine_bf16x3.hpp) with the lane's B fragment read
+// from W: W^T fragment (BT / WL: b[s] = W[col][h*KS + s]) or W fragment (b[s] = W[h*KS + s][col]).
+template <int D, int KS, bool BT>
+__device__ __forceinline__ floatx16 redo_fp32(const float* arow, const float* __restrict__ W,
+                                              int col, int h) {
+  return BT ? mfma_f32_row_mem<KS>(arow, W + (size_t)col * D + h * KS, 1, zero16())
+            : mfma_f32_row_mem<KS>(arow, W + (size_t)h * KS * D + col, D, zero16());
+}
+
 struct NoHook {
   __device__ void operator()() const {}
 };
@@ -231,6 +241,8 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
     hook();
     kc = col_const<PRO>(pa, D, q_me);
   }
+  BPlanes<KS> bp;
+  if constexpr (GINE_BF16X3_BODY && KS <= 64) bp.from(bf);
   for (int tile = tr.first; tile < tr.end; tile += tr.step) {
     const int64_t n0 = (int64_t)tile * kRowTile;
     RG_MARK(1);
@@ -257,13 +269,16 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
     RG_MARK(2);
     floatx16 acc = zero16();
     const float* arow = &s_x[c32 * LD + h * KS];
+    if constexpr (GINE_BF16X3_BODY && KS <= 64) {
 #pragma unroll
-    for (int q = 0; q < KS / 4; ++q) {
-      const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+      for (int s = 0; s < KS / 8; ++s) {
+        const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);
+        const float4 a1 = *reinterpret_cast<const float4*>(&arow[8 * s + 4]);
+        acc = mfma_bf16x3(split8(a0, a1), bp.f[s], acc);
+      }
+      if (wave_any_nan(acc)) acc = redo_fp32<D, KS, BT || WL>(arow, W, col, h);
+    } else {
+      acc = mfma_f32_row<KS>(arow, bf, acc);
     }
 #ifdef GINE_RG_PROFILE
     if (acc[0] == 1.2345e-30f) s_x[0] = 0.f;  // the stamp below waits for the chain
@@ -569,6 +584,8 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
       hook();
       kc = col_const<PRO>(pa, D, q_me);
     }
+    BPlanes<KS> bp;
+    if constexpr (GINE_BF16X3_PIPE && KS <= 64) bp.from(bf);
     __syncthreads();  // W^T fragment reads (WL) are done before the A buffers overwrite them
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) stage_item(tile_of(0), raw[i], i, s_lds);
@@ -587,19 +604,19 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
       // each step's A fragment is read one step ahead (the step boundaries are scheduling
       // barriers: a read issued in the same step would expose the LDS latency every step)
       float4 a4 = *reinterpret_cast<const float4*>(&arow[0]);
+      float4 aprev = a4;  // (split-bf16: the even step's four k values, used by the odd step)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const float4 an =
             *reinterpret_cast<const float4*>(&arow[4 * (q + 1 < NQ ? q + 1 : q)]);
-        if constexpr (GINE_BF16_PROBE) {
-          if (q % 2 == 1)
-            acc = probe6(a4, make_float4(bf[4 * q], bf[4 * q + 1], bf[4 * q + 2], bf[4 * q + 3]),
-                         acc);
+        if constexpr (GINE_BF16X3_PIPE && KS <= 64) {
+          if (q % 2 == 0) aprev = a4;
+          else acc = mfma_bf16x3(split8(aprev, a4), bp.f[q / 2], acc);
         } else {
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
         }
         if (q == 0 && EPI_ON) acc_to_lds(accp);
         if (q == Q_STAGE0) {
@@ -621,6 +638,9 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
         __builtin_amdgcn_sched_barrier(0);
         a4 = an;
       }
+      // (the A buffer of tile k stays until the barrier before chain k + 1)
+      if constexpr (GINE_BF16X3_PIPE && KS <= 64)
+        if (wave_any_nan(acc)) acc = redo_fp32<D, KS, BT || WL>(arow, W, col, h);
       return acc;
     };
 

@@ -28,6 +28,7 @@
 #include "gine_common.hpp"
 #include "gine_bnacc.hpp"
 #include "gine_edge.hpp"
+#include "gine_bf16x3.hpp"
 
 namespace gine {
 namespace {
@@ -156,6 +157,8 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
       bf[4 * q + 3] = v.w;
     }
   }
+  BPlanes<kKS> bp;
+  if constexpr (GINE_BF16X3_FUSED) bp.from(bf);
   __syncthreads();  // (iteration 0: the gather role stages the first tile)
   double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
   const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
@@ -166,18 +169,27 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
     floatx16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    if constexpr (GINE_BF16X3_FUSED) {  // the row-tile GEMM's split-bf16 chain (gine_mlp.hip)
 #pragma unroll
-    for (int q = 0; q < (GINE_FUSED_DBG == 2 ? 1 : kKS / 4); ++q) {
-      const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
-      if constexpr (GINE_BF16_PROBE) {
-        if (q % 2 == 1)
-          acc = probe6(a4, make_float4(bf[4 * q], bf[4 * q + 1], bf[4 * q + 2], bf[4 * q + 3]),
-                       acc);
-      } else {
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+      for (int s = 0; s < (GINE_FUSED_DBG == 2 ? 1 : kKS / 8); ++s) {
+        const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);
+        const float4 a1 = *reinterpret_cast<const float4*>(&arow[8 * s + 4]);
+        acc = mfma_bf16x3(split8(a0, a1), bp.f[s], acc);
+      }
+      if (wave_any_nan(acc)) {  // non-finite operands: the fp32 chain (gine_bf16x3.hpp)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        acc = mfma_f32_row_mem<kKS>(arow, A.W1 + (size_t)(32 * wave + c32) * kD + h * kKS, 1,
+                                    acc);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < (GINE_FUSED_DBG == 2 ? 1 : kKS / 4); ++q) {
+        const float4 a4 = *reinterpret_cast<const float4*>(&arow[4 * q]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bf[4 * q], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
       }
     }
     // this wave's 32x32 block -> row-major through its own LDS tile
