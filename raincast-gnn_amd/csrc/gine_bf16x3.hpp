@@ -10,24 +10,24 @@
 // each exact in the fp32 accumulator's products, accumulated in fp32: the dropped terms
 // (am.bl, al.bm, al.bl) are below 2^-24 |a||b|, the fp32 rounding of a single product -- an
 // fp32 GEMM's accuracy at 6 bf16 MFMAs (192 cycles) per K = 16 instead of 8 fp32 MFMAs (512
-// cycles).  Every kernel that must agree bit for bit with another (fused vs unfused node-MLP
-// GEMMs, the weight-gradient engine in either launch) uses these helpers with the same k
-// permutation, so the agreements hold.
+// cycles).  The fused and the unfused node-MLP Linear1 (gine_mpmlp.hip matrix role,
+// gine_mlp.hip row-tile GEMM) must agree bit for bit: both use these helpers with the same
+// k permutation.
+//
+// Where it is used: the row-tile GEMMs (weights split once per workgroup, the A fragment
+// split as it is read) and the fused forward's matrix chain.  Not in the weight-gradient
+// engine (gine_wgrad.hpp): there both operands stream through LDS, every wave re-splits
+// what it reads, and at one wave per SIMD the split's VALU work serialises with the MFMA
+// chain -- measured slower than the fp32 engine (cfg2 0.5536 / 0.5445 vs 0.5489 / 0.5354 ms
+// even at 4 waves per SIMD; cfg3 2.86 / 2.88 vs 2.84 / 2.84; profiles/r03_s12_*).
 #pragma once
 
 #include "gine_common.hpp"
 
+// GINE_GEMM_BF16X3=0 (A/B builds: make fullvariant V=fp32gemm VDEFS=-DGINE_GEMM_BF16X3=0)
+// keeps the fp32 chains everywhere.
 #ifndef GINE_GEMM_BF16X3
 #define GINE_GEMM_BF16X3 1
-#endif
-#ifndef GINE_BF16X3_BODY
-#define GINE_BF16X3_BODY GINE_GEMM_BF16X3
-#endif
-#ifndef GINE_BF16X3_PIPE
-#define GINE_BF16X3_PIPE GINE_GEMM_BF16X3
-#endif
-#ifndef GINE_BF16X3_FUSED
-#define GINE_BF16X3_FUSED GINE_GEMM_BF16X3
 #endif
 
 namespace gine {

@@ -63,22 +63,6 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// Timing probe only (make fullvariant VDEFS=-DGINE_BF16_PROBE=1): the fp32 MFMA chains
-// replaced by 6 bf16 32x32x16 MFMAs per 16 k on reinterpreted operands -- the cost of a
-// three-way split-bf16 chain, results meaningless.
-#ifndef GINE_BF16_PROBE
-#define GINE_BF16_PROBE 0
-#endif
-typedef __bf16 gine_bf16x8 __attribute__((ext_vector_type(8)));
-typedef float gine_f32x16 __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ gine_f32x16 probe6(float4 a, float4 b, gine_f32x16 acc) {
-  const gine_bf16x8 av = __builtin_bit_cast(gine_bf16x8, a);
-  const gine_bf16x8 bv = __builtin_bit_cast(gine_bf16x8, b);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
-  return acc;
-}
-
 // Non-NaN targets of y [n] as GINE_COUNT_PARTS uint32 partial counts (part p counts the
 // contiguous range p * ceil(n / P) ...), written by the workgroups of the calling launch:
 // workgroup b writes parts b, b + gridDim.x, ...  Blocks of exactly 256 threads.  Integer

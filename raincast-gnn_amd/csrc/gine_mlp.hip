@@ -242,7 +242,7 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
     kc = col_const<PRO>(pa, D, q_me);
   }
   BPlanes<KS> bp;
-  if constexpr (GINE_BF16X3_BODY && KS <= 64) bp.from(bf);
+  if constexpr (GINE_GEMM_BF16X3 && KS <= 64) bp.from(bf);
   for (int tile = tr.first; tile < tr.end; tile += tr.step) {
     const int64_t n0 = (int64_t)tile * kRowTile;
     RG_MARK(1);
@@ -269,7 +269,7 @@ __device__ __forceinline__ void rowgemm_body(const float* __restrict__ W, const 
     RG_MARK(2);
     floatx16 acc = zero16();
     const float* arow = &s_x[c32 * LD + h * KS];
-    if constexpr (GINE_BF16X3_BODY && KS <= 64) {
+    if constexpr (GINE_GEMM_BF16X3 && KS <= 64) {
 #pragma unroll
       for (int s = 0; s < KS / 8; ++s) {
         const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);
@@ -585,7 +585,7 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
       kc = col_const<PRO>(pa, D, q_me);
     }
     BPlanes<KS> bp;
-    if constexpr (GINE_BF16X3_PIPE && KS <= 64) bp.from(bf);
+    if constexpr (GINE_GEMM_BF16X3 && KS <= 64) bp.from(bf);
     __syncthreads();  // W^T fragment reads (WL) are done before the A buffers overwrite them
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) stage_item(tile_of(0), raw[i], i, s_lds);
@@ -609,7 +609,7 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
       for (int q = 0; q < NQ; ++q) {
         const float4 an =
             *reinterpret_cast<const float4*>(&arow[4 * (q + 1 < NQ ? q + 1 : q)]);
-        if constexpr (GINE_BF16X3_PIPE && KS <= 64) {
+        if constexpr (GINE_GEMM_BF16X3 && KS <= 64) {
           if (q % 2 == 0) aprev = a4;
           else acc = mfma_bf16x3(split8(aprev, a4), bp.f[q / 2], acc);
         } else {
@@ -639,7 +639,7 @@ __device__ __forceinline__ void rowgemm_pipe(const float* __restrict__ W, const 
         a4 = an;
       }
       // (the A buffer of tile k stays until the barrier before chain k + 1)
-      if constexpr (GINE_BF16X3_PIPE && KS <= 64)
+      if constexpr (GINE_GEMM_BF16X3 && KS <= 64)
         if (wave_any_nan(acc)) acc = redo_fp32<D, KS, BT || WL>(arow, W, col, h);
       return acc;
     };

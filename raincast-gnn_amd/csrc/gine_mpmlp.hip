@@ -158,7 +158,7 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
     }
   }
   BPlanes<kKS> bp;
-  if constexpr (GINE_BF16X3_FUSED) bp.from(bf);
+  if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
   __syncthreads();  // (iteration 0: the gather role stages the first tile)
   double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
   const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
@@ -169,7 +169,7 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
     floatx16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    if constexpr (GINE_BF16X3_FUSED) {  // the row-tile GEMM's split-bf16 chain (gine_mlp.hip)
+    if constexpr (GINE_GEMM_BF16X3) {  // the row-tile GEMM's split-bf16 chain (gine_mlp.hip)
 #pragma unroll
       for (int s = 0; s < (GINE_FUSED_DBG == 2 ? 1 : kKS / 8); ++s) {
         const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);

@@ -212,16 +212,7 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
         }
       }
       if (s % SP == 0 && s / SP < NITEMS) load_item(s / SP, n1);
-      if constexpr (GINE_BF16_PROBE) {
-        if (s % 8 == 7) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int k = 0; k < NI; ++k)
-              acc[j][k] = probe6(make_float4(a[j], an[j], a[j], an[j]),
-                                 make_float4(b[k], bn[k], b[k], bn[k]), acc[j][k]);
-        }
-      } else if constexpr ((GINE_WG_VARIANT & 1) == 0) {
+      if constexpr ((GINE_WG_VARIANT & 1) == 0) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
