@@ -44,15 +44,15 @@ for s in $STEPS; do
     bench5) run bench_cfg5 600 python bench.py --config 5 --steps 20 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
                python3 bench.py --steps 20 --warmup 5 --no-cpu --no-strong ;;
-    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
-           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5
-           python tools/pmc_summary.py "$OUT"/pmc_fetch/run_counter_collection.csv \
-               "$OUT"/pmc_write/run_counter_collection.csv --traffic-json "$OUT/pmc_traffic.json" \
-               > "$OUT/pmc_summary.txt" 2>&1 ;;
-    rgsweep) for g in 256 512 1024; do export GINE_ROWGEMM_BLOCKS=$g; run bench_rg$g 300 python bench.py --no-cpu --steps 30 ${VARARGS:-}; done; unset GINE_ROWGEMM_BLOCKS ;;
-    mbsweep) for g in 512 1024 2048 4096; do export GINE_MPBWD_BLOCKS=$g; run bench_mb$g 300 python bench.py --no-cpu --steps 30; done; unset GINE_MPBWD_BLOCKS ;;
+    pmc)   # PMC_ARGS: bench options of the configuration (e.g. "--config 3"); PMC_NAME: its name
+           P=${PMC_NAME:-cfg2}
+           run pmc_fetch_$P 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$P" -o run -- \
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ${PMC_ARGS:-}
+           run pmc_write_$P 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$P" -o run -- \
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ${PMC_ARGS:-}
+           python tools/pmc_summary.py "$OUT"/pmc_fetch_$P/run_counter_collection.csv \
+               "$OUT"/pmc_write_$P/run_counter_collection.csv --config $P \
+               --traffic-json "$OUT/${P}_pmc_traffic.json" > "$OUT/${P}_pmc_summary.txt" 2>&1 ;;
     dist2) run bench_dist2_gloo 600 python bench.py --gpus 2 --dist-backend gloo --steps 10 \
                --warmup 3 --no-cpu ;;
     rgprof) GINE_HIP_LIB=raincast-gnn_amd/csrc/build/dbg/libgine_hip_rgprof.so run rg_prof 300 python tools/rg_prof.py ;;
