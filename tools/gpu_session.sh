@@ -47,9 +47,9 @@ for s in $STEPS; do
     pmc)   # PMC_ARGS: bench options of the configuration (e.g. "--config 3"); PMC_NAME: its name
            P=${PMC_NAME:-cfg2}
            run pmc_fetch_$P 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$P" -o run -- \
-               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ${PMC_ARGS:-}
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-strong --no-graph --kernel-reps 5 ${PMC_ARGS:-}
            run pmc_write_$P 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$P" -o run -- \
-               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-graph --kernel-reps 5 ${PMC_ARGS:-}
+               python3 bench.py --steps 5 --warmup 2 --no-cpu --no-strong --no-graph --kernel-reps 5 ${PMC_ARGS:-}
            python tools/pmc_summary.py "$OUT"/pmc_fetch_$P/run_counter_collection.csv \
                "$OUT"/pmc_write_$P/run_counter_collection.csv --config $P \
                --traffic-json "$OUT/${P}_pmc_traffic.json" > "$OUT/${P}_pmc_summary.txt" 2>&1 ;;
