@@ -91,14 +91,20 @@ class StepRunner:
     ``optimizer`` is a :class:`raincast_gnn.optim.FlatAdamW` (one kernel over the flat
     buffer) or any torch optimizer (``capturable=True`` for graph capture).  ``reducer`` is a
     :class:`raincast_gnn.distributed.FlatGradReducer` over the same gradients (data
-    parallelism); with RCCL its all-reduce is captured in the step graph, with other backends
-    it runs between the fwd+bwd graph and the optimizer graph.
+    parallelism).  ``allreduce``: "split" (default) launches the all-reduce between the
+    fwd+bwd graph and the optimizer graph; "graph" captures it inside the one step graph
+    (RCCL only; the capture of a collective has only run at world 1 so far, and costs
+    0.534 -> 0.548 ms per cfg2 step when split, DESIGN.md 5 -- the same choice and default
+    as ``bench.py --allreduce``).  gloo groups always split (their collectives cannot be
+    captured).
     """
 
     def __init__(self, model, optimizer, graphed: bool = True, warmup: int = 2,
-                 reducer=None):
+                 reducer=None, allreduce: str = "split"):
+        if allreduce not in ("split", "graph"):
+            raise ValueError(f"allreduce={allreduce!r}: expected 'split' or 'graph'")
         self.model, self.opt, self.reducer = model, optimizer, reducer
-        self.graphed, self.warmup = graphed, warmup
+        self.graphed, self.warmup, self.allreduce = graphed, warmup, allreduce
         self._seen: dict[int, int] = {}
         self._graphs: dict[int, tuple] = {}
 
@@ -154,10 +160,10 @@ class StepRunner:
                             batch.edge_attr, batch.y.clone(), batch.batch, batch.ptr,
                             batch.num_graphs)
         collective = self.reducer is not None and _world() > 1
-        # RCCL's all-reduce is captured inside the step graph (between the backward and the
-        # optimizer); other backends (gloo rehearsals) cannot be captured: two graphs with
-        # the all-reduce launched between them
-        in_graph = collective and dist.get_backend() == "nccl"
+        # allreduce="graph" with RCCL: the all-reduce inside the step graph (between the
+        # backward and the optimizer); otherwise two graphs with the all-reduce launched
+        # between them (gloo collectives cannot be captured)
+        in_graph = collective and self.allreduce == "graph" and dist.get_backend() == "nccl"
         split = collective and not in_graph
         torch.cuda.synchronize()
         g_fb = torch.cuda.CUDAGraph()
@@ -280,6 +286,9 @@ def main(argv=None) -> dict:
     ap.add_argument("--radius", action="store_true", help="radius graph of params max_dist")
     ap.add_argument("--epochs", type=int, default=None, help="override max_epochs")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay")
+    ap.add_argument("--allreduce", choices=("split", "graph"), default="split",
+                    help="data-parallel all-reduce between the step's two graphs (split) or "
+                         "captured inside one (graph, RCCL); see StepRunner")
     args = ap.parse_args(argv)
 
     rank, local_rank, world = env_rank()
@@ -307,7 +316,8 @@ def main(argv=None) -> dict:
     broadcast_parameters(model)
     opt = FlatAdamW(model.parameters(), lr=config["lr"])
     reducer = FlatGradReducer(model.parameters(), flat=opt.flat_grad) if world > 1 else None
-    runner = StepRunner(model, opt, graphed=not args.eager, reducer=reducer)
+    runner = StepRunner(model, opt, graphed=not args.eager, reducer=reducer,
+                        allreduce=args.allreduce)
     out = fit(model, opt, train_loader, val_loader, device,
               args.epochs or config["max_epochs"], os.path.join(args.dir, "models"),
               args.run_id, example=train_set.batch(torch.tensor([0])), runner=runner)

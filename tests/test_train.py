@@ -90,3 +90,15 @@ def test_data_parallel_loader_needs_equal_shards_and_a_batch():
     assert list(loader) == []
     with pytest.raises(ValueError, match="no batch"):
         T.train_one_epoch(_OracleModel(), loader, None, "cpu")
+
+
+def test_step_runner_allreduce_choice():
+    """The data-parallel all-reduce form is chosen up front, as bench.py's --allreduce:
+    split by default, graph on request, anything else rejected."""
+    import pytest
+    m = torch.nn.Linear(2, 2)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    assert T.StepRunner(m, opt).allreduce == "split"
+    assert T.StepRunner(m, opt, allreduce="graph").allreduce == "graph"
+    with pytest.raises(ValueError):
+        T.StepRunner(m, opt, allreduce="sometimes")
