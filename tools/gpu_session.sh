@@ -55,7 +55,7 @@ for s in $STEPS; do
                --traffic-json "$OUT/${P}_pmc_traffic.json" > "$OUT/${P}_pmc_summary.txt" 2>&1 ;;
     dist2) run bench_dist2_gloo 600 python bench.py --gpus 2 --dist-backend gloo --steps 10 \
                --warmup 3 --no-cpu ;;
-    rgprof) GINE_HIP_LIB=raincast-gnn_amd/csrc/build/dbg/libgine_hip_rgprof.so run rg_prof 300 python tools/rg_prof.py ;;
+    rgprof) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/rgprof/libgine_hip.so run rg_prof 300 python tools/rg_prof.py ;;
     var)   for v in raincast-gnn_amd/csrc/build/var/*/; do n=$(basename "$v")
              GINE_HIP_LIB=${v}libgine_hip.so run var_${n}_base 300 python bench.py --no-cpu --steps 30 ${VARARGS:-}
            done ;;
