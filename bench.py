@@ -400,6 +400,9 @@ def sec8d_launch_work(name: str, w: dict) -> dict:
     }.get(name, {})
 
 
+MALL_BYTES = 256 * 1024 * 1024  # MI355X Infinity Cache (MALL)
+
+
 def roofline_for(kernels: dict, layers: int, work: dict, config: str = "cfg2"):
     """The dominant kernel of the step (largest time per step among the per-layer kernels
     the training step launches) against SURVEY.md 8(d)'s roofline: its ideal time is
@@ -873,6 +876,10 @@ def main():
         graphs_per_rank = cfg.graphs_per_gpu
         scaling = "weak"
     tr, elapsed, pct = measure(cfg, graphs_per_rank, args, device, rank, world)
+    # flag MALL residency when the step's working set is under the 256 MB
+    # Infinity Cache -- the peak of live device allocations over the measured steps (inputs,
+    # parameters, saved activations, workspaces) is the working-set bound used here
+    working_set = torch.cuda.max_memory_allocated(device)
     layers = tr.params["gnn_layers"]
     E_rank = tr.batch.edge_index.size(1)
     loss_val = float(tr.loss.item()) if tr.loss is not None else float("nan")
@@ -905,6 +912,8 @@ def main():
     if rank == 0:
         work = sec8d_work(tr.batch.num_nodes, E_rank, tr.params["gnn_hidden"])
         roof = roofline_for(kernels, layers, work, cfg.name)
+        roof["working_set_bytes"] = int(working_set)
+        roof["mall_resident"] = bool(working_set < MALL_BYTES)
         roof_mp = roofline_mp(kernels, layers, work, cfg.name)
         if roof_mp is not None:
             copy_gbs = copy_ceiling_gbps(device)
