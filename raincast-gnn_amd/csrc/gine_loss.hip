@@ -116,6 +116,21 @@ __device__ __forceinline__ Dual<K> powc(const Dual<K>& a, double c) {  // consta
   const double p = pow(a.v, c);
   return apply(a, p, c * pow(a.v, c - 1.0));
 }
+// the two powers of pareto_crps at the experiments' xi = 0.5 (params.json "xi": 0.5):
+// x^-2 and x^0.5 without pow() -- fp64 pow is the longest routine of the pass, and eight of
+// them per node dominated its dependent chain.  Same values and derivatives as powc up to
+// the last-bit rounding of pow (inf / NaN / signed-zero cases as pow for every argument
+// the pass can produce: 1 + xi*yt and 1 - cdf with cdf <= 1).
+template <int K>
+__device__ __forceinline__ Dual<K> pow_m2(const Dual<K>& a) {  // a^-2, d = -2 a^-3
+  const double p = 1.0 / (a.v * a.v);
+  return apply(a, p, -2.0 * (p / a.v));
+}
+template <int K>
+__device__ __forceinline__ Dual<K> pow_half(const Dual<K>& a) {  // a^0.5, d = 0.5 a^-0.5
+  const double p = sqrt(a.v);
+  return apply(a, p, 0.5 / p);
+}
 // standard normal cdf / pdf (torch.distributions.Normal(0, 1))
 template <int K>
 __device__ __forceinline__ Dual<K> Phi(const Dual<K>& z) {
@@ -165,9 +180,14 @@ template <int K>
 __device__ Dual<K> pareto_crps(const Dual<K>& y, const Dual<K>& u, const Dual<K>& m,
                                const Dual<K>& s, double xi) {
   const Dual<K> yt = (y - u) / s;
-  const Dual<K> cdf = select(yt.v <= 0.0, cst<K>(0.0), 1.0 - powc(1.0 + xi * yt, -1.0 / xi));
+  const bool half = xi == 0.5;  // a kernel argument: uniform
+  const Dual<K> base = 1.0 + xi * yt;
+  const Dual<K> cdf =
+      select(yt.v <= 0.0, cst<K>(0.0), 1.0 - (half ? pow_m2(base) : powc(base, -1.0 / xi)));
   const Dual<K> om = 1.0 - m;
-  return s * (dabs(yt) - (2.0 / (1.0 - xi)) * (om * (1.0 - powc(1.0 - cdf, 1.0 - xi))) +
+  const Dual<K> tail = 1.0 - cdf;
+  return s * (dabs(yt) -
+              (2.0 / (1.0 - xi)) * (om * (1.0 - (half ? pow_half(tail) : powc(tail, 1.0 - xi)))) +
               (1.0 / (2.0 - xi)) * sq(om));
 }
 
