@@ -6,10 +6,11 @@
 // The reference materialises the [N, M, H] pre-activation (90 MB at the 24h_mixed
 // benchmark shape) three times per step (Linear output, ReLU output, ReLU gradient).  Here
 // it never leaves the MFMA accumulators.  Rows are (node, member) pairs; a workgroup walks
-// groups of 32 nodes = 32*M rows as M tiles of 32 rows, and each wave owns 32 hidden units.
+// groups of 2G nodes (G = 16, or 8 for small batches) = 2G*M rows as ceil(G*M/16) tiles of
+// 32 rows, and each wave owns 32 hidden units.
 // Row placement: the accumulator register q of lane half h (v_mfma_f32_32x32x2_f32 output
-// row (q&3)+8(q>>2)+4h) holds group row 16*M*h + 16*t + q in tile t, i.e. half 0 walks the
-// rows of nodes 0-15 and half 1 those of nodes 16-31, both in member order.  So
+// row (q&3)+8(q>>2)+4h) holds group row G*M*h + 16*t + q in tile t, i.e. half 0 walks the
+// rows of nodes 0..G-1 and half 1 those of nodes G..2G-1, both in member order.  So
 //  * forward: bias + ReLU in registers and a running per-node sum per lane, written once
 //    when the node changes (wave-uniform: both halves are at the same local row) -- no
 //    LDS read-modify-write, deterministic member order;
@@ -27,7 +28,12 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int kNodes = 32;  // nodes per group; a group is exactly M tiles of 32 rows
+// A group is 2G nodes (G per lane half), walked as TPG = ceil(G*M/16) tiles of 32 rows:
+// half c's 16 rows of tile t are the group's rows c*G*M + 16t + j (j < 16), and rows with
+// 16t + j >= G*M are padding (staged as zero, ReLU bit cleared, sum not kept).  G = 16 (no
+// padding) when there are enough nodes to fill the chip; G = 8 doubles the workgroups of a
+// small batch (cfg2: 1,000 instead of 500) at the cost of <= 15 padding rows per half.
+__host__ __device__ constexpr int tiles_per_group(int G, int M) { return (G * M + 15) / 16; }
 
 #ifdef GINE_DS_PROFILE
 // Debug build only: block 0 / thread 0 records s_memtime at phase boundaries of its tiles.
@@ -58,17 +64,18 @@ __device__ __forceinline__ int staged_row(int i) {
 }
 
 // Tile t of a group stages, into an LDS tile [32][KP+4], rows 16c+j <- group row
-// 16*M*c + 16*t + j (c = lane half, j < 16): two contiguous runs of 16*F floats.  Offsets
+// G*M*c + 16*t + j (c = lane half, j < 16): two contiguous runs of 16*F floats.  Offsets
 // depend only on the thread, so they are computed once; the loads address a uniform
 // (scalar) tile base plus a 32-bit lane offset.
-template <int NT, int KP>
+template <int NT, int KP, bool PAD>  // PAD: G*M % 16 != 0 is possible (G = 8)
 struct Stager {
   static constexpr int PER = (32 * KP + NT - 1) / NT;  // >= 32*F / NT
   static constexpr int LD = KP + 4;
   int src[PER];  // float offset from the tile's first row (0 if the thread has no element)
   int row[PER];  // group-row offset from the tile's first row (INT_MAX: no element)
   int dst[PER];  // LDS offset (-1: no element)
-  __device__ __forceinline__ void init(int F, int M) {
+  uint32_t jrow[PAD ? PER : 1];
+  __device__ __forceinline__ void init(int F, int M, int G) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = threadIdx.x + i * NT;
@@ -76,12 +83,14 @@ struct Stager {
       const int off = e - c * 16 * F;
       const int j = off / F, f = off - j * F;
       const bool has = e < 32 * F;
-      src[i] = has ? c * 16 * M * F + off : 0;
-      row[i] = has ? c * 16 * M + j : 0x7fffffff;
+      src[i] = has ? c * G * M * F + off : 0;
+      row[i] = has ? c * G * M + j : 0x7fffffff;
       dst[i] = has ? (16 * c + j) * LD + f : -1;
+      if constexpr (PAD) jrow[i] = has ? (uint32_t)j : 0u;
     }
   }
-  // Stage the tile whose first group row is `row0` (rows_total = N*M rows exist).
+  // Stage the tile whose first group row is `row0` (rows_total = N*M rows exist); rows
+  // j >= half_lim of each lane half are padding (half_lim = G*M - 16t).
   // Returns the rows-in-range bits: the zeroing of out-of-range rows waits for store(), so
   // nothing consumes the loaded registers before the tile is staged -- a select right
   // behind each load made the compiler wait for it there and serialised the prefetch.
@@ -89,14 +98,16 @@ struct Stager {
   // (every lane then loads ens[0], which exists since N*M > 0), so no address outside
   // [ens, ens + N*M*F) is ever formed.
   __device__ __forceinline__ uint32_t load(float (&v)[PER], const float* __restrict__ ens,
-                                           int64_t row0, int64_t rows_total, int F) const {
+                                           int64_t row0, int64_t rows_total, int F,
+                                           int half_lim) const {
     const int64_t d = rows_total - row0;
     const int lim = d <= 0 ? 0 : (d > 0x7fffffff ? 0x7fffffff : (int)d);
     const float* __restrict__ base = lim > 0 ? ens + row0 * F : ens;
     uint32_t ok = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const bool in = row[i] < lim;
+      bool in = row[i] < lim;
+      if constexpr (PAD) in = in && (int)jrow[i] < half_lim;
       const int off = in ? src[i] : 0;
 #ifdef GINE_BOUNDS_CHECK
       const int64_t a = (base - ens) + off;
@@ -180,17 +191,17 @@ struct Groups {
 // Position of a tile in the flat walk over (group, tile-in-group), advanced incrementally.
 struct Cursor {
   int g, t;     // group index, tile within the group
-  int64_t row;  // first group row of the tile: g*32*M + 16*t
-  __device__ __forceinline__ void start(int g0, int M) {
+  int64_t row;  // first group row of the tile: g*2G*M + 16*t
+  __device__ __forceinline__ void start(int g0, int GM) {
     g = g0;
     t = 0;
-    row = (int64_t)g0 * kNodes * M;
+    row = (int64_t)g0 * 2 * GM;
   }
-  __device__ __forceinline__ void advance(int M, int step) {
-    if (++t == M) {
+  __device__ __forceinline__ void advance(int GM, int tpg, int step) {
+    if (++t == tpg) {
       t = 0;
       g += step;
-      row = (int64_t)g * kNodes * M;
+      row = (int64_t)g * 2 * GM;
     } else {
       row += 16;
     }
@@ -201,38 +212,50 @@ struct Cursor {
 // and a double-buffered LDS tile: tile k+2 is loaded while tile k computes, tile k+1 is
 // stored after it, one barrier per tile.  With `mask_in`, each thread's 16-bit ReLU mask
 // word of the tile rides in the same ring (registers only: a thread reads its own word).
-template <int NT, int KP, class Body>
-__device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager<NT, KP>& st,
+// UNCOND (the backward): the ring loads past the walk's last tile reload the current tile
+// (never consumed) instead of being skipped, so no register merge at the loop's back edge
+// waits for them (backward 41.4 -> 39.0 us at 16,000 nodes; the forward, whose ring holds
+// no mask word, runs 0.9 us slower that way: profiles/r03_s35).
+template <bool UNCOND, int NT, int KP, bool PAD, class Body>
+__device__ __forceinline__ void walk_tiles(const Groups& gr, int GM, int tpg,
+                                           const Stager<NT, KP, PAD>& st,
                                            const float* __restrict__ ens, int64_t rows_total,
                                            int F, float* buf0, float* buf1,
                                            const uint16_t* __restrict__ mask_in, Body&& tile) {
-  constexpr int PER = Stager<NT, KP>::PER;
+  constexpr int PER = Stager<NT, KP, PAD>::PER;
   if (gr.first >= gr.end) return;
-  const int count = ((gr.end - gr.first + gr.step - 1) / gr.step) * M;
+  const int count = ((gr.end - gr.first + gr.step - 1) / gr.step) * tpg;
   Cursor cur, pf;  // tile being computed, tile being loaded
-  cur.start(gr.first, M);
+  cur.start(gr.first, GM);
   pf = cur;
   auto mload = [&](const Cursor& c) -> uint32_t {
-    return mask_in ? (uint32_t)mask_in[((int64_t)c.g * M + c.t) * NT + threadIdx.x] : 0u;
+    return mask_in ? (uint32_t)mask_in[((int64_t)c.g * tpg + c.t) * NT + threadIdx.x] : 0u;
+  };
+  auto sload = [&](float (&v)[PER], const Cursor& c) -> uint32_t {
+    return st.load(v, ens, c.row, rows_total, F, GM - 16 * c.t);
   };
   float va[PER], vb[PER];
   uint32_t ma = 0, mb = 0, oa = 0, ob = 0;
-  oa = st.load(va, ens, pf.row, rows_total, F);
+  oa = sload(va, pf);
   ma = mload(pf);
   st.store(buf0, va, oa);
   if (count > 1) {
-    pf.advance(M, gr.step);
-    ob = st.load(vb, ens, pf.row, rows_total, F);
+    pf.advance(GM, tpg, gr.step);
+    ob = sload(vb, pf);
     mb = mload(pf);
   }
-  pf.advance(M, gr.step);  // pf: tile k+2
+  pf.advance(GM, tpg, gr.step);  // pf: tile k+2
   __syncthreads();
   auto step = [&](int k, float (&vcur)[PER], uint32_t& mcur, uint32_t& ocur,
                   float (&vnxt)[PER], uint32_t onxt, float* bcur, float* bnxt) {
     const uint32_t bits = mcur;
     DS_MARK(0);
-    if (k + 2 < count) {
-      ocur = st.load(vcur, ens, pf.row, rows_total, F);
+    if constexpr (UNCOND) {
+      const bool more = k + 2 < count;
+      ocur = sload(vcur, more ? pf : cur);
+      mcur = mload(more ? pf : cur);
+    } else if (k + 2 < count) {
+      ocur = sload(vcur, pf);
       mcur = mload(pf);
     }
     DS_MARK(1);
@@ -242,8 +265,8 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
     DS_MARK(5);
     __syncthreads();
     DS_MARK(6);
-    cur.advance(M, gr.step);
-    pf.advance(M, gr.step);
+    cur.advance(GM, tpg, gr.step);
+    pf.advance(GM, tpg, gr.step);
   };
   for (int k = 0; k < count; k += 2) {
     step(k, va, ma, oa, vb, ob, buf0, buf1);
@@ -252,9 +275,10 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
 }
 
 // ---------------------------------------------------------------------------------------
-// Forward.  mask_out (MASK): bit q of word [(g*M + t)*NT + thread] = ReLU active for the
-// row in accumulator register q -- what the backward needs instead of the activation.
-// Node sums go to LDS as nodes complete and to HBM once per group (32 nodes): no global
+// Forward.  mask_out (MASK): bit q of word [(g*TPG + t)*NT + thread] = ReLU active for the
+// row in accumulator register q (0 for padding rows) -- what the backward needs instead of
+// the activation.
+// Node sums go to LDS as nodes complete and to HBM once per group (2G nodes): no global
 // store sits in a data-dependent branch of the tile loop, so the compiler can count the
 // memory operations in flight and the next tiles' loads stay in flight under the MFMAs
 // (a conditional store there made it drain the whole queue -- s_waitcnt vmcnt(0) -- every
@@ -264,7 +288,7 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int M, const Stager
 // forward that follows.  They are dealt first (so they never wait for a free slot behind the
 // walk) and share one LDS buffer with the walk's tiles (so the walk's occupancy is that of
 // the larger of the two, not of their sum).
-template <int H, int KP, bool MASK, bool FOLD = false>
+template <int H, int KP, int G, bool MASK, bool FOLD = false>
 __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__ ens,
                                                        const float* __restrict__ w1,
                                                        const float* __restrict__ b1,
@@ -274,7 +298,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
                                                        int num_groups, FoldArgs fold) {
   constexpr int NT = 2 * H;
   constexpr int LD = KP + 4;
-  constexpr int kWalk = 2 * 32 * LD + kNodes * H;  // two staged tiles + the group's node sums
+  constexpr int kWalk = 2 * 32 * LD + 2 * G * H;  // two staged tiles + the group's node sums
   constexpr int kFold = FOLD ? 32 * (H + 4) + (H / 32) * kSR : 0;
   __shared__ __attribute__((aligned(16))) float s_lds[kWalk > kFold ? kWalk : kFold];
   int nbw = gridDim.x, bw = blockIdx.x;  // workgroups walking the groups, this one's index
@@ -298,14 +322,15 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
   zero_pad<KP>(s_e[0], F);
   zero_pad<KP>(s_e[1], F);
 
-  Stager<NT, KP> st;
-  st.init(F, M);
+  Stager<NT, KP, G != 16> st;
+  st.init(F, M, G);
   const Groups gr(num_groups, nbw, bw);
-  // uniform walk state: node (0..15 within each half's 16) and rows left in it
-  int node = 0, rem = M;
+  const int GM = G * M, tpg = tiles_per_group(G, M);
   float run = 0.f;
-  float* s_mine = s_r + (16 * h) * H + col;  // this lane's column of its half's 16 nodes
-  walk_tiles(gr, M, st, ens, N * M, F, s_e[0], s_e[1], nullptr,
+  float* s_mine = s_r + (G * h) * H + col;  // this lane's column of its half's G nodes
+  // uniform walk state: node (0..G-1 within each half's G; G: padding) and rows left in it
+  int node = 0, rem = M;
+  walk_tiles<false>(gr, GM, tpg, st, ens, N * M, F, s_e[0], s_e[1], nullptr,
              [&](const Cursor& c, const float* buf, uint32_t) {
     if (c.t == 0) {
       node = 0;
@@ -321,19 +346,23 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
       bits |= (v > 0.f ? 1u : 0u) << q;
       run += relu_nan(v);
       if (--rem == 0) {  // last member of this node: keep its sum
-        s_mine[node * H] = run;
+        if (node < G) s_mine[node * H] = run;
         run = 0.f;
         ++node;
         rem = M;
       }
     }
     DS_MARK(3 + 0 * (int)run);
-    if constexpr (MASK) mask_out[((int64_t)c.g * M + c.t) * NT + threadIdx.x] = (uint16_t)bits;
-    if (c.t == M - 1) {  // the group is complete: its 2 x 16 node sums to HBM
-      const int64_t n0 = (int64_t)c.g * kNodes + 16 * h;
+    if (G * M % 16 != 0 && c.t == tpg - 1) {  // padding rows: no ReLU bit
+      const int live = GM - 16 * c.t;
+      bits &= live >= 16 ? 0xffffu : (1u << live) - 1u;
+    }
+    if constexpr (MASK) mask_out[((int64_t)c.g * tpg + c.t) * NT + threadIdx.x] = (uint16_t)bits;
+    if (c.t == tpg - 1) {  // the group is complete: its 2 x G node sums to HBM
+      const int64_t n0 = (int64_t)c.g * 2 * G + G * h;
       const int64_t nvalid = N - n0;
 #pragma unroll
-      for (int n = 0; n < 16; ++n)
+      for (int n = 0; n < G; ++n)
         if (n < nvalid) r[(n0 + n) * H + col] = s_mine[n * H];
     }
   });
@@ -343,7 +372,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
 // Backward for the weights from the forward's ReLU mask:
 //   dh = dr[node] * mask;  dW1 += dh^T ens (MFMA over 32-feature tiles, A = dh straight from
 //   registers, B = staged rows; the last F % 32 features as fp32 FMAs);  db1 += sum dh.
-template <int H, int KP>
+template <int H, int KP, int G>
 __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__ ens,
                                                        const uint16_t* __restrict__ mask,
                                                        const float* __restrict__ dr,
@@ -354,7 +383,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   constexpr int NIF = KP / 32;         // full 32-wide feature tiles (MFMA)
   constexpr int TAIL = KP - 32 * NIF;  // remaining features, multiple of 4 (VALU)
   __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
-  __shared__ float s_dr[kNodes * H];
+  __shared__ float s_dr[2 * G * H];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
@@ -369,19 +398,29 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   for (int j = 0; j < TAIL; ++j) tw[j] = 0.f;
   double gb = 0.0;
 
-  Stager<NT, KP> st;
-  st.init(F, M);
+  Stager<NT, KP, G != 16> st;
+  st.init(F, M, G);
   const Groups gr(num_groups, gridDim.x);
-  const float* my_dr = s_dr + 16 * h * H + col;  // this lane: node j of its half at j*H
+  const int GM = G * M, tpg = tiles_per_group(G, M);
+  const float* my_dr = s_dr + G * h * H + col;  // this lane: node j of its half at j*H
   int node = 0, rem = M;
-  walk_tiles(gr, M, st, ens, N * M, F, s_e[0], s_e[1], mask,
+  walk_tiles<true>(gr, GM, tpg, st, ens, N * M, F, s_e[0], s_e[1], mask,
              [&](const Cursor& c, const float* buf, uint32_t bits) {
     if (c.t == 0) {  // dr of this group, this wave's columns (read by this wave only)
-      const int64_t node0 = (int64_t)c.g * kNodes;
-      for (int i = lane; i < kNodes * 32; i += kWave) {
+      const int64_t node0 = (int64_t)c.g * 2 * G;
+      // all loads in flight before the first LDS store (clamped rows, zero past N)
+      constexpr int kPer = 2 * G * 32 / kWave;
+      float v[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int i = lane + j * kWave;
         const int64_t n = node0 + (i >> 5);
-        const int cc = wave * 32 + (i & 31);
-        s_dr[(i >> 5) * H + cc] = n < N ? dr[n * H + cc] : 0.f;
+        v[j] = dr[(n < N ? n : N - 1) * H + wave * 32 + (i & 31)];
+      }
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int i = lane + j * kWave;
+        s_dr[(i >> 5) * H + wave * 32 + (i & 31)] = node0 + (i >> 5) < N ? v[j] : 0.f;
       }
       node = 0;
       rem = M;
@@ -390,7 +429,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
     float gsum = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {  // independent LDS reads, uniform node walk
-      const float d = my_dr[node * H];  // 0 for nodes >= N
+      const float d = my_dr[(node < G ? node : G - 1) * H];  // 0 for nodes >= N
       const float v = ((bits >> q) & 1u) ? d : 0.f;
       dh[q] = v;
       gsum += v;
@@ -482,10 +521,14 @@ inline int pad_bwd(int F) {
 
 inline bool hidden_ok(int H) { return H == 32 || H == 64 || H == 128 || H == 256; }
 
-inline int bwd_grid(int64_t N) {
-  const int64_t groups = ceil_div(N > 0 ? N : 1, kNodes);
-  return (int)std::min<int64_t>(groups, 512);
+// Nodes per lane half: 8 while 16 would leave at most one group per CU (<= 8,192 nodes: at
+// 4,000 nodes forward 21.4 -> 14.8 us, backward 28.4 -> 20.9 us); at 16,000 nodes 8 is no
+// faster (forward 31.5 vs 33.3 us: two groups per CU already keep it busy; profiles/r03_s35).
+inline int nodes_per_half(int64_t N) { return ceil_div(N > 0 ? N : 1, 32) <= 256 ? 8 : 16; }
+inline int num_groups(int64_t N) {
+  return (int)ceil_div(N > 0 ? N : 1, 2 * nodes_per_half(N));
 }
+inline int bwd_grid(int64_t N) { return std::min(num_groups(N), 512); }
 
 #define DS_FWD_KP(H_, KP_, MACRO)                         \
   switch (KP_) {                                          \
@@ -522,7 +565,10 @@ using namespace gine;
 extern "C" int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32_t hidden,
                                        size_t* bytes) {
   if (!bytes || num_nodes < 0 || members <= 0 || !hidden_ok(hidden)) return GINE_ERR_INVALID;
-  *bytes = (size_t)ceil_div(num_nodes, kNodes) * members * 2 * hidden * sizeof(uint16_t);
+  const int G = nodes_per_half(num_nodes);
+  *bytes = num_nodes == 0 ? 0
+                          : (size_t)num_groups(num_nodes) * tiles_per_group(G, members) * 2 *
+                                hidden * sizeof(uint16_t);
   return GINE_OK;
 }
 
@@ -535,16 +581,22 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   if (num_nodes == 0) return GINE_OK;
   if (!ens || !w1 || !b1 || !r) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
-  const int groups = (int)ceil_div(num_nodes, kNodes);
+  const int groups = num_groups(num_nodes);
   const int grid = std::min(groups, 1024);
+  const bool g8 = nodes_per_half(num_nodes) == 8;
   hipStream_t s = as_stream(stream);
-#define LAUNCH_FWD_M(H_, KP_, MK_)                                                            \
-  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, MK_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, b1, \
-                     r, mask, num_nodes, members, in_features, groups, FoldArgs{})
-#define LAUNCH_FWD(H_, KP_)                     \
-  do {                                          \
-    if (mask) LAUNCH_FWD_M(H_, KP_, true);      \
-    else LAUNCH_FWD_M(H_, KP_, false);          \
+#define LAUNCH_FWD_M(H_, KP_, G_, MK_)                                                        \
+  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, \
+                     b1, r, mask, num_nodes, members, in_features, groups, FoldArgs{})
+#define LAUNCH_FWD(H_, KP_)                                   \
+  do {                                                        \
+    if (g8) {                                                 \
+      if (mask) LAUNCH_FWD_M(H_, KP_, 8, true);               \
+      else LAUNCH_FWD_M(H_, KP_, 8, false);                   \
+    } else {                                                  \
+      if (mask) LAUNCH_FWD_M(H_, KP_, 16, true);              \
+      else LAUNCH_FWD_M(H_, KP_, 16, false);                  \
+    }                                                         \
   } while (0)
   DS_DISPATCH_H(hidden, KP, DS_FWD_KP, LAUNCH_FWD);
 #undef LAUNCH_FWD
@@ -568,18 +620,25 @@ extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const fl
   if (num_nodes < 0 || members <= 0 || !slab) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!ens || !mask || !dr)) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
-  const int groups = (int)ceil_div(num_nodes > 0 ? num_nodes : 1, kNodes);
+  const int groups = num_groups(num_nodes);
   const int grid = bwd_grid(num_nodes);
+  const bool g8 = nodes_per_half(num_nodes) == 8;
   const int64_t per = (int64_t)hidden * in_features + hidden;
   hipStream_t s = as_stream(stream);
   if (num_nodes == 0) {
     GINE_RETURN_IF_HIP(hipMemsetAsync(slab, 0, sizeof(float) * per * grid, s));
   } else {
-#define LAUNCH_BWD(H_, KP_)                                                                   \
-  hipLaunchKernelGGL((k_deepset_bwd<H_, KP_>), dim3(grid), dim3(2 * H_), 0, s, ens, mask, dr, \
-                     slab, num_nodes, members, in_features, groups)
+#define LAUNCH_BWD_G(H_, KP_, G_)                                                             \
+  hipLaunchKernelGGL((k_deepset_bwd<H_, KP_, G_>), dim3(grid), dim3(2 * H_), 0, s, ens, mask,  \
+                     dr, slab, num_nodes, members, in_features, groups)
+#define LAUNCH_BWD(H_, KP_)                       \
+  do {                                            \
+    if (g8) LAUNCH_BWD_G(H_, KP_, 8);             \
+    else LAUNCH_BWD_G(H_, KP_, 16);               \
+  } while (0)
     DS_DISPATCH_H(hidden, KP, DS_BWD_KP, LAUNCH_BWD);
 #undef LAUNCH_BWD
+#undef LAUNCH_BWD_G
     GINE_LAUNCH_STATUS();
   }
   if (!dw1) return GINE_OK;  // slab left for gine_grad_finalize_batch
@@ -633,18 +692,24 @@ extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const fl
   if (!wr1 || !br1 || !wdr || !bdr || !wfold) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!ens || !w1 || !b1 || !r)) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
-  const int groups = (int)ceil_div(num_nodes > 0 ? num_nodes : 1, kNodes);
+  const int groups = num_groups(num_nodes);
   const int walk = num_nodes > 0 ? std::min(groups, 1024) : 0;
+  const bool g8 = nodes_per_half(num_nodes) == 8;
   const FoldArgs fold{wr1, br1, wdr, bdr, wfold, x_features};
   hipStream_t s = as_stream(stream);
-#define LAUNCH_FWD_F(H_, KP_, MK_)                                                            \
-  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, MK_, true>), dim3(walk + kFoldBlocks<H_>),       \
+#define LAUNCH_FWD_F(H_, KP_, G_, MK_)                                                        \
+  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_, true>), dim3(walk + kFoldBlocks<H_>),   \
                      dim3(2 * H_), 0, s, ens, w1, b1, r, mask, num_nodes, members, in_features, \
                      groups, fold)
-#define LAUNCH_FWD(H_, KP_)                     \
-  do {                                          \
-    if (mask) LAUNCH_FWD_F(H_, KP_, true);      \
-    else LAUNCH_FWD_F(H_, KP_, false);          \
+#define LAUNCH_FWD(H_, KP_)                                   \
+  do {                                                        \
+    if (g8) {                                                 \
+      if (mask) LAUNCH_FWD_F(H_, KP_, 8, true);               \
+      else LAUNCH_FWD_F(H_, KP_, 8, false);                   \
+    } else {                                                  \
+      if (mask) LAUNCH_FWD_F(H_, KP_, 16, true);              \
+      else LAUNCH_FWD_F(H_, KP_, 16, false);                  \
+    }                                                         \
   } while (0)
   if (hidden == 64) {
     DS_FWD_KP(64, KP, LAUNCH_FWD);
