@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define GINE_ABI_VERSION 2  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin */
+#define GINE_ABI_VERSION 3  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
+                              3: gine_deepset_bwd_num_partials takes the hidden width */
 
 #define GINE_OK 0
 #define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
@@ -477,7 +478,7 @@ int gine_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out
  * pattern as bits, for the backward.
  * gine_deepset_bwd: weight gradients for dr = d loss / d r from the forward's mask:
  *   dw1 [H, F] = sum_{n,m} (dr[n] * 1[pre > 0])^T ens[n, m],  db1 [H] likewise summed
- * slab: gine_deepset_bwd_num_partials(N) * (H*F + H) floats of per-workgroup partials,
+ * slab: gine_deepset_bwd_num_partials(N, H) * (H*F + H) floats of per-workgroup partials,
  * reduced in fixed order (deterministic).  db1 may be NULL.
  * ---------------------------------------------------------------------------------- */
 int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32_t hidden, size_t* bytes);
@@ -492,7 +493,7 @@ int gine_deepset_fwd_fold(const float* ens, const float* w1, const float* b1, fl
                           int32_t in_features, int32_t hidden, const float* wr1,
                           const float* br1, const float* wdr, const float* bdr, float* wfold,
                           int32_t x_features, void* stream);
-int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t* num_partials);
+int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t hidden, int32_t* num_partials);
 int gine_deepset_bwd(const float* ens, const uint16_t* mask, const float* dr, float* slab,
                      float* dw1, float* db1, int64_t num_nodes, int32_t members,
                      int32_t in_features, int32_t hidden, void* stream);

@@ -521,14 +521,22 @@ inline int pad_bwd(int F) {
 
 inline bool hidden_ok(int H) { return H == 32 || H == 64 || H == 128 || H == 256; }
 
-// Nodes per lane half: 8 while 16 would leave at most one group per CU (<= 8,192 nodes: at
-// 4,000 nodes forward 21.4 -> 14.8 us, backward 28.4 -> 20.9 us); at 16,000 nodes 8 is no
-// faster (forward 31.5 vs 33.3 us: two groups per CU already keep it busy; profiles/r03_s35).
-inline int nodes_per_half(int64_t N) { return ceil_div(N > 0 ? N : 1, 32) <= 256 ? 8 : 16; }
-inline int num_groups(int64_t N) {
-  return (int)ceil_div(N > 0 ? N : 1, 2 * nodes_per_half(N));
+// Nodes per lane half: 8 while 16 would leave at most one wave per SIMD (H/32 waves per
+// group; H = 128: <= 8,192 nodes; at 4,000 nodes forward 21.4 -> 14.8 us, backward 28.4 ->
+// 20.9 us); at 16,000 nodes and H = 128 8 is no faster (forward 31.5 vs 33.3 us: two waves
+// per SIMD already keep it busy; profiles/r03_s35); at 16,000 nodes and H = 64 forward
+// 31.9 -> 22.9 us, backward (1,000 partials) 38.6 -> 32.7 us (profiles/r03_s38, r03_s39).
+inline int nodes_per_half(int64_t N, int H) {
+  return ceil_div(N > 0 ? N : 1, 32) * (H / 32) <= 1024 ? 8 : 16;
 }
-inline int bwd_grid(int64_t N) { return std::min(num_groups(N), 512); }
+inline int num_groups(int64_t N, int H) {
+  return (int)ceil_div(N > 0 ? N : 1, 2 * nodes_per_half(N, H));
+}
+// Backward partials (slab rows): one per group up to 512 (H >= 128) or 1,024 (H <= 64: the
+// same slab bytes) workgroups; a smaller grid walks several groups per workgroup.
+inline int bwd_grid(int64_t N, int H) {
+  return std::min(num_groups(N, H), H >= 128 ? 512 : 1024);
+}
 
 #define DS_FWD_KP(H_, KP_, MACRO)                         \
   switch (KP_) {                                          \
@@ -565,9 +573,9 @@ using namespace gine;
 extern "C" int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32_t hidden,
                                        size_t* bytes) {
   if (!bytes || num_nodes < 0 || members <= 0 || !hidden_ok(hidden)) return GINE_ERR_INVALID;
-  const int G = nodes_per_half(num_nodes);
+  const int G = nodes_per_half(num_nodes, hidden);
   *bytes = num_nodes == 0 ? 0
-                          : (size_t)num_groups(num_nodes) * tiles_per_group(G, members) * 2 *
+                          : (size_t)num_groups(num_nodes, hidden) * tiles_per_group(G, members) * 2 *
                                 hidden * sizeof(uint16_t);
   return GINE_OK;
 }
@@ -581,9 +589,9 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   if (num_nodes == 0) return GINE_OK;
   if (!ens || !w1 || !b1 || !r) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
-  const int groups = num_groups(num_nodes);
+  const int groups = num_groups(num_nodes, hidden);
   const int grid = std::min(groups, 1024);
-  const bool g8 = nodes_per_half(num_nodes) == 8;
+  const bool g8 = nodes_per_half(num_nodes, hidden) == 8;
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD_M(H_, KP_, G_, MK_)                                                        \
   hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, \
@@ -605,9 +613,11 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   return GINE_OK;
 }
 
-extern "C" int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t* num_partials) {
+extern "C" int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t hidden,
+                                             int32_t* num_partials) {
   if (!num_partials || num_nodes < 0) return GINE_ERR_INVALID;
-  *num_partials = bwd_grid(num_nodes);
+  if (!hidden_ok(hidden)) return GINE_ERR_DIM;
+  *num_partials = bwd_grid(num_nodes, hidden);
   return GINE_OK;
 }
 
@@ -620,9 +630,9 @@ extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const fl
   if (num_nodes < 0 || members <= 0 || !slab) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!ens || !mask || !dr)) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
-  const int groups = num_groups(num_nodes);
-  const int grid = bwd_grid(num_nodes);
-  const bool g8 = nodes_per_half(num_nodes) == 8;
+  const int groups = num_groups(num_nodes, hidden);
+  const int grid = bwd_grid(num_nodes, hidden);
+  const bool g8 = nodes_per_half(num_nodes, hidden) == 8;
   const int64_t per = (int64_t)hidden * in_features + hidden;
   hipStream_t s = as_stream(stream);
   if (num_nodes == 0) {
@@ -657,7 +667,7 @@ extern "C" int gine_deepset_bwd_grad_job(int64_t num_nodes, int32_t in_features,
   *job = gine_grad_job{};
   job->kind = GINE_GRAD_JOB_SLAB;
   job->src = slab;
-  job->rows = bwd_grid(num_nodes);
+  job->rows = bwd_grid(num_nodes, hidden);
   job->cstride = per;
   job->nz = 1;
   job->per[0] = per;
@@ -692,9 +702,9 @@ extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const fl
   if (!wr1 || !br1 || !wdr || !bdr || !wfold) return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!ens || !w1 || !b1 || !r)) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
-  const int groups = num_groups(num_nodes);
+  const int groups = num_groups(num_nodes, hidden);
   const int walk = num_nodes > 0 ? std::min(groups, 1024) : 0;
-  const bool g8 = nodes_per_half(num_nodes) == 8;
+  const bool g8 = nodes_per_half(num_nodes, hidden) == 8;
   const FoldArgs fold{wr1, br1, wdr, bdr, wfold, x_features};
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD_F(H_, KP_, G_, MK_)                                                        \

@@ -23,7 +23,7 @@ GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
-ABI_VERSION = 2
+ABI_VERSION = 3
 COUNT_PARTS = 64  # GINE_COUNT_PARTS
 
 _c_void_p = ctypes.c_void_p
@@ -126,7 +126,7 @@ _SIGNATURES = {
     "gine_deepset_mask_bytes": [_i64, _i32, _i32, ctypes.POINTER(_size)],
     "gine_deepset_fwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
                          _i32, _i32, _c_void_p],
-    "gine_deepset_bwd_num_partials": [_i64, ctypes.POINTER(_i32)],
+    "gine_deepset_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_deepset_bwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                          _i64, _i32, _i32, _i32, _c_void_p],
     "gine_head_fwd": [_c_void_p] * 5 + [_i64, _i32, _i32, _c_void_p],

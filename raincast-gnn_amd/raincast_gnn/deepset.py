@@ -76,7 +76,7 @@ class _PhiSumFn(torch.autograd.Function):
         H = ctx.hidden
         dr = dr.contiguous()
         parts = ctypes.c_int32(0)
-        _lib.call("gine_deepset_bwd_num_partials", N, ctypes.byref(parts))
+        _lib.call("gine_deepset_bwd_num_partials", N, H, ctypes.byref(parts))
         slab = torch.empty(parts.value * (H * Fdim + H), dtype=torch.float32, device=dr.device)
         dw = grad_out(ctx.params[0], (H, Fdim), dr.device)
         db = grad_out(ctx.params[1], (H,), dr.device)

@@ -128,4 +128,7 @@ def test_abi_rejects_unsupported_shapes():
                                 35, 96, s) == _lib.GINE_ERR_DIM
     assert not deepset.fusable(x, w, b)
     n = ctypes.c_int32(0)
-    assert lib.gine_deepset_bwd_num_partials(16000, ctypes.byref(n)) == 0 and n.value == 500
+    assert lib.gine_deepset_bwd_num_partials(16000, 128, ctypes.byref(n)) == 0 and n.value == 500
+    # H = 64: groups of 16 nodes up to 16,384 nodes, up to 1,024 partials
+    assert lib.gine_deepset_bwd_num_partials(16000, 64, ctypes.byref(n)) == 0 and n.value == 1000
+    assert lib.gine_deepset_bwd_num_partials(16000, 96, ctypes.byref(n)) == _lib.GINE_ERR_DIM

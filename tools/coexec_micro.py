@@ -28,7 +28,7 @@ def main():
     mask = torch.randint(0, 255, (nb.value,), dtype=torch.uint8, device=dev)
     dr = torch.randn(N, H, device=dev)
     parts = ctypes.c_int32(0)
-    _lib.call("gine_deepset_bwd_num_partials", N, ctypes.byref(parts))
+    _lib.call("gine_deepset_bwd_num_partials", N, H, ctypes.byref(parts))
     ds_slab = torch.empty(parts.value * (H * F + H), device=dev)
     t = {k: torch.randn(N, H, device=dev) for k in ("dh0", "r", "s", "u", "e", "de", "dt", "ds")}
     x = torch.randn(N, F, device=dev)

@@ -34,7 +34,7 @@ def main():
         _lib.call("gine_deepset_mask_bytes", N, a.M, a.H, ctypes.byref(nbytes))
         mask = torch.empty(nbytes.value, dtype=torch.uint8, device=dev)
         parts = ctypes.c_int32(0)
-        _lib.call("gine_deepset_bwd_num_partials", N, ctypes.byref(parts))
+        _lib.call("gine_deepset_bwd_num_partials", N, a.H, ctypes.byref(parts))
         slab = torch.empty(parts.value * (a.H * a.F + a.H), device=dev)
         dw = torch.empty(a.H, a.F, device=dev)
         db = torch.empty(a.H, device=dev)
