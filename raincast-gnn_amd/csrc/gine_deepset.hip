@@ -439,6 +439,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
       }
     }
     gb += (double)gsum;
+    DS_MARK(2 + 0 * (int)gsum);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const float* erow = buf + (16 * h + q) * LD;
@@ -455,6 +456,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
         tw[j + 3] = __builtin_fmaf(dh[q], e4.w, tw[j + 3]);
       }
     }
+    DS_MARK(3 + 0 * (int)gw[0][0]);
   });
   // slab row of this workgroup: [H*F weights | H bias]
   float* out = slab + (size_t)blockIdx.x * ((size_t)H * F + H);

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--M", type=int, default=11)
     ap.add_argument("--F", type=int, default=35)
     ap.add_argument("--H", type=int, default=128)
+    ap.add_argument("--bwd", action="store_true", help="--prof: profile the backward")
     ap.add_argument("--prof", action="store_true",
                     help="phase profile of the forward (needs GINE_HIP_LIB = the dsprof build)")
     a = ap.parse_args()
@@ -49,11 +50,13 @@ def main():
             n = ctypes.c_int(0)
             fwd()
             lib.gine_debug_ds_prof(buf, ctypes.byref(n))   # reset
-            fwd()
+            (bwd if a.bwd else fwd)()
             lib.gine_debug_ds_prof(buf, ctypes.byref(n))
             ev = [(buf[2 * i], buf[2 * i + 1]) for i in range(n.value)]
-            names = {0: "top", 1: "loads issued", 2: "mfma chain", 3: "epilogue",
-                     4: "mask store", 5: "lds store", 6: "barrier"}
+            names = ({0: "top", 1: "loads issued", 2: "dh", 3: "mfma + tail fma",
+                      4: "body end", 5: "lds store", 6: "barrier"} if a.bwd else
+                     {0: "top", 1: "loads issued", 2: "mfma chain", 3: "epilogue",
+                      4: "mask store", 5: "lds store", 6: "barrier"})
             acc, cnt = {}, {}
             for (t0, c0), (t1, c1) in zip(ev, ev[1:]):
                 if t1 == 0:
