@@ -106,3 +106,25 @@ def test_fused_entry_points_validate_without_device():
     assert g(*args, 7, None) == 1                                          # bad epilogue
     assert g(*([p] * 11 + [100, 32, 1, ctypes.byref(plan)] + [p] * 9), 2, None) == 2  # D 32
     assert g(*([p] * 11 + [100, 64, 1, ctypes.byref(plan)] + [p] * 9), 2, None) == 1  # D 64
+
+
+@pytest.mark.parametrize("N,M,H", [(1, 11, 128), (500, 11, 128), (8192, 11, 128),
+                                   (8193, 11, 128), (16000, 11, 128), (16000, 11, 64),
+                                   (16385, 11, 64), (128000, 17, 128), (97, 5, 256),
+                                   (40, 4, 32)])
+def test_deepset_group_layout_sizes(N, M, H):
+    """Host-side sizing of the DeepSet kernels (csrc/gine_deepset.hip): groups of 2G nodes,
+    G = 8 while G = 16 would leave at most one wave per SIMD (H/32 waves per group), each
+    walked as ceil(G*M/16) tiles; one uint16 ReLU mask word per tile and thread (2H
+    threads); backward partials: one per group, capped at 512 (H >= 128) or 1,024."""
+    lib = _lib.load()
+    g16 = -(-N // 32)
+    G = 8 if g16 * (H // 32) <= 1024 else 16
+    groups = -(-N // (2 * G))
+    tpg = -(-(G * M) // 16)
+    nb = ctypes.c_size_t(0)
+    assert lib.gine_deepset_mask_bytes(N, M, H, ctypes.byref(nb)) == 0
+    assert nb.value == groups * tpg * 2 * H * 2
+    n = ctypes.c_int32(0)
+    assert lib.gine_deepset_bwd_num_partials(N, H, ctypes.byref(n)) == 0
+    assert n.value == min(groups, 512 if H >= 128 else 1024)
