@@ -6,7 +6,7 @@
 // The reference materialises the [N, M, H] pre-activation (90 MB at the 24h_mixed
 // benchmark shape) three times per step (Linear output, ReLU output, ReLU gradient).  Here
 // it never leaves the MFMA accumulators.  Rows are (node, member) pairs; a workgroup walks
-// groups of 2G nodes (G = 16, or 8 for small batches) = 2G*M rows as ceil(G*M/16) tiles of
+// groups of 2G nodes (G = 16; 8 or 4 for small batches) = 2G*M rows as ceil(G*M/16) tiles of
 // 32 rows, and each wave owns 32 hidden units.
 // Row placement: the accumulator register q of lane half h (v_mfma_f32_32x32x2_f32 output
 // row (q&3)+8(q>>2)+4h) holds group row G*M*h + 16*t + q in tile t, i.e. half 0 walks the
@@ -528,8 +528,10 @@ inline bool hidden_ok(int H) { return H == 32 || H == 64 || H == 128 || H == 256
 // 20.9 us); at 16,000 nodes and H = 128 8 is no faster (forward 31.5 vs 33.3 us: two waves
 // per SIMD already keep it busy; profiles/r03_s35); at 16,000 nodes and H = 64 forward
 // 31.9 -> 22.9 us, backward (1,000 partials) 38.6 -> 32.7 us (profiles/r03_s38, r03_s39).
+// Below half a wave per SIMD, G = 4 (cfg1's single 500-station graph).
 inline int nodes_per_half(int64_t N, int H) {
-  return ceil_div(N > 0 ? N : 1, 32) * (H / 32) <= 1024 ? 8 : 16;
+  const int64_t waves16 = ceil_div(N > 0 ? N : 1, 32) * (H / 32);
+  return waves16 <= 512 ? 4 : (waves16 <= 1024 ? 8 : 16);
 }
 inline int num_groups(int64_t N, int H) {
   return (int)ceil_div(N > 0 ? N : 1, 2 * nodes_per_half(N, H));
@@ -593,23 +595,25 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   const int groups = num_groups(num_nodes, hidden);
   const int grid = std::min(groups, 1024);
-  const bool g8 = nodes_per_half(num_nodes, hidden) == 8;
+  const int G = nodes_per_half(num_nodes, hidden);
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD_M(H_, KP_, G_, MK_)                                                        \
   hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, \
                      b1, r, mask, num_nodes, members, in_features, groups, FoldArgs{})
+#define LAUNCH_FWD_G(H_, KP_, G_)                             \
+  do {                                                        \
+    if (mask) LAUNCH_FWD_M(H_, KP_, G_, true);                \
+    else LAUNCH_FWD_M(H_, KP_, G_, false);                    \
+  } while (0)
 #define LAUNCH_FWD(H_, KP_)                                   \
   do {                                                        \
-    if (g8) {                                                 \
-      if (mask) LAUNCH_FWD_M(H_, KP_, 8, true);               \
-      else LAUNCH_FWD_M(H_, KP_, 8, false);                   \
-    } else {                                                  \
-      if (mask) LAUNCH_FWD_M(H_, KP_, 16, true);              \
-      else LAUNCH_FWD_M(H_, KP_, 16, false);                  \
-    }                                                         \
+    if (G == 4) LAUNCH_FWD_G(H_, KP_, 4);                     \
+    else if (G == 8) LAUNCH_FWD_G(H_, KP_, 8);                \
+    else LAUNCH_FWD_G(H_, KP_, 16);                           \
   } while (0)
   DS_DISPATCH_H(hidden, KP, DS_FWD_KP, LAUNCH_FWD);
 #undef LAUNCH_FWD
+#undef LAUNCH_FWD_G
 #undef LAUNCH_FWD_M
   GINE_LAUNCH_STATUS();
   return GINE_OK;
@@ -634,7 +638,7 @@ extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const fl
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   const int groups = num_groups(num_nodes, hidden);
   const int grid = bwd_grid(num_nodes, hidden);
-  const bool g8 = nodes_per_half(num_nodes, hidden) == 8;
+  const int G = nodes_per_half(num_nodes, hidden);
   const int64_t per = (int64_t)hidden * in_features + hidden;
   hipStream_t s = as_stream(stream);
   if (num_nodes == 0) {
@@ -645,7 +649,8 @@ extern "C" int gine_deepset_bwd(const float* ens, const uint16_t* mask, const fl
                      dr, slab, num_nodes, members, in_features, groups)
 #define LAUNCH_BWD(H_, KP_)                       \
   do {                                            \
-    if (g8) LAUNCH_BWD_G(H_, KP_, 8);             \
+    if (G == 4) LAUNCH_BWD_G(H_, KP_, 4);         \
+    else if (G == 8) LAUNCH_BWD_G(H_, KP_, 8);    \
     else LAUNCH_BWD_G(H_, KP_, 16);               \
   } while (0)
     DS_DISPATCH_H(hidden, KP, DS_BWD_KP, LAUNCH_BWD);
@@ -706,22 +711,23 @@ extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const fl
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   const int groups = num_groups(num_nodes, hidden);
   const int walk = num_nodes > 0 ? std::min(groups, 1024) : 0;
-  const bool g8 = nodes_per_half(num_nodes, hidden) == 8;
+  const int G = nodes_per_half(num_nodes, hidden);
   const FoldArgs fold{wr1, br1, wdr, bdr, wfold, x_features};
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD_F(H_, KP_, G_, MK_)                                                        \
   hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_, true>), dim3(walk + kFoldBlocks<H_>),   \
                      dim3(2 * H_), 0, s, ens, w1, b1, r, mask, num_nodes, members, in_features, \
                      groups, fold)
+#define LAUNCH_FWD_G(H_, KP_, G_)                             \
+  do {                                                        \
+    if (mask) LAUNCH_FWD_F(H_, KP_, G_, true);                \
+    else LAUNCH_FWD_F(H_, KP_, G_, false);                    \
+  } while (0)
 #define LAUNCH_FWD(H_, KP_)                                   \
   do {                                                        \
-    if (g8) {                                                 \
-      if (mask) LAUNCH_FWD_F(H_, KP_, 8, true);               \
-      else LAUNCH_FWD_F(H_, KP_, 8, false);                   \
-    } else {                                                  \
-      if (mask) LAUNCH_FWD_F(H_, KP_, 16, true);              \
-      else LAUNCH_FWD_F(H_, KP_, 16, false);                  \
-    }                                                         \
+    if (G == 4) LAUNCH_FWD_G(H_, KP_, 4);                     \
+    else if (G == 8) LAUNCH_FWD_G(H_, KP_, 8);                \
+    else LAUNCH_FWD_G(H_, KP_, 16);                           \
   } while (0)
   if (hidden == 64) {
     DS_FWD_KP(64, KP, LAUNCH_FWD);
@@ -729,6 +735,7 @@ extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const fl
     DS_FWD_KP(128, KP, LAUNCH_FWD);
   }
 #undef LAUNCH_FWD
+#undef LAUNCH_FWD_G
 #undef LAUNCH_FWD_F
   GINE_LAUNCH_STATUS();
   return GINE_OK;

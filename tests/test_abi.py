@@ -114,12 +114,14 @@ def test_fused_entry_points_validate_without_device():
                                    (40, 4, 32)])
 def test_deepset_group_layout_sizes(N, M, H):
     """Host-side sizing of the DeepSet kernels (csrc/gine_deepset.hip): groups of 2G nodes,
-    G = 8 while G = 16 would leave at most one wave per SIMD (H/32 waves per group), each
+    G = 8 while G = 16 would leave at most one wave per SIMD (H/32 waves per group), 4 below
+    half a wave per SIMD, each
     walked as ceil(G*M/16) tiles; one uint16 ReLU mask word per tile and thread (2H
     threads); backward partials: one per group, capped at 512 (H >= 128) or 1,024."""
     lib = _lib.load()
     g16 = -(-N // 32)
-    G = 8 if g16 * (H // 32) <= 1024 else 16
+    waves16 = g16 * (H // 32)
+    G = 4 if waves16 <= 512 else (8 if waves16 <= 1024 else 16)
     groups = -(-N // (2 * G))
     tpg = -(-(G * M) // 16)
     nb = ctypes.c_size_t(0)
