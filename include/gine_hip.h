@@ -482,6 +482,12 @@ int gine_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out
  * reduced in fixed order (deterministic).  db1 may be NULL.
  * ---------------------------------------------------------------------------------- */
 int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32_t hidden, size_t* bytes);
+/* Layout of the mask (for test-side decoding of the forward's ReLU decisions): nodes are
+ * walked in groups of 2G (*nodes_per_half = G); the uint16 word
+ * [(g * ceil(G*M/16) + t) * 2H + (c / 32) * 64 + 32 * h + c % 32] holds in bit q the decision
+ * for hidden unit c of group row G*M*h + 16*t + q, i.e. node 2G*g + G*h + (16t+q) / M,
+ * member (16t+q) % M (rows past G*M or past N are padding, bit 0). */
+int gine_deepset_mask_layout(int64_t num_nodes, int32_t hidden, int32_t* nodes_per_half);
 int gine_deepset_fwd(const float* ens, const float* w1, const float* b1, float* r,
                      uint16_t* mask, int64_t num_nodes, int32_t members, int32_t in_features,
                      int32_t hidden, void* stream);

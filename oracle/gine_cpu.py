@@ -44,28 +44,29 @@ import torch.nn.functional as F
 # ---------------------------------------------------------------------------------------
 
 
-def tie_relu(v, decide=None):
-    """relu(v); with ``decide`` = (on, band, log): where |v| <= band * max|v| -- a decision
-    within fp32 rounding of zero, which any fp32 implementation may take either way -- the
-    boolean ``on`` (another implementation's decision) is taken instead of v > 0, and the
-    number of decisions that differ from v > 0 is appended to ``log``.  The tie-break
-    oracle of tests/helpers.check_training_step: the exact gradient on the engine's side
-    of each such tie."""
+def tie_relu(v, decide=None, **ctx):
+    """relu(v); with ``decide`` (a callable ``decide(v, **ctx) -> bool mask``) the ReLU keeps
+    ``v`` where the mask is set instead of where ``v > 0``.  The hook of the tie-break oracle
+    (tests/helpers.EngineTies): an fp64 restatement that follows another implementation's
+    ReLU decisions after checking that each one that differs from ``v > 0`` lies within that
+    implementation's forward rounding bound of zero -- the exact gradient of the branch the
+    implementation took.  ``ctx`` carries the operands the bound is computed from."""
     if decide is None:
         return v.relu()
-    on, band, log = decide
-    amb = v.abs() <= band * v.abs().max()
-    keep = torch.where(amb, on.to(v.device), v > 0)
-    log.append(int((keep != (v > 0)).sum()))
+    keep = decide(v, **ctx)
     return v * keep.to(v.dtype)
 
 
-def gine_aggregate(x, edge_index, edge_attr, lin_w, lin_b, eps, decide=None):
-    """z = scatter_add(relu(x[src] + lin(a)), dst) + (1 + eps) * x  (PyG op sequence)."""
+def gine_aggregate(x, edge_index, edge_attr, lin_w, lin_b, eps, decide=None, record=None):
+    """z = scatter_add(relu(x[src] + lin(a)), dst) + (1 + eps) * x  (PyG op sequence).
+    ``record`` (tests): a dict that receives "dpre" = d loss / d (x_j + lin(a)) in backward."""
     src, dst = edge_index[0], edge_index[1]
     x_j = x.index_select(0, src)
     e = F.linear(edge_attr.reshape(-1, lin_w.size(1)), lin_w, lin_b)
-    m = tie_relu(x_j + e, decide)
+    pre = x_j + e
+    if record is not None and pre.requires_grad:
+        pre.register_hook(lambda g: record.__setitem__("dpre", g.detach()))
+    m = tie_relu(pre, decide, x=x, src=src, edge_attr=edge_attr)
     agg = x.new_zeros(x.size(0), m.size(1)).scatter_add_(0, dst.view(-1, 1).expand_as(m), m)
     return agg + (1 + eps) * x
 
@@ -112,26 +113,33 @@ class OracleGINEConv(nn.Module):
             self.lin = nn.Linear(edge_dim, first.in_features)
         self.eps.data.fill_(eps)
 
-    record = None  # tests may set a list: (x, d z) pairs are appended during backward
-    decide = None  # tests may set {"msg" | "bn" | "res": (on, band, log)} (see tie_relu)
+    record = None  # tests may set a dict: "z" -> (x, d z), "a1" -> d a1, "dpre" -> d message
+    #                pre-activation, filled during backward
+    decide = None  # tests may set {"msg" | "bn" | "res": callable} (see tie_relu)
+    last_r = None  # the ReLU output of the node MLP (the "res" hook's operand)
 
     def _decide(self, key):
         return None if self.decide is None else self.decide.get(key)
 
     def aggregate(self, x, edge_index, edge_attr):
         z = gine_aggregate(x, edge_index, edge_attr, self.lin.weight, self.lin.bias, self.eps,
-                           self._decide("msg"))
+                           self._decide("msg"), self.record)
         if self.record is not None and z.requires_grad:
             xd = x.detach()
-            z.register_hook(lambda g: self.record.append((xd, g.detach())))
+            z.register_hook(lambda g: self.record.__setitem__("z", (xd, g.detach())))
         return z
 
     def forward(self, x, edge_index, edge_attr):
         z = self.aggregate(x, edge_index, edge_attr)
-        if self._decide("bn") is None:
+        if self.decide is None and self.record is None:
             return self.nn(z)
         l1, bn, _, l2 = self.nn
-        return l2(tie_relu(bn(l1(z)), self._decide("bn")))
+        a1 = l1(z)
+        if self.record is not None and a1.requires_grad:
+            a1.register_hook(lambda g: self.record.__setitem__("a1", g.detach()))
+        r = tie_relu(bn(a1), self._decide("bn"), a1=a1, z=z)
+        self.last_r = r
+        return l2(r)
 
 
 class OracleResGnn(nn.Module):
@@ -153,19 +161,27 @@ class OracleResGnn(nn.Module):
         x = x.to(dt)
         edge_attr = edge_attr.to(dt)
         for i, conv in enumerate(self.convolutions):
-            h = tie_relu(conv(x, edge_index, edge_attr), conv._decide("res"))
+            o = conv(x, edge_index, edge_attr)
+            h = tie_relu(o, conv._decide("res"), r=conv.last_r)
             x = h if i == 0 else x + h
         return x
 
 
 class OracleDeepSet(nn.Module):
+    decide = None  # tests may set {"phi" | "rho": callable} (see tie_relu)
+
     def __init__(self, d_in, hidden, out):
         super().__init__()
         self.phi = nn.Sequential(nn.Linear(d_in, hidden), nn.ReLU(), nn.Linear(hidden, hidden))
         self.rho = nn.Sequential(nn.Linear(hidden, hidden), nn.ReLU(), nn.Linear(hidden, out))
 
     def forward(self, ens):
-        return self.rho(self.phi(ens).sum(dim=1))
+        if self.decide is None:
+            return self.rho(self.phi(ens).sum(dim=1))
+        p0, _, p2 = self.phi
+        r0, _, r2 = self.rho
+        s = p2(tie_relu(p0(ens), self.decide.get("phi"))).sum(dim=1)
+        return r2(tie_relu(r0(s), self.decide.get("rho"), s=s))
 
 
 # ---------------------------------------------------------------------------------------

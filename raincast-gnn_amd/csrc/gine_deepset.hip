@@ -584,6 +584,13 @@ extern "C" int gine_deepset_mask_bytes(int64_t num_nodes, int32_t members, int32
   return GINE_OK;
 }
 
+extern "C" int gine_deepset_mask_layout(int64_t num_nodes, int32_t hidden,
+                                        int32_t* nodes_per_half_out) {
+  if (!nodes_per_half_out || num_nodes < 0 || !hidden_ok(hidden)) return GINE_ERR_INVALID;
+  *nodes_per_half_out = nodes_per_half(num_nodes, hidden);
+  return GINE_OK;
+}
+
 extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* b1, float* r,
                                 uint16_t* mask, int64_t num_nodes, int32_t members,
                                 int32_t in_features, int32_t hidden, void* stream) {

@@ -124,7 +124,8 @@ _SIGNATURES = {
     "gine_linear_wgrad": [_c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p, _c_void_p,
                           _c_void_p, _f32, _c_void_p],
     "gine_deepset_mask_bytes": [_i64, _i32, _i32, ctypes.POINTER(_size)],
-    "gine_deepset_fwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
+    "gine_deepset_mask_layout": [_i64, _i32, ctypes.POINTER(_i32)],
+    "gine_deepset_fwd":[_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
                          _i32, _i32, _c_void_p],
     "gine_deepset_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_deepset_bwd": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

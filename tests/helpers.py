@@ -81,22 +81,71 @@ def assert_close_tiebreak(gpu, cpu32, cpu64, tol=1e-5, name="", gpu64=None):
 # ---------------------------------------------------------------------------------------
 # full training step vs the oracle (GPU tests)
 # ---------------------------------------------------------------------------------------
-def _oracle_step(ref, batch, dtype, record=False, decide=None):
+def _oracle_step(ref, batch, dtype, record=False, hooks=None):
+    """One oracle training step in ``dtype``; ``hooks`` = EngineTies.hooks(): the fp64
+    tie-break oracle on the engine's side of every ReLU decision.  ``record``: the model
+    gets ``.scales`` (condition_scales) and each GINE layer's ``.record`` (x, dz, da1)."""
     import copy
     r = copy.deepcopy(ref).to(dtype)
     if record:
         for conv in r.conv.convolutions:
-            conv.record = []
-    if decide is not None:
-        for conv, d in zip(r.conv.convolutions, decide):
+            conv.record = {}
+        r.scales = condition_scales(r)
+    if hooks is not None:
+        conv_hooks, ds_hooks = hooks(r)
+        for conv, d in zip(r.conv.convolutions, conv_hooks):
             conv.decide = d
+        r.deepset.decide = ds_hooks
     b = copy.copy(batch)
     b.x, b.ensemble, b.edge_attr = (t.to(dtype) for t in (batch.x, batch.ensemble,
                                                           batch.edge_attr))
+    r.edge_attr64 = b.edge_attr
     pred = r(b)
     loss = r.crps(pred, batch.y)
     loss.backward()
     return r, pred, loss
+
+
+def condition_scales(model) -> dict:
+    """Per parameter, the sum of the ABSOLUTE values of the terms its gradient adds up:
+    |dY|^T |X| and sum |dY| for every Linear (dY = d loss / d output over all rows, X its
+    input), sum |dY * xhat| and sum |dY| for every BatchNorm1d, filled during backward.
+    A gradient entry g = sum_i t_i computed in floating point is off by at most ~ n u
+    sum_i |t_i|: the componentwise condition scale (``sum |t_i| >= |g|``, equal when the
+    terms do not cancel -- Linear1's bias gradient behind train-mode BN is analytically
+    zero, so its terms cancel completely)."""
+    import torch.nn as tnn
+    scales = {}
+
+    def lin_hook(name):
+        def fwd(mod, inp, out):
+            X = inp[0].detach()
+
+            def bwd(g):
+                G = g.detach().reshape(-1, g.size(-1)).abs()
+                scales[name + ".weight"] = G.t() @ X.reshape(-1, X.size(-1)).abs()
+                scales[name + ".bias"] = G.sum(0)
+            if out.requires_grad:
+                out.register_hook(bwd)
+        return fwd
+
+    def bn_hook(name):
+        def fwd(mod, inp, out):
+            a = inp[0].detach()
+            xhat = (a - a.mean(0)) / torch.sqrt(a.var(0, unbiased=False) + mod.eps)
+
+            def bwd(g):
+                scales[name + ".weight"] = (g.detach() * xhat).abs().sum(0)
+                scales[name + ".bias"] = g.detach().abs().sum(0)
+            if out.requires_grad:
+                out.register_hook(bwd)
+        return fwd
+    for name, m in model.named_modules():
+        if isinstance(m, tnn.Linear):
+            m.register_forward_hook(lin_hook(name))
+        elif isinstance(m, tnn.BatchNorm1d):
+            m.register_forward_hook(bn_hook(name))
+    return scales
 
 
 def fro_rel(a: torch.Tensor, b: torch.Tensor) -> float:
@@ -107,45 +156,258 @@ def fro_rel(a: torch.Tensor, b: torch.Tensor) -> float:
     return (a - b).norm().item() / den if den else (a - b).norm().item()
 
 
-TIE_BAND = 1e-5
+# ---------------------------------------------------------------------------------------
+# the engine's ReLU decisions and their forward rounding bounds
+# ---------------------------------------------------------------------------------------
+U32 = 2.0 ** -24   # unit roundoff of fp32
 
 
-def capture_engine_layers(model):
-    """Wrap the engine's GINE layers so that each layer's output (whose autograd node holds
-    the layer's saved tensors) is kept until ``engine_decisions`` reads it."""
-    outs = []
-    for conv in model.conv.convolutions:
-        for nm in ("forward_relu", "forward_residual_relu"):
-            def wrapped(*a, _fn=getattr(conv, nm), **k):
-                y = _fn(*a, **k)
-                outs.append(y)
-                return y
-            setattr(conv, nm, wrapped)
-    return outs
+def gamma_dot(k: int) -> float:
+    """Forward error factor of one of the engine's K-term fp32 dot products plus bias:
+    |computed - exact| <= gamma_dot(K) * (sum_k |a_k||b_k| + |bias|).  K roundings of the
+    fp32 accumulation and the bias add, plus the split-bf16 products' dropped terms
+    (csrc/gine_bf16x3.hpp: below 2^-22 of |a_k||b_k| per product): (K + 8) u."""
+    return (k + 8) * U32
 
 
-def engine_decisions(outs, model, batch, log):
-    """The engine's ReLU decisions in each GINE layer, restated exactly from the tensors its
-    forward saved (raincast_gnn/functional.py: x, z, a1, y, mask, bn_save): the messages
-    x_j + lin(a) > 0 (lin by the host's CPU Linear, whose rounding the kernels match --
-    functional.edge_linear_flag), the BatchNorm-ReLU a1 * alpha + shift > 0 (gine_mlpsrc.hpp
-    bn_apply) and the output ReLU (the saved residual mask, or y > 0 in layer 0).  As
-    ``decide`` dicts for the oracle's tie_relu, with band TIE_BAND."""
-    import torch.nn.functional as F
-    src = batch.edge_index[0].cpu()
-    ea = batch.edge_attr.float().cpu().reshape(-1, 1)
-    out = []
-    for conv, y in zip(model.conv.convolutions, outs):
-        x, _, a1, ys, mask, bn_save = (t.detach().cpu() if t is not None else None
-                                       for t in y.grad_fn.saved_tensors[:6])
-        lw = conv.lin.weight.detach().float().cpu()
-        lb = conv.lin.bias.detach().float().cpu()
-        msg = (x.index_select(0, src) + F.linear(ea, lw, lb)) > 0
-        bn = (a1 * bn_save[2] + bn_save[3]) > 0
-        res = mask.bool() if mask is not None else ys > 0
-        out.append({"msg": (msg, TIE_BAND, log), "bn": (bn, TIE_BAND, log),
-                    "res": (res, TIE_BAND, log)})
-    return out
+class EngineTies:
+    """The engine's ReLU decisions in one training step, read from the tensors its forward
+    saved, and the hooks through which the fp64 oracle (oracle.gine_cpu.tie_relu) follows
+    them.
+
+    A decision of the engine that differs from the fp64 oracle's own sign is accepted only
+    if the fp64 pre-activation lies within the engine's forward error bound of zero, computed
+    per decision from the saved operands:
+
+    * message ``x_j + lin(a)`` (GINE layer l):  2 (3u (|x_j| + |a||w| + |b|) + |x_j - x64_j|)
+    * BatchNorm-ReLU ``a1 alpha + shift``:  2 (|alpha| dA + |a1||alpha_e - alpha| +
+      |shift_e - shift| + 2u (|a1 alpha_e| + |shift_e|)),
+      dA = |z - z64| |W1|^T + gamma_K (|z| |W1|^T + |b1|)
+    * output ReLU ``o = r W2^T + b2``:  2 (|r - r64| |W2|^T + gamma_K (|r| |W2|^T + |b2|))
+    * DeepSet phi[0] ``ens W0^T + b0``:  2 gamma_F (|ens| |W0|^T + |b0|)  (ens is data)
+    * DeepSet rho[0] ``s Wr^T + br``:  2 (|s - s64| |Wr|^T + gamma_D (|s| |Wr|^T + |br|))
+
+    with the engine's operands (x, z, a1, alpha_e, shift_e, r, s) against the fp64 oracle's
+    on the same branch (x64, z64, ...): local rounding of the engine's own arithmetic plus
+    the propagated difference of its inputs, itself held to ``tol`` (max-norm relative) at
+    every layer input.  The oracle then keeps exactly the engine's decisions, so the
+    gradients it produces are the exact gradients of the branch the engine took, and the
+    engine's gradients are held to ``tol`` against them.  ``log`` rows: (site, decisions,
+    adopted, largest |pre| / bound among the adopted)."""
+
+    def __init__(self, tol=1e-5):
+        self.tol = tol
+        self.layers = []      # per GINE layer: dict of engine tensors (reference order, fp64)
+        self.phi_on = None    # [N, M, H] bool
+        self.s = self.u = None
+        self.log = []
+        self.input_err = []   # (layer, max-norm relative |x_e - x64|)
+        self._outs = []
+        self._front = None
+
+    # ---- capture (before backward: saved tensors are freed by it) ----
+    def attach(self, model):
+        outs = self._outs
+        for conv in model.conv.convolutions:
+            for nm in ("forward_relu", "forward_residual_relu"):
+                def wrapped(*a, _fn=getattr(conv, nm), **k):
+                    y = _fn(*a, **k)
+                    outs.append(y)
+                    return y
+                setattr(conv, nm, wrapped)
+        front = model._front
+
+        def front_wrapped(data, _fn=front):
+            h0 = _fn(data)
+            self._front = h0
+            return h0
+        model._front = front_wrapped
+        return self
+
+    def read(self, model, gb):
+        """Engine tensors of the forward just run on batch ``gb`` (engine order), mapped to
+        the reference order."""
+        import numpy as np
+        import torch.nn.functional as F
+        from raincast_gnn import _lib
+        from raincast_gnn.data import restore_node_order
+
+        def ref(t):
+            return restore_node_order(t.detach(), gb).cpu()
+        src = gb.edge_index[0].cpu()
+        rows = gb.extra.get("node_order")
+        inv = None if rows is None else torch.argsort(rows.cpu())
+        ea = gb.edge_attr.float().cpu().reshape(-1, 1)
+        for conv, y in zip(model.conv.convolutions, self._outs):
+            x, z, a1, ys, mask, bn_save = y.grad_fn.saved_tensors[:6]
+            lw = conv.lin.weight.detach().float().cpu()
+            lb = conv.lin.bias.detach().float().cpu()
+            x_eng = x.detach().cpu()
+            msg = (x_eng.index_select(0, src) + F.linear(ea, lw, lb)) > 0  # engine edge order
+            bn_save = bn_save.detach().cpu()
+            a1r = ref(a1)
+            pre = a1r * bn_save[2] + bn_save[3]                 # gine_mlpsrc.hpp bn_apply
+            self.layers.append({
+                "x": ref(x).double(), "z": ref(z).double(), "a1": a1r.double(),
+                "alpha": bn_save[2].double(), "shift": bn_save[3].double(),
+                "bn_on": pre > 0, "r": pre.clamp_min(0).double(),
+                "res_on": ref(mask).bool() if mask is not None else ref(ys) > 0,
+                "msg_on": msg})  # edges keep their order under the relabelling
+        h0 = self._front
+        assert h0 is not None and h0.grad_fn is not None, "the fused chain did not run"
+        sv = h0.grad_fn.saved_tensors
+        self.s, self.u = ref(sv[2]).double(), ref(sv[3])
+        ds_fn = h0.grad_fn.next_functions[0][0]
+        ens, mask = ds_fn.saved_tensors[:2]
+        N, M, _ = ens.shape
+        H = self.s.size(1)
+        G = ctypes_int(lambda out: _lib.call("gine_deepset_mask_layout", N, H, out))
+        words = mask.detach().cpu().numpy().view(np.uint16)
+        on = torch.from_numpy(decode_deepset_mask(words, N, M, H, G))
+        self.phi_on = on if inv is None else on[inv]
+        self._outs, self._front = [], None
+        return self
+
+    # ---- the oracle's hooks ----
+    def _adopt(self, site, v, on, beta):
+        own = v > 0
+        diff = on != own
+        n = int(diff.sum())
+        worst = float((v.abs() / beta)[diff].max()) if n else 0.0
+        self.log.append((site, v.numel(), n, worst))
+        assert worst <= 1.0, (
+            f"{site}: {n} engine ReLU decisions differ from the fp64 oracle's; the largest "
+            f"|pre| is {worst:.3g}x the engine's forward rounding bound")
+        return on
+
+    def hooks(self, r64):
+        """(per-GINE-layer {"msg", "bn", "res"}, DeepSet {"phi", "rho"}) for the fp64 oracle
+        model ``r64``."""
+        U = U32
+        convs = []
+        for i, (conv, E) in enumerate(zip(r64.conv.convolutions, self.layers)):
+            D = E["z"].size(1)
+            l1, bnm, _, l2 = conv.nn
+
+            def msg(v, x, src, edge_attr, E=E, conv=conv, i=i):
+                xe = E["x"]
+                dx = (xe - x.detach())
+                self.input_err.append((i, float(dx.abs().max() / x.detach().abs().max())))
+                a = edge_attr.detach().reshape(-1, 1).abs()
+                w = conv.lin.weight.detach().reshape(1, -1).abs()
+                b = conv.lin.bias.detach().abs()
+                beta = 2 * (3 * U * (xe.abs().index_select(0, src) + a * w + b)
+                            + dx.abs().index_select(0, src))
+                return self._adopt(f"layer{i}.msg", v.detach(), E["msg_on"], beta)
+
+            def bn(v, a1, z, E=E, l1=l1, bnm=bnm, D=D, i=i):
+                a1d, zd = a1.detach(), z.detach()
+                mean, var = a1d.mean(0), a1d.var(0, unbiased=False)
+                alpha = bnm.weight.detach() / torch.sqrt(var + bnm.eps)
+                shift = bnm.bias.detach() - mean * alpha
+                W = l1.weight.detach().abs().t()
+                dA = ((E["z"] - zd).abs() @ W
+                      + gamma_dot(D) * (E["z"].abs() @ W + l1.bias.detach().abs()))
+                ae = E["a1"]
+                beta = 2 * (alpha.abs() * dA + ae.abs() * (E["alpha"] - alpha).abs()
+                            + (E["shift"] - shift).abs()
+                            + 2 * U * ((ae * E["alpha"]).abs() + E["shift"].abs()))
+                return self._adopt(f"layer{i}.bn", v.detach(), E["bn_on"], beta)
+
+            def res(v, r, E=E, l2=l2, D=D, i=i):
+                W = l2.weight.detach().abs().t()
+                beta = 2 * ((E["r"] - r.detach()).abs() @ W
+                            + gamma_dot(D) * (E["r"].abs() @ W + l2.bias.detach().abs()))
+                return self._adopt(f"layer{i}.res", v.detach(), E["res_on"], beta)
+            convs.append({"msg": msg, "bn": bn, "res": res})
+        p0, r0 = r64.deepset.phi[0], r64.deepset.rho[0]
+
+        def phi(v):
+            K = p0.weight.size(1)
+            beta = 2 * gamma_dot(K) * (self._ens.abs() @ p0.weight.detach().abs().t()
+                                       + p0.bias.detach().abs())
+            return self._adopt("deepset.phi0", v.detach(), self.phi_on, beta)
+
+        def rho(v, s):
+            K = r0.weight.size(1)
+            W = r0.weight.detach().abs().t()
+            beta = 2 * ((self.s - s.detach()).abs() @ W
+                        + gamma_dot(K) * (self.s.abs() @ W + r0.bias.detach().abs()))
+            return self._adopt("deepset.rho0", v.detach(), self.u > 0, beta)
+        return convs, {"phi": phi, "rho": rho}
+
+    def table(self) -> str:
+        lines = [f"{'site':<16} {'decisions':>12} {'adopted':>8} {'max |pre|/bound':>16}"]
+        for site, n, k, w in self.log:
+            lines.append(f"{site:<16} {n:>12} {k:>8} {w:>16.3g}")
+        return "\n".join(lines)
+
+
+def oracle32_ties(ref, batch, tol=1e-5):
+    """An EngineTies whose "engine" is the fp32 oracle itself (CPU tests of the tie-break
+    machinery): one fp32 oracle step with recording hooks -- each ReLU keeps its own
+    decision and stores the operands EngineTies reads from the HIP engine's saved tensors.
+    Returns (ties, fp32 oracle model after backward)."""
+    import copy
+    r = copy.deepcopy(ref).float()
+    t = EngineTies(tol)
+    layers = [dict() for _ in r.conv.convolutions]
+
+    def rec_conv(E, conv):
+        def msg(v, x, src, edge_attr):
+            E["x"] = x.detach().double()
+            E["msg_on"] = v.detach() > 0
+            return E["msg_on"]
+
+        def bn(v, a1, z):
+            bnm = conv.nn[1]
+            a1d = a1.detach()
+            mean, var = a1d.mean(0), a1d.var(0, unbiased=False)
+            alpha = bnm.weight.detach() / torch.sqrt(var + bnm.eps)
+            E.update(z=z.detach().double(), a1=a1d.double(), alpha=alpha.double(),
+                     shift=(bnm.bias.detach() - mean * alpha).double(), bn_on=v.detach() > 0,
+                     r=v.detach().clamp_min(0).double())
+            return E["bn_on"]
+
+        def res(v, r):
+            E["res_on"] = v.detach() > 0
+            return E["res_on"]
+        return {"msg": msg, "bn": bn, "res": res}
+    for conv, E in zip(r.conv.convolutions, layers):
+        conv.decide = rec_conv(E, conv)
+
+    def phi(v):
+        t.phi_on = v.detach() > 0
+        return t.phi_on
+
+    def rho(v, s):
+        t.s, t.u = s.detach().double(), v.detach().clamp_min(0)
+        return v.detach() > 0
+    r.deepset.decide = {"phi": phi, "rho": rho}
+    pred = r(batch)
+    r.crps(pred, batch.y).backward()
+    t.layers = layers
+    t._ens = batch.ensemble.double()
+    return t, r
+
+
+def decode_deepset_mask(words, N, M, H, G):
+    """gine_deepset_fwd's ReLU bit mask (uint16 words, layout of gine_deepset_mask_layout in
+    include/gine_hip.h) -> bool [N, M, H]."""
+    import numpy as np
+    tpg = (G * M + 15) // 16
+    groups = -(-N // (2 * G))
+    w = words.reshape(groups, tpg, H // 32, 2, 32)
+    bits = ((w[..., None] >> np.arange(16, dtype=np.uint16)) & 1).astype(bool)
+    bits = bits.transpose(0, 3, 1, 5, 2, 4).reshape(groups, 2, tpg * 16, H)
+    return np.ascontiguousarray(bits[:, :, :G * M].reshape(groups * 2 * G, M, H)[:N])
+
+
+def ctypes_int(fn) -> int:
+    import ctypes
+    out = ctypes.c_int32(0)
+    fn(ctypes.byref(out))
+    return int(out.value)
 
 
 def engine_order_batch(batch):
@@ -157,42 +419,72 @@ def engine_order_batch(batch):
     return relabel_stations(batch, station_order(batch.edge_index[:, :e1], n))
 
 
-def check_training_step(params, batch, dev, tol=1e-5, seed=42, envelope_threads=None,
-                        relabel=False):
+def branch_grad_table(grads, rb, r32, r64, tol):
+    """Every gradient in ``grads`` (name -> tensor) against the fp64 branch oracle ``rb``
+    (check_training_step, recorded: ``rb.scales``), condition-scaled:
+    max |g - g64| / max S  and  ||g - g64|| / ||S||  with S the parameter's componentwise
+    condition scale (condition_scales; for eps, sum |dz * x|).  Both must be <= ``tol``.
+    Listed for context: the plain normwise error ||g - g64|| / ||g64||, the condition
+    number ||S|| / ||g64||, and the fp32 oracle's own plain normwise error against the
+    plain fp64 oracle.
+    Returns (worst scaled max-norm error, table, names above ``tol``)."""
+    p32, p64 = dict(r32.named_parameters()), dict(r64.named_parameters())
+    pb = dict(rb.named_parameters())
+    rows, fails = [], []
+    worst = 0.0
+    for name, g in grads.items():
+        g, exact = g.detach().double().cpu(), pb[name].grad
+        if name.endswith(".eps"):   # d eps = sum dz * x over N x D terms
+            x64, dz64 = rb.conv.convolutions[int(name.split(".")[2])].record["z"]
+            S = (dz64 * x64).abs().sum().reshape(1)
+        elif ".lin." in name:       # the edge Linear(1, D): sum over edges of d pre (* a)
+            conv = rb.conv.convolutions[int(name.split(".")[2])]
+            dpre = conv.record["dpre"].abs()
+            S = (dpre.sum(0) if name.endswith("bias")
+                 else (dpre * rb.edge_attr64.abs().reshape(-1, 1)).sum(0).reshape(-1, 1))
+        else:
+            S = rb.scales[name]
+        d = (g - exact).reshape(S.shape)
+        e_max = (d.abs().max() / S.abs().max()).item()
+        e_fro = (d.norm() / S.norm()).item()
+        plain = fro_rel(g, exact)
+        kappa = (S.norm() / exact.norm()).item() if exact.norm() > 0 else float("inf")
+        own32 = fro_rel(p32[name].grad, p64[name].grad)
+        ok = e_max <= tol and e_fro <= tol
+        rows.append(f"{name:<36} {e_max:>9.2e} {e_fro:>9.2e} {plain:>9.2e} {kappa:>9.2e} "
+                    f"{own32:>9.2e} {'ok' if ok else 'FAIL'}")
+        if not ok:
+            fails.append(name)
+        worst = max(worst, e_max)
+    table = "\n".join([f"{'parameter':<36} {'max/S':>9} {'norm/S':>9} {'plain':>9} "
+                        f"{'kappa':>9} {'fp32 own':>9}"] + rows)
+    return worst, table, fails
+
+
+def check_training_step(params, batch, dev, tol=1e-5, seed=42, relabel=False, report=None):
     """One training step (DeepSet + dim_red + GINE stack + head + PostProcess + loss +
     backward) of the engine's GNN on ``dev`` against the CPU oracle with the same weights.
 
     Predictions, loss and the BatchNorm running statistics: within ``tol`` (max-norm
     relative) of the fp32 oracle, fp64 oracle as tie-break.
 
-    Gradients, default (small batches): every parameter gradient within ``tol`` of the fp32
-    oracle, fp64 tie-break.  Linear1's bias gradient is analytically zero (train-mode BN
-    follows it), so it always goes through the tie-break.  ``d eps = sum dz*x`` is one
-    cancelling reduction over N*D terms, ill-conditioned in any fp32 implementation: it is
-    checked as |gpu - exact| <= tol * sum |dz*x| with the fp64 oracle as exact.
-
-    ReLU ties (default mode): a decision whose fp64 pre-activation lies within
-    TIE_BAND * max|pre| of zero -- within fp32 rounding -- can go either way in any fp32
-    implementation, and one such decision moves one gradient entry by the whole upstream
-    gradient (e.g. one message x_j + lin(a) of 3e-7 in a GINE layer: 6e-4 on that layer's
-    lin.bias gradient, 2e-5 on the DeepSet's).  The engine's decisions are restated from the
-    tensors its forward saved (engine_decisions) and the fp64 tie-break oracle takes the
-    engine's side of every tie (oracle.gine_cpu.tie_relu); decisions outside the band stay
-    the oracle's own, and at most 1e-5 of all decisions may be adopted.
-
-    Gradients, ``envelope_threads`` given (benchmark-size batches): at 10^4-10^5 nodes a step
-    makes ~10^8 ReLU decisions, and the ones whose fp32 pre-activation lies within rounding
-    of zero go either way in ANY fp32 implementation -- the forward barely notices (ReLU is
-    continuous) but each such decision switches one gradient entry between 0 and the
-    upstream gradient.  The reference restatement itself, run with 1 thread and with all
-    threads, then differs from the exact gradient by 1e-4..5e-3 (tools/diag_grads.py,
-    DESIGN.md 4).  There the bar is the reference's own envelope: for every parameter,
-    ||gpu - fp64|| / ||fp64|| <= max(tol, 2 * the largest such error of the fp32 oracle over
-    the thread counts ``envelope_threads``).
+    Gradients: every parameter gradient within ``tol`` of the fp64 oracle ON THE ENGINE'S
+    BRANCH, both max-norm relative (max |g - g64| / max |g64|) and normwise (||g - g64|| /
+    ||g64||).  A ReLU decision whose pre-activation lies within fp32 rounding of zero can go
+    either way in any fp32 implementation, and each such decision moves one gradient entry by
+    the whole upstream gradient -- at 10^4-10^5 nodes a step makes ~10^8 decisions and the
+    reference restatement itself, at 1 vs all threads, differs from the exact gradient by
+    1e-4..5e-3.  So the fp64 oracle follows the engine's decisions (EngineTies), each
+    differing one checked against the engine's forward error bound computed from the saved
+    operands, and the engine's gradients are then held to ``tol`` against that exact
+    branch gradient.  Two reductions are ill-conditioned in any fp32 implementation and get
+    their condition scale: ``d eps = sum dz*x`` (|err| <= tol * sum |dz*x|) and Linear1's
+    bias gradient, analytically zero behind train-mode BN (|err| <= tol * sum_n |d a1|,
+    normwise over channels).
     ``relabel``: the engine runs the batch in its locality order (engine_order_batch) and
-    its predictions are mapped back to the collated order; the oracle runs the reference
-    order.
-    Returns the worst relative gradient error against the fp32 oracle."""
+    its tensors are mapped back to the collated order; the oracle runs the reference order.
+    ``report``: a list the per-parameter error table and the decision table are appended to.
+    Returns the worst max-norm relative gradient error against the fp64 branch oracle."""
     from oracle import gine_cpu as O
     from raincast_gnn.models import GNN
     torch.manual_seed(seed)
@@ -205,76 +497,36 @@ def check_training_step(params, batch, dev, tol=1e-5, seed=42, envelope_threads=
     model = model.to(dev).train()
     from raincast_gnn.data import restore_node_order
     gb = engine_order_batch(batch) if relabel else batch
-    layer_outs = None if relabel else capture_engine_layers(model)
-    pred = model(gb.to(dev))
-    loss = model.loss_fn.crps(pred, gb.y.to(dev))
-    ties = []
-    decide = None if relabel else engine_decisions(layer_outs, model, batch, ties)
-    layer_outs = None
+    ties = EngineTies(tol).attach(model)
+    gbd = gb.to(dev)
+    pred = model(gbd)
+    loss = model.loss_fn.crps(pred, gbd.y)
+    ties.read(model, gbd)
+    ties._ens = batch.ensemble.double()
     loss.backward()
     pred = restore_node_order(pred, gb)
     r32, pred32, loss32 = _oracle_step(ref, batch, torch.float32)
-    r64, pred64, loss64 = _oracle_step(ref, batch, torch.float64, record=True)
-    # the fp64 oracle on the engine's side of every decision within fp32 rounding of zero
-    # (oracle.gine_cpu.tie_relu): the exact gradient of the branch the engine took
-    p64e = p64t = None
-    if decide is not None:
-        r64t = _oracle_step(ref, batch, torch.float64, decide=decide)[0]
-        p64t = dict(r64t.named_parameters())
-        n_dec = sum(d["msg"][0].numel() + d["bn"][0].numel() + d["res"][0].numel()
-                    for d in decide)
-        adopted = sum(ties)
-        assert adopted <= 1e-5 * n_dec, f"{adopted} tie decisions of {n_dec}"
-        if adopted:
-            print(f"engine took the other side of {adopted} ReLU ties (|pre| <= "
-                  f"{TIE_BAND} max|pre|) of {n_dec} decisions")
+    r64, pred64, loss64 = _oracle_step(ref, batch, torch.float64)
+    # the fp64 oracle on the engine's side of every decision (asserted within its bound)
+    rb = _oracle_step(ref, batch, torch.float64, record=True, hooks=ties.hooks)[0]
+    n_dec = sum(n for _, n, _, _ in ties.log)
+    adopted = sum(k for _, _, k, _ in ties.log)
+    assert adopted <= 1e-5 * n_dec, f"{adopted} adopted decisions of {n_dec}"
+    worst_in = max(e for _, e in ties.input_err)
+    assert worst_in <= tol, f"GINE layer input differs from the branch oracle by {worst_in:.2e}"
     assert loss.dtype == loss32.dtype
     assert pred.shape == pred32.shape
     assert_close_tiebreak(pred.detach().cpu(), pred32.detach(), pred64.detach(), tol, "pred")
     assert_close_tiebreak(loss.detach().cpu().reshape(1), loss32.detach().reshape(1),
                           loss64.detach().reshape(1), tol, "loss")
-    p32, p64 = dict(r32.named_parameters()), dict(r64.named_parameters())
-    p64e = p64t if p64t is not None else p64
-    worst = 0.0
-    if envelope_threads:
-        runs = [p32]
-        nthr = torch.get_num_threads()
-        try:
-            for t in envelope_threads:
-                if t != nthr:
-                    torch.set_num_threads(t)
-                    runs.append(dict(_oracle_step(ref, batch, torch.float32)[0]
-                                     .named_parameters()))
-        finally:
-            torch.set_num_threads(nthr)
-        for name, p in model.named_parameters():
-            exact = p64[name].grad
-            if name.endswith(".nn.0.bias"):   # analytically zero: compare absolute sizes
-                assert p.grad.abs().max() <= 2 * max(r[name].grad.abs().max() for r in runs)
-                continue
-            env = max(fro_rel(r[name].grad, exact) for r in runs)
-            e = fro_rel(p.grad, exact)
-            bar = tol
-            if name.endswith(".eps"):  # a cancelling reduction: its condition scale too
-                i = int(name.split(".")[2])
-                x64, dz64 = r64.conv.convolutions[i].record[0]
-                bar = tol * (dz64 * x64).abs().sum().item() / max(exact.abs().item(), 1e-300)
-            assert e <= max(bar, 2.0 * env), (
-                f"{name}: gpu vs fp64 {e:.3e} > max({bar:.3e}, 2 x reference envelope "
-                f"{env:.3e})")
-            worst = max(worst, rel_err(p.grad, p32[name].grad))
-    else:
-        for name, p in model.named_parameters():
-            if name.endswith(".eps"):
-                i = int(name.split(".")[2])
-                x64, dz64 = r64.conv.convolutions[i].record[0]
-                scale = (dz64 * x64).abs().sum().item()
-                err = abs(p.grad.item() - p64e[name].grad.item())
-                assert err <= tol * scale, f"{name}: |err| {err:.3e} > {tol} * {scale:.3e}"
-                continue
-            e = assert_close_tiebreak(p.grad.cpu(), p32[name].grad, p64[name].grad, tol, name,
-                                      p64e[name].grad)
-            worst = max(worst, e)
+    grads = {n: p.grad for n, p in model.named_parameters()}
+    worst, table, fails = branch_grad_table(grads, rb, r32, r64, tol)
+    if report is not None:
+        report.append(table)
+        report.append(ties.table())
+    print(table)
+    print(ties.table())
+    assert not fails, f"gradients above {tol} against the fp64 branch oracle: {fails}"
     # BatchNorm running statistics after the step (train mode updates them once)
     for (name, buf), (rname, rbuf) in zip(model.named_buffers(), r32.named_buffers()):
         assert name == rname
