@@ -437,6 +437,7 @@ def roof_of(name: str, rec: dict, layers: int, work: dict, config: str = "cfg2")
     t = pmc_traffic(name, config)
     roof["traffic"] = t["bytes"] if t else None
     roof["traffic_source"] = t["source"] if t else None
+    roof["traffic_tree"] = t["tree"] if t else None
     return roof
 
 
@@ -461,18 +462,29 @@ def roofline_mp(kernels: dict, layers: int, work: dict, config: str = "cfg2"):
 
 
 def copy_ceiling_gbps(device, nbytes=1 << 30, reps=10):
-    """Measured HBM ceiling: device-to-device copy of a 1 GiB buffer (read + write bytes)."""
+    """Measured HBM ceiling: a 1 GiB device-to-device copy by gine_copy_f4 (16-byte-per-lane
+    streaming loads and stores, csrc/gine_probe.hip -- MI355X_MICROARCH.md's measured copy
+    form), read + write bytes per second, on the current stream."""
+    from raincast_gnn import _lib
     src = torch.empty(nbytes // 4, dtype=torch.float32, device=device).fill_(1.0)
     dst = torch.empty_like(src)
-    dst.copy_(src)
+    stream = torch.cuda.current_stream(device)
+    s = _lib.stream_handle(device)
+
+    def copy():
+        _lib.call("gine_copy_f4", _lib.ptr(src), _lib.ptr(dst), nbytes, s)
+    copy()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
+    ev0.record(stream)
     for _ in range(reps):
-        dst.copy_(src)
-    ev1.record()
+        copy()
+    ev1.record(stream)
     ev1.synchronize()
     sec = ev0.elapsed_time(ev1) * 1e-3 / reps
+    ok = torch.equal(dst[:1024], src[:1024]) and torch.equal(dst[-1024:], src[-1024:])
     del src, dst
+    if not ok:
+        raise RuntimeError("gine_copy_f4 copied wrong data")
     return round(2 * nbytes / sec / 1e9, 1)
 
 
@@ -496,15 +508,34 @@ PMC_KERNELS = {
 }
 
 
+def source_tree_hash() -> str:
+    """sha256 (first 16 hex digits) of the sources the library is built from (csrc/*.hip,
+    *.hpp, the Makefile, include/gine_hip.h): the tree a PMC traffic summary was collected
+    on must be this one for its bytes to be reported (tools/pmc_summary.py --tree-hash)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "raincast-gnn_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp"))
+                   + [os.path.join(csrc, "Makefile"), os.path.join(ROOT, "include", "gine_hip.h")])
+    for path in files:
+        h.update(os.path.relpath(path, ROOT).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(kernel: str, config: str = "cfg2"):
     """HBM bytes per call of entry point ``kernel`` from the committed rocprofv3 PMC summary
     (profiles/*pmc_traffic.json: per-kernel (2 x FETCH_SIZE + WRITE_SIZE) bytes per launch,
     the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md), summed over the kernels the
-    call launches; None when no summary of THIS configuration covers them (a summary names
-    its configuration in "_config"; untagged ones were taken on the default cfg2 run)."""
+    call launches; None when no summary of THIS configuration AND THIS source tree covers
+    them (a summary names its configuration in "_config" -- untagged: cfg2 -- and the
+    source_tree_hash() it was collected on in "_tree"; a summary of another tree is not
+    used)."""
     names = PMC_KERNELS.get(kernel)
     if not names:
         return None
+    tree = source_tree_hash()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")),
                        reverse=True):
         try:
@@ -512,12 +543,12 @@ def pmc_traffic(kernel: str, config: str = "cfg2"):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("_config", "cfg2") != config:
+        if d.get("_config", "cfg2") != config or d.get("_tree") != tree:
             continue
         hits = [next((v for alt in (n if isinstance(n, tuple) else (n,))
                       for k, v in d.items() if k.startswith(alt)), None) for n in names]
         if all(h is not None for h in hits):
-            return {"bytes": int(sum(hits)), "source": os.path.basename(path)}
+            return {"bytes": int(sum(hits)), "source": os.path.basename(path), "tree": tree}
     return None
 
 
@@ -929,7 +960,8 @@ def main():
             "value": round(value, 2), "unit": "graphs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic (k-NN station graphs, random-init weights)",
+            "dtype": "f32 (split-bf16x3 GEMM products, fp32 accumulate)",
+            "data": "synthetic (k-NN station graphs, random-init weights)",
             "backend": dist.get_backend() if dist.is_initialized() else None,
             "rccl_world_size": (dist.get_world_size() if dist.is_initialized()
                                 and dist.get_backend() == "nccl" else None),

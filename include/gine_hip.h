@@ -30,8 +30,9 @@
 extern "C" {
 #endif
 
-#define GINE_ABI_VERSION 3  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
-                              3: gine_deepset_bwd_num_partials takes the hidden width */
+#define GINE_ABI_VERSION 4  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
+                              3: gine_deepset_bwd_num_partials takes the hidden width;
+                              4: bn_acc grows two grid-barrier words (gine_mp_fwd_layer) */
 
 #define GINE_OK 0
 #define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
@@ -312,7 +313,7 @@ int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in
 
 /* BatchNorm statistics without a finish launch (training, momentum >= 0; csrc/gine_bnacc.hpp).
  * bn_acc: int64[gine_bn_acc_words(D)] (query it: the size follows the build-time replica count
- * R = GINE_BNACC_REPLICAS, (3R + 1 + 2R) * 2D + 3 words), zeroed once by the caller at allocation,
+ * R = GINE_BNACC_REPLICAS, (3R + 1 + 8) * 2D + 5 words), zeroed once by the caller at allocation,
  * then owned by the kernels (the sums only grow; each consumer differences them against a
  * snapshot the previous consumer left), so one buffer serves every step of one BatchNorm,
  * HIP-graph replays included.  Every producer launch must be followed by exactly one
@@ -341,6 +342,19 @@ int gine_mlp_bwd1_bn(const float* dbn, const float* a1, const float* bn_save, in
                      const float* gamma, float* dgamma, float* dbeta, float* coef,
                      const float* w1, float* dz, int64_t num_nodes, int32_t channels,
                      void* stream);
+/* gine_mlp_bwd2_acc + gine_mlp_bwd1_bn in ONE launch (models/gnn.py:21-26 backward of
+ * Linear2 -> ReLU -> BatchNorm1d -> Linear1's input gradient): the two halves separated by a
+ * grid barrier (csrc/gine_mlp.hip k_mlp_bwd_layer), each workgroup's dbn and a1 tiles kept in
+ * LDS between them, W1 loaded under the barrier's wait.  Same outputs, bit for bit (dbn, coef,
+ * dgamma, dbeta, dz), same pairing protocol on bn_acc.  Applies where gine_mlp_bwd_layer_ok
+ * says so: channels 64 or 128, at most 2 row tiles per workgroup and the whole grid resident
+ * at once (occupancy query, cached per device); GINE_ERR_INVALID otherwise. */
+int gine_mlp_bwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t* ok);
+int gine_mlp_bwd_layer(const float* dy, const float* y, const uint8_t* mask, const float* a1,
+                       const float* bn_save, const float* w2, const float* w1, float* dbn,
+                       int64_t* bn_acc, const float* gamma, float* dgamma, float* dbeta,
+                       float* coef, float* dz, int64_t num_nodes, int32_t channels,
+                       int32_t epilogue, void* stream);
 int gine_mlp_fwd1_acc(const float* z, const float* w1, const float* b1, float* a1,
                       double* partials, int64_t* bn_acc, int64_t num_nodes, int32_t channels,
                       void* stream);
@@ -349,6 +363,25 @@ int gine_mp_fwd_mlp1_acc(const float* x, const int32_t* in_rowptr, const int32_t
                          const float* eps, const float* w1, const float* b1, float* z,
                          float* a1, double* partials, int64_t* bn_acc, int64_t num_nodes,
                          int32_t channels, int32_t max_in_degree, int32_t flags, void* stream);
+/* The whole node-MLP forward of a GINE layer in ONE launch (models/gnn.py:41-44: propagate +
+ * nn + ResGnn's ReLU / residual): gine_mp_fwd_mlp1_acc and gine_mlp_fwd2_bn on the same
+ * workgroups, separated by a grid barrier (csrc/gine_mpmlp.hip k_mp_fwd_layer) -- every a1
+ * tile stays in LDS between the halves, W2 is staged under the barrier's wait.  Same
+ * outputs, bit for bit, as the pair (z, a1, bn_save, running statistics, y, mask), same
+ * pairing protocol on bn_acc (the two barrier words at its end, gine_bn_acc_words).
+ * Applies where gine_mp_fwd_layer_ok says so: channels = 128, max_in_degree <=
+ * GINE_MP_FUSED_MAX_DEGREE, at most 2 row tiles per workgroup and the whole grid resident
+ * on the device at once (occupancy query, cached per device); GINE_ERR_INVALID otherwise. */
+int gine_mp_fwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_degree, int32_t* ok);
+int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                      const float* in_attr, const float* lin_w, const float* lin_b,
+                      const float* eps, const float* w1, const float* b1, float* z, float* a1,
+                      int64_t* bn_acc, const float* gamma, const float* beta,
+                      float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                      float* bn_save, float momentum, float bn_eps, int32_t update_running,
+                      const float* w2, const float* b2, float* y, uint8_t* mask,
+                      int64_t num_nodes, int32_t channels, int32_t max_in_degree, int32_t flags,
+                      int32_t epilogue, void* stream);
 int gine_mlp_fwd2_bn(const float* a1, int64_t* bn_acc, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, int64_t* num_batches_tracked,
                      float* bn_save, float momentum, float bn_eps, int32_t update_running,
@@ -608,6 +641,11 @@ int gine_chain_wgrad_folded_grad_job(int64_t num_nodes, int32_t hidden, int32_t 
 int gine_chain_unfold_grads(const float* gfold, const float* wr1, const float* br1,
                             const float* wdr, float* dwdr, float* dbdr, float* dwr1,
                             float* dbr1, int32_t hidden, int32_t in_features, void* stream);
+
+/* Measurement utility (not on the hot path): copy `bytes` (a multiple of 16) from src to dst
+ * with 16-byte-per-lane streaming loads and stores -- the HBM copy ceiling bench.py prices
+ * the message-passing kernels against (csrc/gine_probe.hip). */
+int gine_copy_f4(const void* src, void* dst, int64_t bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -29,7 +29,10 @@
 // Layout of acc (int64), W = 2 * D words per quantity (sum | sum of squares, or in the
 // backward sum dbn | sum dbn * xhat):
 //   [replica: R][hi | mid | lo: W]   [count: W]
-//   [snapshot: 2][hi | mid | lo | count: W]   phase   consumed[2]
+//   [snapshot: 2][hi | mid | lo | count: W]   phase   consumed[2]   barrier[2]
+// The two barrier words (arrival count, generation; zero at allocation) belong to the
+// one-launch layer forward (gine_mp_fwd_layer), whose producer and consumer halves are
+// separated by a grid barrier instead of a launch boundary (grid_barrier below).
 #pragma once
 
 #include "gine_common.hpp"
@@ -51,7 +54,7 @@ constexpr int kBnAccCountBits = 21;
 constexpr int kBnAccSnap = kBnAccWords + kBnAccCounts;
 
 __host__ __device__ constexpr int64_t bnacc_words(int D) {
-  return (int64_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * 2 * D + 3;
+  return (int64_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * 2 * D + 3 + 2;
 }
 
 __device__ __forceinline__ long long* bnacc_counts(long long* acc, int W) {
@@ -64,6 +67,12 @@ __device__ __forceinline__ long long* bnacc_phase(long long* acc, int W) {
   return acc + (size_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * W;
 }
 
+__device__ __forceinline__ long long* bnacc_barrier(long long* acc, int W) {
+  return bnacc_phase(acc, W) + 3;
+}
+
+// PHASE = false: the caller (gine_mp_fwd_layer) keeps the phase word itself.
+template <bool PHASE = true>
 __device__ __forceinline__ void bnacc_add(long long* acc, int W, int c, double v) {
   if (__builtin_fabs(v) < 4503599627370496.0) {  // 2^52; false for NaN
     long long* r = acc + (size_t)(blockIdx.x % kBnAccReplicas) * kBnAccWords * W;
@@ -80,7 +89,7 @@ __device__ __forceinline__ void bnacc_add(long long* acc, int W, int c, double v
     __hip_atomic_fetch_add(bnacc_counts(acc, W) + c, 1ll << (kBnAccCountBits * k),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (blockIdx.x == 0 && c == 0) {  // one producer launch = one phase (read by the consumer)
+  if (PHASE && blockIdx.x == 0 && c == 0) {  // one producer launch = one phase (read by the consumer)
     long long* ph = bnacc_phase(acc, W);
     *ph = *ph + 1;
   }
@@ -95,7 +104,20 @@ __device__ __forceinline__ void bnacc_add(long long* acc, int W, int c, double v
 // stream, whose start invalidates the L2s.  The consumed phase is kept the same way: a
 // consumer at phase p checks slot (p-1)&1 == p-1 (what a correctly paired previous
 // consumer wrote) and workgroup 0 writes p into slot p&1 (bnacc_mark_consumed).
-__device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool write_snap) {
+// LIVE (the one-launch layer forward, after its grid barrier): the replica and count words
+// are read with agent-scope atomic loads -- the producer's atomics of the same launch were
+// performed at the memory side, and no launch boundary has invalidated this XCD's L2 since
+// -- and the phase / consumed words come from the caller (read before the barrier).
+template <bool LIVE = false>
+__device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool write_snap,
+                                              long long ph_live = 0,
+                                              long long consumed_live = 0) {
+  auto rd = [](long long* p) -> unsigned long long {
+    if constexpr (LIVE)
+      return (unsigned long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      return (unsigned long long)*p;
+  };
   unsigned long long cur_v[kBnAccSnap];
 #pragma unroll
   for (int k = 0; k < kBnAccSnap; ++k) cur_v[k] = 0;
@@ -103,13 +125,14 @@ __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool
   for (int r = 0; r < kBnAccReplicas; ++r) {
 #pragma unroll
     for (int k = 0; k < kBnAccWords; ++k)
-      cur_v[k] += (unsigned long long)acc[(size_t)(r * kBnAccWords + k) * W + t];
+      cur_v[k] += rd(acc + (size_t)(r * kBnAccWords + k) * W + t);
   }
-  const long long* cnt = bnacc_counts(acc, W);
+  long long* cnt = bnacc_counts(acc, W);
 #pragma unroll
-  for (int k = 0; k < kBnAccCounts; ++k) cur_v[kBnAccWords + k] = (unsigned long long)cnt[k * W + t];
+  for (int k = 0; k < kBnAccCounts; ++k) cur_v[kBnAccWords + k] = rd(cnt + k * W + t);
   long long* phw = bnacc_phase(acc, W);
-  const long long ph = phw[0], consumed = phw[1 + ((ph - 1) & 1)];
+  const long long ph = LIVE ? ph_live : phw[0];
+  const long long consumed = LIVE ? consumed_live : phw[1 + ((ph - 1) & 1)];
   long long* prev = bnacc_snap(acc, W) + ((ph - 1) & 1) * kBnAccSnap * W;
   long long* cur = bnacc_snap(acc, W) + (ph & 1) * kBnAccSnap * W;
   long long d[kBnAccSnap];
@@ -133,6 +156,34 @@ __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool
     v = ((double)d[2] * 5.421010862427522e-20 + (double)d[1] * 2.3283064365386963e-10) +
         (double)d[0];  // lo * 2^-64 + mid * 2^-32 + hi, smallest first
   return v;
+}
+
+// Grid-wide barrier of a launch whose workgroups are all resident at once (one per CU; the
+// host checks the occupancy before choosing such a launch): one thread per workgroup, after a
+// __syncthreads.  bar = [arrivals, generation], both zero at allocation; the last arriver
+// resets the count and bumps the generation, so any grid size can reuse the words launch
+// after launch (HIP-graph replays included).  Relaxed agent-scope atomics: the barrier orders
+// only the producer's fixed-point atomics (performed at the memory side; the arriving thread
+// waited for every one of its workgroup's before the __syncthreads, see the caller) against
+// the consumer's atomic loads -- no L2 write-back or invalidate.  A watchdog on the constant
+// 100 MHz clock gives up after ~2 s (a grid that was not co-resident after all) rather than
+// hanging the device: that launch's results are then wrong, which the parity tests see.
+__device__ __forceinline__ void grid_barrier(long long* bar, int nblocks) {
+  const long long gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the generation is read before the arrival is performed (else the last arriver's bump
+  // could be seen here as the old generation)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const long long old = __hip_atomic_fetch_add(bar, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == nblocks - 1) {
+    __hip_atomic_store(bar, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(bar + 1, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;  // ~2 s: give up
+  }
 }
 
 // Record the consumed phase (one thread of workgroup 0 of the consumer).

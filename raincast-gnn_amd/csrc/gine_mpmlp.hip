@@ -29,6 +29,10 @@
 #include "gine_bnacc.hpp"
 #include "gine_edge.hpp"
 #include "gine_bf16x3.hpp"
+#include "gine_mlpsrc.hpp"
+
+#include <algorithm>
+#include <mutex>
 
 namespace gine {
 namespace {
@@ -125,8 +129,12 @@ struct FusedLds {
 static_assert(4 * 32 * kTLD * 4 + 2 * 8 * kD * 8 <= kD * kLD * 4, "scratch fits in w");
 
 // Matrix role (waves 0-3).  Barriers: 1 + (nt + 1), as the gather role.
+// LAYER (gine_mp_fwd_layer): every a1 tile is also kept in LDS (a1k[it], row-major, at most
+// kLayerTiles of them) for the second half of the layer, and the producer's phase word is
+// left to the caller.
+template <bool LAYER = false>
 __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, const TileSeq& ts,
-                                            int nt) {
+                                            int nt, float* a1k = nullptr) {
   const int tid = threadIdx.x;
   const int wave = tid / kWave, lane = tid % kWave;
   const int h = lane >> 5, c32 = lane & 31;
@@ -212,6 +220,9 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
       }
       *reinterpret_cast<float4*>(A.a1 + n * kD + 32 * wave + 4 * cq) =
           make_float4(o4[0], o4[1], o4[2], o4[3]);
+      if constexpr (LAYER)
+        *reinterpret_cast<float4*>(&a1k[(it - 1) * kTileRows * kLD + row * kLD + 32 * wave +
+                                        4 * cq]) = make_float4(o4[0], o4[1], o4[2], o4[3]);
     }
     __builtin_amdgcn_wave_barrier();  // the next tile's transposition writes come after
     __syncthreads();
@@ -230,7 +241,13 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
 #pragma unroll
   for (int g = 0; g < 8; ++g) s += sr[(which * 8 + g) * kD + cc];
   if (A.partials) A.partials[(size_t)blockIdx.x * 2 * kD + which * kD + cc] = s;
-  if (A.bnacc) bnacc_add(A.bnacc, 2 * kD, which * kD + cc, s);
+  if constexpr (LAYER) {
+    bnacc_add<false>(A.bnacc, 2 * kD, which * kD + cc, s);
+    // the atomics are performed before this workgroup arrives at the grid barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (A.bnacc) {
+    bnacc_add(A.bnacc, 2 * kD, which * kD + cc, s);
+  }
 }
 
 // Gather role (waves 4-11).  Barriers: 1 + (nt + 1), as the matrix role.
@@ -346,6 +363,194 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_mlp1(FusedArgs A) {
   else gather_role<FMA>(A, L, ts, nt);
 }
 
+// ---------------------------------------------------------------------------------------
+// The whole node-MLP forward of the layer in one launch (gine_mp_fwd_layer):
+//   phase A = k_mp_fwd_mlp1 (gather -> z, Linear1 -> a1, BatchNorm sums into the fixed-point
+//             accumulator), a1 tiles also kept in LDS;
+//   grid barrier (every workgroup resident: one per CU, host-checked);
+//   phase B = k_fwd2_bnacc on the workgroup's own tiles: BatchNorm finish from the
+//             accumulator totals, r = relu(bn(a1)) from the LDS tiles, Linear2 on the matrix
+//             waves, epilogue (bias, ResGnn ReLU / residual + mask) on the gather waves.
+// W2's fragments and the residual rows are loaded before the barrier, under its wait.
+// Same tile -> workgroup map, same arithmetic and order as the two-launch pair (bit-identical:
+// the BatchNorm totals are integer sums, the MFMA chains and epilogues are the row GEMM's).
+// ---------------------------------------------------------------------------------------
+constexpr int kLayerTiles = 2;  // a1 tiles a workgroup keeps in LDS
+
+struct LayerArgs {
+  const float* W2;
+  const float* b2;
+  float* y;
+  uint8_t* mask;
+  BnFwdParams q;
+};
+
+struct LayerLds {
+  FusedLds f;
+  float a1k[kLayerTiles][kTileRows * kLD];
+  float bn[2 * kD];  // alpha | shift
+  double tot[2 * kD];
+};
+
+template <bool FMA, int EPI>
+__global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, LayerArgs B) {
+  __shared__ __attribute__((aligned(16))) LayerLds L;
+  const TileSeq ts = tile_seq(A.num_tiles, blockIdx.x, gridDim.x);
+  const int nt = ts.count();
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const bool mat = wave < kMatThreads / kWave;
+  long long* phw = bnacc_phase(A.bnacc, 2 * kD);
+  // written by earlier launches only (workgroup 0 moves them after the barrier)
+  const long long ph = phw[0] + 1, consumed = phw[1 + ((ph - 1) & 1)];
+
+  // ---- phase A ----
+  if (mat) matrix_role<true>(A, L.f, ts, nt, &L.a1k[0][0]);
+  else gather_role<FMA>(A, L.f, ts, nt);
+  __syncthreads();  // phase A's LDS use is over (L.f.w is free)
+
+  // ---- W2 fragments and the residual rows, before the barrier ----
+  const int lane = tid % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int col = 32 * wave + c32;  // (matrix waves)
+  if (mat) {
+    const float4* w4 = reinterpret_cast<const float4*>(B.W2);
+    float4 wt[kD * kD4 / kMatThreads];
+#pragma unroll
+    for (int j = 0; j < kD * kD4 / kMatThreads; ++j) wt[j] = w4[tid + kMatThreads * j];
+#pragma unroll
+    for (int j = 0; j < kD * kD4 / kMatThreads; ++j) {
+      const int idx = tid + kMatThreads * j;
+      *reinterpret_cast<float4*>(&L.f.w[(idx / kD4) * kLD + 4 * (idx % kD4)]) = wt[j];
+    }
+  }
+  // epilogue items of the gather waves: rows p / 32 and p / 32 + 16 of a tile, column chunk
+  // p % 32 (p = tid - 256 < 512)
+  const int p = tid - kMatThreads;
+  const int eq = p & 31, er = p >> 5;
+  __syncthreads();  // W2 staged
+  float bf[kKS];
+  BPlanes<kKS> bp;
+  if (mat) {
+    const float* wr = &L.f.w[col * kLD + h * kKS];
+#pragma unroll
+    for (int q = 0; q < kKS / 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(&wr[4 * q]);
+      bf[4 * q] = v.x;
+      bf[4 * q + 1] = v.y;
+      bf[4 * q + 2] = v.z;
+      bf[4 * q + 3] = v.w;
+    }
+    if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
+  }
+  if (tid == 0) grid_barrier(bnacc_barrier(A.bnacc, 2 * kD), gridDim.x);
+  __syncthreads();
+  // the gather waves' epilogue operands, in flight under the BatchNorm finish
+  float4 xres[kLayerTiles][2];
+  float4 bias2 = f4_zero();
+  if (!mat) {
+    bias2 = *reinterpret_cast<const float4*>(B.b2 + 4 * eq);
+#pragma unroll
+    for (int k = 0; k < kLayerTiles; ++k)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        xres[k][i] = f4_zero();
+        if constexpr (EPI == EPI_OUT_RES) {
+          int64_t n = (int64_t)ts.at(k < nt ? k : 0) * kTileRows + er + 16 * i;
+          n = n < A.N ? n : A.N - 1;
+          xres[k][i] = *reinterpret_cast<const float4*>(A.x + n * kD + 4 * eq);
+        }
+      }
+  }
+
+  // ---- phase B: BatchNorm finish (the arithmetic of k_fwd2_bnacc's prologue) ----
+  if (tid < 2 * kD) L.tot[tid] = bnacc_total<true>(A.bnacc, 2 * kD, tid, blockIdx.x == 0, ph,
+                                                  consumed);
+  __syncthreads();
+  if (tid < kD)
+    bn_finish_channel(B.q, kD, tid, L.tot[tid], L.tot[kD + tid], blockIdx.x == 0, &L.bn[tid],
+                      &L.bn[kD + tid]);
+  if (blockIdx.x == 0 && tid == 0) {
+    if (B.q.update_running && B.q.nbt != nullptr) B.q.nbt[0] = B.q.nbt[0] + 1;
+    phw[0] = ph;
+    phw[1 + (ph & 1)] = ph;  // bnacc_mark_consumed
+  }
+  __syncthreads();
+  // r = relu(bn(a1)) in place; rows past N are zero (the row GEMM stages them as zero)
+  for (int e = tid; e < nt * kTileRows * kD4; e += kThreads) {
+    const int k = e / (kTileRows * kD4), r = (e / kD4) % kTileRows, q4 = e % kD4;
+    float* a = &L.a1k[k][r * kLD + 4 * q4];
+    float4 v = *reinterpret_cast<const float4*>(a);
+    const float4 al = *reinterpret_cast<const float4*>(&L.bn[4 * q4]);
+    const float4 sh = *reinterpret_cast<const float4*>(&L.bn[kD + 4 * q4]);
+    v = make_float4(relu_nan(bn_apply(v.x, al.x, sh.x)), relu_nan(bn_apply(v.y, al.y, sh.y)),
+                    relu_nan(bn_apply(v.z, al.z, sh.z)), relu_nan(bn_apply(v.w, al.w, sh.w)));
+    if ((int64_t)ts.at(k) * kTileRows + r >= A.N) v = f4_zero();
+    *reinterpret_cast<float4*>(a) = v;
+  }
+  __syncthreads();
+  for (int k = 0; k < nt; ++k) {
+    float* sO = L.f.z[k & 1];
+    if (mat) {  // Linear2 chain of tile k (the row GEMM's split-bf16 chain and k order)
+      const float* arow = &L.a1k[k][c32 * kLD + h * kKS];
+      floatx16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+      if constexpr (GINE_GEMM_BF16X3) {
+#pragma unroll
+        for (int s8 = 0; s8 < kKS / 8; ++s8) {
+          const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s8]);
+          const float4 a1v = *reinterpret_cast<const float4*>(&arow[8 * s8 + 4]);
+          acc = mfma_bf16x3(split8(a0, a1v), bp.f[s8], acc);
+        }
+        if (wave_any_nan(acc)) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+          acc = mfma_f32_row_mem<kKS>(arow, B.W2 + (size_t)col * kD + h * kKS, 1, acc);
+        }
+      } else {
+        acc = mfma_f32_row<kKS>(arow, bf, acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sO[((r & 3) + 8 * (r >> 2) + 4 * h) * kLD + col] = acc[r];
+    }
+    __syncthreads();  // output tile k in LDS
+    if (!mat) {  // epilogue of tile k (beside the matrix waves' next chain)
+      const int T = ts.at(k);
+      const float bb[4] = {bias2.x, bias2.y, bias2.z, bias2.w};
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = er + 16 * i;
+        const int64_t n = (int64_t)T * kTileRows + r;
+        const float4 v = *reinterpret_cast<const float4*>(&sO[r * kLD + 4 * eq]);
+        if (n >= A.N) continue;
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        const int64_t off = n * kD + 4 * eq;
+        float o4[4];
+        if constexpr (EPI == EPI_OUT_RES) {
+          const float4 xv = k == 0 ? xres[0][i] : xres[1][i];
+          const float xr[4] = {xv.x, xv.y, xv.z, xv.w};
+          unsigned char mk[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float o = vv[c] + bb[c];
+            o4[c] = xr[c] + relu_nan(o);
+            mk[c] = (o > 0.f) ? 1 : 0;
+          }
+          *reinterpret_cast<uchar4*>(B.mask + off) = make_uchar4(mk[0], mk[1], mk[2], mk[3]);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float o = vv[c] + bb[c];
+            o4[c] = (EPI == EPI_OUT_RELU) ? relu_nan(o) : o;
+          }
+        }
+        *reinterpret_cast<float4*>(B.y + off) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+      }
+    }
+  }
+}
+
 }  // namespace
 }  // namespace gine
 
@@ -380,6 +585,118 @@ int mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
   return GINE_OK;
 }
 }  // namespace
+
+namespace {
+// Workgroups of k_mp_fwd_layer the device holds at once (one per CU at most): its grid
+// barrier needs every workgroup resident.  Queried once per device.
+int layer_capacity() {
+  static std::mutex mu;
+  static int cap[64];
+  static bool known[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!known[dev]) {
+    int cus = 0, c = 1 << 30;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    const void* ks[] = {(const void*)k_mp_fwd_layer<true, EPI_OUT>,
+                        (const void*)k_mp_fwd_layer<true, EPI_OUT_RELU>,
+                        (const void*)k_mp_fwd_layer<true, EPI_OUT_RES>,
+                        (const void*)k_mp_fwd_layer<false, EPI_OUT>,
+                        (const void*)k_mp_fwd_layer<false, EPI_OUT_RELU>,
+                        (const void*)k_mp_fwd_layer<false, EPI_OUT_RES>};
+    for (const void* k : ks) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess)
+        return 0;
+      c = std::min(c, nb * cus);
+    }
+    cap[dev] = c;
+    known[dev] = true;
+  }
+  return cap[dev];
+}
+
+// Largest number of tiles one workgroup of the fused grid walks (tile_seq).
+int max_tiles_per_block(int tiles, int grid) {
+  const int span = (tiles + kNumXcd - 1) / kNumXcd;
+  int worst = 0;
+  for (int xcd = 0; xcd < kNumXcd; ++xcd) {
+    const int here = grid / kNumXcd + (xcd < grid % kNumXcd ? 1 : 0);
+    const int range = std::max(0, std::min(tiles, (xcd + 1) * span) - xcd * span);
+    if (range > 0 && here == 0) return 1 << 30;
+    if (range > 0) worst = std::max(worst, (range + here - 1) / here);
+  }
+  return worst;
+}
+
+bool layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_degree) {
+  if (channels != kD || num_nodes <= 0 || max_in_degree < 0 ||
+      max_in_degree > GINE_MP_FUSED_MAX_DEGREE || num_nodes * channels * 4 >= (int64_t(1) << 32))
+    return false;
+  int32_t grid = 0;
+  if (gine_mlp_num_partials(num_nodes, channels, &grid) != GINE_OK) return false;
+  const int tiles = (int)ceil_div(num_nodes, kTileRows);
+  return grid <= layer_capacity() && max_tiles_per_block(tiles, grid) <= kLayerTiles;
+}
+}  // namespace
+
+extern "C" int gine_mp_fwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_degree,
+                                    int32_t* ok) {
+  if (!ok) return GINE_ERR_INVALID;
+  *ok = layer_ok(num_nodes, channels, max_in_degree) ? 1 : 0;
+  return GINE_OK;
+}
+
+extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
+                                 const float* in_attr, const float* lin_w, const float* lin_b,
+                                 const float* eps, const float* w1, const float* b1, float* z,
+                                 float* a1, int64_t* bn_acc, const float* gamma,
+                                 const float* beta, float* running_mean, float* running_var,
+                                 int64_t* num_batches_tracked, float* bn_save, float momentum,
+                                 float bn_eps, int32_t update_running, const float* w2,
+                                 const float* b2, float* y, uint8_t* mask, int64_t num_nodes,
+                                 int32_t channels, int32_t max_in_degree, int32_t flags,
+                                 int32_t epilogue, void* stream) {
+  if (channels != kD) return GINE_ERR_DIM;
+  if ((flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
+  if (!x || !in_rowptr || !in_src || !in_attr || !lin_w || !lin_b || !eps || !w1 || !b1 || !z ||
+      !a1 || !bn_acc || !bn_save || !w2 || !b2 || !y)
+    return GINE_ERR_INVALID;
+  if (!(momentum >= 0.f)) return GINE_ERR_INVALID;
+  if (update_running && (!running_mean || !running_var)) return GINE_ERR_INVALID;
+  if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
+  if (!layer_ok(num_nodes, channels, max_in_degree)) return GINE_ERR_INVALID;
+  int32_t grid = 0;
+  const int st = gine_mlp_num_partials(num_nodes, channels, &grid);
+  if (st != GINE_OK) return st;
+  const int tiles = (int)ceil_div(num_nodes, kTileRows);
+  hipStream_t s = as_stream(stream);
+  const FusedArgs A{x,  in_rowptr, in_src, in_attr, lin_w, lin_b,
+                    eps, w1,       b1,     z,       a1,    nullptr,
+                    reinterpret_cast<long long*>(bn_acc), (int)num_nodes, tiles};
+  const LayerArgs B{w2, b2, y, mask,
+                    BnFwdParams{gamma, beta, running_mean, running_var, num_batches_tracked,
+                                bn_save, num_nodes, momentum, bn_eps, update_running}};
+  const bool fma = !(flags & GINE_MP_LIN_MULADD);
+#define LAYER_LAUNCH(F_, E_) \
+  hipLaunchKernelGGL((k_mp_fwd_layer<F_, E_>), dim3((unsigned)grid), dim3(kThreads), 0, s, A, B)
+  switch (epilogue) {
+    case GINE_EPI_NONE:
+      if (fma) LAYER_LAUNCH(true, EPI_OUT); else LAYER_LAUNCH(false, EPI_OUT);
+      break;
+    case GINE_EPI_RELU:
+      if (fma) LAYER_LAUNCH(true, EPI_OUT_RELU); else LAYER_LAUNCH(false, EPI_OUT_RELU);
+      break;
+    default:
+      if (fma) LAYER_LAUNCH(true, EPI_OUT_RES); else LAYER_LAUNCH(false, EPI_OUT_RES);
+  }
+#undef LAYER_LAUNCH
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
 
 extern "C" int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                                 const float* in_attr, const float* lin_w, const float* lin_b,

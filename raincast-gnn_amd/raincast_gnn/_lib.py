@@ -23,7 +23,7 @@ GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
-ABI_VERSION = 3
+ABI_VERSION = 4
 COUNT_PARTS = 64  # GINE_COUNT_PARTS
 
 _c_void_p = ctypes.c_void_p
@@ -89,12 +89,17 @@ _SIGNATURES = {
     "gine_mlp_fwd1": [_c_void_p] * 5 + [_i64, _i32, _c_void_p],
     "gine_mp_fwd_mlp1": [_c_void_p] * 12 + [_i64, _i32, _i32, _i32, _c_void_p],
     "gine_mp_fwd_mlp1_acc": [_c_void_p] * 13 + [_i64, _i32, _i32, _i32, _c_void_p],
+    "gine_mp_fwd_layer_ok": [_i64, _i32, _i32, ctypes.POINTER(_i32)],
+    "gine_mp_fwd_layer": [_c_void_p] * 18 + [_f32, _f32, _i32] + [_c_void_p] * 4
+                         + [_i64, _i32, _i32, _i32, _i32, _c_void_p],
     "gine_mlp_fwd1_acc": [_c_void_p] * 6 + [_i64, _i32, _c_void_p],
     "gine_mlp_fwd2_bn": [_c_void_p] * 8 + [_f32, _f32, _i32] + [_c_void_p] * 5
                         + [_i64, _i32, _i32, _c_void_p],
     "gine_bn_acc_words": [_i32, _c_void_p],
     "gine_mlp_bwd2_acc": [_c_void_p] * 9 + [_i64, _i32, _i32, _c_void_p],
     "gine_mlp_bwd1_bn": [_c_void_p] * 10 + [_i64, _i32, _c_void_p],
+    "gine_mlp_bwd_layer_ok": [_i64, _i32, ctypes.POINTER(_i32)],
+    "gine_mlp_bwd_layer": [_c_void_p] * 14 + [_i64, _i32, _i32, _c_void_p],
     "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,
                                                                    _i32, _c_void_p],
     "gine_mlp_fwd2": [_c_void_p] * 7 + [_i64, _i32, _i32, _c_void_p],
@@ -125,6 +130,7 @@ _SIGNATURES = {
                           _c_void_p, _f32, _c_void_p],
     "gine_deepset_mask_bytes": [_i64, _i32, _i32, ctypes.POINTER(_size)],
     "gine_deepset_mask_layout": [_i64, _i32, ctypes.POINTER(_i32)],
+    "gine_copy_f4": [_c_void_p, _c_void_p, _i64, _c_void_p],
     "gine_deepset_fwd":[_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
                          _i32, _i32, _c_void_p],
     "gine_deepset_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],

@@ -231,6 +231,38 @@ def engine_in_mp_ok(graph, D: int) -> bool:
     return plan is not None and plan.slice_channels == 32
 
 
+_LAYER_OK = {}
+
+
+def layer_forward_ok(N: int, D: int, max_in_degree) -> bool:
+    """gine_mp_fwd_layer applies (include/gine_hip.h: D = 128, in-degree <= 32, at most two row
+    tiles per workgroup and the whole grid resident at once on this device)."""
+    if max_in_degree is None or not options.LAYER_FWD:
+        return False
+    dev = torch.cuda.current_device()
+    key = (dev, N, D, int(max_in_degree))
+    ok = _LAYER_OK.get(key)
+    if ok is None:
+        out = ctypes.c_int32(0)
+        call("gine_mp_fwd_layer_ok", N, D, int(max_in_degree), ctypes.byref(out))
+        ok = _LAYER_OK[key] = bool(out.value)
+    return ok
+
+
+def layer_backward_ok(N: int, D: int) -> bool:
+    """gine_mlp_bwd_layer applies (include/gine_hip.h: D = 64 or 128, at most two row tiles
+    per workgroup and the whole grid resident at once on this device)."""
+    if not options.LAYER_BWD:
+        return False
+    key = (torch.cuda.current_device(), N, D, "bwd")
+    ok = _LAYER_OK.get(key)
+    if ok is None:
+        out = ctypes.c_int32(0)
+        call("gine_mlp_bwd_layer_ok", N, D, ctypes.byref(out))
+        ok = _LAYER_OK[key] = bool(out.value)
+    return ok
+
+
 _BN_ACC = weakref.WeakKeyDictionary()
 
 
@@ -308,8 +340,17 @@ class GineLayer(torch.autograd.Function):
             partials = torch.empty(P, 2, D, dtype=torch.float64, device=dev)
         else:  # statistics summed by integer atomics, finished inside the second GEMM
             partials = None
+        layer = fused and acc is not None and layer_forward_ok(N, D, graph.max_in_degree)
         with _paired(acc):
-            if fused:
+            if layer:
+                # the whole layer forward in one launch (grid barrier between its halves)
+                call("gine_mp_fwd_layer", ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src),
+                     ptr(graph.in_attr), ptr(lw), ptr(lb), ptr(ep), ptr(w1c), ptr(b1c), ptr(z),
+                     ptr(a1), ptr(acc), ptr(g), ptr(bt), ptr(bn.running_mean),
+                     ptr(bn.running_var), nbt, ptr(bn_save), bn.momentum, bn.eps,
+                     update_running, ptr(w2c), ptr(b2c), ptr(y), ptr(mask), N, D,
+                     graph.max_in_degree, edge_linear_flag(), epilogue, stream)
+            elif fused:
                 # gather of the next tile beside the matrix chain of this one: one launch
                 args = (ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
                         ptr(lw), ptr(lb), ptr(ep), ptr(w1c), ptr(b1c), ptr(z), ptr(a1),
@@ -325,7 +366,9 @@ class GineLayer(torch.autograd.Function):
             else:
                 call("gine_mlp_fwd1_acc", ptr(z), ptr(w1c), ptr(b1c), ptr(a1), None,
                      ptr(acc), N, D, stream)
-            if acc is None:
+            if layer:
+                pass
+            elif acc is None:
                 call("gine_bn_fwd_finalize", ptr(partials), P, ptr(g), ptr(bt),
                      ptr(bn.running_mean), ptr(bn.running_var), nbt, ptr(bn_save), N, D,
                      bn.momentum, bn.eps, int(bn.use_batch_stats), update_running, stream)
@@ -387,11 +430,17 @@ class GineLayer(torch.autograd.Function):
                      ptr(dz), N, D, stream)
             else:
                 with _paired(acc):  # producer + consumer back to back
-                    call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1),
-                         ptr(bn_save), ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi, stream)
-                    call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc),
-                         ptr(g), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz), N, D,
-                         stream)
+                    if layer_backward_ok(N, D):  # both in one launch (grid barrier)
+                        call("gine_mlp_bwd_layer", ptr(dy), ptr(y), ptr(mask), ptr(a1),
+                             ptr(bn_save), ptr(w2c), ptr(w1c), ptr(dbn), ptr(acc), ptr(g),
+                             ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dz), N, D, epi, stream)
+                    else:
+                        call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1),
+                             ptr(bn_save), ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi,
+                             stream)
+                        call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc),
+                             ptr(g), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz),
+                             N, D, stream)
             engine = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epi)
         else:
             # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch

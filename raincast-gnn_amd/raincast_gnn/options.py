@@ -17,6 +17,11 @@ ENGINE_IN_MP True: the node-MLP weight-gradient engine runs inside the window ba
 BN_ACC       True: BatchNorm statistics through the fixed-point accumulator (no finish
              launch) in training mode; False: fp64 partials + finish launch.
 BN_ACC_BWD   the same for the BatchNorm backward sums.
+LAYER_FWD    True: where the fused forward and the accumulator apply and the grid fits the
+             device at once, the whole layer forward in one launch (gine_mp_fwd_layer: the
+             fused forward and the second GEMM separated by a grid barrier); False: the pair.
+LAYER_BWD    True: the BatchNorm-accumulator backward pair (dbn GEMM + BN finish + dz GEMM)
+             in one launch where its grid fits the device at once (gine_mlp_bwd_layer).
 """
 from __future__ import annotations
 
@@ -26,3 +31,5 @@ WINDOW_NODES = 128
 ENGINE_IN_MP = True
 BN_ACC = True
 BN_ACC_BWD = True
+LAYER_FWD = True
+LAYER_BWD = True

@@ -52,6 +52,7 @@ for s in $STEPS; do
                python3 bench.py --steps 5 --warmup 2 --no-cpu --no-strong --no-graph --kernel-reps 5 ${PMC_ARGS:-}
            python tools/pmc_summary.py "$OUT"/pmc_fetch_$P/run_counter_collection.csv \
                "$OUT"/pmc_write_$P/run_counter_collection.csv --config $P \
+               --tree-hash "$(python -c 'import bench; print(bench.source_tree_hash())')" \
                --traffic-json "$OUT/${P}_pmc_traffic.json" > "$OUT/${P}_pmc_summary.txt" 2>&1 ;;
     dist2) run bench_dist2_gloo 600 python bench.py --gpus 2 --dist-backend gloo --steps 10 \
                --warmup 3 --no-cpu ;;

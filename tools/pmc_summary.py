@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--traffic-json")
     ap.add_argument("--filter", default="gine::")
     ap.add_argument("--config", default="cfg2", help="bench configuration the counters ran on")
+    ap.add_argument("--tree-hash", default=None,
+                    help="bench.source_tree_hash() of the tree the counters ran on")
     a = ap.parse_args()
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in a.files:
@@ -40,6 +42,8 @@ def main():
             traffic[k] = round((2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024)
     if a.traffic_json:
         traffic["_config"] = a.config
+        if a.tree_hash:
+            traffic["_tree"] = a.tree_hash
         json.dump(traffic, open(a.traffic_json, "w"), indent=1, sort_keys=True)
 
 
