@@ -128,6 +128,7 @@ class Trainer:
         self.graph_fb = self.graph_opt = None
         self.loss = None
         self.allreduce_in_graph = False
+        self.ar_events = None  # a list: (start, end) HIP events around each split all-reduce
 
     def fwd_bwd(self):
         self.opt.zero_grad()            # set_to_none: kernels write grads into flat slices
@@ -185,7 +186,15 @@ class Trainer:
             return self.eager_step()
         self.graph_fb.replay()
         if self.graph_opt is not None:
-            self.reducer.all_reduce_()
+            if self.ar_events is not None and self.collective:
+                stream = torch.cuda.current_stream(self.device)
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(stream)
+                self.reducer.all_reduce_()
+                ev[1].record(stream)
+                self.ar_events.append(ev)
+            else:
+                self.reducer.all_reduce_()
             self.graph_opt.replay()
         return self.loss
 
@@ -650,6 +659,7 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     # reported time is the wall clock between the synchronised barriers)
     stream = torch.cuda.current_stream(device)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    tr.ar_events = []
     t0 = time.perf_counter()
     evs[0].record(stream)
     for i in range(args.steps):
@@ -662,11 +672,29 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     pct = {q: round(per_step[min(len(per_step) - 1, int(q / 100 * len(per_step)))], 4)
            for q in (10, 50, 90)}
+    # the split all-reduce alone (between the fwd+bwd and AdamW graphs), per step
+    ar = sorted(a.elapsed_time(b) for a, b in tr.ar_events)
+    tr.ar_events = None
+    pct["allreduce_p50"] = round(ar[len(ar) // 2], 4) if ar else None
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+        pct["per_rank"] = gather_per_rank(pct[50], pct["allreduce_p50"], world, device)
     return tr, elapsed, pct
+
+
+def gather_per_rank(step_p50, allreduce_p50, world, device):
+    """Every rank's p50 step time and p50 all-reduce time (ms), for the N > 1 line's
+    decomposition (a tensor all_gather: on the GPU over RCCL, on the CPU over gloo)."""
+    mine = torch.tensor([step_p50, -1.0 if allreduce_p50 is None else allreduce_p50],
+                        device=device if dist.get_backend() == "nccl" else "cpu",
+                        dtype=torch.float64)
+    every = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    return [{"rank": r, "step_ms_p50": round(v[0].item(), 4),
+             "allreduce_ms_p50": round(v[1].item(), 4) if v[1].item() >= 0 else None}
+            for r, v in enumerate(every)]
 
 
 # -----------------------------------------------------------------------------------------
@@ -759,12 +787,17 @@ def dry_run(args, rank: int, world: int) -> None:
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    per = []
     for _ in range(args.steps):
         reducer.flat.fill_(float(rank + 1))
+        t1 = time.perf_counter()
         reducer.all_reduce_()
+        per.append((time.perf_counter() - t1) * 1e3)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ar_p50 = sorted(per)[len(per) // 2] if per else None
+    per_rank = gather_per_rank(ar_p50, ar_p50, world, "cpu") if world > 1 else None
     expect = (world + 1) / 2.0  # mean over ranks of (rank + 1)
     assert torch.allclose(reducer.flat, torch.full_like(reducer.flat, expect)), "all-reduce"
     t = torch.tensor([elapsed], dtype=torch.float64)
@@ -789,7 +822,9 @@ def dry_run(args, rank: int, world: int) -> None:
             "config": {"workload": cfg.name, "global_batch": graphs_per_rank * world,
                        "graphs_per_gpu": graphs_per_rank, "nodes_global": nodes_total,
                        "allreduce_floats": reducer.numel, "parameters": n_params,
-                       "parallelism": f"dp{world}"}}), flush=True)
+                       "parallelism": f"dp{world}"},
+            "allreduce_ms_p50": round(ar_p50, 4) if ar_p50 is not None else None,
+            "per_rank": per_rank}), flush=True)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
@@ -978,6 +1013,11 @@ def main():
                        "allreduce_in_graph": tr.allreduce_in_graph},
             "edges_aggregated_per_s": round(edges_per_s, 1),
             "step_ms_p10_p50_p90": [pct[10], pct[50], pct[90]],
+            # N > 1 decomposition: the gradient all-reduce between the fwd+bwd and AdamW
+            # graphs (HIP events on the step's stream; null when it is captured in the
+            # graph or there is no collective), and every rank's p50 step
+            "allreduce_ms_p50": pct.get("allreduce_p50"),
+            "per_rank": pct.get("per_rank"),
             "roofline": roof, "roofline_step": roof_step,
             "roofline_message_passing": roof_mp,
             "strong_scaling_cfg4": strong,

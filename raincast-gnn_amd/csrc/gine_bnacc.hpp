@@ -29,10 +29,10 @@
 // Layout of acc (int64), W = 2 * D words per quantity (sum | sum of squares, or in the
 // backward sum dbn | sum dbn * xhat):
 //   [replica: R][hi | mid | lo: W]   [count: W]
-//   [snapshot: 2][hi | mid | lo | count: W]   phase   consumed[2]   barrier[2]
-// The two barrier words (arrival count, generation; zero at allocation) belong to the
-// one-launch layer forward (gine_mp_fwd_layer), whose producer and consumer halves are
-// separated by a grid barrier instead of a launch boundary (grid_barrier below).
+//   [snapshot: 2][hi | mid | lo | count: W]   phase   consumed[2]   barrier[kBarWords]
+// The barrier words (zero at allocation) belong to the one-launch layer kernels
+// (gine_mp_fwd_layer, gine_mlp_bwd_layer), whose producer and consumer halves are separated
+// by a grid barrier instead of a launch boundary (grid_barrier below).
 #pragma once
 
 #include "gine_common.hpp"
@@ -52,9 +52,14 @@ constexpr int kBnAccWords = 3;   // hi, mid, lo
 constexpr int kBnAccCounts = 1;  // nan | +inf << 21 | -inf << 42
 constexpr int kBnAccCountBits = 21;
 constexpr int kBnAccSnap = kBnAccWords + kBnAccCounts;
+// grid barrier: one 128-byte line each for the global arrival count, the 8 per-XCD arrival
+// counts and the 8 per-XCD generations
+constexpr int kBarLine = 16;  // int64 words per line
+constexpr int kBarWords = (2 + 2 * kNumXcd) * kBarLine;
 
 __host__ __device__ constexpr int64_t bnacc_words(int D) {
-  return (int64_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * 2 * D + 3 + 2;
+  return (int64_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * 2 * D + 3 +
+         kBarWords;
 }
 
 __device__ __forceinline__ long long* bnacc_counts(long long* acc, int W) {
@@ -160,28 +165,45 @@ __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool
 
 // Grid-wide barrier of a launch whose workgroups are all resident at once (one per CU; the
 // host checks the occupancy before choosing such a launch): one thread per workgroup, after a
-// __syncthreads.  bar = [arrivals, generation], both zero at allocation; the last arriver
-// resets the count and bumps the generation, so any grid size can reuse the words launch
-// after launch (HIP-graph replays included).  Relaxed agent-scope atomics: the barrier orders
-// only the producer's fixed-point atomics (performed at the memory side; the arriving thread
-// waited for every one of its workgroup's before the __syncthreads, see the caller) against
-// the consumer's atomic loads -- no L2 write-back or invalidate.  A watchdog on the constant
-// 100 MHz clock gives up after ~2 s (a grid that was not co-resident after all) rather than
-// hanging the device: that launch's results are then wrong, which the parity tests see.
+// __syncthreads.  Two levels, every word on its own 128-byte line: a workgroup arrives on its
+// XCD's count (blocks are dealt round-robin, so b % 8 is its XCD), the last arriver of each
+// XCD on the global count, and the last of those bumps the 8 per-XCD generations, which each
+// workgroup polls on its own XCD's line.  Same-address atomics serialise at the memory side
+// (256 arrivals on one word cost ~4 us, gine_bnacc.hpp replicas), and 256 pollers on one
+// line contend with the arrivals; this way at most 32 + 8 arrivals and 32 pollers share a
+// line.  Counts are reset by their last arriver, generations only grow, so the words serve
+// any grid size launch after launch (HIP-graph replays included).  Relaxed agent-scope
+// atomics: the barrier orders only the producer's fixed-point atomics (performed at the
+// memory side; the arriving thread waited for every one of its workgroup's before the
+// __syncthreads, see the callers) against the consumer's atomic loads -- no L2 write-back or
+// invalidate.  A watchdog on the constant 100 MHz clock gives up after ~2 s (a grid that was
+// not co-resident after all) rather than hanging the device: that launch's results are then
+// wrong, which the parity tests see.
 __device__ __forceinline__ void grid_barrier(long long* bar, int nblocks) {
-  const long long gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int b = blockIdx.x, x = b % kNumXcd;
+  long long* glob = bar;
+  long long* cnt = bar + (2 + x) * kBarLine;
+  long long* gen = bar + (2 + kNumXcd + x) * kBarLine;
+  const int here = nblocks / kNumXcd + (x < nblocks % kNumXcd ? 1 : 0);
+  const int xcds = nblocks < kNumXcd ? nblocks : kNumXcd;
+  const long long g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the generation is read before the arrival is performed (else the last arriver's bump
   // could be seen here as the old generation)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const long long old = __hip_atomic_fetch_add(bar, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (old == nblocks - 1) {
-    __hip_atomic_store(bar, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(bar + 1, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
+  if (__hip_atomic_fetch_add(cnt, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == here - 1) {
+    __hip_atomic_store(cnt, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(glob, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        xcds - 1) {
+      __hip_atomic_store(glob, 0ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int y = 0; y < xcds; ++y)
+        __hip_atomic_fetch_add(bar + (2 + kNumXcd + y) * kBarLine, 1ll, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
   }
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-    __builtin_amdgcn_s_sleep(1);
+  while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+    __builtin_amdgcn_s_sleep(2);
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;  // ~2 s: give up
   }
 }

@@ -528,10 +528,14 @@ inline bool hidden_ok(int H) { return H == 32 || H == 64 || H == 128 || H == 256
 // 20.9 us); at 16,000 nodes and H = 128 8 is no faster (forward 31.5 vs 33.3 us: two waves
 // per SIMD already keep it busy; profiles/r03_s35); at 16,000 nodes and H = 64 forward
 // 31.9 -> 22.9 us, backward (1,000 partials) 38.6 -> 32.7 us (profiles/r03_s38, r03_s39).
-// Below half a wave per SIMD, G = 4 (cfg1's single 500-station graph).
+// G = 4 at a quarter wave per SIMD or less, i.e. N <= 2,048 nodes at H = 128 and <= 4,096 at
+// H = 64 (cfg1's single 500-station graph: forward / backward 13.1 / 17.1 -> 8.6 / 12.9 us,
+// profiles/r03_s42).  The earlier bound of half a wave per SIMD also put 4,000-node batches
+// at H = 128 on G = 4, where the backward measured slower (21.5 -> 22.4 us), so it stops
+// below that size.
 inline int nodes_per_half(int64_t N, int H) {
   const int64_t waves16 = ceil_div(N > 0 ? N : 1, 32) * (H / 32);
-  return waves16 <= 512 ? 4 : (waves16 <= 1024 ? 8 : 16);
+  return waves16 <= 256 ? 4 : (waves16 <= 1024 ? 8 : 16);
 }
 inline int num_groups(int64_t N, int H) {
   return (int)ceil_div(N > 0 ? N : 1, 2 * nodes_per_half(N, H));

@@ -211,11 +211,11 @@ def _canonical(edge_index, edge_attr, flow="source_to_target"):
 
 
 class _HostFlag:
-    """One pinned host int32 per device that gine_graph_same_edges writes through its device
-    mapping: the answer of a content check reaches the host without a copy operation."""
+    """Pinned host int32 slots per device that gine_graph_same_edges writes through their
+    device mapping: the answers of content checks reach the host without a copy operation."""
 
-    def __init__(self, device):
-        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    def __init__(self, device, slots: int):
+        self.host = torch.zeros(slots, dtype=torch.int32, pin_memory=True)
         dp = ctypes.c_void_p(0)
         _lib.call("gine_host_device_ptr", self.host.data_ptr(), ctypes.byref(dp))
         self.dev_ptr = dp.value
@@ -231,18 +231,26 @@ class _GraphCache:
     * Content: the reference's training loop copies every batch to the device
       (``batch.to(device)``, train.py:62), so each step brings a NEW edge_index tensor
       holding the same static station graph (block-diagonally collated, utils/data.py:300).
-      On an identity miss, a graph built for the same (N, E, flow) is checked against the
-      new edge list on the device (gine_graph_same_edges, one pass over both) and, when
-      equal, reused with its CSRs, window plans and degree bound -- no sort, no host copy of
-      the CSRs, no planning; the only wait is for that one check.  Inside a stream capture
-      (no synchronisation allowed) a miss builds as before.
+      On an identity miss, the graphs built for the same (N, E, flow) -- up to
+      ``per_shape`` distinct edge lists of that size, e.g. two station sets or radius graphs
+      used alternately -- are checked against the new edge list on the device
+      (gine_graph_same_edges, one pass over both per candidate, all candidates in one go)
+      and the first equal one is reused with its CSRs, window plans and degree bound -- no
+      sort, no host copy of the CSRs, no planning.
+      COST: a content check waits for the current stream (one event synchronisation) before
+      it can read its answer, i.e. it drains every kernel queued on that stream first.  The
+      drop-in training loop syncs every step anyway (train.py:71 ``loss.item()``); a loop
+      that passes the SAME edge_index tensor each step never pays it (identity hit).  Inside
+      a stream capture (no synchronisation allowed) a miss builds as before.
     """
 
-    def __init__(self, capacity: int = 8, content_capacity: int = 4):
+    def __init__(self, capacity: int = 8, content_capacity: int = 4, per_shape: int = 4):
         self.capacity = capacity
         self.content_capacity = content_capacity
+        self.per_shape = per_shape
         self._entries: OrderedDict = OrderedDict()
-        self._content: OrderedDict = OrderedDict()   # (shape key, n) -> (graph, ei, attr)
+        # shape key -> [(graph, ei, attr), ...] most recently used first
+        self._content: OrderedDict = OrderedDict()
         self._flags: dict = {}
         self.stats = {"identity_hits": 0, "content_hits": 0, "builds": 0}
 
@@ -259,20 +267,27 @@ class _GraphCache:
         while len(self._entries) > self.capacity:
             self._entries.popitem(last=False)
 
-    def _same(self, dev, ei, attr, ref_ei, ref_attr) -> bool:
+    def _first_same(self, dev, ei, attr, cands) -> int:
+        """Index of the first candidate (graph, ref_ei, ref_attr) whose edge list (and
+        attributes) equal ``ei`` / ``attr``, or -1: one device check per candidate into its
+        own flag slot, then ONE synchronisation of the current stream."""
         flag = self._flags.get(dev)
         if flag is None:
             with torch.cuda.device(dev):
-                flag = self._flags[dev] = _HostFlag(dev)
+                flag = self._flags[dev] = _HostFlag(dev, self.per_shape)
         flag.host.zero_()
         stream = torch.cuda.current_stream(dev)
-        _lib.call("gine_graph_same_edges", ref_ei.data_ptr(), ei.data_ptr(),
-                  _lib.ptr(ref_attr), _lib.ptr(attr), ei.size(1), flag.dev_ptr,
-                  stream.cuda_stream)
+        for i, (_, ref_ei, ref_attr) in enumerate(cands):
+            _lib.call("gine_graph_same_edges", ref_ei.data_ptr(), ei.data_ptr(),
+                      _lib.ptr(ref_attr), _lib.ptr(attr), ei.size(1), flag.dev_ptr + 4 * i,
+                      stream.cuda_stream)
         done = torch.cuda.Event()
         done.record(stream)
         done.synchronize()
-        return int(flag.host[0]) == 0
+        for i in range(len(cands)):
+            if int(flag.host[i]) == 0:
+                return i
+        return -1
 
     def get(self, edge_index, edge_attr, num_nodes, flow="source_to_target") -> GineGraph:
         key = self._key(edge_index, edge_attr, num_nodes, flow)
@@ -287,17 +302,19 @@ class _GraphCache:
         capturing = torch.cuda.is_current_stream_capturing()
         ckey = (int(num_nodes), int(edge_index.size(-1)), flow, edge_index.device,
                 edge_attr is None)
-        if not capturing and edge_index.is_cuda:
-            cand = self._content.get(ckey)
-            if cand is not None:
-                graph, ref_ei, ref_attr = cand
-                ei, attr = _canonical(edge_index, edge_attr, flow)
-                if graph._checked and self._same(edge_index.device, ei, attr, ref_ei,
-                                                  ref_attr):
-                    self._content.move_to_end(ckey)
-                    self._remember(key, graph, edge_index, edge_attr)
-                    self.stats["content_hits"] += 1
-                    return graph
+        cands = self._content.get(ckey) if not capturing and edge_index.is_cuda else None
+        if cands:
+            ei, attr = _canonical(edge_index, edge_attr, flow)
+            usable = [c for c in cands if c[0]._checked]
+            i = self._first_same(edge_index.device, ei, attr, usable) if usable else -1
+            if i >= 0:
+                c = usable[i]
+                cands.remove(c)
+                cands.insert(0, c)
+                self._content.move_to_end(ckey)
+                self._remember(key, c[0], edge_index, edge_attr)
+                self.stats["content_hits"] += 1
+                return c[0]
         graph = GineGraph(edge_index, edge_attr, num_nodes, flow)
         self.stats["builds"] += 1
         self._remember(key, graph, edge_index, edge_attr)
@@ -305,7 +322,9 @@ class _GraphCache:
             ei, attr = _canonical(edge_index, edge_attr, flow)
             # private copies: an in-place change of the caller's tensor must not change
             # what later content checks compare against
-            self._content[ckey] = (graph, ei.clone(), None if attr is None else attr.clone())
+            lst = self._content.setdefault(ckey, [])
+            lst.insert(0, (graph, ei.clone(), None if attr is None else attr.clone()))
+            del lst[self.per_shape:]
             self._content.move_to_end(ckey)
             while len(self._content) > self.content_capacity:
                 self._content.popitem(last=False)

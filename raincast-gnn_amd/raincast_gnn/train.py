@@ -286,12 +286,21 @@ def main(argv=None) -> dict:
     ap.add_argument("--radius", action="store_true", help="radius graph of params max_dist")
     ap.add_argument("--epochs", type=int, default=None, help="override max_epochs")
     ap.add_argument("--eager", action="store_true", help="no HIP-graph replay")
+    ap.epilog = ("Data parallel (torchrun, one process per GPU): the world size must divide "
+                 "params.json's batch_size, so every rank gets an equal shard of each batch.")
     ap.add_argument("--allreduce", choices=("split", "graph"), default="split",
                     help="data-parallel all-reduce between the step's two graphs (split) or "
                          "captured inside one (graph, RCCL); see StepRunner")
     args = ap.parse_args(argv)
 
     rank, local_rank, world = env_rank()
+    config = load_params(os.path.join(args.dir, "params.json"))
+    bs = config["batch_size"]
+    if world > 1 and bs % world:
+        # DeviceLoader's condition (equal shards in every full batch), reported up front
+        raise SystemExit(f"params.json batch_size {bs} is not a multiple of the {world} "
+                         f"data-parallel ranks; run with a world size that divides it "
+                         f"(24h_mixed: batch_size 8 -> 1, 2, 4 or 8 GPUs)")
     if world > 1 and not dist.is_initialized():
         dist.init_process_group("nccl")
     os.makedirs(os.path.join(args.dir, "logs"), exist_ok=True)
@@ -300,7 +309,6 @@ def main(argv=None) -> dict:
                             args.dir, "logs", f"train_{args.run_id}.log"), mode="w"),
                             logging.StreamHandler(sys.stdout)])
     set_seed(args.seed)
-    config = load_params(os.path.join(args.dir, "params.json"))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     samples = synthetic_samples(args.stations, args.samples, k=args.k, seed=args.seed,
@@ -308,7 +316,6 @@ def main(argv=None) -> dict:
     full = DeviceDataset(samples, device)
     train_set, val_set = split_train_val(full)
     log.info(f"Dataset sizes => Train: {len(train_set)}, Val: {len(val_set)}")
-    bs = config["batch_size"]
     train_loader = DeviceLoader(train_set, bs, shuffle=True, seed=args.seed, rank=rank,
                                 world=world)
     val_loader = DeviceLoader(val_set, bs, shuffle=False)

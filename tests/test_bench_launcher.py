@@ -41,6 +41,13 @@ def test_dry_run_reports_requested_ranks(gpus):
     assert d["backend"] == ("gloo" if gpus > 1 else None)
     assert d["launcher"] is (gpus > 1)
     assert d["value"] > 0
+    # the N > 1 decomposition: the all-reduce time and every rank's p50
+    assert d["allreduce_ms_p50"] is not None and d["allreduce_ms_p50"] >= 0
+    if gpus > 1:
+        assert [r["rank"] for r in d["per_rank"]] == list(range(gpus))
+        assert all(r["allreduce_ms_p50"] >= 0 for r in d["per_rank"])
+    else:
+        assert d["per_rank"] is None
 
 
 @pytest.mark.timeout(300)

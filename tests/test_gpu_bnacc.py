@@ -32,10 +32,18 @@ def _words(D):
     return w.value
 
 
+BAR_WORDS = (2 + 2 * 8) * 16  # gine_bnacc.hpp kBarWords: the grid-barrier lines at the end
+
+
 def _replicas(D):
-    """Replica count of the accumulator layout (gine_bnacc.hpp): words = (3R + 9) 2D + 5
-    (phase, two consumed words, two grid-barrier words at the end)."""
-    return ((_words(D) - 5) // (2 * D) - 9) // 3
+    """Replica count of the accumulator layout (gine_bnacc.hpp): words = (3R + 9) 2D + 3 +
+    BAR_WORDS (phase, two consumed words, then the grid-barrier words)."""
+    return ((_words(D) - 3 - BAR_WORDS) // (2 * D) - 9) // 3
+
+
+def phase_index(D):
+    """Offset of the phase word (consumed[2] follow it)."""
+    return _words(D) - 3 - BAR_WORDS
 
 
 def _conv(D, seed):
@@ -77,8 +85,9 @@ def test_bn_acc_matches_finish_launch(D, epilogue, monkeypatch):
     torch.testing.assert_close(got[2], ref[2], rtol=TOL, atol=TOL)
     assert got[3] == ref[3] == 3
     acc = Fn._BN_ACC[conv.nn[1]][(DEV, "fwd")]
-    assert acc.numel() == _words(D) and int(acc[-5]) == 3   # phase: one per producer launch
-    assert int(acc[-4 + (3 & 1)]) == 3                       # consumed: the last consumer
+    ph = phase_index(D)
+    assert acc.numel() == _words(D) and int(acc[ph]) == 3   # phase: one per producer launch
+    assert int(acc[ph + 1 + (3 & 1)]) == 3                   # consumed: the last consumer
 
 
 def test_bn_acc_deterministic(monkeypatch):
@@ -144,8 +153,9 @@ def test_fused_forward_acc_equals_unfused(n, max_deg):
     tot = (rep[0].double() + rep[1].double() * 2.0**-32 + rep[2].double() * 2.0**-64).view(2, D)
     torch.testing.assert_close(tot[0], a64.sum(0), rtol=1e-12, atol=1e-9)
     torch.testing.assert_close(tot[1], (a64 * a64).sum(0), rtol=1e-12, atol=1e-9)
-    assert int(acc0[R * 3 * W:-5].abs().sum()) == 0       # no non-finite counts, no snapshot
-    assert int(acc0[-5]) == 1 and int(acc0[-4:].abs().sum()) == 0
+    ph = phase_index(D)
+    assert int(acc0[R * 3 * W:ph].abs().sum()) == 0       # no non-finite counts, no snapshot
+    assert int(acc0[ph]) == 1 and int(acc0[ph + 1:].abs().sum()) == 0
 
 
 def test_bn_acc_entry_points_validate():
@@ -153,8 +163,9 @@ def test_bn_acc_entry_points_validate():
     a = torch.zeros(64, 64, device=DEV)
     words = ctypes.c_int64(0)
     assert _lib.load().gine_bn_acc_words(64, ctypes.byref(words)) == 0
-    # [R replicas x 3 words | 1 packed count word | 2 snapshots x 4 words] x 2D + 5
-    assert words.value == (3 * _replicas(64) + 1 + 8) * 128 + 5 and _replicas(64) == 4
+    # [R replicas x 3 words | 1 packed count word | 2 snapshots x 4 words] x 2D + 3 + barrier
+    assert words.value == (3 * _replicas(64) + 1 + 8) * 128 + 3 + BAR_WORDS
+    assert _replicas(64) == 4
     acc = torch.zeros(words.value, dtype=torch.int64, device=DEV)
     save = torch.empty(4, 64, device=DEV)
     w = torch.zeros(64, 64, device=DEV)

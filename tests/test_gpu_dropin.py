@@ -53,6 +53,24 @@ def test_content_hit_reuses_graph_and_miss_rebuilds():
     assert g4 is not g0 and cache.stats["builds"] == 4
 
 
+def test_content_cache_alternating_graphs_of_one_size():
+    """Two distinct edge lists of the same size (two station sets) used alternately, each
+    step a fresh device copy: after one build each, every step is a content hit."""
+    cache = _GraphCache()
+    ba = collate(synthetic_samples(120, 3, k=6, seed=2))
+    bb = collate(synthetic_samples(120, 3, k=6, seed=9))
+    assert ba.edge_index.shape == bb.edge_index.shape and not torch.equal(ba.edge_index,
+                                                                           bb.edge_index)
+    n = ba.num_nodes
+    ga = cache.get(ba.edge_index.to(DEV), ba.edge_attr.to(DEV), n)
+    gb = cache.get(bb.edge_index.to(DEV), bb.edge_attr.to(DEV), n)
+    assert ga is not gb and cache.stats["builds"] == 2
+    for step in range(6):
+        b, g = (ba, ga) if step % 2 == 0 else (bb, gb)
+        assert cache.get(b.edge_index.to(DEV), b.edge_attr.to(DEV), n) is g
+    assert cache.stats["builds"] == 2 and cache.stats["content_hits"] == 6
+
+
 def test_content_check_odd_sizes():
     """Edge counts whose int64 list is not a whole number of 16-byte vectors, unaligned
     views, and E = 0."""

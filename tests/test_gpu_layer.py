@@ -77,9 +77,15 @@ def test_layer_forward_equals_pair(nodes, graphs, k, epilogue, monkeypatch):
             assert torch.equal(a, b)
     assert torch.equal(mixed[1], pair[1]) and torch.equal(mixed[2], pair[2])
     assert mixed[3] == pair[3] == 3
+    from test_gpu_bnacc import BAR_WORDS, phase_index
     acc = Fn._BN_ACC[conv.nn[1]][(DEV, "fwd")]
-    assert int(acc[-5]) == 6 and int(acc[-4 + (6 & 1)]) == 6   # phase / consumed, both runs
-    assert int(acc[-2]) == 0                                   # barrier count back at zero
+    ph = phase_index(128)
+    assert int(acc[ph]) == 6 and int(acc[ph + 1 + (6 & 1)]) == 6   # phase / consumed
+    bar = acc[ph + 3:].view(-1, 16)[:, 0]                 # one word per 128-byte line
+    assert bar.numel() == BAR_WORDS // 16
+    assert int(bar[:10].abs().sum()) == 0                 # every arrival count back at zero
+    gens = bar[10:18]                                     # per-XCD generations: one per launch
+    assert int(gens.max()) == 2 and int(gens.min()) >= 0
 
 
 def test_layer_forward_ok_limits():

@@ -92,6 +92,20 @@ def test_data_parallel_loader_needs_equal_shards_and_a_batch():
         T.train_one_epoch(_OracleModel(), loader, None, "cpu")
 
 
+def test_cli_rejects_a_world_size_that_does_not_divide_the_batch(tmp_path, monkeypatch):
+    """24h_mixed's batch_size 8 over 3 ranks: the train CLI stops before any process group
+    or device is set up, naming the constraint."""
+    import json
+    import pytest
+    from raincast_gnn.params import EXPERIMENTS
+    (tmp_path / "params.json").write_text(json.dumps(EXPERIMENTS["24h_mixed"]))
+    monkeypatch.setenv("WORLD_SIZE", "3")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    with pytest.raises(SystemExit, match="not a multiple of the 3"):
+        T.main(["--dir", str(tmp_path), "--run_id", "x"])
+
+
 def test_step_runner_allreduce_choice():
     """The data-parallel all-reduce form is chosen up front, as bench.py's --allreduce:
     split by default, graph on request, anything else rejected."""
