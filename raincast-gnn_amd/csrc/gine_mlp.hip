@@ -1094,6 +1094,10 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
   const long long ph = phw[0] + 1, consumed = phw[1 + ((ph - 1) & 1)];
   const TileRange tr = xcd_tile_range(num_tiles, blockIdx.x, gridDim.x);
   const int nt = tr.first < tr.end ? (tr.end - tr.first + tr.step - 1) / tr.step : 0;
+  // rgprof build (tools/layer_prof.py): workgroup 0's phase stamps
+  [[maybe_unused]] const int vb = blockIdx.x;
+  RG_DECL;
+  RG_MARK(10);
 
   // ---- phase A: dbn = relu'(BN) . (do W2), BatchNorm backward sums ----
   // tile k+1's inputs are in flight during tile k's chain (tile 0's under the W2 loads); the
@@ -1115,6 +1119,7 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
   load_wk<D, KS>(W2, col, h, bf);
   BPlanes<KS> bp;
   if constexpr (GINE_GEMM_BF16X3 && KS <= 64) bp.from(bf);
+  RG_MARK(11);
   const ColConst kc = col_const<PDO>(pa, D, q_me);
   const BnView bv = bn_view(pa.bn, D);
   const float4 al4 = *reinterpret_cast<const float4*>(bv.alpha + 4 * q_me);
@@ -1134,8 +1139,13 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
       *reinterpret_cast<float4*>(&L.ka[k][r * LD + 4 * q_me]) = ep[i];
     }
     __syncthreads();
+    RG_MARK(12);
     if (k + 1 < nt) load_tile(k + 1);
     const floatx16 c = chain_tile<D, KS>(&L.a[c32 * LD + h * KS], bp, bf, W2, col, h);
+#ifdef GINE_RG_PROFILE
+    if (c[0] == 1.2345e-30f) L.a[0] = 0.f;  // the stamp below waits for the chain
+#endif
+    RG_MARK(13);
     __syncthreads();  // every wave's A-fragment reads of L.a are done
 #pragma unroll
     for (int r = 0; r < 16; ++r) L.a[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + col] = c[r];
@@ -1164,6 +1174,7 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
       *reinterpret_cast<float4*>(dbn + n * D + 4 * q_me) = o;
       *reinterpret_cast<float4*>(&L.kd[k][r * LD + 4 * q_me]) = o;
     }
+    RG_MARK(14);
   }
   {  // per-column sums of the workgroup: the RSTEP row groups added in fixed order
     __syncthreads();
@@ -1184,12 +1195,15 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
     // the atomics are performed before this workgroup arrives at the grid barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  RG_MARK(15);
   // ---- W1 fragments, then the grid barrier ----
   load_wk<D, KS>(W1, col, h, bf);
   if constexpr (GINE_GEMM_BF16X3 && KS <= 64) bp.from(bf);
+  RG_MARK(16);
   __syncthreads();
   if (tid == 0) grid_barrier(bnacc_barrier(acc, 2 * D), gridDim.x);
   __syncthreads();
+  RG_MARK(17);
 
   // ---- phase B: BatchNorm backward finish (k_bwd1_bnacc's arithmetic), dz = da1 W1 ----
   L.tot[tid] = bnacc_total<true>(acc, 2 * D, tid, blockIdx.x == 0, ph, consumed);
@@ -1219,6 +1233,7 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
   ProArgs p2 = pa;
   p2.coef = L.coef;
   const ColConst kb = col_const<PRO_DA1>(p2, D, q_me);
+  RG_MARK(18);
   for (int k = 0; k < nt; ++k) {
     const int64_t n0 = (int64_t)(tr.first + k * tr.step) * kRowTile;
     __syncthreads();  // the previous tile's output reads of L.a are done
@@ -1235,6 +1250,10 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
     }
     __syncthreads();
     const floatx16 c = chain_tile<D, KS>(&L.a[c32 * LD + h * KS], bp, bf, W1, col, h);
+#ifdef GINE_RG_PROFILE
+    if (c[0] == 1.2345e-30f) L.a[0] = 0.f;
+#endif
+    RG_MARK(19);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) L.a[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + col] = c[r];
@@ -1247,7 +1266,9 @@ __global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict
         *reinterpret_cast<float4*>(dz + n * D + 4 * q_me) =
             *reinterpret_cast<const float4*>(&L.a[r * LD + 4 * q_me]);
     }
+    RG_MARK(20);
   }
+  RG_FLUSH();
 }
 
 template <int D, int PDO>

@@ -1,0 +1,298 @@
+// PyTorch binding of the GINE layer for the drop-in path (raincast_gnn.nn.GINEConv called
+// from the reference's own models/gnn.py structure and train.py loop, without HIP graphs).
+//
+// The same launches as raincast_gnn/functional.py's GineLayer (forward: the one-launch layer,
+// the fused gather + Linear1 or the unfused pair, BatchNorm sums through the fixed-point
+// accumulator or fp64 partials; backward: the non-deferred form -- dbn GEMM, BatchNorm
+// backward finish, dz GEMM beside the node-MLP weight-gradient engine, message-passing
+// backward reducing that slab in the same launch, then its own finish), issued from a C++
+// torch::autograd::Function: one Python call per layer forward and none in backward, where
+// the Python Function spends ~50 us and ~190 us of host time per layer on argument
+// marshalling, allocations and per-launch ctypes calls (profiles/r04_s02_dropin_prof.txt).
+// The kernels and their order are unchanged, so the results are the same bits as the
+// Python path's (tests/test_gpu_dropin.py).  Everything goes through the C ABI of
+// include/gine_hip.h; this file owns no kernels.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include <vector>
+
+#include "gine_hip.h"
+
+namespace {
+
+using torch::Tensor;
+using torch::autograd::AutogradContext;
+using torch::autograd::tensor_list;
+
+void* P(const Tensor& t) { return t.defined() ? t.data_ptr() : nullptr; }
+
+void ok(int st, const char* what) {
+  TORCH_CHECK(st == GINE_OK, what, " failed with status ", st, ": ", gine_status_string(st));
+}
+
+void* stream_of(const Tensor& t) {
+  return reinterpret_cast<void*>(at::hip::getCurrentHIPStream(t.device().index()).stream());
+}
+
+int32_t query(int (*fn)(int64_t, int32_t, int32_t*), int64_t n, int32_t d, const char* what) {
+  int32_t v = 0;
+  ok(fn(n, d, &v), what);
+  return v;
+}
+
+// Indices into the integer / float option vectors the Python side passes.
+enum IntOpt {
+  kEpi = 0,        // GINE_EPI_*
+  kLinFlag,        // 0 | GINE_MP_LIN_MULADD (the host CPU's Linear(1,D) rounding)
+  kBatchStats,     // BatchNorm uses batch statistics
+  kUpdateRunning,  // ... and updates the running buffers
+  kFused,          // gine_mp_fwd_mlp1 applies
+  kLayer,          // gine_mp_fwd_layer applies
+  kMaxInDegree,
+  kPlanIn,         // address of the forward gine_window_plan (0: none)
+  kPlanOut,        // address of the backward gine_window_plan (0: none)
+  kIntOpts
+};
+enum FloatOpt { kMomentum = 0, kBnEps, kFloatOpts };
+
+struct ZeroOnError {  // csrc/gine_bnacc.hpp pairing: re-zero the accumulator if a launch fails
+  Tensor acc;
+  bool armed = true;
+  ~ZeroOnError() {
+    if (armed && acc.defined()) acc.zero_();
+  }
+};
+
+class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
+ public:
+  // graph: in_rowptr, in_src, in_attr, out_rowptr, out_dst, out_attr
+  // bn: running_mean, running_var, num_batches_tracked, accumulator (undefined: partials)
+  static Tensor forward(AutogradContext* ctx, Tensor x, Tensor lin_w, Tensor lin_b, Tensor eps,
+                        Tensor w1, Tensor b1, Tensor gamma, Tensor beta, Tensor w2, Tensor b2,
+                        std::vector<Tensor> graph, std::vector<Tensor> bn,
+                        std::vector<int64_t> io, std::vector<double> fo) {
+    x = x.contiguous();
+    const int64_t N = x.size(0);
+    const int32_t D = (int32_t)x.size(1);
+    void* s = stream_of(x);
+    Tensor lw = lin_w.reshape({-1}).contiguous(), lb = lin_b.reshape({-1}).contiguous();
+    Tensor ep = eps.contiguous();
+    Tensor w1c = w1.contiguous(), b1c = b1.contiguous(), w2c = w2.contiguous(),
+           b2c = b2.contiguous();
+    Tensor g = gamma.defined() ? gamma.contiguous() : gamma;
+    Tensor bt = beta.defined() ? beta.contiguous() : beta;
+    const int epi = (int)io[kEpi], lin_flag = (int)io[kLinFlag];
+    const bool batch_stats = io[kBatchStats] != 0;
+    const int update_running = (int)io[kUpdateRunning];
+    const bool fused = io[kFused] != 0, layer = io[kLayer] != 0;
+    const int32_t max_deg = (int32_t)io[kMaxInDegree];
+    const auto* plan_in = reinterpret_cast<const gine_window_plan*>(io[kPlanIn]);
+    const Tensor &in_rowptr = graph[0], &in_src = graph[1], &in_attr = graph[2];
+    const Tensor &rmean = bn[0], &rvar = bn[1], &nbt = bn[2], &acc = bn[3];
+    TORCH_CHECK(!(batch_stats && N <= 1), "Expected more than 1 value per channel when "
+                "training, got input size [", N, ", ", D, "]");
+    const float momentum = (float)fo[kMomentum], bn_eps = (float)fo[kBnEps];
+
+    Tensor a1 = torch::empty_like(x), y = torch::empty_like(x);
+    Tensor bn_save = torch::empty({4, D}, x.options());
+    Tensor mask = epi == GINE_EPI_RESIDUAL_RELU
+                      ? torch::empty({N, D}, x.options().dtype(torch::kUInt8))
+                      : Tensor();
+    void* nbt_p = update_running ? P(nbt) : nullptr;
+    const int upd = (update_running && rmean.defined()) ? 1 : 0;
+    Tensor z = torch::empty_like(x);
+    if (!fused) {  // the gather (or window) forward, unpaired
+      if (plan_in)
+        ok(gine_mp_fwd_win((const float*)P(x), (const int32_t*)P(in_rowptr),
+                           (const int32_t*)P(in_src), (const float*)P(in_attr),
+                           (const float*)P(lw), (const float*)P(lb), (const float*)P(ep),
+                           (float*)P(z), N, D, lin_flag, plan_in, s),
+           "gine_mp_fwd_win");
+      else
+        ok(gine_mp_fwd((const float*)P(x), (const int32_t*)P(in_rowptr),
+                       (const int32_t*)P(in_src), (const float*)P(in_attr),
+                       (const float*)P(lw), (const float*)P(lb), (const float*)P(ep),
+                       (float*)P(z), N, D, lin_flag, s),
+           "gine_mp_fwd");
+    }
+    Tensor partials;
+    int32_t Pn = 0;
+    if (!acc.defined()) {
+      Pn = query(gine_mlp_num_partials, N, D, "gine_mlp_num_partials");
+      partials = torch::empty({Pn, 2, D}, x.options().dtype(torch::kFloat64));
+    }
+    {
+      ZeroOnError guard{acc};
+      if (layer) {
+        ok(gine_mp_fwd_layer((const float*)P(x), (const int32_t*)P(in_rowptr),
+                             (const int32_t*)P(in_src), (const float*)P(in_attr),
+                             (const float*)P(lw), (const float*)P(lb), (const float*)P(ep),
+                             (const float*)P(w1c), (const float*)P(b1c), (float*)P(z),
+                             (float*)P(a1), (int64_t*)P(acc), (const float*)P(g),
+                             (const float*)P(bt), (float*)P(rmean), (float*)P(rvar),
+                             (int64_t*)nbt_p, (float*)P(bn_save), momentum, bn_eps, upd,
+                             (const float*)P(w2c), (const float*)P(b2c), (float*)P(y),
+                             (uint8_t*)P(mask), N, D, max_deg, lin_flag, epi, s),
+           "gine_mp_fwd_layer");
+      } else {
+        if (fused) {
+          if (acc.defined())
+            ok(gine_mp_fwd_mlp1_acc((const float*)P(x), (const int32_t*)P(in_rowptr),
+                                    (const int32_t*)P(in_src), (const float*)P(in_attr),
+                                    (const float*)P(lw), (const float*)P(lb),
+                                    (const float*)P(ep), (const float*)P(w1c),
+                                    (const float*)P(b1c), (float*)P(z), (float*)P(a1),
+                                    (double*)P(partials), (int64_t*)P(acc), N, D, max_deg,
+                                    lin_flag, s),
+               "gine_mp_fwd_mlp1_acc");
+          else
+            ok(gine_mp_fwd_mlp1((const float*)P(x), (const int32_t*)P(in_rowptr),
+                                (const int32_t*)P(in_src), (const float*)P(in_attr),
+                                (const float*)P(lw), (const float*)P(lb), (const float*)P(ep),
+                                (const float*)P(w1c), (const float*)P(b1c), (float*)P(z),
+                                (float*)P(a1), (double*)P(partials), N, D, max_deg, lin_flag,
+                                s),
+               "gine_mp_fwd_mlp1");
+        } else if (acc.defined()) {
+          ok(gine_mlp_fwd1_acc((const float*)P(z), (const float*)P(w1c), (const float*)P(b1c),
+                               (float*)P(a1), nullptr, (int64_t*)P(acc), N, D, s),
+             "gine_mlp_fwd1_acc");
+        } else {
+          ok(gine_mlp_fwd1((const float*)P(z), (const float*)P(w1c), (const float*)P(b1c),
+                           (float*)P(a1), (double*)P(partials), N, D, s),
+             "gine_mlp_fwd1");
+        }
+        if (acc.defined()) {
+          ok(gine_mlp_fwd2_bn((const float*)P(a1), (int64_t*)P(acc), (const float*)P(g),
+                              (const float*)P(bt), (float*)P(rmean), (float*)P(rvar),
+                              (int64_t*)nbt_p, (float*)P(bn_save), momentum, bn_eps, upd,
+                              (const float*)P(w2c), (const float*)P(b2c), (const float*)P(x),
+                              (float*)P(y), (uint8_t*)P(mask), N, D, epi, s),
+             "gine_mlp_fwd2_bn");
+        } else {
+          ok(gine_bn_fwd_finalize((const double*)P(partials), Pn, (const float*)P(g),
+                                  (const float*)P(bt), (float*)P(rmean), (float*)P(rvar),
+                                  (int64_t*)nbt_p, (float*)P(bn_save), N, D, momentum, bn_eps,
+                                  batch_stats ? 1 : 0, upd, s),
+             "gine_bn_fwd_finalize");
+          ok(gine_mlp_fwd2((const float*)P(a1), (const float*)P(bn_save),
+                           (const float*)P(w2c), (const float*)P(b2c), (const float*)P(x),
+                           (float*)P(y), (uint8_t*)P(mask), N, D, epi, s),
+             "gine_mlp_fwd2");
+        }
+      }
+      guard.armed = false;
+    }
+    ctx->save_for_backward({x, z, a1, epi == GINE_EPI_RELU ? y : Tensor(), mask, bn_save, lw,
+                            lb, ep, w1c, w2c, g, graph[3], graph[4], graph[5]});
+    ctx->saved_data["io"] = io;
+    ctx->saved_data["beta"] = beta.defined();
+    ctx->saved_data["lin_w_shape"] = lin_w.sizes().vec();
+    return y;
+  }
+
+  static tensor_list backward(AutogradContext* ctx, tensor_list grads) {
+    auto sv = ctx->get_saved_variables();
+    Tensor x = sv[0], z = sv[1], a1 = sv[2], y = sv[3], mask = sv[4], bn_save = sv[5],
+           lw = sv[6], lb = sv[7], ep = sv[8], w1c = sv[9], w2c = sv[10], g = sv[11];
+    const Tensor &out_rowptr = sv[12], &out_dst = sv[13], &out_attr = sv[14];
+    const std::vector<int64_t> io = ctx->saved_data["io"].toIntVector();
+    const bool has_beta = ctx->saved_data["beta"].toBool();
+    const std::vector<int64_t> lin_w_shape = ctx->saved_data["lin_w_shape"].toIntVector();
+    Tensor dy = grads[0].contiguous();
+    const int64_t N = x.size(0);
+    const int32_t D = (int32_t)x.size(1);
+    void* s = stream_of(x);
+    const int epi = (int)io[kEpi], lin_flag = (int)io[kLinFlag];
+    const auto* plan_out = reinterpret_cast<const gine_window_plan*>(io[kPlanOut]);
+    auto fo = x.options();
+    Tensor dgamma = g.defined() ? torch::empty({D}, fo) : Tensor();
+    Tensor dbeta = has_beta ? torch::empty({D}, fo) : Tensor();
+    Tensor dw1 = torch::empty({D, D}, fo), db1 = torch::empty({D}, fo);
+    Tensor dw2 = torch::empty({D, D}, fo), db2 = torch::empty({D}, fo);
+    Tensor dbn = torch::empty_like(x), coef = torch::empty({3, D}, fo), dz = torch::empty_like(x);
+    const int32_t C = query(gine_mlp_wgrad_num_chunks, N, D, "gine_mlp_wgrad_num_chunks");
+    Tensor slab = torch::empty({2 * (int64_t)C * ((int64_t)D * D + D)}, fo);
+    const int32_t Pn = query(gine_mlp_num_partials, N, D, "gine_mlp_num_partials");
+    Tensor partials = torch::empty({Pn, 2, D}, fo.dtype(torch::kFloat64));
+    ok(gine_mlp_bwd2((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
+                     (const float*)P(a1), (const float*)P(bn_save), (const float*)P(w2c),
+                     (float*)P(dbn), (double*)P(partials), N, D, epi, s),
+       "gine_mlp_bwd2");
+    ok(gine_bn_bwd_finalize((const double*)P(partials), Pn, (const float*)P(g),
+                            (const float*)P(bn_save), (float*)P(dgamma), (float*)P(dbeta),
+                            (float*)P(coef), N, D, io[kBatchStats] ? 1 : 0, s),
+       "gine_bn_bwd_finalize");
+    // dz = da1 W1 and the dW1 / dW2 partial slab side by side in one launch
+    ok(gine_mlp_bwd1_wgrad((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
+                           (const float*)P(a1), (const float*)P(bn_save), (const float*)P(dbn),
+                           (const float*)P(coef), (const float*)P(z), (const float*)P(w1c),
+                           (float*)P(dz), (float*)P(slab), nullptr, nullptr, nullptr, nullptr,
+                           N, D, epi, s),
+       "gine_mlp_bwd1_wgrad");
+    // message-passing backward; its extra workgroups reduce the slab
+    Tensor dres = epi == GINE_EPI_RESIDUAL_RELU ? dy : Tensor();
+    Tensor dx = torch::empty_like(x);
+    Tensor dlw = torch::empty({D}, fo), dlb = torch::empty({D}, fo), deps = torch::empty({1}, fo);
+    const int32_t flags = GINE_MP_BWD_SELF | lin_flag;
+    if (plan_out) {
+      const int32_t P2 = plan_out->num_tiles;
+      Tensor part2 = torch::empty({P2, 3, D}, fo.dtype(torch::kFloat64));
+      ok(gine_mp_bwd_win_side((const float*)P(dz), (const float*)P(x),
+                              (const int32_t*)P(out_rowptr), (const int32_t*)P(out_dst),
+                              (const float*)P(out_attr), (const float*)P(lw),
+                              (const float*)P(lb), (const float*)P(ep), (const float*)P(dres),
+                              (float*)P(dx), (double*)P(part2), N, D, flags, plan_out,
+                              (const float*)P(slab), C, D, (float*)P(dw1), (float*)P(db1),
+                              (float*)P(dw2), (float*)P(db2), s),
+         "gine_mp_bwd_win_side");
+      ok(gine_mp_bwd_win_finalize((const double*)P(part2), P2, D, plan_out->slice_channels,
+                                  (float*)P(dlw), (float*)P(dlb), (float*)P(deps), s),
+         "gine_mp_bwd_win_finalize");
+    } else {
+      const int32_t P2 = query(gine_mp_bwd_num_partials, N, D, "gine_mp_bwd_num_partials");
+      Tensor part2 = torch::empty({P2, 3, D}, fo.dtype(torch::kFloat64));
+      ok(gine_mp_bwd_side((const float*)P(dz), (const float*)P(x), (const int32_t*)P(out_rowptr),
+                          (const int32_t*)P(out_dst), (const float*)P(out_attr),
+                          (const float*)P(lw), (const float*)P(lb), (const float*)P(ep),
+                          (const float*)P(dres), (float*)P(dx), (double*)P(part2), N, D, flags,
+                          (const float*)P(slab), C, D, (float*)P(dw1), (float*)P(db1),
+                          (float*)P(dw2), (float*)P(db2), s),
+         "gine_mp_bwd_side");
+      ok(gine_mp_bwd_finalize((const double*)P(part2), P2, D, (float*)P(dlw), (float*)P(dlb),
+                              (float*)P(deps), s),
+         "gine_mp_bwd_finalize");
+    }
+    // x, lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2, graph, bn, io, fo
+    return {dx,     dlw.view(lin_w_shape), dlb,  deps.view_as(ep), dw1,      db1,     dgamma,
+            dbeta,  dw2,                   db2,  Tensor(),          Tensor(), Tensor(), Tensor()};
+  }
+};
+
+Tensor opt(const c10::optional<Tensor>& t) { return t.has_value() ? *t : Tensor(); }
+
+// The Python entry point: one call per layer forward.
+Tensor gine_layer(Tensor x, Tensor lin_w, Tensor lin_b, Tensor eps, Tensor w1, Tensor b1,
+                  c10::optional<Tensor> gamma, c10::optional<Tensor> beta, Tensor w2, Tensor b2,
+                  std::vector<Tensor> graph, std::vector<c10::optional<Tensor>> bn,
+                  std::vector<int64_t> io, std::vector<double> fo) {
+  TORCH_CHECK(graph.size() == 6, "graph: in_rowptr, in_src, in_attr, out_rowptr, out_dst, "
+              "out_attr");
+  TORCH_CHECK(bn.size() == 4, "bn: running_mean, running_var, num_batches_tracked, acc");
+  TORCH_CHECK(io.size() == kIntOpts && fo.size() == kFloatOpts, "option vectors");
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.dim() == 2,
+              "x: fp32 [N, D] on a HIP device");
+  std::vector<Tensor> bnt;
+  for (const auto& t : bn) bnt.push_back(opt(t));
+  return GineLayerFn::apply(x, lin_w, lin_b, eps, w1, b1, opt(gamma), opt(beta), w2, b2,
+                            graph, bnt, io, fo);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "C++ autograd binding of the GINE layer (drop-in path; include/gine_hip.h)";
+  m.def("gine_layer", &gine_layer, "GINE layer forward (autograd: the non-deferred backward)");
+  m.attr("ABI_VERSION") = GINE_ABI_VERSION;
+}

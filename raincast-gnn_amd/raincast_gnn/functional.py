@@ -69,16 +69,27 @@ def edge_linear_flag() -> int:
     return _LIN_FLAG
 
 
+_COUNTS: dict = {}  # size queries of the library (pure functions of their arguments)
+
+
 def _count(fn: str, n: int, d: int) -> int:
-    out = ctypes.c_int32(0)
-    call(fn, n, d, ctypes.byref(out))
-    return int(out.value)
+    key = (fn, n, d)
+    v = _COUNTS.get(key)
+    if v is None:
+        out = ctypes.c_int32(0)
+        call(fn, n, d, ctypes.byref(out))
+        v = _COUNTS[key] = int(out.value)
+    return v
 
 
 def _count64(fn: str, d: int) -> int:
-    out = ctypes.c_int64(0)
-    call(fn, d, ctypes.byref(out))
-    return int(out.value)
+    key = (fn, d)
+    v = _COUNTS.get(key)
+    if v is None:
+        out = ctypes.c_int64(0)
+        call(fn, d, ctypes.byref(out))
+        v = _COUNTS[key] = int(out.value)
+    return v
 
 
 def _as_vec(p: torch.Tensor) -> torch.Tensor:

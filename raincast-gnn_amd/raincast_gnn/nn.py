@@ -18,12 +18,14 @@ import torch
 from torch import Tensor
 from torch.nn import BatchNorm1d, Linear, Parameter, ReLU, Sequential
 
-from . import _lib
+from . import _lib, gradbuf, torch_ext
 from .functional import (EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU, BnConfig, GineLayer,
                          GineMessagePassing)
 from .graph import get_graph
 
 FUSED_CHANNELS = (32, 64, 128, 256)
+# False: the Python autograd Function everywhere (the tests compare the two bindings)
+USE_TORCH_EXT = True
 
 
 def _reset(module) -> None:
@@ -137,6 +139,11 @@ class GINEConv(torch.nn.Module):
         graph = get_graph(edge_index, edge_attr, x.size(0), self.flow)
         if self._fusable(x):
             l1, bn, _, l2 = self.nn
+            ext = torch_ext.get() if USE_TORCH_EXT else None
+            if ext is not None and gradbuf.slice_of(l1.weight) is None:
+                # the drop-in path (no flat gradient buffer: the non-deferred backward) from
+                # the C++ autograd binding -- the same launches, far less host time
+                return torch_ext.layer(ext, x, self, graph, epilogue)
             return GineLayer.apply(x, self.lin.weight, self.lin.bias, self.eps, l1.weight,
                                    l1.bias, bn.weight, bn.bias, l2.weight, l2.bias, graph,
                                    BnConfig(bn), epilogue)

@@ -1,0 +1,96 @@
+"""The C++ autograd binding of the GINE layer (csrc/torch/gine_torch.cpp) for the drop-in path.
+
+``raincast_gnn.nn.GINEConv`` called from the reference's own module tree and training loop
+(models/gnn.py:41,44; train.py:61-71: eager autograd, no HIP graph) spends its time on the
+host: the Python autograd Function issues one ctypes call per launch and marshals ~30
+arguments each time (profiles/r04_s02_dropin_prof.txt).  The extension issues the same
+launches from one C++ torch::autograd::Function -- one Python call per layer forward, none in
+backward.  It is built in-tree next to libgine_hip.so (``build()``, called by
+``__graft_entry__.build``) and loaded from there; a missing extension leaves the Python
+Function in charge (same kernels, same bits), it is never a CPU fallback.
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import threading
+
+import torch
+
+from . import _lib
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+EXT_DIR = os.path.join(_HERE, "_native", "torch_ext")
+EXT_PATH = os.path.join(EXT_DIR, "gine_torch.so")
+SOURCE = os.path.join(os.path.dirname(_HERE), "csrc", "torch", "gine_torch.cpp")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
+
+_lock = threading.Lock()
+_ext = None
+_tried = False
+
+
+def build(verbose: bool = False) -> str:
+    """Compile the extension in-tree (g++ against torch's headers, linked to libgine_hip.so
+    with an $ORIGIN rpath).  Returns the path of the built module."""
+    from torch.utils.cpp_extension import load
+    os.makedirs(EXT_DIR, exist_ok=True)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    load(name="gine_torch", sources=[SOURCE], build_directory=EXT_DIR, verbose=verbose,
+         extra_include_paths=[INCLUDE],
+         extra_cflags=["-O2", "-D__HIP_PLATFORM_AMD__", f"-I{rocm}/include"],
+         extra_ldflags=[f"-L{os.path.dirname(_lib.LIB_PATH)}", "-lgine_hip",
+                        "-Wl,-rpath,\\$$ORIGIN/..", "-lc10_hip", "-ltorch_hip"])
+    return EXT_PATH
+
+
+def get():
+    """The loaded extension module, or None when it was not built (or was built against
+    another ABI version of the library)."""
+    global _ext, _tried
+    if _tried:
+        return _ext
+    with _lock:
+        if not _tried:
+            _tried = True
+            if os.path.exists(EXT_PATH) and os.environ.get("GINE_HIP_LIB") is None:
+                _lib.load()   # the same libgine_hip.so the extension links (rpath $ORIGIN/..)
+                spec = importlib.util.spec_from_file_location("gine_torch", EXT_PATH)
+                mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(mod)
+                if mod.ABI_VERSION == _lib.ABI_VERSION:
+                    _ext = mod
+    return _ext
+
+
+# io option order of gine_torch.cpp (IntOpt)
+IO_EPI, IO_LIN, IO_BATCH, IO_UPDATE, IO_FUSED, IO_LAYER, IO_DEG, IO_PLAN_IN, IO_PLAN_OUT = range(9)
+
+
+def plan_address(plan) -> int:
+    import ctypes
+    return 0 if plan is None else ctypes.addressof(plan)
+
+
+def layer(ext, x, conv, graph, epilogue: int) -> torch.Tensor:
+    """GINEConv.forward's fused layer through the extension (the caller checked that the
+    layer's parameters are not flat-buffer slices, i.e. its backward is the non-deferred
+    form)."""
+    from . import functional as Fn
+    l1, bn_mod, _, l2 = conv.nn
+    N, D = x.shape
+    bn = Fn.BnConfig(bn_mod)
+    acc = Fn.bn_accumulator(bn, D, x.device)
+    fused = Fn.fused_forward_ok(graph, N, D)
+    lay = fused and acc is not None and Fn.layer_forward_ok(N, D, graph.max_in_degree)
+    io = [epilogue, Fn.edge_linear_flag(), int(bn.use_batch_stats),
+          int(bn.update_running), int(fused), int(lay),
+          int(graph.max_in_degree if graph.max_in_degree is not None else -1),
+          plan_address(graph.window_plan("in", D)), plan_address(graph.window_plan("out", D))]
+    fo = [bn.momentum, bn.eps]
+    return ext.gine_layer(x, conv.lin.weight, conv.lin.bias, conv.eps, l1.weight, l1.bias,
+                          bn_mod.weight, bn_mod.bias, l2.weight, l2.bias,
+                          [graph.in_rowptr, graph.in_src, graph.in_attr, graph.out_rowptr,
+                           graph.out_dst, graph.out_attr],
+                          [bn.running_mean, bn.running_var,
+                           bn.num_batches_tracked if bn.update_running else None, acc], io, fo)

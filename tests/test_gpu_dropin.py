@@ -132,3 +132,46 @@ def test_dropin_training_loop_builds_the_graph_once():
     # the fused layer form was used (D = 128, Linear-BN-ReLU-Linear nn)
     assert Fn.fused_forward_ok(graph_cache.get(batch.edge_index, batch.edge_attr.float(),
                                                batch.num_nodes), batch.num_nodes, 128)
+
+
+@pytest.mark.parametrize("order", ["dataset", "locality"])
+def test_dropin_cpp_binding_same_bits_as_python_function(order, monkeypatch):
+    """The C++ autograd binding of the layer (raincast_gnn.torch_ext, csrc/torch/
+    gine_torch.cpp) issues the Python Function's launches: the drop-in model's predictions,
+    loss, every gradient and the BatchNorm buffers are the same bits over three training
+    steps, with the graph in the dataset order (gather backward) and in the locality order
+    (window backward)."""
+    import copy
+    from raincast_gnn import nn as rnn, torch_ext
+    from raincast_gnn.dropin import reference_struct_from_params
+    from raincast_gnn.params import EXPERIMENTS
+    from helpers import engine_order_batch
+    assert torch_ext.get() is not None, "the C++ binding was not built / did not load"
+    batch = collate(synthetic_samples(500, 8, k=10, seed=6))
+    if order == "locality":
+        batch = engine_order_batch(batch)
+    batch = batch.to(DEV)
+    torch.manual_seed(3)
+    base = reference_struct_from_params(EXPERIMENTS["24h_mixed"]).to(DEV).train()
+
+    def run(use_ext):
+        monkeypatch.setattr(rnn, "USE_TORCH_EXT", use_ext)
+        m = copy.deepcopy(base)
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+        out = []
+        for _ in range(3):
+            pred = m(batch)
+            loss = m.loss_fn.crps(pred, batch.y)
+            opt.zero_grad()
+            loss.backward()
+            out.append([pred.detach().clone(), loss.detach().clone()]
+                       + [p.grad.clone() for p in m.parameters()]
+                       + [b.clone() for b in m.buffers()])
+            opt.step()
+        torch.cuda.synchronize()
+        return out
+
+    py, cpp = run(False), run(True)
+    for a_step, b_step in zip(cpp, py):
+        for a, b in zip(a_step, b_step):
+            assert torch.equal(a, b)
