@@ -871,19 +871,25 @@ def dropin_bench(args, cfg, device) -> dict:
     elapsed = time.perf_counter() - t0
     stats = {k: graph_cache.stats[k] - stats0[k] for k in stats0}
 
-    # the GINE stack alone (4 GINEConv + torch ReLU / residual), forward + backward
+    # the GINE stack alone (4 GINEConv + torch ReLU / residual), forward + backward, with
+    # the training loop's set_to_none gradients; every step gets edge tensors of its own
+    # (copied to the device before the timed region: a fresh tensor per step as in the
+    # loop above, without the host-to-device copy that the whole-step number holds)
     D = params["gnn_hidden"]
     x0 = torch.randn(host[0].num_nodes, D, device=device, requires_grad=True)
     gy = torch.randn(host[0].num_nodes, D, device=device)
-    ea_host = host[0].edge_attr
+    edges = [(host[i % 2].edge_index.to(device), host[i % 2].edge_attr.to(device))
+             for i in range(args.steps + 3)]
 
     def gine_step(i):
-        ei = host[i % 2].edge_index.to(device)
-        out = model.conv(x0, ei, ea_host.to(device))
+        model.conv.zero_grad(set_to_none=True)
+        x0.grad = None
+        ei, ea = edges[i]
+        out = model.conv(x0, ei, ea)
         out.backward(gy)
 
     for i in range(3):
-        gine_step(i)
+        gine_step(args.steps + i)
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
     for i in range(args.steps):

@@ -532,6 +532,15 @@ int gine_deepset_fwd_fold(const float* ens, const float* w1, const float* b1, fl
                           int32_t in_features, int32_t hidden, const float* wr1,
                           const float* br1, const float* wdr, const float* bdr, float* wfold,
                           int32_t x_features, void* stream);
+/* gine_deepset_fwd_fold plus the doubly folded chain's [Wf | bf] (Wf = Wr0 Wp2 [D][D],
+ * bf = members * Wr0 bp2 + br0 [D]) into wfold2 [D*D + D], by a second set of extra
+ * workgroups, for gine_chain_fwd_folded2 (wr0 / br0 = rho[0], wp2 / bp2 = phi[2]). */
+int gine_deepset_fwd_fold2(const float* ens, const float* w1, const float* b1, float* r,
+                           uint16_t* mask, int64_t num_nodes, int32_t members,
+                           int32_t in_features, int32_t hidden, const float* wr1,
+                           const float* br1, const float* wdr, const float* bdr, float* wfold,
+                           int32_t x_features, const float* wr0, const float* br0,
+                           const float* wp2, const float* bp2, float* wfold2, void* stream);
 int gine_deepset_bwd_num_partials(int64_t num_nodes, int32_t hidden, int32_t* num_partials);
 int gine_deepset_bwd(const float* ens, const uint16_t* mask, const float* dr, float* slab,
                      float* dw1, float* db1, int64_t num_nodes, int32_t members,
@@ -641,6 +650,37 @@ int gine_chain_wgrad_folded_grad_job(int64_t num_nodes, int32_t hidden, int32_t 
 int gine_chain_unfold_grads(const float* gfold, const float* wr1, const float* br1,
                             const float* wdr, float* dwdr, float* dbdr, float* dwr1,
                             float* dbr1, int32_t hidden, int32_t in_features, void* stream);
+
+/* Doubly folded chain (raincast_gnn.chain.FOLD2): phi[2] is followed by rho[0] with only the
+ * member sum between them, so pre = s Wr0^T + br0 = r Wf^T + bf with Wf = Wr0 Wp2,
+ * bf = M Wr0 bp2 + br0 (wfold2, from gine_deepset_fwd_fold2); s / ds are never formed.
+ * gine_chain_fwd_folded2: u = relu(r Wf^T + bf), h0 = [x | u] W'^T + b' (one launch).
+ * gine_chain_bwd_folded2: dt = (dh0 Wc) * 1[u > 0], dr = dt Wf (one launch).
+ * gine_chain_wgrad_folded2: one engine launch for G = dh0^T [x | u] | g (gfold
+ *   [D*(F+D) + D]) and G2 = dt^T r | g2 = sum_n dt (g2fold [D*D + D]); gfold = g2fold = NULL
+ *   leaves the slab for gine_grad_finalize_batch (job: gine_chain_wgrad_folded2_grad_job).
+ * gine_chain_unfold_grads2, after the reduction, one launch: gine_chain_unfold_grads's
+ *   outputs plus dWr0 = G2 Wp2^T + M g2 bp2^T, dbr0 = g2, dWp2 = Wr0^T G2,
+ *   dbp2 = M Wr0^T g2 (M = members; bias outputs may be NULL). */
+int gine_chain_fwd_folded2(const float* r, const float* x, const float* wfold,
+                           const float* wfold2, float* u, float* h0, int64_t num_nodes,
+                           int32_t hidden, int32_t in_features, void* stream);
+int gine_chain_bwd_folded2(const float* dh0, const float* u, const float* wfold,
+                           const float* wfold2, float* dt, float* dr, int64_t num_nodes,
+                           int32_t hidden, int32_t in_features, void* stream);
+int gine_chain_wgrad_folded2(const float* dh0, const float* x, const float* r, const float* u,
+                             const float* dt, float* slab, float* gfold, float* g2fold,
+                             int64_t num_nodes, int32_t hidden, int32_t in_features,
+                             void* stream);
+int gine_chain_wgrad_folded2_grad_job(int64_t num_nodes, int32_t hidden, int32_t in_features,
+                                      const float* slab, float* gfold, float* g2fold,
+                                      gine_grad_job* job);
+int gine_chain_unfold_grads2(const float* gfold, const float* wr1, const float* br1,
+                             const float* wdr, float* dwdr, float* dbdr, float* dwr1,
+                             float* dbr1, const float* g2fold, const float* wp2,
+                             const float* bp2, const float* wr0, float* dwr0, float* dbr0,
+                             float* dwp2, float* dbp2, float members, int32_t hidden,
+                             int32_t in_features, void* stream);
 
 /* Measurement utility (not on the hot path): copy `bytes` (a multiple of 16) from src to dst
  * with 16-byte-per-lane streaming loads and stores -- the HBM copy ceiling bench.py prices

@@ -180,8 +180,10 @@ class OracleDeepSet(nn.Module):
             return self.rho(self.phi(ens).sum(dim=1))
         p0, _, p2 = self.phi
         r0, _, r2 = self.rho
-        s = p2(tie_relu(p0(ens), self.decide.get("phi"))).sum(dim=1)
-        return r2(tie_relu(r0(s), self.decide.get("rho"), s=s))
+        hp = tie_relu(p0(ens), self.decide.get("phi"))
+        s = p2(hp).sum(dim=1)
+        # r (the member sum of phi's hidden layer): the doubly folded engine's rho[0] input
+        return r2(tie_relu(r0(s), self.decide.get("rho"), s=s, r=hp.sum(dim=1)))
 
 
 # ---------------------------------------------------------------------------------------

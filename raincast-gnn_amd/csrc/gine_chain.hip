@@ -40,8 +40,12 @@ constexpr int kRowTile = 32;
 // two: dt -> ds -> dr, each stage's output the next one's A tile in LDS).
 // F3: the folded chain's whole forward in one launch (s -> u -> h0 = [x | u] W'^T + b',
 // with W' folded beforehand by gine_deepset_fwd_fold).
+// F2D / B2D: the doubly folded chain (gine_chain_fwd_folded2): phi[2] folded into rho[0]
+// as well (Wf = Wr0 Wp2, bf = M Wr0 bp2 + br0, gine_deepset_fwd_fold2), F2D: u = relu(r Wf^T
+// + bf) -> h0 = [x | u] W'^T + b', B2D: dt = (dh0 Wc) * 1[u > 0] -> dr = dt Wf.
 enum ChainKind {
-  CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3, CH_F2F = 4, CH_B1F = 5, CH_B3 = 6, CH_F3 = 7
+  CH_F1 = 0, CH_F2 = 1, CH_B1 = 2, CH_B2 = 3, CH_F2F = 4, CH_B1F = 5, CH_B3 = 6, CH_F3 = 7,
+  CH_F2D = 8, CH_B2D = 9
 };
 
 struct ChainArgs {
@@ -60,9 +64,9 @@ struct ChainArgs {
   // ([D][F + D] then [D]) once the tiles are done (NULL: not folded)
   const float *fw_r1, *fb_r1, *fw_dr, *fb_dr;
   float* wfold;
-  const float* w3;  // B3: stage-3 weight (Wp2); F3: W'^T
-  float* out3;      // B3: stage-3 output (dr); F3: h0
-  const float* b3;  // F3: b'
+  const float* w3;  // B3: stage-3 weight (Wp2); F3 / F2D: W'^T
+  float* out3;      // B3: stage-3 output (dr); F3 / F2D: h0
+  const float* b3;  // F3 / F2D: b'
 };
 
 __device__ __forceinline__ floatx16 zero16() {
@@ -178,11 +182,14 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   constexpr int RSTEP = NT / D4;                    // 8
   constexpr int XITEMS = (kRowTile * FP + NT - 1) / NT;
   constexpr bool kF3 = KIND == CH_F3;
-  constexpr bool kX = kDimRed || kF3;               // stages x rows
-  constexpr int LDC = FP + D + 4;                   // F3: stage-3 A tile [x | u]
+  constexpr bool kF2D = KIND == CH_F2D, kB2D = KIND == CH_B2D;
+  constexpr bool kLast = kF3 || kF2D;               // last stage h0 = [x | u] W'^T + b'
+  constexpr bool kMaskIn = KIND == CH_B3 || kB2D;   // stage 1 dt = (dh0 Wc) * 1[u > 0]
+  constexpr bool kX = kDimRed || kLast;             // stages x rows
+  constexpr int LDC = FP + D + 4;                   // F3 / F2D: last stage's A tile [x | u]
   __shared__ __attribute__((aligned(16))) float sA[kRowTile * LDA];
-  __shared__ __attribute__((aligned(16))) float sB[kRowTile * LDB];
-  __shared__ __attribute__((aligned(16))) float sC[kF3 ? kRowTile * LDC : 4];
+  __shared__ __attribute__((aligned(16))) float sB[kF2D ? 4 : kRowTile * LDB];
+  __shared__ __attribute__((aligned(16))) float sC[kLast ? kRowTile * LDC : 4];
 
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
@@ -212,9 +219,12 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       frag_t<D>(bf1, a.w1, D, col, h);
       frag_t<D>(bf2, a.w2, D, col, h);
     }
+  } else if constexpr (kF2D) {
+    if (w16) frag_t4<D>(bf1, a.w1, D, col, h);
+    else frag_t<D>(bf1, a.w1, D, col, h);
   } else if constexpr (KIND == CH_F2) {
     frag_t<D>(bf1, a.w1, D, col, h);
-  } else if constexpr (KIND == CH_B1 || KIND == CH_B1F || KIND == CH_B3) {
+  } else if constexpr (KIND == CH_B1 || KIND == CH_B1F || kMaskIn) {
     frag_n<D>(bf1, a.w1, a.F + D, a.F, col, h);     // dim_red (B1F / B3: W') weight, e columns
   } else if constexpr (KIND == CH_B2) {
     frag_n<D>(bf1, a.w1, D, 0, col, h);
@@ -223,16 +233,16 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     frag_dimred<FP, D>(bf2, a.w2, a.F, col, h);
   } else if constexpr (KIND == CH_F2F) {
     frag_dimred_t<FP, D>(bf2, a.w2, a.F, col, h);  // w2 = W'^T
-  } else if constexpr (KIND == CH_B1 || KIND == CH_B2 || KIND == CH_B3) {
-    frag_n<D>(bf2, a.w2, D, 0, col, h);
+  } else if constexpr (KIND == CH_B1 || KIND == CH_B2 || kMaskIn) {
+    frag_n<D>(bf2, a.w2, D, 0, col, h);   // B2D: w2 = Wf
   }
-  float bf3[KIND == CH_B3 ? D / 2 : (kF3 ? (FP + D) / 2 : 1)];
+  float bf3[KIND == CH_B3 ? D / 2 : (kLast ? (FP + D) / 2 : 1)];
   if constexpr (KIND == CH_B3) frag_n<D>(bf3, a.w3, D, 0, col, h);
-  if constexpr (kF3) frag_dimred_t<FP, D>(bf3, a.w3, a.F, col, h);  // w3 = W'^T
+  if constexpr (kLast) frag_dimred_t<FP, D>(bf3, a.w3, a.F, col, h);  // w3 = W'^T
   float bias1 = 0.f, bias2 = 0.f, bias3 = 0.f;
-  if constexpr (KIND == CH_F1 || KIND == CH_F2 || kF3) bias1 = a.b1[col] * a.bias1_scale;
+  if constexpr (KIND == CH_F1 || KIND == CH_F2 || kLast) bias1 = a.b1[col] * a.bias1_scale;
   if constexpr (KIND == CH_F1 || kDimRed || kF3) bias2 = a.b2[col];
-  if constexpr (kF3) bias3 = a.b3[col];
+  if constexpr (kLast) bias3 = a.b3[col];
 
   auto load_tile = [&](int tile, float4 (&raw)[ITEMS], float (&xr)[XITEMS]) {
     const int64_t n0 = (int64_t)tile * kRowTile;
@@ -271,8 +281,8 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       *reinterpret_cast<float4*>(dst) = v;
     }
     if constexpr (kX) {
-      float* sx = kF3 ? sC : sB;
-      constexpr int LDX = kF3 ? LDC : LDB;
+      float* sx = kLast ? sC : sB;
+      constexpr int LDX = kLast ? LDC : LDB;
 #pragma unroll
       for (int i = 0; i < XITEMS; ++i) {
         const int idx = threadIdx.x + i * NT;
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     __syncthreads();
     if (tile + tr.step < tr.end) load_tile(tile + tr.step, raw, xr);  // next tile in flight
     float ep[16];
-    if constexpr (KIND == CH_B1 || KIND == CH_B1F || KIND == CH_B3) {  // ReLU mask, in flight
+    if constexpr (KIND == CH_B1 || KIND == CH_B1F || kMaskIn) {  // ReLU mask, in flight
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -309,28 +319,35 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
         const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t n = n0 + rr;
         float v = acc[r] + bias1;
-        if constexpr (KIND == CH_B3) v = ep[r] > 0.f ? acc[r] : 0.f;  // dt = du * 1[u > 0]
-        sB[rr * LDB + BOFF + col] = v;
+        if constexpr (kMaskIn) v = ep[r] > 0.f ? acc[r] : 0.f;  // dt = du * 1[u > 0]
+        if constexpr (kF2D) {
+          v = relu_nan(v);                                       // u = relu(r Wf^T + bf)
+          sC[rr * LDC + FP + col] = v;                           // the last stage's A tile
+        } else {
+          sB[rr * LDB + BOFF + col] = v;
+        }
         if (n < N) a.out1[n * D + col] = v;
       }
       __syncthreads();
     }
 
     // stage 2
-    acc = tile_mma<K2>(sB, LDB, bf2, c32, h);
+    if constexpr (!kF2D) {
+      acc = tile_mma<K2>(sB, LDB, bf2, c32, h);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int64_t n = n0 + rr;
-      float v = acc[r] + bias2;
-      if constexpr (KIND == CH_F1 || kF3) v = relu_nan(v);      // u = relu(rho[0](s))
-      if constexpr (kF3) sC[rr * LDC + FP + col] = v;           // stage 3's A tile
-      if constexpr (KIND == CH_B1) v = ep[r] > 0.f ? v : 0.f;   // dt = du * 1[u > 0]
-      if constexpr (KIND == CH_B3) sA[rr * LDA + col] = v;      // stage 3's A tile
-      if (n < N) a.out2[n * D + col] = v;
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t n = n0 + rr;
+        float v = acc[r] + bias2;
+        if constexpr (KIND == CH_F1 || kF3) v = relu_nan(v);      // u = relu(rho[0](s))
+        if constexpr (kF3) sC[rr * LDC + FP + col] = v;           // stage 3's A tile
+        if constexpr (KIND == CH_B1) v = ep[r] > 0.f ? v : 0.f;   // dt = du * 1[u > 0]
+        if constexpr (KIND == CH_B3) sA[rr * LDA + col] = v;      // stage 3's A tile
+        if (n < N) a.out2[n * D + col] = v;
+      }
     }
-    if constexpr (kF3) {  // stage 3: h0 = [x | u] W'^T + b'
-      __syncthreads();
+    if constexpr (kLast) {  // last stage: h0 = [x | u] W'^T + b'
+      if constexpr (kF3) __syncthreads();
       acc = tile_mma<FP + D>(sC, LDC, bf3, c32, h);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -613,53 +630,71 @@ extern "C" int gine_chain_wgrad_grad_job(int64_t num_nodes, int32_t hidden, int3
 namespace gine {
 namespace {
 
-// 2 (D/32)^2 workgroups, one [32 x 32] tile each (ksplit_tile): tiles of dWdr's e columns,
-// G_u Wr1^T + g br1^T (G_u rows staged, B = Wr1^T read along Wr1's rows), then tiles of
-// dWr1 = Wdr_e^T G_u (Wdr_e columns staged as rows, B = G_u); the x columns and dbdr (resp.
-// dbr1) by the tiles of column 0.
+// One unfold job: G = gf ([D][F + D] then g [D]) of the product dY^T [x | q] where the
+// rows of q feed a Linear (w1, bias b1 * bscale) whose output meets Wdr's q columns, e.g.
+//   h0 = [x | u Wr1^T + br1] Wdr^T + bdr:   dWdr = [G_x | G_u Wr1^T + g br1^T], dbdr = g,
+//                                           dWr1 = Wdr_e^T G_u, dbr1 = Wdr_e^T g,
+// and the same with F = 0 for pre = (r Wp2^T + M bp2) Wr0^T + br0 (the double fold):
+//   dWr0 = G2 Wp2^T + M g2 bp2^T, dbr0 = g2, dWp2 = Wr0^T G2, dbp2 = M Wr0^T g2.
+struct UnfoldJob {
+  const float *gf, *w1, *b1, *wdr;  // w1 [D][D]; wdr [D][F + D] (its last D columns used)
+  float *dwdr, *dbdr, *dw1, *db1;
+  int F;
+  float bscale;
+};
+
+// 2 (D/32)^2 workgroups per job, one [32 x 32] tile each (ksplit_tile): tiles of dWdr's q
+// columns, G_q W1^T + g (bscale b1)^T (G_q rows staged, B = W1^T read along W1's rows), then
+// tiles of dW1 = Wdr_q^T G_q (Wdr_q columns staged as rows, B = G_q); the x columns and dbdr
+// (resp. db1) by the tiles of column 0.
 template <int D>
-__global__ __launch_bounds__(2 * D) void k_chain_unfold(const float* __restrict__ gf,
-                                                        const float* __restrict__ wr1,
-                                                        const float* __restrict__ br1,
-                                                        const float* __restrict__ wdr,
-                                                        float* __restrict__ dwdr,
-                                                        float* __restrict__ dbdr,
-                                                        float* __restrict__ dwr1,
-                                                        float* __restrict__ dbr1, int F) {
+__global__ __launch_bounds__(2 * D) void k_chain_unfold(UnfoldJob j0, UnfoldJob j1) {
   constexpr int NT = 2 * D, LDA = D + 4, T = D / 32, TT = T * T;
   constexpr int SI = 32 * D / NT, XI = 32 * 64 / NT;
   __shared__ __attribute__((aligned(16))) float sA[32 * LDA];
   __shared__ float sR[T * kSR];
   __shared__ float svec[D];
+  const bool second = (int)blockIdx.x >= 2 * TT;
+  // field by field (uniform selects; no private copy of a kernel argument)
+  const UnfoldJob J{second ? j1.gf : j0.gf,     second ? j1.w1 : j0.w1,
+                    second ? j1.b1 : j0.b1,     second ? j1.wdr : j0.wdr,
+                    second ? j1.dwdr : j0.dwdr, second ? j1.dbdr : j0.dbdr,
+                    second ? j1.dw1 : j0.dw1,   second ? j1.db1 : j0.db1,
+                    second ? j1.F : j0.F,       second ? j1.bscale : j0.bscale};
+  const int blk = (int)blockIdx.x - (second ? 2 * TT : 0);
+  const float* __restrict__ gf = J.gf;
+  const int F = J.F;
   const int LW = F + D;
   const float* g = gf + (size_t)D * LW;
   const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
-  const bool e_cols = (int)blockIdx.x < TT;
-  const int t = e_cols ? (int)blockIdx.x : (int)blockIdx.x - TT;
+  const bool e_cols = blk < TT;
+  const int t = e_cols ? blk : blk - TT;
   const int r0 = 32 * (t / T), c0 = 32 * (t % T);
   float bf[16], st[SI];
   if (e_cols) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) bf[s] = wr1[(size_t)(c0 + c32) * D + w * 32 + h * 16 + s];
+    for (int s = 0; s < 16; ++s) bf[s] = J.w1[(size_t)(c0 + c32) * D + w * 32 + h * 16 + s];
 #pragma unroll
     for (int i = 0; i < SI; ++i) {
       const int idx = threadIdx.x + i * NT;
       st[i] = gf[(size_t)(r0 + idx / D) * LW + F + idx % D];
     }
     if (c0 == 0) {
-      float xv[XI];
+      if (F > 0) {
+        float xv[XI];
 #pragma unroll
-      for (int i = 0; i < XI; ++i) {
-        const int idx = min(threadIdx.x + i * NT, 32 * F - 1);
-        xv[i] = gf[(size_t)(r0 + idx / F) * LW + idx % F];
-      }
+        for (int i = 0; i < XI; ++i) {
+          const int idx = min(threadIdx.x + i * NT, 32 * F - 1);
+          xv[i] = gf[(size_t)(r0 + idx / F) * LW + idx % F];
+        }
 #pragma unroll
-      for (int i = 0; i < XI; ++i) {
-        const int idx = threadIdx.x + i * NT;
-        if (idx < 32 * F) dwdr[(size_t)(r0 + idx / F) * LW + idx % F] = xv[i];
+        for (int i = 0; i < XI; ++i) {
+          const int idx = threadIdx.x + i * NT;
+          if (idx < 32 * F) J.dwdr[(size_t)(r0 + idx / F) * LW + idx % F] = xv[i];
+        }
       }
-      if (threadIdx.x < 32 && dbdr != nullptr) dbdr[r0 + threadIdx.x] = g[r0 + threadIdx.x];
+      if (threadIdx.x < 32 && J.dbdr != nullptr) J.dbdr[r0 + threadIdx.x] = g[r0 + threadIdx.x];
     }
 #pragma unroll
     for (int i = 0; i < SI; ++i) {
@@ -669,11 +704,11 @@ __global__ __launch_bounds__(2 * D) void k_chain_unfold(const float* __restrict_
   } else {
 #pragma unroll
     for (int s = 0; s < 16; ++s)
-      bf[s] = gf[(size_t)(w * 32 + h * 16 + s) * LW + F + c0 + c32];  // G_u[k][c0 + c32]
+      bf[s] = gf[(size_t)(w * 32 + h * 16 + s) * LW + F + c0 + c32];  // G_q[k][c0 + c32]
 #pragma unroll
     for (int i = 0; i < SI; ++i) {
       const int idx = threadIdx.x + i * NT;
-      st[i] = wdr[(size_t)(idx / 32) * LW + F + r0 + idx % 32];
+      st[i] = J.wdr[(size_t)(idx / 32) * LW + F + r0 + idx % 32];
     }
     const float gv = threadIdx.x < D ? g[threadIdx.x] : 0.f;
 #pragma unroll
@@ -686,9 +721,9 @@ __global__ __launch_bounds__(2 * D) void k_chain_unfold(const float* __restrict_
   __syncthreads();
   ksplit_tile<D>(sA, bf, sR, c32, h);
   if (!e_cols && c0 == 0) {
-    const float v = rows_dot<D>(sA, svec);  // (Wdr_e^T g)[r0 + r]
+    const float v = rows_dot<D>(sA, svec);  // (Wdr_q^T g)[r0 + r]
     constexpr int TPR = NT / 32;
-    if (threadIdx.x % TPR == 0 && dbr1 != nullptr) dbr1[r0 + threadIdx.x / TPR] = v;
+    if (threadIdx.x % TPR == 0 && J.db1 != nullptr) J.db1[r0 + threadIdx.x / TPR] = v * J.bscale;
   }
   __syncthreads();
 #pragma unroll
@@ -696,10 +731,23 @@ __global__ __launch_bounds__(2 * D) void k_chain_unfold(const float* __restrict_
     const int o = threadIdx.x + i * NT, rr = o / 32, cc = o % 32;
     const float v = ksplit_sum<D>(sR, rr, cc);
     if (e_cols)
-      dwdr[(size_t)(r0 + rr) * LW + F + c0 + cc] = fmaf(g[r0 + rr], br1[c0 + cc], v);
+      J.dwdr[(size_t)(r0 + rr) * LW + F + c0 + cc] =
+          fmaf(g[r0 + rr], J.b1[c0 + cc] * J.bscale, v);
     else
-      dwr1[(size_t)(r0 + rr) * D + c0 + cc] = v;
+      J.dw1[(size_t)(r0 + rr) * D + c0 + cc] = v;
   }
+}
+
+int launch_unfold(int D, const UnfoldJob& j0, const UnfoldJob* j1, hipStream_t st) {
+  const int jobs = j1 ? 2 : 1;
+  const UnfoldJob second = j1 ? *j1 : j0;
+  if (D == 64)
+    hipLaunchKernelGGL((k_chain_unfold<64>), dim3(jobs * 2 * 4), dim3(128), 0, st, j0, second);
+  else
+    hipLaunchKernelGGL((k_chain_unfold<128>), dim3(jobs * 2 * 16), dim3(256), 0, st, j0,
+                       second);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
 }
 
 }  // namespace
@@ -826,13 +874,112 @@ extern "C" int gine_chain_unfold_grads(const float* gfold, const float* wr1, con
                                        void* stream) {
   if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
   if (!gfold || !wr1 || !br1 || !wdr || !dwdr || !dwr1) return GINE_ERR_INVALID;
+  return launch_unfold(hidden,
+                       UnfoldJob{gfold, wr1, br1, wdr, dwdr, dbdr, dwr1, dbr1, in_features, 1.f},
+                       nullptr, as_stream(stream));
+}
+
+// ---------------------------------------------------------------------------------------
+// Doubly folded chain: phi[2] folded into rho[0] as well,
+//   pre = s Wr0^T + br0 = r Wf^T + bf,  Wf = Wr0 Wp2,  bf = M Wr0 bp2 + br0
+// (wfold2 = [Wf | bf], folded by gine_deepset_fwd_fold2's workgroups), so neither s nor ds is
+// formed: forward u -> h0 in one 2-stage launch, backward dt -> dr in one, the weight
+// gradients from two engine products, G = dh0^T [x | u] and G2 = dt^T r (+ g2 = sum dt),
+// unfolded together: dWdr, dWr1 from G as before, dWr0 = G2 Wp2^T + M g2 bp2^T,
+// dbr0 = g2, dWp2 = Wr0^T G2, dbp2 = M Wr0^T g2.
+// ---------------------------------------------------------------------------------------
+extern "C" int gine_chain_fwd_folded2(const float* r, const float* x, const float* wfold,
+                                      const float* wfold2, float* u, float* h0,
+                                      int64_t num_nodes, int32_t hidden, int32_t in_features,
+                                      void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes < 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (num_nodes == 0) return GINE_OK;
+  if (!r || !x || !wfold || !wfold2 || !u || !h0) return GINE_ERR_INVALID;
   hipStream_t st = as_stream(stream);
-  if (hidden == 64)
-    hipLaunchKernelGGL((k_chain_unfold<64>), dim3(2 * 4), dim3(128), 0, st, gfold, wr1, br1,
-                       wdr, dwdr, dbdr, dwr1, dbr1, in_features);
-  else
-    hipLaunchKernelGGL((k_chain_unfold<128>), dim3(2 * 16), dim3(256), 0, st, gfold, wr1, br1,
-                       wdr, dwdr, dbdr, dwr1, dbr1, in_features);
-  GINE_LAUNCH_STATUS();
+  const int D = hidden, F = in_features;
+  const float* bfold = wfold + (size_t)D * (F + D);
+  ChainArgs f{r, x, nullptr, wfold2, wfold2 + (size_t)D * D, nullptr, nullptr, u, nullptr,
+              1.f, F};
+  f.w3 = bfold + D;  // W'^T
+  f.b3 = bfold;
+  f.out3 = h0;
+  int rc = GINE_OK;
+#define CALL_F(DD, FF) rc = launch_chain<DD, FF, CH_F2D>(f, num_nodes, st)
+  GINE_CHAIN_DISPATCH(D, F, CALL_F);
+#undef CALL_F
+  return rc;
+}
+
+extern "C" int gine_chain_bwd_folded2(const float* dh0, const float* u, const float* wfold,
+                                      const float* wfold2, float* dt, float* dr,
+                                      int64_t num_nodes, int32_t hidden, int32_t in_features,
+                                      void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0) return GINE_ERR_INVALID;
+  if (num_nodes >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
+  if (!dh0 || !u || !wfold || !wfold2 || !dt || !dr) return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  const int F = in_features;
+  const ChainArgs b{dh0, nullptr, u, wfold, nullptr, wfold2, nullptr, dt, dr, 1.f, F};
+  int rc = GINE_OK;
+#define CALL_B(DD, FF) rc = launch_chain<DD, FF, CH_B2D>(b, num_nodes, st)
+  GINE_CHAIN_DISPATCH(hidden, F, CALL_B);
+#undef CALL_B
+  return rc;
+}
+
+extern "C" int gine_chain_wgrad_folded2(const float* dh0, const float* x, const float* r,
+                                        const float* u, const float* dt, float* slab,
+                                        float* gfold, float* g2fold, int64_t num_nodes,
+                                        int32_t hidden, int32_t in_features, void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0) return GINE_ERR_INVALID;
+  if (!dh0 || !x || !r || !u || !dt || !slab) return GINE_ERR_INVALID;
+  // gfold, g2fold both NULL: the slab is left for gine_grad_finalize_batch
+  const bool reduce = gfold || g2fold;
+  if (reduce && (!gfold || !g2fold)) return GINE_ERR_INVALID;
+  hipStream_t st = as_stream(stream);
+  const int D = hidden, F = in_features;
+  const WgPlan p = chain_wgrad_plan(num_nodes, D, F, 2);
+  const size_t per = (size_t)D * (D + F) + D;
+  const ChainWgradSrc<2> src{{dh0, dt, nullptr, nullptr}, {u, r, nullptr, nullptr}, x, D, F};
+  int rc = launch_wgrad_engine<64>(src, num_nodes, D, D + F, chain_wgrad_tiles(D, F, 2), p,
+                                   per * p.chunks, per, slab, st);
+  if (rc != GINE_OK || !reduce) return rc;
+  return launch_slab_sum(slab, p.chunks, (int64_t)per, per, per * p.chunks, 2,
+                         ChainWgradOut{{gfold, g2fold, nullptr, nullptr},
+                                       {gfold + (size_t)D * (F + D), g2fold + (size_t)D * D,
+                                        nullptr, nullptr},
+                                       D, F, 2, 1.f},
+                         st);
+}
+
+extern "C" int gine_chain_wgrad_folded2_grad_job(int64_t num_nodes, int32_t hidden,
+                                                 int32_t in_features, const float* slab,
+                                                 float* gfold, float* g2fold,
+                                                 gine_grad_job* job) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (num_nodes <= 0 || !slab || !gfold || !g2fold || !job) return GINE_ERR_INVALID;
+  float* w[2] = {gfold, g2fold};  // product order of ChainWgradSrc<2>
+  float* b[2] = {gfold + (size_t)hidden * (hidden + in_features),
+                 g2fold + (size_t)hidden * hidden};
+  chain_slab_job(num_nodes, hidden, in_features, 2, slab, 1.f, w, b, job);
   return GINE_OK;
+}
+
+extern "C" int gine_chain_unfold_grads2(const float* gfold, const float* wr1, const float* br1,
+                                        const float* wdr, float* dwdr, float* dbdr, float* dwr1,
+                                        float* dbr1, const float* g2fold, const float* wp2,
+                                        const float* bp2, const float* wr0, float* dwr0,
+                                        float* dbr0, float* dwp2, float* dbp2, float members,
+                                        int32_t hidden, int32_t in_features, void* stream) {
+  if (!chain_dims_ok(hidden, in_features)) return GINE_ERR_DIM;
+  if (!gfold || !wr1 || !br1 || !wdr || !dwdr || !dwr1) return GINE_ERR_INVALID;
+  if (!g2fold || !wp2 || !bp2 || !wr0 || !dwr0 || !dwp2) return GINE_ERR_INVALID;
+  const UnfoldJob j1{g2fold, wp2, bp2, wr0, dwr0, dbr0, dwp2, dbp2, 0, members};
+  return launch_unfold(hidden,
+                       UnfoldJob{gfold, wr1, br1, wdr, dwdr, dbdr, dwr1, dbr1, in_features, 1.f},
+                       &j1, as_stream(stream));
 }

@@ -146,6 +146,60 @@ __device__ void fold_tile(const FoldArgs& a, int ft, float* sA, float* sR, int c
   }
 }
 
+// The double fold (gine_chain_fwd_folded2): phi[2] is followed by rho[0] with no
+// nonlinearity between them either (the member sum sits in between, and a Linear commutes
+// with it), so  rho[0](s) = r Wf^T + bf  with  Wf = Wr0 Wp2,  bf = M Wr0 bp2 + br0.
+// One [32 x 32] tile (rows k0, columns c0) of Wf into wfold2 ([D][D], then bf [D] by the
+// tiles of column 0): A = Wr0's rows staged in sA, B = Wp2's columns.  Run by the second
+// set of fold workgroups of gine_deepset_fwd_fold2.
+struct Fold2Args {
+  const float *w_r0, *b_r0, *w_p2, *b_p2;
+  float members;
+  float* wfold2;  // NULL: no double fold
+};
+
+template <int D>
+__device__ void fold2_tile(const Fold2Args& a, int ft, float* sA, float* sR, int c32, int h) {
+  constexpr int NT = 2 * D, LDA = D + 4, T = D / 32;
+  const int k0 = 32 * (ft / T), c0 = 32 * (ft % T);
+  const int w = threadIdx.x / kWave;
+  __shared__ float svec2[D];
+  float bf[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) bf[s] = a.w_p2[(size_t)(w * 32 + h * 16 + s) * D + c0 + c32];
+  constexpr int SI = 32 * D / NT;
+  float st[SI];
+#pragma unroll
+  for (int i = 0; i < SI; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    st[i] = a.w_r0[(size_t)(k0 + idx / D) * D + idx % D];
+  }
+  const float bv = threadIdx.x < D ? a.b_p2[threadIdx.x] : 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < SI; ++i) {
+    const int idx = threadIdx.x + i * NT;
+    sA[(idx / D) * LDA + idx % D] = st[i];
+  }
+  if (threadIdx.x < D) svec2[threadIdx.x] = bv;
+  __syncthreads();
+  ksplit_tile<D>(sA, bf, sR, c32, h);
+  if (c0 == 0) {
+    const float v = rows_dot<D>(sA, svec2);  // (Wr0 bp2)[k0 + r]
+    constexpr int TPR = NT / 32;
+    if (threadIdx.x % TPR == 0) {
+      const int r = threadIdx.x / TPR;
+      a.wfold2[(size_t)D * D + k0 + r] = a.members * v + a.b_r0[k0 + r];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int o = threadIdx.x + i * NT;
+    a.wfold2[(size_t)(k0 + o / 32) * D + c0 + o % 32] = ksplit_sum<D>(sR, o / 32, o % 32);
+  }
+}
+
 // F1 of the folded chain launches (D/32)^2 workgroups more than its chain grid: block
 // chain_blocks + t folds tile t of W' beside the chain tiles (they fit on the CUs next to
 // the one chain workgroup per CU).

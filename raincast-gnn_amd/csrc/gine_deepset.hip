@@ -295,7 +295,8 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
                                                        float* __restrict__ r,
                                                        uint16_t* __restrict__ mask_out,
                                                        int64_t N, int M, int F,
-                                                       int num_groups, FoldArgs fold) {
+                                                       int num_groups, FoldArgs fold,
+                                                       Fold2Args fold2) {
   constexpr int NT = 2 * H;
   constexpr int LD = KP + 4;
   constexpr int kWalk = 2 * 32 * LD + 2 * G * H;  // two staged tiles + the group's node sums
@@ -303,11 +304,16 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
   __shared__ __attribute__((aligned(16))) float s_lds[kWalk > kFold ? kWalk : kFold];
   int nbw = gridDim.x, bw = blockIdx.x;  // workgroups walking the groups, this one's index
   if constexpr (FOLD) {
-    nbw -= kFoldBlocks<H>;
-    bw -= kFoldBlocks<H>;
+    const int nfold = kFoldBlocks<H> * (fold2.wfold2 != nullptr ? 2 : 1);
+    nbw -= nfold;
+    bw -= nfold;
     if (bw < 0) {
       const int lane = threadIdx.x % kWave;
-      fold_tile<H>(fold, blockIdx.x, s_lds, s_lds + 32 * (H + 4), lane & 31, lane >> 5);
+      if ((int)blockIdx.x < kFoldBlocks<H>)
+        fold_tile<H>(fold, blockIdx.x, s_lds, s_lds + 32 * (H + 4), lane & 31, lane >> 5);
+      else
+        fold2_tile<H>(fold2, blockIdx.x - kFoldBlocks<H>, s_lds, s_lds + 32 * (H + 4),
+                      lane & 31, lane >> 5);
       return;
     }
   }
@@ -610,7 +616,8 @@ extern "C" int gine_deepset_fwd(const float* ens, const float* w1, const float* 
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD_M(H_, KP_, G_, MK_)                                                        \
   hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_>), dim3(grid), dim3(2 * H_), 0, s, ens, w1, \
-                     b1, r, mask, num_nodes, members, in_features, groups, FoldArgs{})
+                     b1, r, mask, num_nodes, members, in_features, groups, FoldArgs{},       \
+                     Fold2Args{})
 #define LAUNCH_FWD_G(H_, KP_, G_)                             \
   do {                                                        \
     if (mask) LAUNCH_FWD_M(H_, KP_, G_, true);                \
@@ -707,28 +714,29 @@ extern "C" int gine_debug_ds_prof(long long* out, int* n) {
 }
 #endif
 
-extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const float* b1,
-                                     float* r, uint16_t* mask, int64_t num_nodes,
-                                     int32_t members, int32_t in_features, int32_t hidden,
-                                     const float* wr1, const float* br1, const float* wdr,
-                                     const float* bdr, float* wfold, int32_t x_features,
-                                     void* stream) {
+namespace {
+int deepset_fwd_fold(const float* ens, const float* w1, const float* b1, float* r,
+                     uint16_t* mask, int64_t num_nodes, int32_t members, int32_t in_features,
+                     int32_t hidden, const FoldArgs& fold, const Fold2Args& fold2,
+                     void* stream) {
   const int KP = pad_fwd(in_features);
   if ((hidden != 64 && hidden != 128) || KP < 0 || in_features <= 0) return GINE_ERR_DIM;
-  if (x_features < 1 || x_features > 64) return GINE_ERR_DIM;
+  if (fold.F < 1 || fold.F > 64) return GINE_ERR_DIM;
   if (num_nodes < 0 || members <= 0) return GINE_ERR_INVALID;
-  if (!wr1 || !br1 || !wdr || !bdr || !wfold) return GINE_ERR_INVALID;
+  if (!fold.fw_r1 || !fold.fb_r1 || !fold.fw_dr || !fold.fb_dr || !fold.wfold)
+    return GINE_ERR_INVALID;
   if (num_nodes > 0 && (!ens || !w1 || !b1 || !r)) return GINE_ERR_INVALID;
   if (num_nodes * members >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   const int groups = num_groups(num_nodes, hidden);
   const int walk = num_nodes > 0 ? std::min(groups, 1024) : 0;
   const int G = nodes_per_half(num_nodes, hidden);
-  const FoldArgs fold{wr1, br1, wdr, bdr, wfold, x_features};
+  const int nfold = (hidden == 64 ? kFoldBlocks<64> : kFoldBlocks<128>) *
+                    (fold2.wfold2 != nullptr ? 2 : 1);
   hipStream_t s = as_stream(stream);
 #define LAUNCH_FWD_F(H_, KP_, G_, MK_)                                                        \
-  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_, true>), dim3(walk + kFoldBlocks<H_>),   \
+  hipLaunchKernelGGL((k_deepset_fwd<H_, KP_, G_, MK_, true>), dim3(walk + nfold),             \
                      dim3(2 * H_), 0, s, ens, w1, b1, r, mask, num_nodes, members, in_features, \
-                     groups, fold)
+                     groups, fold, fold2)
 #define LAUNCH_FWD_G(H_, KP_, G_)                             \
   do {                                                        \
     if (mask) LAUNCH_FWD_F(H_, KP_, G_, true);                \
@@ -750,4 +758,29 @@ extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const fl
 #undef LAUNCH_FWD_F
   GINE_LAUNCH_STATUS();
   return GINE_OK;
+}
+}  // namespace
+
+extern "C" int gine_deepset_fwd_fold(const float* ens, const float* w1, const float* b1,
+                                     float* r, uint16_t* mask, int64_t num_nodes,
+                                     int32_t members, int32_t in_features, int32_t hidden,
+                                     const float* wr1, const float* br1, const float* wdr,
+                                     const float* bdr, float* wfold, int32_t x_features,
+                                     void* stream) {
+  return deepset_fwd_fold(ens, w1, b1, r, mask, num_nodes, members, in_features, hidden,
+                          FoldArgs{wr1, br1, wdr, bdr, wfold, x_features}, Fold2Args{},
+                          stream);
+}
+
+extern "C" int gine_deepset_fwd_fold2(const float* ens, const float* w1, const float* b1,
+                                      float* r, uint16_t* mask, int64_t num_nodes,
+                                      int32_t members, int32_t in_features, int32_t hidden,
+                                      const float* wr1, const float* br1, const float* wdr,
+                                      const float* bdr, float* wfold, int32_t x_features,
+                                      const float* wr0, const float* br0, const float* wp2,
+                                      const float* bp2, float* wfold2, void* stream) {
+  if (!wr0 || !br0 || !wp2 || !bp2 || !wfold2) return GINE_ERR_INVALID;
+  return deepset_fwd_fold(ens, w1, b1, r, mask, num_nodes, members, in_features, hidden,
+                          FoldArgs{wr1, br1, wdr, bdr, wfold, x_features},
+                          Fold2Args{wr0, br0, wp2, bp2, (float)members, wfold2}, stream);
 }

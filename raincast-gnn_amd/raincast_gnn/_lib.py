@@ -157,6 +157,13 @@ _SIGNATURES = {
     "gine_chain_wgrad_folded_grad_job": [_i64, _i32, _i32, _c_void_p, _f32] + [_c_void_p] * 5
                                         + [_job_p],
     "gine_chain_unfold_grads": [_c_void_p] * 8 + [_i32, _i32, _c_void_p],
+    "gine_deepset_fwd_fold2": [_c_void_p] * 5 + [_i64, _i32, _i32, _i32] + [_c_void_p] * 5
+                              + [_i32] + [_c_void_p] * 6,
+    "gine_chain_fwd_folded2": [_c_void_p] * 6 + [_i64, _i32, _i32, _c_void_p],
+    "gine_chain_bwd_folded2": [_c_void_p] * 6 + [_i64, _i32, _i32, _c_void_p],
+    "gine_chain_wgrad_folded2": [_c_void_p] * 8 + [_i64, _i32, _i32, _c_void_p],
+    "gine_chain_wgrad_folded2_grad_job": [_i64, _i32, _i32] + [_c_void_p] * 3 + [_job_p],
+    "gine_chain_unfold_grads2": [_c_void_p] * 16 + [_f32, _i32, _i32, _c_void_p],
 }
 
 EXPORTED_SYMBOLS = ("gine_abi_version", "gine_status_string") + tuple(_SIGNATURES)

@@ -184,6 +184,79 @@ class _ChainFoldedFn(torch.autograd.Function):
         return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None, None)
 
 
+class _ChainFolded2Fn(torch.autograd.Function):
+    """The doubly folded chain (gine_chain_fwd_folded2, include/gine_hip.h): phi[2] meets
+    rho[0] with only the member sum between them, so ``rho[0](s) = r Wf^T + bf`` with
+    ``Wf = Wr0 Wp2``, ``bf = M Wr0 bp2 + br0`` (folded by the DeepSet launch into the tail
+    of ``wfold``).  Neither s nor its gradient is formed: one 2-stage launch forward
+    (u, h0), one backward (dt, dr), two weight-gradient products (G = dh0^T [x | u],
+    G2 = dt^T r) unfolded into all six chain gradients by one launch."""
+
+    @staticmethod
+    def forward(ctx, r, x, wp2, bp2, wr0, br0, wr1, br1, wdr, bdr, members, wfold):
+        r = r.contiguous()
+        x = x.contiguous()
+        N, D = r.shape
+        F = x.size(1)
+        dev = r.device
+        n1 = 2 * D * (F + D) + D
+        wf1, wf2 = wfold[:n1], wfold[n1:]
+        u, h0 = (torch.empty(N, D, dtype=torch.float32, device=dev) for _ in range(2))
+        P = _lib.ptr
+        _lib.call("gine_chain_fwd_folded2", P(r), P(x), P(wf1), P(wf2), P(u), P(h0), N, D, F,
+                  _lib.stream_handle(dev))
+        ws = [t.detach().contiguous() for t in (wp2, bp2, wr0, wr1, br1, wdr)]
+        ctx.save_for_backward(r, x, u, wfold, *ws)
+        ctx.params = (wp2, bp2, wr0, br0, wr1, br1, wdr, bdr)
+        ctx.members = float(members)
+        return h0
+
+    @staticmethod
+    def backward(ctx, dh0):
+        r, x, u, wfold, wp2, bp2, wr0, wr1, br1, wdr = ctx.saved_tensors
+        N, D = r.shape
+        F = x.size(1)
+        dev = r.device
+        n1 = 2 * D * (F + D) + D
+        wf1, wf2 = wfold[:n1], wfold[n1:]
+        dh0 = dh0.contiguous()
+        dt, dr = (torch.empty(N, D, dtype=torch.float32, device=dev) for _ in range(2))
+        floats = ctypes.c_size_t(0)
+        _lib.call("gine_chain_bwd_slab_floats", N, D, F, ctypes.byref(floats))
+        slab = torch.empty(floats.value, dtype=torch.float32, device=dev)
+        gf = torch.empty(D * (F + D) + D + D * D + D, dtype=torch.float32, device=dev)
+        gfold, g2fold = gf[:D * (F + D) + D], gf[D * (F + D) + D:]
+        p = ctx.params
+        g = [grad_out(p[0], (D, D), dev), grad_out(p[1], (D,), dev),
+             grad_out(p[2], (D, D), dev), grad_out(p[3], (D,), dev),
+             grad_out(p[4], (D, D), dev), grad_out(p[5], (D,), dev),
+             grad_out(p[6], (D, F + D), dev), grad_out(p[7], (D,), dev)]
+        P = _lib.ptr
+        stream = _lib.stream_handle(dev)
+        _lib.call("gine_chain_bwd_folded2", P(dh0), P(u), P(wf1), P(wf2), P(dt), P(dr), N, D, F,
+                  stream)
+        # raw pointers only (see _ChainFoldedFn.backward)
+        ptrs = (P(gfold), P(wr1), P(br1), P(wdr), P(g[6]), P(g[7]), P(g[4]), P(g[5]),
+                P(g2fold), P(wp2), P(bp2), P(wr0), P(g[2]), P(g[3]), P(g[0]), P(g[1]),
+                ctx.members)
+
+        def unfold(st):
+            _lib.call("gine_chain_unfold_grads2", *ptrs, D, F, st)
+
+        if gradbuf.deferrable(*g):
+            _lib.call("gine_chain_wgrad_folded2", P(dh0), P(x), P(r), P(u), P(dt), P(slab), None,
+                      None, N, D, F, stream)
+            job = _lib.GradJob()
+            _lib.call("gine_chain_wgrad_folded2_grad_job", N, D, F, P(slab), P(gfold),
+                      P(g2fold), ctypes.byref(job))
+            gradbuf.defer(job, dev, (slab, gf, wp2, bp2, wr0, wr1, br1, wdr), post=unfold)
+        else:
+            _lib.call("gine_chain_wgrad_folded2", P(dh0), P(x), P(r), P(u), P(dt), P(slab),
+                      P(gfold), P(g2fold), N, D, F, stream)
+            unfold(stream)
+        return (dr, None, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], None, None)
+
+
 # False: the unfolded chain (four GEMM stages forward, e materialised); measured slower
 # (cfg2 0.5749 vs 0.5595 ms per step, r02_s38), kept for the tests that compare the two
 FOLD = True
@@ -195,11 +268,19 @@ FOLD = True
 F3 = True
 F3_MAX_NODES = 32768
 
+# True: on the one-launch path (F3) phi[2] is folded into rho[0] as well (_ChainFolded2Fn)
+FOLD2 = True
+
 
 def chain(r: torch.Tensor, x: torch.Tensor, lins, members: int, wfold=None) -> torch.Tensor:
     """``dim_red(cat([x, rho(phi[2](r) summed over members)]))`` on the fused kernels;
-    ``wfold`` = the folded dim_red weight from gine_deepset_fwd_fold (folded chain only)."""
+    ``wfold`` = the folded dim_red weight from gine_deepset_fwd_fold (folded chain only; with
+    [Wf | bf] appended by gine_deepset_fwd_fold2, the doubly folded chain)."""
     p2, r0, r1, dr = lins
+    D = r.size(1)
+    if FOLD and wfold is not None and wfold.numel() > 2 * D * (x.size(1) + D) + D:
+        return _ChainFolded2Fn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight,
+                                     r1.bias, dr.weight, dr.bias, members, wfold)
     if FOLD:
         return _ChainFoldedFn.apply(r, x, p2.weight, p2.bias, r0.weight, r0.bias, r1.weight,
                                     r1.bias, dr.weight, dr.bias, members, wfold)

@@ -56,12 +56,20 @@ class _PhiSumFn(torch.autograd.Function):
             _lib.call("gine_deepset_fwd", _lib.ptr(ens), _lib.ptr(weight), _lib.ptr(bias),
                       _lib.ptr(r), _lib.ptr(mask), N, M, Fdim, H, stream)
             return r
-        wr1, br1, wdr, bdr = (t.detach().contiguous() for t in fold)
+        wr1, br1, wdr, bdr, *more = (t.detach().contiguous() for t in fold)
         F = wdr.size(1) - H
-        wfold = torch.empty(2 * H * (F + H) + H, dtype=torch.float32, device=ens.device)
-        _lib.call("gine_deepset_fwd_fold", _lib.ptr(ens), _lib.ptr(weight), _lib.ptr(bias),
-                  _lib.ptr(r), _lib.ptr(mask), N, M, Fdim, H, _lib.ptr(wr1), _lib.ptr(br1),
-                  _lib.ptr(wdr), _lib.ptr(bdr), _lib.ptr(wfold), F, stream)
+        n1 = 2 * H * (F + H) + H
+        P = _lib.ptr
+        if not more:
+            wfold = torch.empty(n1, dtype=torch.float32, device=ens.device)
+            _lib.call("gine_deepset_fwd_fold", P(ens), P(weight), P(bias), P(r), P(mask), N, M,
+                      Fdim, H, P(wr1), P(br1), P(wdr), P(bdr), P(wfold), F, stream)
+        else:  # the double fold: [W' | b' | W'^T] then [Wf | bf] in one buffer
+            wr0, br0, wp2, bp2 = more
+            wfold = torch.empty(n1 + H * H + H, dtype=torch.float32, device=ens.device)
+            _lib.call("gine_deepset_fwd_fold2", P(ens), P(weight), P(bias), P(r), P(mask), N, M,
+                      Fdim, H, P(wr1), P(br1), P(wdr), P(bdr), P(wfold), F, P(wr0), P(br0),
+                      P(wp2), P(bp2), P(wfold[n1:]), stream)
         ctx.mark_non_differentiable(wfold)
         # no zero-filled gradient for wfold in the backward (a fill launch per step)
         ctx.set_materialize_grads(False)
@@ -95,9 +103,10 @@ class _PhiSumFn(torch.autograd.Function):
 
 def phi_sum(ens: torch.Tensor, lin1: torch.nn.Linear, fold=None):
     """``relu(lin1(ens)).sum(dim=1)`` for ens [N, M, F] on the fused kernels; with
-    ``fold`` = (rho[2], dim_red) Linears, (r, wfold) for the one-launch folded chain."""
+    ``fold`` = (rho[2], dim_red) Linears, (r, wfold) for the one-launch folded chain; with
+    ``fold`` = (rho[2], dim_red, rho[0], phi[2]), (r, wfold) for the doubly folded chain
+    (wfold then also holds [Wf | bf], gine_deepset_fwd_fold2)."""
     if fold is None:
         return _PhiSumFn.apply(ens, lin1.weight, lin1.bias)
-    r1, dr = fold
     return _PhiSumFn.apply(ens, lin1.weight, lin1.bias,
-                           (r1.weight, r1.bias, dr.weight, dr.bias))
+                           tuple(t for m in fold for t in (m.weight, m.bias)))

@@ -125,7 +125,9 @@ class GNN(nn.Module):
             if (fused_chain.FOLD and fused_chain.F3 and ens.size(0) <= fused_chain.F3_MAX_NODES
                     and fused_chain.fusable_dims(lin1.out_features, x, lins)):
                 # the DeepSet launch also folds dim_red; the chain forward is one launch
-                r, wfold = deepset.phi_sum(ens, lin1, fold=(rho1, self.dim_red))
+                fold = ((rho1, self.dim_red, rho0, lin2) if fused_chain.FOLD2
+                        else (rho1, self.dim_red))
+                r, wfold = deepset.phi_sum(ens, lin1, fold=fold)
                 return fused_chain.chain(r, x, lins, ens.size(1), wfold=wfold)
             r = deepset.phi_sum(ens, lin1)
             if fused_chain.fusable(r, x, lins):

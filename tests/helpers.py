@@ -199,7 +199,7 @@ class EngineTies:
         self.tol = tol
         self.layers = []      # per GINE layer: dict of engine tensors (reference order, fp64)
         self.phi_on = None    # [N, M, H] bool
-        self.s = self.u = None
+        self.s = self.u = self.r_e = None
         self.log = []
         self.input_err = []   # (layer, max-norm relative |x_e - x64|)
         self._outs = []
@@ -256,11 +256,22 @@ class EngineTies:
         h0 = self._front
         assert h0 is not None and h0.grad_fn is not None, "the fused chain did not run"
         sv = h0.grad_fn.saved_tensors
-        self.s, self.u = ref(sv[2]).double(), ref(sv[3])
+        if type(h0.grad_fn).__name__.startswith("_ChainFolded2Fn"):
+            # doubly folded chain (r, x, u, wfold, ...): rho[0]'s pre-activation is
+            # r Wf^T + bf with the engine's folded [Wf | bf] at the tail of wfold
+            r_e, u, wfold = sv[0], sv[2], sv[3]
+            H = u.size(1)
+            tail = wfold.detach().cpu().double()[-(H * H + H):]
+            self.s, self.r_e = None, ref(r_e).double()
+            self.wf, self.bf = tail[:H * H].view(H, H), tail[H * H:]
+            self.u = ref(u)
+        else:
+            self.s, self.u, self.r_e = ref(sv[2]).double(), ref(sv[3]), None
         ds_fn = h0.grad_fn.next_functions[0][0]
         ens, mask = ds_fn.saved_tensors[:2]
         N, M, _ = ens.shape
-        H = self.s.size(1)
+        self.members = M
+        H = self.u.size(1)
         G = ctypes_int(lambda out: _lib.call("gine_deepset_mask_layout", N, H, out))
         words = mask.detach().cpu().numpy().view(np.uint16)
         on = torch.from_numpy(decode_deepset_mask(words, N, M, H, G))
@@ -328,8 +339,19 @@ class EngineTies:
                                        + p0.bias.detach().abs())
             return self._adopt("deepset.phi0", v.detach(), self.phi_on, beta)
 
-        def rho(v, s):
+        def rho(v, s, r=None):
             K = r0.weight.size(1)
+            if self.s is None:  # doubly folded: pre_e = fl(r_e Wf_e^T + bf_e)
+                p2 = r64.deepset.phi[2]
+                Wr0, br0 = r0.weight.detach(), r0.bias.detach()
+                wf64 = Wr0 @ p2.weight.detach()
+                bf64 = self.members * (Wr0 @ p2.bias.detach()) + br0
+                We = self.wf.abs().t()
+                re, r64_ = self.r_e, r.detach()
+                beta = 2 * ((re - r64_).abs() @ We + r64_.abs() @ (self.wf - wf64).abs().t()
+                            + (self.bf - bf64).abs()
+                            + gamma_dot(K) * (re.abs() @ We + self.bf.abs()))
+                return self._adopt("deepset.rho0", v.detach(), self.u > 0, beta)
             W = r0.weight.detach().abs().t()
             beta = 2 * ((self.s - s.detach()).abs() @ W
                         + gamma_dot(K) * (self.s.abs() @ W + r0.bias.detach().abs()))
@@ -380,7 +402,7 @@ def oracle32_ties(ref, batch, tol=1e-5):
         t.phi_on = v.detach() > 0
         return t.phi_on
 
-    def rho(v, s):
+    def rho(v, s, r=None):
         t.s, t.u = s.detach().double(), v.detach().clamp_min(0)
         return v.detach() > 0
     r.deepset.decide = {"phi": phi, "rho": rho}
@@ -499,11 +521,18 @@ def check_training_step(params, batch, dev, tol=1e-5, seed=42, relabel=False, re
     gb = engine_order_batch(batch) if relabel else batch
     ties = EngineTies(tol).attach(model)
     gbd = gb.to(dev)
+    # the benchmarked path (bench.py Trainer.fwd_bwd): gradients written into FlatAdamW's
+    # flat buffer by the deferred backward, reduced by the end-of-backward batch
+    from raincast_gnn import gradbuf
+    from raincast_gnn.optim import FlatAdamW
+    opt = FlatAdamW(model.parameters(), lr=1e-3)
+    opt.zero_grad()
     pred = model(gbd)
     loss = model.loss_fn.crps(pred, gbd.y)
     ties.read(model, gbd)
     ties._ens = batch.ensemble.double()
-    loss.backward()
+    gradbuf.loss_backward(loss)
+    opt.gather_grads()
     pred = restore_node_order(pred, gb)
     r32, pred32, loss32 = _oracle_step(ref, batch, torch.float32)
     r64, pred64, loss64 = _oracle_step(ref, batch, torch.float64)

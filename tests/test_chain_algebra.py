@@ -42,3 +42,31 @@ def test_folded_chain_identities():
         assert torch.allclose(Wdr_e.T @ gs, dbr1, rtol=1e-12, atol=1e-12)
         # the input gradient of u (before the ReLU mask) is dh0 Wc
         assert torch.allclose(dh0 @ Wc, grads[8], rtol=1e-12, atol=1e-12)
+
+
+def test_double_folded_chain_identities():
+    """phi[2] folded into rho[0] too (gine_chain_*_folded2):  pre = r Wf^T + bf with
+    Wf = Wr0 Wp2, bf = M Wr0 bp2 + br0;  with dt the gradient of pre, G2 = dt^T r and
+    g2 = sum_n dt:  dWr0 = G2 Wp2^T + M g2 bp2^T, dbr0 = g2, dWp2 = Wr0^T G2,
+    dbp2 = M Wr0^T g2, dr = dt Wf."""
+    g = torch.Generator().manual_seed(1)
+    N, D, M = 301, 16, 7.0
+    d = dict(dtype=torch.float64)
+    r = torch.randn(N, D, generator=g, **d).requires_grad_()
+    Wp2, Wr0 = (torch.randn(D, D, generator=g, **d) / 4 for _ in range(2))
+    bp2, br0 = (torch.randn(D, generator=g, **d) for _ in range(2))
+    params = [t.requires_grad_() for t in (Wp2, bp2, Wr0, br0)]
+    pre = (r @ Wp2.T + M * bp2) @ Wr0.T + br0
+    dt = torch.randn(N, D, generator=g, **d)
+    dWp2, dbp2, dWr0, dbr0, dr = torch.autograd.grad(pre, params + [r], dt)
+    with torch.no_grad():
+        Wf = Wr0 @ Wp2
+        bf = M * (Wr0 @ bp2) + br0
+        kw = dict(rtol=1e-12, atol=1e-12)
+        assert torch.allclose(r @ Wf.T + bf, pre, **kw)
+        G2, g2 = dt.T @ r, dt.sum(0)
+        assert torch.allclose(G2 @ Wp2.T + M * torch.outer(g2, bp2), dWr0, **kw)
+        assert torch.allclose(g2, dbr0, **kw)
+        assert torch.allclose(Wr0.T @ G2, dWp2, **kw)
+        assert torch.allclose(M * (Wr0.T @ g2), dbp2, **kw)
+        assert torch.allclose(dt @ Wf, dr, **kw)

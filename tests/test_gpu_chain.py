@@ -214,3 +214,112 @@ def test_chain_one_launch_forward_matches_two_launch(N, D, F):
                                      for p in (m.weight, m.bias)])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def _ens_lin1(N, D, M=11, Fe=36, seed=0):
+    torch.manual_seed(seed)
+    return torch.randn(N, M, Fe, device=DEV), torch.nn.Linear(Fe, D).to(DEV)
+
+
+@pytest.mark.parametrize("N,D,F", [(33, 128, 35), (300, 64, 35), (2000, 128, 64),
+                                   (16000, 128, 35)])
+def test_chain_folded2_intermediates(N, D, F):
+    """The doubly folded chain's pieces (C ABI) against fp64 torch: [Wf | bf] from the
+    DeepSet launch (whose r and [W' | b' | W'^T] equal the single fold's bit for bit), u / h0
+    forward, dt / dr backward, G and G2 from the engine and all eight weight gradients
+    unfolded from them.  References use the engine's u for the ReLU mask."""
+    import ctypes
+
+    from raincast_gnn import _lib, deepset
+    M = 11
+    ens, lin1 = _ens_lin1(N, D, M, seed=N + D)
+    lins = _lins(D, F, N + 1)
+    p2, r0, r1, dr_ = lins
+    x = torch.randn(N, F, device=DEV)
+    with torch.no_grad():
+        r, wfold = deepset.phi_sum(ens, lin1, fold=(r1, dr_, r0, p2))
+        r_1, wfold_1 = deepset.phi_sum(ens, lin1, fold=(r1, dr_))
+    n1 = 2 * D * (F + D) + D
+    assert wfold.numel() == n1 + D * D + D
+    assert torch.equal(r, r_1) and torch.equal(wfold[:n1], wfold_1)
+    d = lambda t: t.detach().double()  # noqa: E731
+    wp2, bp2, wr0, br0 = d(p2.weight), d(p2.bias), d(r0.weight), d(r0.bias)
+    wr1, br1, wdr, bdr = d(r1.weight), d(r1.bias), d(dr_.weight), d(dr_.bias)
+    assert _rel(wfold[n1:n1 + D * D].view(D, D), wr0 @ wp2) <= TOL
+    assert _rel(wfold[n1 + D * D:], M * (wr0 @ bp2) + br0) <= TOL
+
+    P = _lib.ptr
+    st = _lib.stream_handle(DEV)
+    u, h0 = (torch.empty(N, D, device=DEV) for _ in range(2))
+    wf1, wf2 = wfold[:n1], wfold[n1:]
+    _lib.call("gine_chain_fwd_folded2", P(r), P(x), P(wf1), P(wf2), P(u), P(h0), N, D, F, st)
+    s64 = d(r) @ wp2.T + M * bp2
+    u64 = torch.relu(s64 @ wr0.T + br0)
+    h64 = torch.cat([d(x), d(u) @ wr1.T + br1], 1) @ wdr.T + bdr
+    torch.cuda.synchronize()
+    assert _rel(u, u64) <= TOL and _rel(h0, h64) <= TOL
+
+    dh0 = torch.randn(N, D, device=DEV)
+    dt, dr = (torch.empty(N, D, device=DEV) for _ in range(2))
+    _lib.call("gine_chain_bwd_folded2", P(dh0), P(u), P(wf1), P(wf2), P(dt), P(dr), N, D, F, st)
+    fl = ctypes.c_size_t(0)
+    _lib.call("gine_chain_bwd_slab_floats", N, D, F, ctypes.byref(fl))
+    slab = torch.empty(fl.value, device=DEV)
+    gfold = torch.empty(D * (F + D) + D, device=DEV)
+    g2fold = torch.empty(D * D + D, device=DEV)
+    g = [torch.full((D, D), 5.0, device=DEV), torch.empty(D, device=DEV),
+         torch.full((D, D), 5.0, device=DEV), torch.empty(D, device=DEV),
+         torch.full((D, D), 5.0, device=DEV), torch.empty(D, device=DEV),
+         torch.full((D, F + D), 5.0, device=DEV), torch.empty(D, device=DEV)]
+    _lib.call("gine_chain_wgrad_folded2", P(dh0), P(x), P(r), P(u), P(dt), P(slab), P(gfold),
+              P(g2fold), N, D, F, st)
+    wr1_, br1_, wdr_ = (t.detach().contiguous() for t in (r1.weight, r1.bias, dr_.weight))
+    wp2_, bp2_, wr0_ = (t.detach().contiguous() for t in (p2.weight, p2.bias, r0.weight))
+    _lib.call("gine_chain_unfold_grads2", P(gfold), P(wr1_), P(br1_), P(wdr_), P(g[6]),
+              P(g[7]), P(g[4]), P(g[5]), P(g2fold), P(wp2_), P(bp2_), P(wr0_), P(g[2]), P(g[3]),
+              P(g[0]), P(g[1]), float(M), D, F, st)
+    torch.cuda.synchronize()
+    de64 = d(dh0) @ wdr[:, F:]
+    dt64 = (de64 @ wr1) * (u > 0).double()
+    ds64 = dt64 @ wr0
+    assert _rel(dt, dt64) <= TOL, "dt"
+    assert _rel(dr, ds64 @ wp2) <= TOL, "dr"
+    assert _rel(g2fold[:D * D].view(D, D), dt64.T @ d(r)) <= TOL, "G2"
+    assert _rel(g2fold[D * D:], dt64.sum(0)) <= TOL, "g2"
+    xe = torch.cat([d(x), d(u) @ wr1.T + br1], 1)
+    for name, got, ref in (("dWp2", g[0], ds64.T @ d(r)), ("dbp2", g[1], M * ds64.sum(0)),
+                           ("dWr0", g[2], dt64.T @ s64), ("dbr0", g[3], dt64.sum(0)),
+                           ("dWr1", g[4], de64.T @ d(u)), ("dbr1", g[5], de64.sum(0)),
+                           ("dWdr", g[6], d(dh0).T @ xe), ("dbdr", g[7], d(dh0).sum(0))):
+        assert _rel(got, ref) <= TOL, (name, _rel(got, ref))
+
+
+@pytest.mark.parametrize("N,D,F", [(2000, 128, 35), (33, 64, 20), (4000, 128, 64)])
+def test_chain_folded2_module_path(N, D, F):
+    """chain() on the doubly folded buffer (the models.py path) against the single fold
+    within TOL (only the rounding of Wf / bf differs; sizes small enough that no ReLU
+    decision of rho[0] sits inside that rounding -- the model parity tests hold the full
+    sizes to the branch oracle) and bit-identical when repeated; the deferred-gradient form
+    (flat buffer) is covered by the model tests."""
+    from raincast_gnn import deepset
+    M = 11
+    ens, lin1 = _ens_lin1(N, D, M, seed=N)
+    lins = _lins(D, F, N)
+    x = torch.randn(N, F, device=DEV)
+    outs = []
+    for fold in ((lins[2], lins[3]), (lins[2], lins[3], lins[1], lins[0]),
+                 (lins[2], lins[3], lins[1], lins[0])):
+        for m in lins + (lin1,):
+            m.zero_grad(set_to_none=True)
+        r, wfold = deepset.phi_sum(ens, lin1, fold=fold)
+        h0 = fused_chain.chain(r, x, lins, M, wfold=wfold)
+        assert type(h0.grad_fn).__name__.startswith(
+            "_ChainFolded2Fn" if len(fold) == 4 else "_ChainFoldedFn")
+        h0.backward(torch.ones_like(h0))
+        outs.append([h0.detach()] + [p.grad.clone() for m in lins + (lin1,)
+                                     for p in (m.weight, m.bias)])
+    for a, b in zip(outs[1], outs[2]):
+        assert torch.equal(a, b)
+    names = ["h0"] + [f"{m}.{p}" for m in ("p2", "r0", "r1", "dr", "phi0") for p in ("w", "b")]
+    for name, a, b in zip(names, outs[0], outs[1]):
+        assert _rel(b, a) <= 2 * TOL, (name, _rel(b, a))
