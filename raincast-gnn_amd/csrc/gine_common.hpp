@@ -49,6 +49,21 @@ __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 
 // and a select.  A NaN comes out quieted (its payload may differ from the CPU's).
 __device__ __forceinline__ float relu_nan(float v) { return __builtin_elementwise_maximum(v, 0.0f); }
 
+// True in every thread when `pred` holds in any thread of the workgroup.  `word`: an int of
+// the caller's LDS that nothing else touches during the call (no static LDS of its own,
+// unlike __syncthreads_or: kernels that raise their dynamic-LDS ceiling to the whole 160 KiB
+// cannot have any).  Four barriers; every thread has read the answer before any returns.
+__device__ __forceinline__ bool block_any(bool pred, int* word) {
+  __syncthreads();
+  if (threadIdx.x == 0) *word = 0;
+  __syncthreads();
+  if (pred) *word = 1;  // the same value from every writer
+  __syncthreads();
+  const bool any = *word != 0;
+  __syncthreads();
+  return any;
+}
+
 // Edge Linear(1, D): a*w + b, rounded like the host CPU's PyG path (see gine_hip.h).
 template <bool FMA>
 __device__ __forceinline__ float edge_lin(float a, float w, float b) {

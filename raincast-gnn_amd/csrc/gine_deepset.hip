@@ -20,6 +20,7 @@
 //    that B -- read from the staged ens rows 16h+q -- follows too).
 #include "gine_common.hpp"
 #include "gine_chainfold.hpp"
+#include "gine_bf16x3.hpp"
 
 #include <algorithm>
 
@@ -34,6 +35,49 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // padding) when there are enough nodes to fill the chip; G = 8 doubles the workgroups of a
 // small batch (cfg2: 1,000 instead of 500) at the cost of <= 15 padding rows per half.
 __host__ __device__ constexpr int tiles_per_group(int G, int M) { return (G * M + 15) / 16; }
+
+// The forward's pre-activation chain on the bf16 matrix cores in three-way split form
+// (gine_bf16x3.hpp): each staged ens value is split ONCE, by the thread that stages it, into
+// three bf16 planes (images [32][RS] per plane, k padded to a multiple of 16 with zeros;
+// rows of RS*2 = 16 x odd bytes, so the 16-byte row reads of 16 consecutive rows cover all
+// banks), W1 is split once per workgroup into register planes, and a 32-row tile costs
+// ceil(K/16) x 6 v_mfma_f32_32x32x16_bf16 (192 cycles per 16 k) instead of K/2
+// v_mfma_f32_32x32x2_f32 (64 cycles per 2 k): 576 instead of 1,280 cycles at K = 35.  A
+// wave whose accumulators see a NaN (a non-finite ens value or weight) redoes its tile on
+// the fp32 chain from global memory, which is the fp32 form's exact result.
+// GINE_DS_BF16X3=0 (A/B builds) keeps the fp32 chain.
+#ifndef GINE_DS_BF16X3
+#define GINE_DS_BF16X3 1
+#endif
+template <int KP>
+struct DsImg {
+  static constexpr int KX = (KP + 15) / 16 * 16;  // k of the split chain
+  static constexpr int RS = KX + 8;               // row stride (bf16 elements)
+  static constexpr int PLANE = 32 * RS;           // elements per plane
+  static constexpr int FLOATS = 3 * PLANE / 2;    // one tile's three planes, in floats
+};
+// The backward's images: 32 or 64 features (all on the matrix cores), rows of RS bf16 with
+// RS % 128 in {32, 96}, so the four rows of a half's transposed read land 16 banks apart.
+template <int KI>
+struct DsBwdImg {
+  static_assert(KI == 32 || KI == 64, "feature tiles");
+  static constexpr int RS = KI == 32 ? 32 : 96;   // RS % 128 in {32, 96}
+  static constexpr int PLANE = 32 * RS;
+  static constexpr int FLOATS = 3 * PLANE / 2;
+};
+constexpr int ds_bwd_ki(int KP) { return KP <= 32 ? 32 : 64; }
+template <int KP, bool X3, int KI>
+constexpr int stager_ld() {
+  if constexpr (!X3) return KP + 4;
+  else if constexpr (KI == 0) return DsImg<KP>::RS;
+  else return DsBwdImg<KI>::RS;
+}
+template <int KP, bool X3, int KI>
+constexpr int stager_plane() {
+  if constexpr (!X3) return 0;
+  else if constexpr (KI == 0) return DsImg<KP>::PLANE;
+  else return DsBwdImg<KI>::PLANE;
+}
 
 #ifdef GINE_DS_PROFILE
 // Debug build only: block 0 / thread 0 records s_memtime at phase boundaries of its tiles.
@@ -67,10 +111,13 @@ __device__ __forceinline__ int staged_row(int i) {
 // G*M*c + 16*t + j (c = lane half, j < 16): two contiguous runs of 16*F floats.  Offsets
 // depend only on the thread, so they are computed once; the loads address a uniform
 // (scalar) tile base plus a 32-bit lane offset.
-template <int NT, int KP, bool PAD>  // PAD: G*M % 16 != 0 is possible (G = 8)
+// X3: the staged tile is three bf16 planes (dst in bf16 elements): DsImg<KP>'s (the
+// forward, KI = 0) or DsBwdImg<KI>'s (the backward)
+template <int NT, int KP, bool PAD, bool X3 = false, int KI = 0>  // PAD: G*M % 16 != 0 possible
 struct Stager {
   static constexpr int PER = (32 * KP + NT - 1) / NT;  // >= 32*F / NT
-  static constexpr int LD = KP + 4;
+  static constexpr int LD = stager_ld<KP, X3, KI>();
+  static constexpr int kPlane = stager_plane<KP, X3, KI>();
   int src[PER];  // float offset from the tile's first row (0 if the thread has no element)
   int row[PER];  // group-row offset from the tile's first row (INT_MAX: no element)
   int dst[PER];  // LDS offset (-1: no element)
@@ -124,9 +171,32 @@ struct Stager {
     return ok;
   }
   __device__ __forceinline__ void store(float* s_e, const float (&v)[PER], uint32_t ok) const {
+    if constexpr (X3) {
+      constexpr int PL = kPlane;
+      uint16_t* img = reinterpret_cast<uint16_t*>(s_e);
 #pragma unroll
-    for (int i = 0; i < PER; ++i)
-      if (dst[i] >= 0) s_e[dst[i]] = ((ok >> i) & 1u) ? v[i] : 0.f;
+      for (int i = 0; i < PER; i += 2) {  // values split in pairs (v_cvt_pk_bf16_f32)
+        const int i1 = i + 1 < PER ? i + 1 : i;
+        const float a = ((ok >> i) & 1u) ? v[i] : 0.f;
+        const float b = ((ok >> i1) & 1u) ? v[i1] : 0.f;
+        uint32_t ph, pm, pl;
+        split2(a, b, ph, pm, pl);
+        if (dst[i] >= 0) {
+          img[dst[i]] = (uint16_t)ph;
+          img[PL + dst[i]] = (uint16_t)pm;
+          img[2 * PL + dst[i]] = (uint16_t)pl;
+        }
+        if (i + 1 < PER && dst[i1] >= 0) {
+          img[dst[i1]] = (uint16_t)(ph >> 16);
+          img[PL + dst[i1]] = (uint16_t)(pm >> 16);
+          img[2 * PL + dst[i1]] = (uint16_t)(pl >> 16);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (dst[i] >= 0) s_e[dst[i]] = ((ok >> i) & 1u) ? v[i] : 0.f;
+    }
   }
 };
 
@@ -136,6 +206,17 @@ __device__ __forceinline__ void zero_pad(float* s_e, int F) {
   for (int i = threadIdx.x; i < 32 * (LD - F); i += blockDim.x) {
     const int r = i / (LD - F), c = F + i % (LD - F);
     s_e[r * LD + c] = 0.f;
+  }
+}
+// The planes' columns F.. of every row (never written by the stager)
+template <int KP>
+__device__ __forceinline__ void zero_pad_x3(float* s_e, int F) {
+  using I = DsImg<KP>;
+  uint16_t* img = reinterpret_cast<uint16_t*>(s_e);
+  const int w = I::RS - F;
+  for (int i = threadIdx.x; i < 3 * 32 * w; i += blockDim.x) {
+    const int pr = i / w, c = F + i % w;  // pr = plane * 32 + row
+    img[pr * I::RS + c] = 0;
   }
 }
 
@@ -154,6 +235,61 @@ __device__ __forceinline__ floatx16 pre_tile(const float* s_e, const float (&bf)
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bf[4 * q + 1], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bf[4 * q + 2], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// The split chain: A fragments (ds_read_b128 of 8 k per plane) from the tile's planes, B =
+// W1's register planes (wb[b]: k = 16b + 8h + j of this lane's column).
+template <int KP>
+__device__ __forceinline__ floatx16 pre_tile_x3(const float* s_e,
+                                                const Bf16x3 (&wb)[DsImg<KP>::KX / 16],
+                                                int c32, int h) {
+  using I = DsImg<KP>;
+  const uint16_t* img = reinterpret_cast<const uint16_t*>(s_e) + staged_row(c32) * I::RS + 8 * h;
+  floatx16 acc = zero16();
+#pragma unroll
+  for (int b = 0; b < I::KX / 16; ++b) {
+    Bf16x3 a;
+    a.h = *reinterpret_cast<const bf16x8_t*>(img + 16 * b);
+    a.m = *reinterpret_cast<const bf16x8_t*>(img + I::PLANE + 16 * b);
+    a.l = *reinterpret_cast<const bf16x8_t*>(img + 2 * I::PLANE + 16 * b);
+    acc = mfma_bf16x3(a, wb[b], acc);
+  }
+  return acc;
+}
+template <int KP>
+__device__ __forceinline__ void load_b_x3(const float* __restrict__ w1, int col, int h, int F,
+                                          Bf16x3 (&wb)[DsImg<KP>::KX / 16]) {
+#pragma unroll
+  for (int b = 0; b < DsImg<KP>::KX / 16; ++b) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * b + 8 * h + j;
+      v[j] = k < F ? w1[(size_t)col * F + k] : 0.f;
+    }
+    wb[b] = split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+  }
+}
+// The rare path: this wave's tile on the fp32 chain, A rows and W1 read from global memory
+// (same operands and k order as pre_tile, so the same bits as the fp32 form).
+template <int KP>
+__device__ __noinline__ floatx16 pre_tile_mem(const float* __restrict__ ens,
+                                              const float* __restrict__ w1, int64_t row0,
+                                              int64_t rows_total, int GM, int half_lim, int F,
+                                              int col, int c32, int h) {
+  constexpr int KS = KP / 2;
+  const int tr = staged_row(c32), c = tr >> 4, j = tr & 15;
+  const int64_t grow = row0 + (int64_t)c * GM + j;
+  const bool valid = grow < rows_total && j < half_lim;
+  floatx16 acc = zero16();
+#pragma unroll 1
+  for (int s = 0; s < KS; ++s) {
+    const int k = h * KS + s;
+    const float a = (valid && k < F) ? ens[grow * F + k] : 0.f;
+    const float b = k < F ? w1[(size_t)col * F + k] : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
   }
   return acc;
 }
@@ -216,13 +352,13 @@ struct Cursor {
 // (never consumed) instead of being skipped, so no register merge at the loop's back edge
 // waits for them (backward 41.4 -> 39.0 us at 16,000 nodes; the forward, whose ring holds
 // no mask word, runs 0.9 us slower that way: profiles/r03_s35).
-template <bool UNCOND, int NT, int KP, bool PAD, class Body>
+template <bool UNCOND, int NT, int KP, bool PAD, bool X3, int KI, class Body>
 __device__ __forceinline__ void walk_tiles(const Groups& gr, int GM, int tpg,
-                                           const Stager<NT, KP, PAD>& st,
+                                           const Stager<NT, KP, PAD, X3, KI>& st,
                                            const float* __restrict__ ens, int64_t rows_total,
                                            int F, float* buf0, float* buf1,
                                            const uint16_t* __restrict__ mask_in, Body&& tile) {
-  constexpr int PER = Stager<NT, KP, PAD>::PER;
+  constexpr int PER = Stager<NT, KP, PAD, X3, KI>::PER;
   if (gr.first >= gr.end) return;
   const int count = ((gr.end - gr.first + gr.step - 1) / gr.step) * tpg;
   Cursor cur, pf;  // tile being computed, tile being loaded
@@ -289,7 +425,7 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int GM, int tpg,
 // walk) and share one LDS buffer with the walk's tiles (so the walk's occupancy is that of
 // the larger of the two, not of their sum).
 template <int H, int KP, int G, bool MASK, bool FOLD = false>
-__global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__ ens,
+__global__ __launch_bounds__(2 * H, 4) void k_deepset_fwd(const float* __restrict__ ens,
                                                        const float* __restrict__ w1,
                                                        const float* __restrict__ b1,
                                                        float* __restrict__ r,
@@ -298,8 +434,9 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
                                                        int num_groups, FoldArgs fold,
                                                        Fold2Args fold2) {
   constexpr int NT = 2 * H;
-  constexpr int LD = KP + 4;
-  constexpr int kWalk = 2 * 32 * LD + 2 * G * H;  // two staged tiles + the group's node sums
+  constexpr bool X3 = GINE_DS_BF16X3 != 0;
+  constexpr int TILEF = X3 ? DsImg<KP>::FLOATS : 32 * (KP + 4);  // one staged tile (floats)
+  constexpr int kWalk = 2 * TILEF + 2 * G * H;  // two staged tiles + the group's node sums
   constexpr int kFold = FOLD ? 32 * (H + 4) + (H / 32) * kSR : 0;
   __shared__ __attribute__((aligned(16))) float s_lds[kWalk > kFold ? kWalk : kFold];
   int nbw = gridDim.x, bw = blockIdx.x;  // workgroups walking the groups, this one's index
@@ -317,18 +454,25 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
       return;
     }
   }
-  float(*s_e)[32 * LD] = reinterpret_cast<float(*)[32 * LD]>(s_lds);
-  float* s_r = s_lds + 2 * 32 * LD;  // node sums of the current group
+  float(*s_e)[TILEF] = reinterpret_cast<float(*)[TILEF]>(s_lds);
+  float* s_r = s_lds + 2 * TILEF;  // node sums of the current group
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
-  float bf[KP / 2];
-  load_b<KP>(w1, col, h, F, bf);
+  float bf[X3 ? 1 : KP / 2];
+  Bf16x3 wb[X3 ? DsImg<KP>::KX / 16 : 1];
+  if constexpr (X3) {
+    load_b_x3<KP>(w1, col, h, F, wb);
+    zero_pad_x3<KP>(s_e[0], F);
+    zero_pad_x3<KP>(s_e[1], F);
+  } else {
+    load_b<KP>(w1, col, h, F, bf);
+    zero_pad<KP>(s_e[0], F);
+    zero_pad<KP>(s_e[1], F);
+  }
   const float bias = b1[col];
-  zero_pad<KP>(s_e[0], F);
-  zero_pad<KP>(s_e[1], F);
 
-  Stager<NT, KP, G != 16> st;
+  Stager<NT, KP, G != 16, X3> st;
   st.init(F, M, G);
   const Groups gr(num_groups, nbw, bw);
   const int GM = G * M, tpg = tiles_per_group(G, M);
@@ -343,7 +487,14 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
       rem = M;
       run = 0.f;
     }
-    const floatx16 acc = pre_tile<KP>(buf, bf, c32, h);
+    floatx16 acc;
+    if constexpr (X3) {
+      acc = pre_tile_x3<KP>(buf, wb, c32, h);
+      if (wave_any_nan(acc))  // non-finite operand: the fp32 chain's result instead
+        acc = pre_tile_mem<KP>(ens, w1, c.row, N * M, GM, GM - 16 * c.t, F, col, c32, h);
+    } else {
+      acc = pre_tile<KP>(buf, bf, c32, h);
+    }
     DS_MARK(2 + 0 * (int)acc[15]);
     uint32_t bits = 0;
 #pragma unroll
@@ -376,25 +527,52 @@ __global__ __launch_bounds__(2 * H) void k_deepset_fwd(const float* __restrict__
 
 // ---------------------------------------------------------------------------------------
 // Backward for the weights from the forward's ReLU mask:
-//   dh = dr[node] * mask;  dW1 += dh^T ens (MFMA over 32-feature tiles, A = dh straight from
-//   registers, B = staged rows; the last F % 32 features as fp32 FMAs);  db1 += sum dh.
-template <int H, int KP, int G>
-__global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__ ens,
-                                                       const uint16_t* __restrict__ mask,
-                                                       const float* __restrict__ dr,
-                                                       float* __restrict__ slab, int64_t N,
-                                                       int M, int F, int num_groups) {
+//   dh = dr[node] * mask;  dW1 += dh^T ens;  db1 += sum dh.
+// fp32 form: MFMA over 32-feature tiles, A = dh straight from registers, B = staged rows;
+// the last F % 32 features as fp32 FMAs.
+// Split form (X3): A = dh split into bf16 planes in registers (k-block s, element j of lane
+// half h = staged row 16h + 8s + j), B = the staged ens planes read transposed
+// (ds_read_b64_tr_b16: rows 16h + 8s + q and + 4, this lane's feature column), all features
+// on the matrix cores (the planes are zero past F).  Image rows of DsBwdImg<KI>::RS bf16:
+// the four rows of a half's transposed read land 16 banks apart.  A workgroup whose
+// accumulators see a NaN (non-finite ens or dr) writes nothing and runs the fp32 form
+// instead, which gives the fp32 result.
+
+template <int H, int KP, int G, bool X3>
+__device__ __forceinline__ bool ds_bwd_body(const float* __restrict__ ens,
+                                            const uint16_t* __restrict__ mask,
+                                            const float* __restrict__ dr,
+                                            float* __restrict__ slab, int64_t N, int M, int F,
+                                            int num_groups, float* s_lds) {
   constexpr int NT = 2 * H;
-  constexpr int LD = KP + 4;
-  constexpr int NIF = KP / 32;         // full 32-wide feature tiles (MFMA)
-  constexpr int TAIL = KP - 32 * NIF;  // remaining features, multiple of 4 (VALU)
-  __shared__ __attribute__((aligned(16))) float s_e[2][32 * LD];
-  __shared__ float s_dr[2 * G * H];
+  constexpr int KI = ds_bwd_ki(KP);
+  using I = DsBwdImg<KI>;
+  constexpr int LD = X3 ? I::RS : KP + 4;
+  constexpr int TILEF = X3 ? I::FLOATS : 32 * (KP + 4);
+  constexpr int NIF = X3 ? KI / 32 : KP / 32;  // 32-wide feature tiles on the matrix cores
+  constexpr int TAIL = X3 ? 0 : KP - 32 * NIF; // fp32 form: remaining features (VALU)
+  float* s_e0 = s_lds;
+  float* s_e1 = s_lds + TILEF;
+  float* s_dr = s_lds + 2 * TILEF;
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
-  zero_pad<KP>(s_e[0], F);
-  zero_pad<KP>(s_e[1], F);
+  if constexpr (X3) {
+    uint16_t* i0 = reinterpret_cast<uint16_t*>(s_e0);
+    uint16_t* i1 = reinterpret_cast<uint16_t*>(s_e1);
+    const int w = I::RS - F;
+    for (int i = threadIdx.x; i < 3 * 32 * w; i += blockDim.x) {
+      const int pr = i / w, c = F + i % w;
+      i0[pr * I::RS + c] = 0;
+      i1[pr * I::RS + c] = 0;
+    }
+  } else {
+    zero_pad<KP>(s_e0, F);
+    zero_pad<KP>(s_e1, F);
+  }
+  // transposed-read coordinates (X3): lane 4q+p of its 16-lane group reads rows q / q + 4
+  // of the block, 4 columns from 16 * g1 + 4p (g1 = which 16 of the 32 columns)
+  const int tq = (lane & 15) >> 2, tcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
   floatx16 gw[NIF > 0 ? NIF : 1];
 #pragma unroll
@@ -404,13 +582,13 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   for (int j = 0; j < TAIL; ++j) tw[j] = 0.f;
   double gb = 0.0;
 
-  Stager<NT, KP, G != 16> st;
+  Stager<NT, KP, G != 16, X3, KI> st;
   st.init(F, M, G);
   const Groups gr(num_groups, gridDim.x);
   const int GM = G * M, tpg = tiles_per_group(G, M);
   const float* my_dr = s_dr + G * h * H + col;  // this lane: node j of its half at j*H
   int node = 0, rem = M;
-  walk_tiles<true>(gr, GM, tpg, st, ens, N * M, F, s_e[0], s_e[1], mask,
+  walk_tiles<true>(gr, GM, tpg, st, ens, N * M, F, s_e0, s_e1, mask,
              [&](const Cursor& c, const float* buf, uint32_t bits) {
     if (c.t == 0) {  // dr of this group, this wave's columns (read by this wave only)
       const int64_t node0 = (int64_t)c.g * 2 * G;
@@ -446,24 +624,50 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
     }
     gb += (double)gsum;
     DS_MARK(2 + 0 * (int)gsum);
+    if constexpr (X3) {
+      const char* img = reinterpret_cast<const char*>(buf);
+      constexpr int PB = 2 * I::PLANE;  // plane bytes
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float* erow = buf + (16 * h + q) * LD;
+      for (int s8 = 0; s8 < 2; ++s8) {
+        const Bf16x3 a = split8(make_float4(dh[8 * s8], dh[8 * s8 + 1], dh[8 * s8 + 2],
+                                            dh[8 * s8 + 3]),
+                                make_float4(dh[8 * s8 + 4], dh[8 * s8 + 5], dh[8 * s8 + 6],
+                                            dh[8 * s8 + 7]));
+        const int ra = 16 * h + 8 * s8 + tq;
 #pragma unroll
-      for (int it = 0; it < NIF; ++it)
-        gw[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(dh[q], erow[32 * it + c32], gw[it], 0,
-                                                      0, 0);
+        for (int it = 0; it < NIF; ++it) {
+          const int o0 = 2 * (ra * I::RS + 32 * it + tcol);
+          const int o1 = o0 + 2 * 4 * I::RS;
+          const Bf16x3 b = tr_frag_x3(img, PB, o0, o1);
+          gw[it] = mfma_bf16x3(a, b, gw[it]);
+        }
+      }
+    } else {
 #pragma unroll
-      for (int j = 0; j < TAIL; j += 4) {
-        const float4 e4 = *reinterpret_cast<const float4*>(erow + 32 * NIF + j);
-        tw[j] = __builtin_fmaf(dh[q], e4.x, tw[j]);
-        tw[j + 1] = __builtin_fmaf(dh[q], e4.y, tw[j + 1]);
-        tw[j + 2] = __builtin_fmaf(dh[q], e4.z, tw[j + 2]);
-        tw[j + 3] = __builtin_fmaf(dh[q], e4.w, tw[j + 3]);
+      for (int q = 0; q < 16; ++q) {
+        const float* erow = buf + (16 * h + q) * LD;
+#pragma unroll
+        for (int it = 0; it < NIF; ++it)
+          gw[it] = __builtin_amdgcn_mfma_f32_32x32x2f32(dh[q], erow[32 * it + c32], gw[it], 0,
+                                                        0, 0);
+#pragma unroll
+        for (int j = 0; j < TAIL; j += 4) {
+          const float4 e4 = *reinterpret_cast<const float4*>(erow + 32 * NIF + j);
+          tw[j] = __builtin_fmaf(dh[q], e4.x, tw[j]);
+          tw[j + 1] = __builtin_fmaf(dh[q], e4.y, tw[j + 1]);
+          tw[j + 2] = __builtin_fmaf(dh[q], e4.z, tw[j + 2]);
+          tw[j + 3] = __builtin_fmaf(dh[q], e4.w, tw[j + 3]);
+        }
       }
     }
     DS_MARK(3 + 0 * (int)gw[0][0]);
   });
+  if constexpr (X3) {
+    bool bad = false;
+#pragma unroll
+    for (int it = 0; it < NIF; ++it) bad = bad || wave_any_nan(gw[it]);
+    if (block_any(bad, reinterpret_cast<int*>(s_e0))) return false;
+  }
   // slab row of this workgroup: [H*F weights | H bias]
   float* out = slab + (size_t)blockIdx.x * ((size_t)H * F + H);
 #pragma unroll
@@ -481,6 +685,28 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
   }
   gb += shfl_xor_d(gb, 32);
   if (h == 0) out[(size_t)H * F + col] = (float)gb;
+  return true;
+}
+
+template <int H, int KP, int G>
+constexpr int ds_bwd_lds_floats() {
+  constexpr int f32 = 2 * 32 * (KP + 4);
+  constexpr int x3 = GINE_DS_BF16X3 ? 2 * DsBwdImg<ds_bwd_ki(KP)>::FLOATS : 0;
+  return (f32 > x3 ? f32 : x3) + 2 * G * H;
+}
+
+template <int H, int KP, int G>
+__global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__ ens,
+                                                       const uint16_t* __restrict__ mask,
+                                                       const float* __restrict__ dr,
+                                                       float* __restrict__ slab, int64_t N,
+                                                       int M, int F, int num_groups) {
+  __shared__ __attribute__((aligned(16))) float s_lds[ds_bwd_lds_floats<H, KP, G>()];
+#if GINE_DS_BF16X3
+  if (ds_bwd_body<H, KP, G, true>(ens, mask, dr, slab, N, M, F, num_groups, s_lds)) return;
+  __syncthreads();  // a non-finite operand: the fp32 form
+#endif
+  ds_bwd_body<H, KP, G, false>(ens, mask, dr, slab, N, M, F, num_groups, s_lds);
 }
 
 // 16 consecutive slab elements x 16 chunk groups per workgroup (many workgroups for the

@@ -1009,8 +1009,9 @@ __global__ __launch_bounds__(256) void k_bwd1_wgrad(const float* __restrict__ w1
                                                     int chunks, int rows_per_chunk,
                                                     size_t zstride, size_t cstride,
                                                     float* __restrict__ slab, int eng_blocks) {
-  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (kMlpWgTO + 4)];
-  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
+  __shared__ __attribute__((aligned(16))) float s_eng[wg_lds_bytes<kMlpWgTO>() / sizeof(float)];
+  float* sP = s_eng;
+  float* sQ = s_eng + kWgRows * (kMlpWgTO + 4);
   const int b = blockIdx.x;
   if (b < eng_blocks) {
     // the output tiles of one row chunk run back to back on ONE XCD: they read the same

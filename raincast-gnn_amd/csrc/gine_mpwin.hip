@@ -241,10 +241,11 @@ struct WinEngine {
   int nblocks, tiles, rows_per_chunk;
   int D;  // node-MLP width (64 or 128): the engine's O = I
 };
-constexpr size_t kWinEngineLds = sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
+constexpr size_t kWinEngineLds = wg_lds_bytes<64>();
 
-// GINE_WIN_ENG_OCC (tuning experiments): workgroups per CU the combined launch is compiled
-// for (register budget); the plan's LDS must allow as many.
+// GINE_WIN_ENG_OCC (tuning experiments): waves per SIMD the combined launch is compiled
+// for (register budget: 4 = two 512-thread workgroups per CU, 128 VGPRs); the plan's LDS
+// must allow as many workgroups.
 // Cross-lane double sums for the block reduction of the window backward, without the LDS
 // round trip of ds_bpermute: DPP within a row of 16 lanes, v_permlane16/32_swap across rows.
 // Each returns, in every lane, the same-order sum of the two lanes it pairs (so all lanes
@@ -286,7 +287,7 @@ __device__ __forceinline__ double sum_x32(double v) {
 }
 
 #ifndef GINE_WIN_ENG_OCC
-#define GINE_WIN_ENG_OCC 2
+#define GINE_WIN_ENG_OCC 4
 #endif
 template <int CS, bool FMA, bool ENG = false, int PDO = PRO_PLAIN>
 __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_bwd_win(
@@ -510,11 +511,17 @@ WinPlan device_plan(const gine_window_plan* p) {
 
 // Raise the kernel's dynamic-LDS ceiling once per instantiation (thread-safe static init).
 
+// (the whole 160 KiB less the kernel's static LDS, which the attribute must leave room for)
 template <auto K>
 int set_lds_limit() {
-  static const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(K),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  160 * 1024);
+  static const hipError_t e = [] {
+    hipFuncAttributes fa{};
+    hipError_t r = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(K));
+    if (r != hipSuccess) return r;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(K),
+                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024 - (int)fa.sharedSizeBytes);
+  }();
   return e == hipSuccess ? GINE_OK : GINE_ERR_HIP_BASE + (int)e;
 }
 

@@ -15,9 +15,17 @@
 // 64-long MFMA chain and transformed only when staged, so their HBM latency hides under
 // the matrix pipe.  Each (chunk, tile) writes an fp32 partial slab; slabs are reduced over
 // chunks in fixed order in fp64 (deterministic, no float atomics).
+//
+// The chain runs on the bf16 matrix cores in three-way split form (gine_bf16x3.hpp,
+// wgrad_body_x3): each staged value is split ONCE, by the thread that stages it, into three
+// bf16 planes kept in LDS, and the waves read their MFMA fragments from the planes with the
+// transposed LDS read (ds_read_b64_tr_b16) -- no per-wave re-split (the form measured
+// slower in round 3) and 2.7x the MFMA rate of v_mfma_f32_32x32x2_f32.  A workgroup whose
+// accumulators see a NaN (a non-finite operand) redoes its tile with the fp32 chain.
 #pragma once
 
 #include "gine_common.hpp"
+#include "gine_bf16x3.hpp"
 
 // Diagnostic switches (tools/wg_micro.hip only; 0 in the library): bit 0 skips the MFMA
 // chain, bit 1 replaces the operand loads by zeros, bit 2 skips the slab stores, bit 3
@@ -47,6 +55,36 @@ constexpr int kWgMinSubtiles = 2;             // per chunk
 #define GINE_WG_WAVES64 8
 #endif
 constexpr int kWgWaves64 = GINE_WG_WAVES64;   // waves per workgroup of the 64-row tiles
+
+// GINE_WG_BF16X3=0 (A/B builds) keeps the fp32 chain.
+#ifndef GINE_WG_BF16X3
+#define GINE_WG_BF16X3 1
+#endif
+
+// LDS image of one staged operand for the split chain: three bf16 planes [kWgRows][C]
+// (h, m, l), rows of 2C bytes; the 8-byte chunks (4 columns) are XOR-swizzled per row so the
+// transposed reads of four consecutive rows (one 16-lane group: 4 rows x 16 columns) land
+// on four different 16-bank groups (C = 64: rows 2 apart share a bank group unswizzled,
+// C = 128: all rows do).
+template <int C>
+struct WgImg {
+  static_assert(C == 64 || C == 128, "plane width");
+  static constexpr int kCpr = C / 4;           // 8-byte chunks per row
+  static constexpr int kPlane = kWgRows * C * 2;
+  static constexpr int kBytes = 3 * kPlane;
+  __device__ static __forceinline__ int off(int r, int chunk) {
+    return r * (C * 2) + 8 * (chunk ^ (8 * ((r * kCpr / 32) % (kCpr / 8))));
+  }
+};
+
+// Bytes of LDS one engine workgroup needs (sP followed by sQ in ONE region: the fp32
+// layout, or the split planes, whichever is larger).
+template <int TO>
+constexpr size_t wg_lds_bytes() {
+  constexpr size_t f32 = sizeof(float) * kWgRows * ((TO + 4) + kWgLdQ);
+  constexpr size_t x3 = (size_t)3 * kWgRows * 2 * (TO + kWgTI);
+  return GINE_WG_BF16X3 ? (f32 > x3 ? f32 : x3) : f32;
+}
 
 struct WgPlan {
   int tiles_o, tiles_i, chunks, rows_per_chunk;
@@ -265,6 +303,186 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   }
 }
 
+// One staged float4 (row r, columns 4c..4c+3) as 4 bf16 in each of the three planes.
+__device__ __forceinline__ void wg_store_planes(char* img, int plane, int off, float4 v) {
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split2(v.x, v.y, h0, m0, l0);
+  split2(v.z, v.w, h1, m1, l1);
+  *reinterpret_cast<uint2*>(img + off) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(img + plane + off) = make_uint2(m0, m1);
+  *reinterpret_cast<uint2*>(img + 2 * plane + off) = make_uint2(l0, l1);
+}
+
+// wgrad_body on the split chain.  Staging as there (same threads, rows and transforms;
+// the bias partials from the fp32 values), but each value is stored as its three bf16
+// planes; per 64-row sub-tile every wave runs 4 K-blocks of 16 rows, each 6 bf16 MFMAs
+// (mfma_bf16x3) per accumulator, its fragments read transposed from the plane images
+// (element j of lane half h: row 16b + 8h + j -- the same k order for both operands).
+// The next sub-tile's raw loads are spread over the K-blocks.
+template <class Src, int Z, int TO, int NW>
+__device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, int I,
+                                              int chunk, int tile, int rows_per_chunk,
+                                              size_t zstride, size_t cstride,
+                                              float* __restrict__ slab, float* __restrict__ sP,
+                                              float* __restrict__ sQ) {
+  using Raw = typename Src::Raw;
+  using Col = typename Src::Col;
+  using IP = WgImg<TO>;
+  using IQ = WgImg<kWgTI>;
+  char* imgP = reinterpret_cast<char*>(sP);  // sP.. is one region (wg_lds_bytes)
+  char* imgQ = imgP + IP::kBytes;
+  constexpr int NT = 64 * NW;
+  constexpr int PQ = TO / 4;
+  constexpr int PG = NT / PQ;
+  constexpr int PITEMS = kWgRows / PG;
+  constexpr int QQ = kWgTI / 4, QG = NT / QQ;
+  constexpr int QITEMS = kWgRows / QG;
+  constexpr int NJ = NW == 8 ? 1 : 2;
+  constexpr int NI = (NW == 4 && TO == 128) ? 2 : 1;
+  static_assert(NW == 4 || (NW == 8 && TO == 64), "engine shapes");
+
+  const int tiles_i = (int)ceil_div(I, kWgTI);
+  const int o0 = (tile / tiles_i) * TO, i0 = (tile % tiles_i) * kWgTI;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int lane = threadIdx.x % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int ob = NW == 8 ? 32 * (wave >> 2) : (TO == 128 ? 64 * (wave >> 1) : 0);
+  const int ib = NW == 8 ? 32 * (wave & 3) : (TO == 128 ? 64 * (wave & 1) : 32 * wave);
+  const bool bias_block = (i0 == 0);
+
+  const int pq = threadIdx.x % PQ, pr = threadIdx.x / PQ;
+  const int qq = threadIdx.x % QQ, qr = threadIdx.x / QQ;
+  const bool p_ok = o0 + 4 * pq < O, q_ok = i0 + 4 * qq < I;
+  const int pqa = p_ok ? o0 / 4 + pq : 0, qqa = q_ok ? i0 / 4 + qq : 0;
+  const Col pc = src.template p_col<Z>(pqa);
+  const Col qc = src.template q_col<Z>(qqa);
+  // transposed reads: lane 4q+p of a 16-lane group addresses row q (and q + 4) of the
+  // block, chunk p of the group's 16 columns (group g1 = (lane >> 4) & 1 of the 32)
+  const int tq = (lane & 15) >> 2, tch = 4 * ((lane >> 4) & 1) + (lane & 3);
+
+  const int64_t r_begin = (int64_t)chunk * rows_per_chunk;
+  const int64_t r_end = min<int64_t>(R, r_begin + rows_per_chunk);
+
+  wg_floatx16 acc[NJ][NI];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][k][e] = 0.f;
+  double bsum[4] = {0.0, 0.0, 0.0, 0.0};
+
+  Raw rp[PITEMS]{}, rq[QITEMS]{};
+  auto load_item = [&](int j, int64_t n0) {
+    if (j < PITEMS) {
+      const int64_t n = n0 + pr + PG * j;
+      rp[j] = src.template p_load<Z>(n < r_end ? n : r_end - 1, pqa);
+    } else {
+      const int k = j - PITEMS;
+      const int64_t n = n0 + qr + QG * k;
+      rq[k] = src.template q_load<Z>(n < r_end ? n : r_end - 1, qqa);
+    }
+  };
+  constexpr int NITEMS = PITEMS + QITEMS;
+  constexpr int KB = kWgRows / 16;             // K-blocks per sub-tile
+
+  if (r_begin < r_end) {
+#pragma unroll
+    for (int j = 0; j < NITEMS; ++j) load_item(j, r_begin);
+  }
+  for (int64_t n0 = r_begin; n0 < r_end; n0 += kWgRows) {
+#pragma unroll
+    for (int k = 0; k < PITEMS; ++k) {
+      const int r = pr + PG * k;
+      float4 v = src.template p_xform<Z>(rp[k], pc);
+      if (n0 + r >= r_end || !p_ok) v = f4_zero();
+      wg_store_planes(imgP, IP::kPlane, IP::off(r, pq), v);
+      bsum[0] += (double)v.x;
+      bsum[1] += (double)v.y;
+      bsum[2] += (double)v.z;
+      bsum[3] += (double)v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < QITEMS; ++k) {
+      const int r = qr + QG * k;
+      float4 v = src.template q_xform<Z>(rq[k], qc);
+      if (n0 + r >= r_end || !q_ok) v = f4_zero();
+      wg_store_planes(imgQ, IQ::kPlane, IQ::off(r, qq), v);
+    }
+    __syncthreads();
+    const int64_t n1 = n0 + kWgRows;
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+      const int ra = 16 * b + 8 * h + tq;
+      Bf16x3 fa[NJ], fb[NI];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int ch = (ob + 32 * j) / 4 + tch;
+        fa[j] = tr_frag_x3(imgP, IP::kPlane, IP::off(ra, ch), IP::off(ra + 4, ch));
+      }
+#pragma unroll
+      for (int k = 0; k < NI; ++k) {
+        const int ch = (ib + 32 * k) / 4 + tch;
+        fb[k] = tr_frag_x3(imgQ, IQ::kPlane, IQ::off(ra, ch), IQ::off(ra + 4, ch));
+      }
+#pragma unroll
+      for (int j = 0; j < NITEMS; ++j)
+        if (j % KB == b) load_item(j, n1);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int k = 0; k < NI; ++k) acc[j][k] = mfma_bf16x3(fa[j], fb[k], acc[j][k]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+
+  // a NaN in any wave's accumulators (non-finite operand): the tile again on the fp32 chain
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int k = 0; k < NI; ++k) bad = bad || wave_any_nan(acc[j][k]);
+  if (block_any(bad, reinterpret_cast<int*>(imgP))) {
+    wgrad_body<Src, Z, TO, NW>(src, R, O, I, chunk, tile, rows_per_chunk, zstride, cstride,
+                               slab, sP, sQ);
+    return;
+  }
+
+  float* out = slab + (size_t)Z * zstride + (size_t)chunk * cstride;
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int i = i0 + ib + 32 * k + c32;
+    if (i >= I) continue;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = o0 + ob + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (o < O) out[(size_t)o * I + i] = acc[j][k][r];
+      }
+    }
+  }
+  if (bias_block) {  // fixed-order sum of the row groups' partials through LDS
+    double* sb = reinterpret_cast<double*>(imgQ);  // [PG][TO], the planes are free now
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sb[pr * TO + 4 * pq + j] = bsum[j];
+    __syncthreads();
+    if ((int)threadIdx.x < TO && o0 + (int)threadIdx.x < O) {
+      double t = 0.0;
+#pragma unroll 8
+      for (int g = 0; g < PG; ++g) t += sb[g * TO + threadIdx.x];
+      out[(size_t)O * I + o0 + threadIdx.x] = (float)t;
+    }
+  }
+}
+
+#if GINE_WG_BF16X3
+#define GINE_WG_BODY wgrad_body_x3
+#else
+#define GINE_WG_BODY wgrad_body
+#endif
+
 // Output tiles of product z: tiles_o * ceil(I_z / 128).
 template <class Src, int Z>
 __device__ __forceinline__ int wg_tiles(const Src& src, int O, int I, int TO) {
@@ -272,7 +490,8 @@ __device__ __forceinline__ int wg_tiles(const Src& src, int O, int I, int TO) {
 }
 
 // One engine workgroup: output tile y of the concatenated per-product tile lists, rows of
-// chunk `chunk`.  sP / sQ: kWgRows * (TO + 4) and kWgRows * kWgLdQ floats of LDS.
+// chunk `chunk`.  sP / sQ: ONE LDS region of wg_lds_bytes<TO>(), sQ = sP + kWgRows * (TO + 4)
+// (the fp32 body's two arrays; the split body uses the region as its plane images).
 template <class Src, int TO, int NW>
 __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, int I, int chunk,
                                             int y, int rows_per_chunk, size_t zstride,
@@ -280,7 +499,7 @@ __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, in
                                             float* sP, float* sQ) {
   const int t0 = wg_tiles<Src, 0>(src, O, I, TO);
   if (y < t0) {
-    wgrad_body<Src, 0, TO, NW>(src, R, O, src.template i_dim<0>(I), chunk, y, rows_per_chunk,
+    GINE_WG_BODY<Src, 0, TO, NW>(src, R, O, src.template i_dim<0>(I), chunk, y, rows_per_chunk,
                                zstride, cstride, slab, sP, sQ);
     return;
   }
@@ -288,7 +507,7 @@ __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, in
   if constexpr (Src::kZ > 1) {
     const int t1 = wg_tiles<Src, 1>(src, O, I, TO);
     if (y < t1) {
-      wgrad_body<Src, 1, TO, NW>(src, R, O, src.template i_dim<1>(I), chunk, y,
+      GINE_WG_BODY<Src, 1, TO, NW>(src, R, O, src.template i_dim<1>(I), chunk, y,
                                  rows_per_chunk, zstride, cstride, slab, sP, sQ);
       return;
     }
@@ -297,14 +516,14 @@ __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, in
   if constexpr (Src::kZ > 2) {
     const int t2 = wg_tiles<Src, 2>(src, O, I, TO);
     if (y < t2) {
-      wgrad_body<Src, 2, TO, NW>(src, R, O, src.template i_dim<2>(I), chunk, y,
+      GINE_WG_BODY<Src, 2, TO, NW>(src, R, O, src.template i_dim<2>(I), chunk, y,
                                  rows_per_chunk, zstride, cstride, slab, sP, sQ);
       return;
     }
     y -= t2;
   }
   if constexpr (Src::kZ > 3) {
-    wgrad_body<Src, 3, TO, NW>(src, R, O, src.template i_dim<3>(I), chunk, y, rows_per_chunk,
+    GINE_WG_BODY<Src, 3, TO, NW>(src, R, O, src.template i_dim<3>(I), chunk, y, rows_per_chunk,
                                zstride, cstride, slab, sP, sQ);
   }
 }
@@ -318,11 +537,10 @@ __global__ __launch_bounds__(64 * NW) void k_wgrad_engine(Src src, int64_t R, in
                                                           size_t cstride,
                                                           float* __restrict__ slab,
                                                           int total_tiles) {
-  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (TO + 4)];
-  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
+  __shared__ __attribute__((aligned(16))) float s_eng[wg_lds_bytes<TO>() / sizeof(float)];
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   wgrad_block<Src, TO, NW>(src, R, O, I, lb / total_tiles, lb % total_tiles, rows_per_chunk,
-                           zstride, cstride, slab, sP, sQ);
+                           zstride, cstride, slab, s_eng, s_eng + kWgRows * (TO + 4));
 }
 
 // Z must equal Src::kZ; total_tiles = sum of the products' output tiles (the plan's).

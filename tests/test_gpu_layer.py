@@ -21,6 +21,14 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
+@pytest.fixture(autouse=True)
+def _python_binding(monkeypatch):
+    """These tests read the Python autograd Function's saved tensors; the C++ binding (the
+    drop-in default) issues the same launches (tests/test_gpu_dropin.py)."""
+    from raincast_gnn import nn as rnn
+    monkeypatch.setattr(rnn, "USE_TORCH_EXT", False)
+
+
 def _conv(seed):
     torch.manual_seed(seed)
     D = 128

@@ -173,6 +173,30 @@ def test_linear_wgrad_kernel(rows, O, I):
         assert torch.count_nonzero(lin.weight.grad) == 0
 
 
+def test_linear_wgrad_nonfinite_operands():
+    """The weight-gradient engine's split-bf16 chain turns an inf operand into NaN planes;
+    such a tile is redone on the fp32 chain, so inf / NaN land where fp32 puts them (torch's
+    dy^T x): +-inf columns for an inf in x, NaN columns for a NaN, the rest unchanged."""
+    from raincast_gnn.linear import Linear
+    torch.manual_seed(5)
+    rows, O, I = 5000, 64, 200
+    lin = Linear(I, O).to(DEV)
+    x = torch.randn(rows, I, device=DEV)
+    x[17, 3] = float("inf")
+    x[4000, 150] = float("nan")
+    dy = torch.randn(rows, O, device=DEV)
+    lin(x).backward(dy)
+    got, ref = lin.weight.grad.cpu(), (dy.T @ x).cpu()
+    assert torch.equal(torch.isnan(got), torch.isnan(ref))
+    assert torch.equal(torch.isinf(got), torch.isinf(ref))
+    assert torch.equal(got[torch.isinf(ref)], ref[torch.isinf(ref)])
+    fin = torch.isfinite(ref)
+    assert int(fin.sum()) == O * (I - 2)
+    ref64 = (dy.double().T @ torch.nan_to_num(x.double(), nan=0.0, posinf=0.0)).cpu()
+    scale = (dy.double().abs().T @ torch.nan_to_num(x.double(), nan=0.0, posinf=0.0).abs())
+    assert ((got.double() - ref64).abs()[fin] <= 1e-6 * scale.cpu().max()).all()
+
+
 def test_grads_land_in_flat_buffer_without_copies():
     """Backward kernels write every parameter gradient straight into its FlatAdamW slice,
     and the resulting training trajectory equals torch.optim.AdamW's on ordinary grads."""
