@@ -129,32 +129,6 @@ __device__ __forceinline__ bool wave_any_nan(const f32x16_t& acc) {
   return __any(bad);
 }
 
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) bf16x4_t* lds_bf16x4_p;
-
-// The split fragment of one 32x32x16 operand read TRANSPOSED from three row-major bf16 plane
-// images (h at img, m at img + plane, l at img + 2 plane; ds_read_b64_tr_b16, T10 of the
-// CDNA guide): rows k0..k0+7 of this lane's column, from the byte offsets of its two
-// transposed-read blocks (lane 4q+p of each 16-lane group addresses rows k0+q and k0+4+q,
-// its group's columns 4p..4p+3; the lane receives its own column).  EXEC must be full.
-__device__ __forceinline__ Bf16x3 tr_frag_x3(const char* img, int plane, int o0, int o1) {
-  Bf16x3 f;
-  const bf16x4_t h0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_p)(img + o0));
-  const bf16x4_t h1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_p)(img + o1));
-  const bf16x4_t m0 =
-      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_p)(img + plane + o0));
-  const bf16x4_t m1 =
-      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_p)(img + plane + o1));
-  const bf16x4_t l0 =
-      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_p)(img + 2 * plane + o0));
-  const bf16x4_t l1 =
-      __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_p)(img + 2 * plane + o1));
-  f.h = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-  f.m = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
-  f.l = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
-  return f;
-}
-
 // The register-resident B operand of the row-tile GEMMs: a lane's KS fp32 weights
 // (k = h*KS + s, s < KS: the lane half's contiguous k range) as KS/8 split fragments.
 template <int KS>

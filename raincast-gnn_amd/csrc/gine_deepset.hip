@@ -56,13 +56,14 @@ struct DsImg {
   static constexpr int PLANE = 32 * RS;           // elements per plane
   static constexpr int FLOATS = 3 * PLANE / 2;    // one tile's three planes, in floats
 };
-// The backward's images: 32 or 64 features (all on the matrix cores), rows of RS bf16 with
-// RS % 128 in {32, 96}, so the four rows of a half's transposed read land 16 banks apart.
+// The backward's images: COLUMN-major planes, one column of 32 staged rows (+ 8 padding,
+// 80 bytes: 16-byte reads of 16 consecutive columns hit 16 different bank groups) per
+// feature, 32 or 64 features (all on the matrix cores; zero past F).
 template <int KI>
 struct DsBwdImg {
   static_assert(KI == 32 || KI == 64, "feature tiles");
-  static constexpr int RS = KI == 32 ? 32 : 96;   // RS % 128 in {32, 96}
-  static constexpr int PLANE = 32 * RS;
+  static constexpr int RS = 40;                   // column stride (bf16 elements)
+  static constexpr int PLANE = KI * RS;
   static constexpr int FLOATS = 3 * PLANE / 2;
 };
 constexpr int ds_bwd_ki(int KP) { return KP <= 32 ? 32 : 64; }
@@ -132,7 +133,10 @@ struct Stager {
       const bool has = e < 32 * F;
       src[i] = has ? c * G * M * F + off : 0;
       row[i] = has ? c * G * M + j : 0x7fffffff;
-      dst[i] = has ? (16 * c + j) * LD + f : -1;
+      if constexpr (X3 && KI != 0)
+        dst[i] = has ? f * LD + (16 * c + j) : -1;  // the backward's column-major planes
+      else
+        dst[i] = has ? (16 * c + j) * LD + f : -1;
       if constexpr (PAD) jrow[i] = has ? (uint32_t)j : 0u;
     }
   }
@@ -531,10 +535,9 @@ __global__ __launch_bounds__(2 * H, 4) void k_deepset_fwd(const float* __restric
 // fp32 form: MFMA over 32-feature tiles, A = dh straight from registers, B = staged rows;
 // the last F % 32 features as fp32 FMAs.
 // Split form (X3): A = dh split into bf16 planes in registers (k-block s, element j of lane
-// half h = staged row 16h + 8s + j), B = the staged ens planes read transposed
-// (ds_read_b64_tr_b16: rows 16h + 8s + q and + 4, this lane's feature column), all features
-// on the matrix cores (the planes are zero past F).  Image rows of DsBwdImg<KI>::RS bf16:
-// the four rows of a half's transposed read land 16 banks apart.  A workgroup whose
+// half h = staged row 16h + 8s + j), B = the staged ens planes, stored column-major by the
+// stager, so this lane's 8 rows of its feature are one 16-byte read per plane; all features
+// on the matrix cores (the planes are zero past F).  A workgroup whose
 // accumulators see a NaN (non-finite ens or dr) writes nothing and runs the fp32 form
 // instead, which gives the fp32 result.
 
@@ -557,22 +560,19 @@ __device__ __forceinline__ bool ds_bwd_body(const float* __restrict__ ens,
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
-  if constexpr (X3) {
+  if constexpr (X3) {  // the feature columns F.. of every plane (never staged)
     uint16_t* i0 = reinterpret_cast<uint16_t*>(s_e0);
     uint16_t* i1 = reinterpret_cast<uint16_t*>(s_e1);
-    const int w = I::RS - F;
-    for (int i = threadIdx.x; i < 3 * 32 * w; i += blockDim.x) {
-      const int pr = i / w, c = F + i % w;
-      i0[pr * I::RS + c] = 0;
-      i1[pr * I::RS + c] = 0;
+    const int w = (KI - F) * I::RS;
+    for (int i = threadIdx.x; i < 3 * w; i += blockDim.x) {
+      const int pl = i / w, e = F * I::RS + i % w;
+      i0[pl * I::PLANE + e] = 0;
+      i1[pl * I::PLANE + e] = 0;
     }
   } else {
     zero_pad<KP>(s_e0, F);
     zero_pad<KP>(s_e1, F);
   }
-  // transposed-read coordinates (X3): lane 4q+p of its 16-lane group reads rows q / q + 4
-  // of the block, 4 columns from 16 * g1 + 4p (g1 = which 16 of the 32 columns)
-  const int tq = (lane & 15) >> 2, tcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
   floatx16 gw[NIF > 0 ? NIF : 1];
 #pragma unroll
@@ -625,20 +625,20 @@ __device__ __forceinline__ bool ds_bwd_body(const float* __restrict__ ens,
     gb += (double)gsum;
     DS_MARK(2 + 0 * (int)gsum);
     if constexpr (X3) {
-      const char* img = reinterpret_cast<const char*>(buf);
-      constexpr int PB = 2 * I::PLANE;  // plane bytes
+      const uint16_t* img = reinterpret_cast<const uint16_t*>(buf);
 #pragma unroll
       for (int s8 = 0; s8 < 2; ++s8) {
         const Bf16x3 a = split8(make_float4(dh[8 * s8], dh[8 * s8 + 1], dh[8 * s8 + 2],
                                             dh[8 * s8 + 3]),
                                 make_float4(dh[8 * s8 + 4], dh[8 * s8 + 5], dh[8 * s8 + 6],
                                             dh[8 * s8 + 7]));
-        const int ra = 16 * h + 8 * s8 + tq;
 #pragma unroll
-        for (int it = 0; it < NIF; ++it) {
-          const int o0 = 2 * (ra * I::RS + 32 * it + tcol);
-          const int o1 = o0 + 2 * 4 * I::RS;
-          const Bf16x3 b = tr_frag_x3(img, PB, o0, o1);
+        for (int it = 0; it < NIF; ++it) {  // B: rows 16h + 8s8 .. +7 of feature 32it + c32
+          const uint16_t* col = img + (32 * it + c32) * I::RS + 16 * h + 8 * s8;
+          Bf16x3 b;
+          b.h = *reinterpret_cast<const bf16x8_t*>(col);
+          b.m = *reinterpret_cast<const bf16x8_t*>(col + I::PLANE);
+          b.l = *reinterpret_cast<const bf16x8_t*>(col + 2 * I::PLANE);
           gw[it] = mfma_bf16x3(a, b, gw[it]);
         }
       }

@@ -241,7 +241,11 @@ struct WinEngine {
   int nblocks, tiles, rows_per_chunk;
   int D;  // node-MLP width (64 or 128): the engine's O = I
 };
-constexpr size_t kWinEngineLds = wg_lds_bytes<64>();
+#ifndef GINE_WIN_ENG_LDS  // (experiments: a larger floor limits workgroups per CU)
+#define GINE_WIN_ENG_LDS 0
+#endif
+constexpr size_t kWinEngineLds =
+    wg_lds_bytes<64>() > GINE_WIN_ENG_LDS ? wg_lds_bytes<64>() : GINE_WIN_ENG_LDS;
 
 // GINE_WIN_ENG_OCC (tuning experiments): waves per SIMD the combined launch is compiled
 // for (register budget: 4 = two 512-thread workgroups per CU, 128 VGPRs); the plan's LDS
@@ -287,7 +291,15 @@ __device__ __forceinline__ double sum_x32(double v) {
 }
 
 #ifndef GINE_WIN_ENG_OCC
+#if GINE_WG_BF16X3
+// the split engine at 132 registers, one workgroup per CU: capped to 128 registers for two
+// workgroups per CU, the message-passing half of this launch came out wrong and varied from
+// run to run (odd float columns of dx; tools/determinism_layer.py --flat, r04_s09/s11),
+// with no spill and no shared state between the roles -- a miscompile or hazard not found
+#define GINE_WIN_ENG_OCC 2
+#else
 #define GINE_WIN_ENG_OCC 4
+#endif
 #endif
 template <int CS, bool FMA, bool ENG = false, int PDO = PRO_PLAIN>
 __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_bwd_win(

@@ -18,8 +18,9 @@
 //
 // The chain runs on the bf16 matrix cores in three-way split form (gine_bf16x3.hpp,
 // wgrad_body_x3): each staged value is split ONCE, by the thread that stages it, into three
-// bf16 planes kept in LDS, and the waves read their MFMA fragments from the planes with the
-// transposed LDS read (ds_read_b64_tr_b16) -- no per-wave re-split (the form measured
+// bf16 planes kept in LDS column-major (a thread stages consecutive rows of one float4
+// column quad, so each column gets its k run in one store per plane), and the waves read
+// their MFMA fragments as plain 16-byte LDS reads -- no per-wave re-split (the form measured
 // slower in round 3) and 2.7x the MFMA rate of v_mfma_f32_32x32x2_f32.  A workgroup whose
 // accumulators see a NaN (a non-finite operand) redoes its tile with the fp32 chain.
 #pragma once
@@ -61,19 +62,18 @@ constexpr int kWgWaves64 = GINE_WG_WAVES64;   // waves per workgroup of the 64-r
 #define GINE_WG_BF16X3 1
 #endif
 
-// LDS image of one staged operand for the split chain: three bf16 planes [kWgRows][C]
-// (h, m, l), rows of 2C bytes; the 8-byte chunks (4 columns) are XOR-swizzled per row so the
-// transposed reads of four consecutive rows (one 16-lane group: 4 rows x 16 columns) land
-// on four different 16-bank groups (C = 64: rows 2 apart share a bank group unswizzled,
-// C = 128: all rows do).
+// LDS image of one staged operand for the split chain: three bf16 planes (h, m, l), each
+// COLUMN-major -- C columns of kWgRows (64) k values, 128 bytes per column -- so an MFMA
+// fragment (8 consecutive k of one column) is one 16-byte ds_read_b128.  The 16-byte chunks
+// of a column are XOR-swizzled by (column >> 1) & 7, so the reads of 16 consecutive columns
+// at one k offset land on 16 different bank groups.
 template <int C>
 struct WgImg {
-  static_assert(C == 64 || C == 128, "plane width");
-  static constexpr int kCpr = C / 4;           // 8-byte chunks per row
-  static constexpr int kPlane = kWgRows * C * 2;
+  static constexpr int kPlane = C * kWgRows * 2;
   static constexpr int kBytes = 3 * kPlane;
-  __device__ static __forceinline__ int off(int r, int chunk) {
-    return r * (C * 2) + 8 * (chunk ^ (8 * ((r * kCpr / 32) % (kCpr / 8))));
+  // byte offset of (column c, k) in a plane
+  __device__ static __forceinline__ int off(int c, int k) {
+    return c * (kWgRows * 2) + 16 * ((k >> 3) ^ ((c >> 1) & 7)) + 2 * (k & 7);
   }
 };
 
@@ -303,22 +303,56 @@ __device__ __forceinline__ void wgrad_body(const Src& src, int64_t R, int O, int
   }
 }
 
-// One staged float4 (row r, columns 4c..4c+3) as 4 bf16 in each of the three planes.
-__device__ __forceinline__ void wg_store_planes(char* img, int plane, int off, float4 v) {
-  uint32_t h0, m0, l0, h1, m1, l1;
-  split2(v.x, v.y, h0, m0, l0);
-  split2(v.z, v.w, h1, m1, l1);
-  *reinterpret_cast<uint2*>(img + off) = make_uint2(h0, h1);
-  *reinterpret_cast<uint2*>(img + plane + off) = make_uint2(m0, m1);
-  *reinterpret_cast<uint2*>(img + 2 * plane + off) = make_uint2(l0, l1);
+// ITEMS consecutive rows (k0 .. k0+ITEMS-1, ITEMS in {2, 4, 8}, k0 % ITEMS == 0) of one
+// float4 column quad (columns 4cq .. 4cq+3): per column and plane one store of ITEMS bf16.
+template <int C, int ITEMS>
+__device__ __forceinline__ void wg_store_cols(char* img, int cq, int k0, const float4 (&v)[ITEMS]) {
+  static_assert(ITEMS == 2 || ITEMS == 4 || ITEMS == 8, "column runs");
+  using Img = WgImg<C>;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    uint32_t ph[ITEMS / 2], pm[ITEMS / 2], pl[ITEMS / 2];
+#pragma unroll
+    for (int k = 0; k < ITEMS; k += 2) {
+      const float a = e == 0 ? v[k].x : e == 1 ? v[k].y : e == 2 ? v[k].z : v[k].w;
+      const float b = e == 0 ? v[k + 1].x : e == 1 ? v[k + 1].y : e == 2 ? v[k + 1].z : v[k + 1].w;
+      split2(a, b, ph[k / 2], pm[k / 2], pl[k / 2]);
+    }
+    const int o = Img::off(4 * cq + e, k0);
+    char* d[3] = {img + o, img + Img::kPlane + o, img + 2 * Img::kPlane + o};
+    const uint32_t* src[3] = {ph, pm, pl};
+#pragma unroll
+    for (int pl3 = 0; pl3 < 3; ++pl3) {
+      if constexpr (ITEMS == 2) {
+        *reinterpret_cast<uint32_t*>(d[pl3]) = src[pl3][0];
+      } else if constexpr (ITEMS == 4) {
+        *reinterpret_cast<uint2*>(d[pl3]) = make_uint2(src[pl3][0], src[pl3][1]);
+      } else {
+        *reinterpret_cast<uint4*>(d[pl3]) =
+            make_uint4(src[pl3][0], src[pl3][1], src[pl3][2], src[pl3][3]);
+      }
+    }
+  }
 }
 
-// wgrad_body on the split chain.  Staging as there (same threads, rows and transforms;
-// the bias partials from the fp32 values), but each value is stored as its three bf16
-// planes; per 64-row sub-tile every wave runs 4 K-blocks of 16 rows, each 6 bf16 MFMAs
-// (mfma_bf16x3) per accumulator, its fragments read transposed from the plane images
-// (element j of lane half h: row 16b + 8h + j -- the same k order for both operands).
-// The next sub-tile's raw loads are spread over the K-blocks.
+// The split fragment (8 consecutive k from k0, column c) from a column-major plane image.
+template <int C>
+__device__ __forceinline__ Bf16x3 wg_col_frag(const char* img, int c, int k0) {
+  using Img = WgImg<C>;
+  const int o = Img::off(c, k0);
+  Bf16x3 f;
+  f.h = *reinterpret_cast<const bf16x8_t*>(img + o);
+  f.m = *reinterpret_cast<const bf16x8_t*>(img + Img::kPlane + o);
+  f.l = *reinterpret_cast<const bf16x8_t*>(img + 2 * Img::kPlane + o);
+  return f;
+}
+
+// wgrad_body on the split chain.  Staging as there (same transforms; the bias partials
+// from the fp32 values), but a thread stages ITEMS CONSECUTIVE rows of its column quad and
+// stores them as three bf16 planes column-major; per 64-row sub-tile every wave runs 4
+// K-blocks of 16 rows, each 6 bf16 MFMAs (mfma_bf16x3) per accumulator, its fragments plain
+// 16-byte reads of the plane images (element j of lane half h: row 16b + 8h + j -- the same
+// k order for both operands).  The next sub-tile's raw loads are spread over the K-blocks.
 template <class Src, int Z, int TO, int NW>
 __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, int I,
                                               int chunk, int tile, int rows_per_chunk,
@@ -356,9 +390,7 @@ __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, 
   const int pqa = p_ok ? o0 / 4 + pq : 0, qqa = q_ok ? i0 / 4 + qq : 0;
   const Col pc = src.template p_col<Z>(pqa);
   const Col qc = src.template q_col<Z>(qqa);
-  // transposed reads: lane 4q+p of a 16-lane group addresses row q (and q + 4) of the
-  // block, chunk p of the group's 16 columns (group g1 = (lane >> 4) & 1 of the 32)
-  const int tq = (lane & 15) >> 2, tch = 4 * ((lane >> 4) & 1) + (lane & 3);
+  static_assert(PITEMS % 2 == 0 && QITEMS % 2 == 0, "column runs of 2, 4 or 8 rows");
 
   const int64_t r_begin = (int64_t)chunk * rows_per_chunk;
   const int64_t r_end = min<int64_t>(R, r_begin + rows_per_chunk);
@@ -373,13 +405,14 @@ __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, 
   double bsum[4] = {0.0, 0.0, 0.0, 0.0};
 
   Raw rp[PITEMS]{}, rq[QITEMS]{};
+  // this thread's rows: pr * PITEMS + k (P) and qr * QITEMS + k (Q)
   auto load_item = [&](int j, int64_t n0) {
     if (j < PITEMS) {
-      const int64_t n = n0 + pr + PG * j;
+      const int64_t n = n0 + pr * PITEMS + j;
       rp[j] = src.template p_load<Z>(n < r_end ? n : r_end - 1, pqa);
     } else {
       const int k = j - PITEMS;
-      const int64_t n = n0 + qr + QG * k;
+      const int64_t n = n0 + qr * QITEMS + k;
       rq[k] = src.template q_load<Z>(n < r_end ? n : r_end - 1, qqa);
     }
   };
@@ -391,40 +424,39 @@ __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, 
     for (int j = 0; j < NITEMS; ++j) load_item(j, r_begin);
   }
   for (int64_t n0 = r_begin; n0 < r_end; n0 += kWgRows) {
+    {
+      float4 vp[PITEMS], vq[QITEMS];
 #pragma unroll
-    for (int k = 0; k < PITEMS; ++k) {
-      const int r = pr + PG * k;
-      float4 v = src.template p_xform<Z>(rp[k], pc);
-      if (n0 + r >= r_end || !p_ok) v = f4_zero();
-      wg_store_planes(imgP, IP::kPlane, IP::off(r, pq), v);
-      bsum[0] += (double)v.x;
-      bsum[1] += (double)v.y;
-      bsum[2] += (double)v.z;
-      bsum[3] += (double)v.w;
-    }
+      for (int k = 0; k < PITEMS; ++k) {
+        const int r = pr * PITEMS + k;
+        float4 v = src.template p_xform<Z>(rp[k], pc);
+        if (n0 + r >= r_end || !p_ok) v = f4_zero();
+        vp[k] = v;
+        bsum[0] += (double)v.x;
+        bsum[1] += (double)v.y;
+        bsum[2] += (double)v.z;
+        bsum[3] += (double)v.w;
+      }
+      wg_store_cols<TO, PITEMS>(imgP, pq, pr * PITEMS, vp);
 #pragma unroll
-    for (int k = 0; k < QITEMS; ++k) {
-      const int r = qr + QG * k;
-      float4 v = src.template q_xform<Z>(rq[k], qc);
-      if (n0 + r >= r_end || !q_ok) v = f4_zero();
-      wg_store_planes(imgQ, IQ::kPlane, IQ::off(r, qq), v);
+      for (int k = 0; k < QITEMS; ++k) {
+        const int r = qr * QITEMS + k;
+        float4 v = src.template q_xform<Z>(rq[k], qc);
+        if (n0 + r >= r_end || !q_ok) v = f4_zero();
+        vq[k] = v;
+      }
+      wg_store_cols<kWgTI, QITEMS>(imgQ, qq, qr * QITEMS, vq);
     }
     __syncthreads();
     const int64_t n1 = n0 + kWgRows;
 #pragma unroll
     for (int b = 0; b < KB; ++b) {
-      const int ra = 16 * b + 8 * h + tq;
+      const int k0 = 16 * b + 8 * h;
       Bf16x3 fa[NJ], fb[NI];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int ch = (ob + 32 * j) / 4 + tch;
-        fa[j] = tr_frag_x3(imgP, IP::kPlane, IP::off(ra, ch), IP::off(ra + 4, ch));
-      }
+      for (int j = 0; j < NJ; ++j) fa[j] = wg_col_frag<TO>(imgP, ob + 32 * j + c32, k0);
 #pragma unroll
-      for (int k = 0; k < NI; ++k) {
-        const int ch = (ib + 32 * k) / 4 + tch;
-        fb[k] = tr_frag_x3(imgQ, IQ::kPlane, IQ::off(ra, ch), IQ::off(ra + 4, ch));
-      }
+      for (int k = 0; k < NI; ++k) fb[k] = wg_col_frag<kWgTI>(imgQ, ib + 32 * k + c32, k0);
 #pragma unroll
       for (int j = 0; j < NITEMS; ++j)
         if (j % KB == b) load_item(j, n1);
@@ -443,7 +475,10 @@ __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, 
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int k = 0; k < NI; ++k) bad = bad || wave_any_nan(acc[j][k]);
-  if (block_any(bad, reinterpret_cast<int*>(imgP))) {
+#ifndef GINE_WG_X3_NANCHECK
+#define GINE_WG_X3_NANCHECK 1
+#endif
+  if (GINE_WG_X3_NANCHECK && block_any(bad, reinterpret_cast<int*>(imgP))) {
     wgrad_body<Src, Z, TO, NW>(src, R, O, I, chunk, tile, rows_per_chunk, zstride, cstride,
                                slab, sP, sQ);
     return;

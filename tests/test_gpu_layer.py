@@ -139,6 +139,8 @@ def test_model_step_same_bits_with_and_without_layer_launches(hidden, monkeypatc
         return out
 
     n = batch.num_nodes
+    monkeypatch.setattr(options, "LAYER_FWD", True)   # (LAYER_BWD is off by default)
+    monkeypatch.setattr(options, "LAYER_BWD", True)
     assert F.layer_backward_ok(n, hidden)
     if hidden == 128:
         assert F.layer_forward_ok(n, hidden, c.k + 1)
