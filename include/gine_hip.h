@@ -313,7 +313,8 @@ int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in
 
 /* BatchNorm statistics without a finish launch (training, momentum >= 0; csrc/gine_bnacc.hpp).
  * bn_acc: int64[gine_bn_acc_words(D)] (query it: the size follows the build-time replica count
- * R = GINE_BNACC_REPLICAS, (3R + 1 + 8) * 2D + 5 words), zeroed once by the caller at allocation,
+ * R = GINE_BNACC_REPLICAS, (3R + 1 + 8) * 2D + 3 + 288 words, the 288 being the one-launch
+ * layer's grid barrier: 18 lines of 16 words), zeroed once by the caller at allocation,
  * then owned by the kernels (the sums only grow; each consumer differences them against a
  * snapshot the previous consumer left), so one buffer serves every step of one BatchNorm,
  * HIP-graph replays included.  Every producer launch must be followed by exactly one

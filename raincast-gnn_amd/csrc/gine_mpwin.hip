@@ -241,11 +241,22 @@ struct WinEngine {
   int nblocks, tiles, rows_per_chunk;
   int D;  // node-MLP width (64 or 128): the engine's O = I
 };
+// The engine in this launch runs the fp32 chain (wgrad_body), not the split one the
+// stand-alone engines use: with the split chain the launch needs 132 registers, i.e. one
+// workgroup per CU, and measured 30.3 against 26.8 us per launch (profiles/r04_s13); capped to
+// 128 registers for two workgroups per CU, its message-passing half came out wrong and varied
+// from run to run (even float columns of dx; tools/determinism_layer.py --flat, r04_s09 /
+// r04_s11) with no spill and no state shared between the roles -- not diagnosed further.
+#ifndef GINE_WIN_ENG_X3
+#define GINE_WIN_ENG_X3 0
+#endif
 #ifndef GINE_WIN_ENG_LDS  // (experiments: a larger floor limits workgroups per CU)
 #define GINE_WIN_ENG_LDS 0
 #endif
+constexpr size_t kWinEngineLdsNeed =
+    GINE_WIN_ENG_X3 ? wg_lds_bytes<64>() : sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
 constexpr size_t kWinEngineLds =
-    wg_lds_bytes<64>() > GINE_WIN_ENG_LDS ? wg_lds_bytes<64>() : GINE_WIN_ENG_LDS;
+    kWinEngineLdsNeed > GINE_WIN_ENG_LDS ? kWinEngineLdsNeed : GINE_WIN_ENG_LDS;
 
 // GINE_WIN_ENG_OCC (tuning experiments): waves per SIMD the combined launch is compiled
 // for (register budget: 4 = two 512-thread workgroups per CU, 128 VGPRs); the plan's LDS
@@ -291,15 +302,7 @@ __device__ __forceinline__ double sum_x32(double v) {
 }
 
 #ifndef GINE_WIN_ENG_OCC
-#if GINE_WG_BF16X3
-// the split engine at 132 registers, one workgroup per CU: capped to 128 registers for two
-// workgroups per CU, the message-passing half of this launch came out wrong and varied from
-// run to run (odd float columns of dx; tools/determinism_layer.py --flat, r04_s09/s11),
-// with no spill and no shared state between the roles -- a miscompile or hazard not found
-#define GINE_WIN_ENG_OCC 2
-#else
 #define GINE_WIN_ENG_OCC 4
-#endif
 #endif
 template <int CS, bool FMA, bool ENG = false, int PDO = PRO_PLAIN>
 __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_bwd_win(
@@ -319,7 +322,8 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
       float* sP = reinterpret_cast<float*>(s_dyn);
       float* sQ = sP + kWgRows * (64 + 4);
       const int e = xcd_remap(blockIdx.x, eng.nblocks);
-      wgrad_block<MlpWgradSrc<PDO>, 64, 8>(eng.src, eng.N, eng.D, eng.D, e / eng.tiles,
+      wgrad_block<MlpWgradSrc<PDO>, 64, 8, GINE_WIN_ENG_X3 != 0>(eng.src, eng.N, eng.D, eng.D,
+                                                                 e / eng.tiles,
                                            e % eng.tiles, eng.rows_per_chunk, eng.zstride,
                                            eng.cstride, eng.slab, sP, sQ);
       return;

@@ -512,11 +512,18 @@ __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, 
   }
 }
 
-#if GINE_WG_BF16X3
-#define GINE_WG_BODY wgrad_body_x3
-#else
-#define GINE_WG_BODY wgrad_body
-#endif
+template <bool X3, class Src, int Z, int TO, int NW>
+__device__ __forceinline__ void wg_body(const Src& src, int64_t R, int O, int I, int chunk,
+                                        int tile, int rows_per_chunk, size_t zstride,
+                                        size_t cstride, float* __restrict__ slab, float* sP,
+                                        float* sQ) {
+  if constexpr (X3)
+    wgrad_body_x3<Src, Z, TO, NW>(src, R, O, I, chunk, tile, rows_per_chunk, zstride, cstride,
+                                  slab, sP, sQ);
+  else
+    wgrad_body<Src, Z, TO, NW>(src, R, O, I, chunk, tile, rows_per_chunk, zstride, cstride,
+                               slab, sP, sQ);
+}
 
 // Output tiles of product z: tiles_o * ceil(I_z / 128).
 template <class Src, int Z>
@@ -527,14 +534,15 @@ __device__ __forceinline__ int wg_tiles(const Src& src, int O, int I, int TO) {
 // One engine workgroup: output tile y of the concatenated per-product tile lists, rows of
 // chunk `chunk`.  sP / sQ: ONE LDS region of wg_lds_bytes<TO>(), sQ = sP + kWgRows * (TO + 4)
 // (the fp32 body's two arrays; the split body uses the region as its plane images).
-template <class Src, int TO, int NW>
+// X3: the split chain (wgrad_body_x3) or the fp32 one (wgrad_body).
+template <class Src, int TO, int NW, bool X3 = GINE_WG_BF16X3 != 0>
 __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, int I, int chunk,
                                             int y, int rows_per_chunk, size_t zstride,
                                             size_t cstride, float* __restrict__ slab,
                                             float* sP, float* sQ) {
   const int t0 = wg_tiles<Src, 0>(src, O, I, TO);
   if (y < t0) {
-    GINE_WG_BODY<Src, 0, TO, NW>(src, R, O, src.template i_dim<0>(I), chunk, y, rows_per_chunk,
+    wg_body<X3, Src, 0, TO, NW>(src, R, O, src.template i_dim<0>(I), chunk, y, rows_per_chunk,
                                zstride, cstride, slab, sP, sQ);
     return;
   }
@@ -542,7 +550,7 @@ __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, in
   if constexpr (Src::kZ > 1) {
     const int t1 = wg_tiles<Src, 1>(src, O, I, TO);
     if (y < t1) {
-      GINE_WG_BODY<Src, 1, TO, NW>(src, R, O, src.template i_dim<1>(I), chunk, y,
+      wg_body<X3, Src, 1, TO, NW>(src, R, O, src.template i_dim<1>(I), chunk, y,
                                  rows_per_chunk, zstride, cstride, slab, sP, sQ);
       return;
     }
@@ -551,14 +559,14 @@ __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, in
   if constexpr (Src::kZ > 2) {
     const int t2 = wg_tiles<Src, 2>(src, O, I, TO);
     if (y < t2) {
-      GINE_WG_BODY<Src, 2, TO, NW>(src, R, O, src.template i_dim<2>(I), chunk, y,
+      wg_body<X3, Src, 2, TO, NW>(src, R, O, src.template i_dim<2>(I), chunk, y,
                                  rows_per_chunk, zstride, cstride, slab, sP, sQ);
       return;
     }
     y -= t2;
   }
   if constexpr (Src::kZ > 3) {
-    GINE_WG_BODY<Src, 3, TO, NW>(src, R, O, src.template i_dim<3>(I), chunk, y, rows_per_chunk,
+    wg_body<X3, Src, 3, TO, NW>(src, R, O, src.template i_dim<3>(I), chunk, y, rows_per_chunk,
                                zstride, cstride, slab, sP, sQ);
   }
 }

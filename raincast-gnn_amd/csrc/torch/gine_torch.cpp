@@ -90,7 +90,7 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
     const auto* plan_in = reinterpret_cast<const gine_window_plan*>(io[kPlanIn]);
     const Tensor &in_rowptr = graph[0], &in_src = graph[1], &in_attr = graph[2];
     const Tensor &rmean = bn[0], &rvar = bn[1], &nbt = bn[2], &acc = bn[3];
-    TORCH_CHECK(!(batch_stats && N <= 1), "Expected more than 1 value per channel when "
+    TORCH_CHECK_VALUE(!(batch_stats && N <= 1), "Expected more than 1 value per channel when "
                 "training, got input size [", N, ", ", D, "]");
     const float momentum = (float)fo[kMomentum], bn_eps = (float)fo[kBnEps];
 
