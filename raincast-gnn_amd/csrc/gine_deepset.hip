@@ -765,9 +765,12 @@ inline bool hidden_ok(int H) { return H == 32 || H == 64 || H == 128 || H == 256
 // profiles/r03_s42).  The earlier bound of half a wave per SIMD also put 4,000-node batches
 // at H = 128 on G = 4, where the backward measured slower (21.5 -> 22.4 us), so it stops
 // below that size.
+#ifndef GINE_DS_G8_WAVES  // (experiments)
+#define GINE_DS_G8_WAVES 1024
+#endif
 inline int nodes_per_half(int64_t N, int H) {
   const int64_t waves16 = ceil_div(N > 0 ? N : 1, 32) * (H / 32);
-  return waves16 <= 256 ? 4 : (waves16 <= 1024 ? 8 : 16);
+  return waves16 <= 256 ? 4 : (waves16 <= GINE_DS_G8_WAVES ? 8 : 16);
 }
 inline int num_groups(int64_t N, int H) {
   return (int)ceil_div(N > 0 ? N : 1, 2 * nodes_per_half(N, H));
