@@ -103,11 +103,12 @@ class GineGraph:
 
     __slots__ = ("num_nodes", "num_edges", "device", "in_rowptr", "in_src", "in_attr",
                  "out_rowptr", "out_dst", "out_attr", "_error", "_checked", "_windows",
-                 "max_in_degree")
+                 "max_in_degree", "_ext_opts")
 
     def __init__(self, edge_index: torch.Tensor, edge_attr: torch.Tensor | None,
                  num_nodes: int, flow: str = "source_to_target"):
         _lib.require_device(edge_index, "GineGraph")
+        self._ext_opts = {}  # torch_ext's per-size option cache
         if edge_index.dim() != 2 or edge_index.size(0) != 2:
             raise ValueError(f"edge_index must have shape [2, E], got {tuple(edge_index.shape)}")
         if flow not in ("source_to_target", "target_to_source"):

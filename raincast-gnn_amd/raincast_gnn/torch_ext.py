@@ -72,6 +72,25 @@ def plan_address(plan) -> int:
     return 0 if plan is None else ctypes.addressof(plan)
 
 
+def _graph_opts(graph, N: int, D: int, has_acc: bool) -> list:
+    """The io options that depend only on the graph, the sizes and the path switches, cached
+    on the graph object (one dict lookup per layer call instead of the plan and occupancy
+    queries)."""
+    from . import functional as Fn
+    from . import options
+    key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD)
+    cache = graph._ext_opts
+    got = cache.get(key)
+    if got is None:
+        fused = Fn.fused_forward_ok(graph, N, D)
+        lay = fused and has_acc and Fn.layer_forward_ok(N, D, graph.max_in_degree)
+        got = cache[key] = [int(fused), int(lay),
+                            int(graph.max_in_degree if graph.max_in_degree is not None else -1),
+                            plan_address(graph.window_plan("in", D)),
+                            plan_address(graph.window_plan("out", D))]
+    return got
+
+
 def layer(ext, x, conv, graph, epilogue: int) -> torch.Tensor:
     """GINEConv.forward's fused layer through the extension (the caller checked that the
     layer's parameters are not flat-buffer slices, i.e. its backward is the non-deferred
@@ -81,12 +100,8 @@ def layer(ext, x, conv, graph, epilogue: int) -> torch.Tensor:
     N, D = x.shape
     bn = Fn.BnConfig(bn_mod)
     acc = Fn.bn_accumulator(bn, D, x.device)
-    fused = Fn.fused_forward_ok(graph, N, D)
-    lay = fused and acc is not None and Fn.layer_forward_ok(N, D, graph.max_in_degree)
     io = [epilogue, Fn.edge_linear_flag(), int(bn.use_batch_stats),
-          int(bn.update_running), int(fused), int(lay),
-          int(graph.max_in_degree if graph.max_in_degree is not None else -1),
-          plan_address(graph.window_plan("in", D)), plan_address(graph.window_plan("out", D))]
+          int(bn.update_running)] + _graph_opts(graph, N, D, acc is not None)
     fo = [bn.momentum, bn.eps]
     return ext.gine_layer(x, conv.lin.weight, conv.lin.bias, conv.eps, l1.weight, l1.bias,
                           bn_mod.weight, bn_mod.bias, l2.weight, l2.bias,

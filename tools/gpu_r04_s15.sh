@@ -18,3 +18,8 @@ for rep in 1 2; do
     python -c "import json;d=json.loads(open('$O/b.json').read().strip().splitlines()[-1]);print('$v', d['ms_per_step'], d['step_ms_p10_p50_p90'])" | tee -a $O/ab.txt
   done
 done
+unset GINE_HIP_LIB
+timeout -k 10 200 python tools/dropin_prof.py > $O/dropin_prof.txt 2>&1; st $? dropin_prof
+head -2 $O/dropin_prof.txt
+timeout -k 10 300 python bench.py --dropin --steps 30 --warmup 5 > $O/bench_dropin.json 2> $O/bench_dropin.err; st $? bench_dropin
+python -c "import json;d=json.loads(open('$O/bench_dropin.json').read().strip().splitlines()[-1]);print('dropin', d['value'], d['ms_per_step'], d['gine_stack_ms_fwd_bwd'])"
