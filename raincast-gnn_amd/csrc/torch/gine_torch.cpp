@@ -56,6 +56,34 @@ enum IntOpt {
 };
 enum FloatOpt { kMomentum = 0, kBnEps, kFloatOpts };
 
+// Several tensors from ONE allocation (each 256-byte aligned): the caching allocator's
+// per-call cost dominates the drop-in path's host time, and these are internal buffers or
+// gradients handed to autograd (a view with the parameter's shape and strides is adopted as
+// .grad without a copy).  An empty shape list entry gives an undefined tensor.
+struct Spec {
+  std::vector<int64_t> shape;
+  c10::ScalarType dtype;
+  bool want;
+};
+std::vector<Tensor> carve(const Tensor& like, const std::vector<Spec>& specs) {
+  std::vector<int64_t> off(specs.size(), 0), bytes(specs.size(), 0);
+  int64_t total = 0;
+  for (size_t i = 0; i < specs.size(); ++i) {
+    if (!specs[i].want) continue;
+    int64_t n = (int64_t)c10::elementSize(specs[i].dtype);
+    for (int64_t d : specs[i].shape) n *= d;
+    bytes[i] = n;
+    off[i] = total;
+    total += (n + 255) / 256 * 256;
+  }
+  Tensor buf = torch::empty({std::max<int64_t>(total, 256)}, like.options().dtype(torch::kUInt8));
+  std::vector<Tensor> out(specs.size());
+  for (size_t i = 0; i < specs.size(); ++i)
+    if (specs[i].want)
+      out[i] = buf.narrow(0, off[i], bytes[i]).view(specs[i].dtype).view(specs[i].shape);
+  return out;
+}
+
 struct ZeroOnError {  // csrc/gine_bnacc.hpp pairing: re-zero the accumulator if a launch fails
   Tensor acc;
   bool armed = true;
@@ -94,14 +122,18 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
                 "training, got input size [", N, ", ", D, "]");
     const float momentum = (float)fo[kMomentum], bn_eps = (float)fo[kBnEps];
 
-    Tensor a1 = torch::empty_like(x), y = torch::empty_like(x);
-    Tensor bn_save = torch::empty({4, D}, x.options());
-    Tensor mask = epi == GINE_EPI_RESIDUAL_RELU
-                      ? torch::empty({N, D}, x.options().dtype(torch::kUInt8))
-                      : Tensor();
+    Tensor y = torch::empty_like(x);  // the user's tensor: its own storage
+    int32_t Pn = 0;
+    if (!acc.defined()) Pn = query(gine_mlp_num_partials, N, D, "gine_mlp_num_partials");
+    // saved for the backward / scratch: one allocation
+    std::vector<Tensor> t = carve(x, {{{N, D}, torch::kFloat32, true},
+                                      {{N, D}, torch::kFloat32, true},
+                                      {{4, D}, torch::kFloat32, true},
+                                      {{N, D}, torch::kUInt8, epi == GINE_EPI_RESIDUAL_RELU},
+                                      {{Pn, 2, D}, torch::kFloat64, !acc.defined()}});
+    Tensor a1 = t[0], z = t[1], bn_save = t[2], mask = t[3], partials = t[4];
     void* nbt_p = update_running ? P(nbt) : nullptr;
     const int upd = (update_running && rmean.defined()) ? 1 : 0;
-    Tensor z = torch::empty_like(x);
     if (!fused) {  // the gather (or window) forward, unpaired
       if (plan_in)
         ok(gine_mp_fwd_win((const float*)P(x), (const int32_t*)P(in_rowptr),
@@ -115,12 +147,6 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
                        (const float*)P(lw), (const float*)P(lb), (const float*)P(ep),
                        (float*)P(z), N, D, lin_flag, s),
            "gine_mp_fwd");
-    }
-    Tensor partials;
-    int32_t Pn = 0;
-    if (!acc.defined()) {
-      Pn = query(gine_mlp_num_partials, N, D, "gine_mlp_num_partials");
-      partials = torch::empty({Pn, 2, D}, x.options().dtype(torch::kFloat64));
     }
     {
       ZeroOnError guard{acc};
@@ -207,15 +233,29 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
     const int epi = (int)io[kEpi], lin_flag = (int)io[kLinFlag];
     const auto* plan_out = reinterpret_cast<const gine_window_plan*>(io[kPlanOut]);
     auto fo = x.options();
-    Tensor dgamma = g.defined() ? torch::empty({D}, fo) : Tensor();
-    Tensor dbeta = has_beta ? torch::empty({D}, fo) : Tensor();
-    Tensor dw1 = torch::empty({D, D}, fo), db1 = torch::empty({D}, fo);
-    Tensor dw2 = torch::empty({D, D}, fo), db2 = torch::empty({D}, fo);
-    Tensor dbn = torch::empty_like(x), coef = torch::empty({3, D}, fo), dz = torch::empty_like(x);
     const int32_t C = query(gine_mlp_wgrad_num_chunks, N, D, "gine_mlp_wgrad_num_chunks");
-    Tensor slab = torch::empty({2 * (int64_t)C * ((int64_t)D * D + D)}, fo);
     const int32_t Pn = query(gine_mlp_num_partials, N, D, "gine_mlp_num_partials");
-    Tensor partials = torch::empty({Pn, 2, D}, fo.dtype(torch::kFloat64));
+    const int32_t P2 = plan_out ? plan_out->num_tiles
+                                : query(gine_mp_bwd_num_partials, N, D, "gine_mp_bwd_num_partials");
+    // the parameter gradients from one allocation, the scratch from another
+    std::vector<Tensor> gr = carve(x, {{{D}, torch::kFloat32, g.defined()},
+                                       {{D}, torch::kFloat32, has_beta},
+                                       {{D, D}, torch::kFloat32, true},
+                                       {{D}, torch::kFloat32, true},
+                                       {{D, D}, torch::kFloat32, true},
+                                       {{D}, torch::kFloat32, true},
+                                       {{D}, torch::kFloat32, true},
+                                       {{D}, torch::kFloat32, true},
+                                       {{1}, torch::kFloat32, true}});
+    Tensor dgamma = gr[0], dbeta = gr[1], dw1 = gr[2], db1 = gr[3], dw2 = gr[4], db2 = gr[5];
+    Tensor dlw = gr[6], dlb = gr[7], deps = gr[8];
+    std::vector<Tensor> sc = carve(x, {{{N, D}, torch::kFloat32, true},
+                                       {{3, D}, torch::kFloat32, true},
+                                       {{N, D}, torch::kFloat32, true},
+                                       {{2 * (int64_t)C * ((int64_t)D * D + D)}, torch::kFloat32, true},
+                                       {{Pn, 2, D}, torch::kFloat64, true},
+                                       {{P2, 3, D}, torch::kFloat64, true}});
+    Tensor dbn = sc[0], coef = sc[1], dz = sc[2], slab = sc[3], partials = sc[4], part2 = sc[5];
     ok(gine_mlp_bwd2((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
                      (const float*)P(a1), (const float*)P(bn_save), (const float*)P(w2c),
                      (float*)P(dbn), (double*)P(partials), N, D, epi, s),
@@ -234,11 +274,8 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
     // message-passing backward; its extra workgroups reduce the slab
     Tensor dres = epi == GINE_EPI_RESIDUAL_RELU ? dy : Tensor();
     Tensor dx = torch::empty_like(x);
-    Tensor dlw = torch::empty({D}, fo), dlb = torch::empty({D}, fo), deps = torch::empty({1}, fo);
     const int32_t flags = GINE_MP_BWD_SELF | lin_flag;
     if (plan_out) {
-      const int32_t P2 = plan_out->num_tiles;
-      Tensor part2 = torch::empty({P2, 3, D}, fo.dtype(torch::kFloat64));
       ok(gine_mp_bwd_win_side((const float*)P(dz), (const float*)P(x),
                               (const int32_t*)P(out_rowptr), (const int32_t*)P(out_dst),
                               (const float*)P(out_attr), (const float*)P(lw),
@@ -251,8 +288,6 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
                                   (float*)P(dlw), (float*)P(dlb), (float*)P(deps), s),
          "gine_mp_bwd_win_finalize");
     } else {
-      const int32_t P2 = query(gine_mp_bwd_num_partials, N, D, "gine_mp_bwd_num_partials");
-      Tensor part2 = torch::empty({P2, 3, D}, fo.dtype(torch::kFloat64));
       ok(gine_mp_bwd_side((const float*)P(dz), (const float*)P(x), (const int32_t*)P(out_rowptr),
                           (const int32_t*)P(out_dst), (const float*)P(out_attr),
                           (const float*)P(lw), (const float*)P(lb), (const float*)P(ep),

@@ -19,6 +19,8 @@ for rep in 1 2; do
   done
 done
 unset GINE_HIP_LIB
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dropin.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > $O/pytest_dropin.log 2>&1; rc=$?; tail -2 $O/pytest_dropin.log; st $rc dropin_tests
+[ $rc -eq 0 ] || exit 1
 timeout -k 10 200 python tools/dropin_prof.py > $O/dropin_prof.txt 2>&1; st $? dropin_prof
 head -2 $O/dropin_prof.txt
 timeout -k 10 300 python bench.py --dropin --steps 30 --warmup 5 > $O/bench_dropin.json 2> $O/bench_dropin.err; st $? bench_dropin
