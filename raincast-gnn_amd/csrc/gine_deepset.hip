@@ -438,7 +438,9 @@ __global__ __launch_bounds__(2 * H, 4) void k_deepset_fwd(const float* __restric
                                                        int num_groups, FoldArgs fold,
                                                        Fold2Args fold2) {
   constexpr int NT = 2 * H;
-  constexpr bool X3 = GINE_DS_BF16X3 != 0;
+  // the split chain for the large-batch group size only: at 4,000 nodes (8-node groups) it
+  // measured 16.2 against 14.1 us, at 16,000 27.7 against 31.3 (profiles/r04_s15_ds_*.txt)
+  constexpr bool X3 = GINE_DS_BF16X3 != 0 && G == 16;
   constexpr int TILEF = X3 ? DsImg<KP>::FLOATS : 32 * (KP + 4);  // one staged tile (floats)
   constexpr int kWalk = 2 * TILEF + 2 * G * H;  // two staged tiles + the group's node sums
   constexpr int kFold = FOLD ? 32 * (H + 4) + (H / 32) * kSR : 0;
@@ -688,10 +690,15 @@ __device__ __forceinline__ bool ds_bwd_body(const float* __restrict__ ens,
   return true;
 }
 
+// The split backward (GINE_DS_BWD_BF16X3=1) measured no faster than the fp32 one (16,000
+// nodes 39.5 vs 40.1 us, 4,000 nodes 22.8 vs 22.0; profiles/r04_s15_ds_*.txt): off.
+#ifndef GINE_DS_BWD_BF16X3
+#define GINE_DS_BWD_BF16X3 0
+#endif
 template <int H, int KP, int G>
 constexpr int ds_bwd_lds_floats() {
   constexpr int f32 = 2 * 32 * (KP + 4);
-  constexpr int x3 = GINE_DS_BF16X3 ? 2 * DsBwdImg<ds_bwd_ki(KP)>::FLOATS : 0;
+  constexpr int x3 = GINE_DS_BWD_BF16X3 ? 2 * DsBwdImg<ds_bwd_ki(KP)>::FLOATS : 0;
   return (f32 > x3 ? f32 : x3) + 2 * G * H;
 }
 
@@ -702,7 +709,7 @@ __global__ __launch_bounds__(2 * H) void k_deepset_bwd(const float* __restrict__
                                                        float* __restrict__ slab, int64_t N,
                                                        int M, int F, int num_groups) {
   __shared__ __attribute__((aligned(16))) float s_lds[ds_bwd_lds_floats<H, KP, G>()];
-#if GINE_DS_BF16X3
+#if GINE_DS_BWD_BF16X3
   if (ds_bwd_body<H, KP, G, true>(ens, mask, dr, slab, N, M, F, num_groups, s_lds)) return;
   __syncthreads();  // a non-finite operand: the fp32 form
 #endif
