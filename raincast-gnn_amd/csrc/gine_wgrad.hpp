@@ -574,25 +574,30 @@ __device__ __forceinline__ void wgrad_block(const Src& src, int64_t R, int O, in
 // 1-D grid of chunks x tiles (tiles = sum over z of the product's output tiles).  The
 // tiles of one row chunk run back to back on ONE XCD (xcd_remap): they read the same rows,
 // which that XCD's L2 then serves.
-template <class Src, int TO, int NW>
+template <class Src, int TO, int NW, bool X3>
 __global__ __launch_bounds__(64 * NW) void k_wgrad_engine(Src src, int64_t R, int O, int I,
                                                           int rows_per_chunk, size_t zstride,
                                                           size_t cstride,
                                                           float* __restrict__ slab,
                                                           int total_tiles) {
-  __shared__ __attribute__((aligned(16))) float s_eng[wg_lds_bytes<TO>() / sizeof(float)];
+  constexpr size_t kBytes =
+      X3 ? wg_lds_bytes<TO>() : sizeof(float) * kWgRows * ((TO + 4) + kWgLdQ);
+  __shared__ __attribute__((aligned(16))) float s_eng[kBytes / sizeof(float)];
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  wgrad_block<Src, TO, NW>(src, R, O, I, lb / total_tiles, lb % total_tiles, rows_per_chunk,
-                           zstride, cstride, slab, s_eng, s_eng + kWgRows * (TO + 4));
+  wgrad_block<Src, TO, NW, X3>(src, R, O, I, lb / total_tiles, lb % total_tiles,
+                               rows_per_chunk, zstride, cstride, slab, s_eng,
+                               s_eng + kWgRows * (TO + 4));
 }
 
 // Z must equal Src::kZ; total_tiles = sum of the products' output tiles (the plan's).
-template <int TO, class Src>
+// X3: the split chain (the node-MLP engines keep the fp32 one, so the stand-alone engine
+// and the one inside the window backward give the same bits).
+template <int TO, class Src, bool X3 = GINE_WG_BF16X3 != 0>
 inline int launch_wgrad_engine(const Src& src, int64_t R, int O, int I, int total_tiles,
                                const WgPlan& p, size_t zstride, size_t cstride, float* slab,
                                hipStream_t s) {
   constexpr int NW = TO == 64 ? kWgWaves64 : 4;
-  hipLaunchKernelGGL((k_wgrad_engine<Src, TO, NW>), dim3(p.chunks * total_tiles),
+  hipLaunchKernelGGL((k_wgrad_engine<Src, TO, NW, X3>), dim3(p.chunks * total_tiles),
                      dim3(64 * NW), 0, s, src, R, O, I, p.rows_per_chunk, zstride, cstride,
                      slab, total_tiles);
   GINE_LAUNCH_STATUS();
