@@ -268,7 +268,10 @@ FOLD = True
 F3 = True
 F3_MAX_NODES = 32768
 
-# True: on the one-launch path (F3) phi[2] is folded into rho[0] as well (_ChainFolded2Fn)
+# True: on the one-launch path (F3) phi[2] is folded into rho[0] as well (_ChainFolded2Fn),
+# at every size: its forward has two stages, not three, and wins at cfg3 (128,000 nodes:
+# 2.749 -> 2.665 ms per step) and cfg5 (80,000: 1.715 -> 1.622) too, where the singly folded
+# one-launch form lost (F3_MAX_NODES; profiles/r04_s18_chain_fold2_large.txt)
 FOLD2 = True
 
 

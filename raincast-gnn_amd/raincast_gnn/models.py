@@ -122,7 +122,8 @@ class GNN(nn.Module):
         lins = (lin2, rho0, rho1, self.dim_red)
         if (isinstance(act, nn.ReLU) and isinstance(rho_act, nn.ReLU)
                 and deepset.fusable(ens, lin1.weight, lin1.bias)):
-            if (fused_chain.FOLD and fused_chain.F3 and ens.size(0) <= fused_chain.F3_MAX_NODES
+            if (fused_chain.FOLD and fused_chain.F3
+                    and (fused_chain.FOLD2 or ens.size(0) <= fused_chain.F3_MAX_NODES)
                     and fused_chain.fusable_dims(lin1.out_features, x, lins)):
                 # the DeepSet launch also folds dim_red; the chain forward is one launch
                 fold = ((rho1, self.dim_red, rho0, lin2) if fused_chain.FOLD2

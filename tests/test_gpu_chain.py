@@ -222,7 +222,7 @@ def _ens_lin1(N, D, M=11, Fe=36, seed=0):
 
 
 @pytest.mark.parametrize("N,D,F", [(33, 128, 35), (300, 64, 35), (2000, 128, 64),
-                                   (16000, 128, 35)])
+                                   (16000, 128, 35), (40000, 128, 35)])
 def test_chain_folded2_intermediates(N, D, F):
     """The doubly folded chain's pieces (C ABI) against fp64 torch: [Wf | bf] from the
     DeepSet launch (whose r and [W' | b' | W'^T] equal the single fold's bit for bit), u / h0
