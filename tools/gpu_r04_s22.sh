@@ -14,6 +14,6 @@ ab() {  # ab <cfg> <variant...>
     done
   done
 }
-ab 2 WINDOW_NODES=128 WINDOW_NODES=64 WINDOW_NODES=256
-ab 3 WINDOW_NODES=128 WINDOW_NODES=64 WINDOW_NODES=256
+
+ab 3 WINDOW_NODES=128 WINDOW_NODES=64
 ab 5 MP_WINDOW=auto MP_WINDOW=all
