@@ -36,10 +36,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from raincast_gnn import functional as Fn  # noqa: E402
-from raincast_gnn import gradbuf  # noqa: E402
+from raincast_gnn import gradbuf, options  # noqa: E402
 from raincast_gnn.data import relabel_stations, synthetic_batch  # noqa: E402
 from raincast_gnn.data import station_order as station_order_of  # noqa: E402
-from raincast_gnn.distributed import FlatGradReducer, broadcast_parameters, env_rank  # noqa: E402
+from raincast_gnn.distributed import (FlatGradReducer, broadcast_parameters, env_rank,  # noqa: E402
+                                      note_device_sharing)
 from raincast_gnn.graph import get_graph  # noqa: E402
 from raincast_gnn.models import gnn_from_params  # noqa: E402
 from raincast_gnn.optim import FlatAdamW  # noqa: E402
@@ -329,6 +330,41 @@ def time_kernels(tr: Trainer, reps: int):
              1 | lin, ctypes.byref(win), ptr(dz), None, ptr(mask), ptr(a1), ptr(bn_save),
              ptr(dbn), ptr(coef), ptr(z), ptr(slab), 2, S[0])
 
+    # the one-launch layer forward (fused gather + Linear1 + BN sums | grid barrier | BN
+    # finish + Linear2 + residual epilogue) where the step runs it, on an accumulator of its
+    # own (each launch is a paired producer + consumer)
+    if Fn.fused_forward_ok(g, N, D) and Fn.layer_forward_ok(N, D, g.max_in_degree):
+        words = Fn._count64("gine_bn_acc_words", D)
+        lacc = torch.zeros(words, dtype=torch.int64, device=dev)
+        y_l = torch.empty_like(x)
+        bsave_l = torch.empty(4, D, device=dev)
+        rm_l, rv_l = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+
+        def mp_fwd_layer():
+            call("gine_mp_fwd_layer", ptr(x), ptr(g.in_rowptr), ptr(g.in_src), ptr(g.in_attr),
+                 ptr(lw), ptr(lb), ptr(ep), ptr(w1), ptr(b1), ptr(z), ptr(a1), ptr(lacc),
+                 ptr(bn.weight), ptr(bn.bias), ptr(rm_l), ptr(rv_l), None, ptr(bsave_l), 0.1,
+                 1e-5, 1, ptr(w2), ptr(b2), ptr(y_l), ptr(mask), N, D, g.max_in_degree, lin, 2,
+                 S[0])
+        # bytes: the message passing's B_f + a1 and y written, mask, x re-read for the residual
+        kernels["gine_mp_fwd_layer"] = (mp_fwd_layer, {
+            "flops": 4 * N * D * D,
+            "bytes": 4 * (2 * N * D + 2 * E + N + 1) + 4 * N * D + 4 * N * D + N * D + 4 * N * D})
+
+    if Fn.engine_in_mp_ok(g, D) and options.BN_ACC_BWD:
+        # the backward's BatchNorm-accumulator pair (dbn GEMM + sums | BN finish + dz GEMM):
+        # two launches that must run as a pair on their accumulator, timed together
+        bacc = torch.zeros(Fn._count64("gine_bn_acc_words", D), dtype=torch.int64, device=dev)
+        dg, dbt = torch.empty(D, device=dev), torch.empty(D, device=dev)
+
+        def mlp_bwd_pair_acc():
+            call("gine_mlp_bwd2_acc", ptr(dz), None, ptr(mask), ptr(a1), ptr(bn_save), ptr(w2),
+                 ptr(dbn), None, ptr(bacc), N, D, 2, S[0])
+            call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(bacc), ptr(bn.weight),
+                 ptr(dg), ptr(dbt), ptr(coef), ptr(w1), ptr(dx), N, D, S[0])
+        kernels["gine_mlp_bwd_pair_acc"] = (mlp_bwd_pair_acc, {
+            "flops": 4 * N * D * D, "bytes": 25 * N * D})
+
     if Fn.engine_in_mp_ok(g, D):  # what the training step's backward runs at this size
         # bytes: the message-passing backward's B_b (dz, x, dx, CSR, dres = dy) + the
         # engine's other operands read once (mask u8, dbn, a1, z) + its fp32 slab
@@ -401,6 +437,8 @@ def sec8d_launch_work(name: str, w: dict) -> dict:
         "gine_mp_fwd": {"bytes": w["B_f"]}, "gine_mp_fwd_win": {"bytes": w["B_f"]},
         "gine_mp_bwd": {"bytes": w["B_b"]},
         "gine_mp_fwd_mlp1": {"bytes": w["B_f"], "flops": half_fwd},
+        "gine_mp_fwd_layer": {"bytes": w["B_f"], "flops": 2 * half_fwd},
+        "gine_mlp_bwd_pair_acc": {"flops": 2 * half_bwd},
         "gine_mp_bwd_mlp_wgrad": {"bytes": w["B_b"], "flops": 2 * half_bwd},
         "gine_mlp_fwd1": {"flops": half_fwd}, "gine_mlp_fwd2": {"flops": half_fwd},
         "gine_mlp_bwd2": {"flops": half_bwd}, "gine_mlp_bwd1": {"flops": half_bwd},
@@ -421,9 +459,20 @@ def roofline_for(kernels: dict, layers: int, work: dict, config: str = "cfg2"):
     if "gine_mp_bwd_mlp_wgrad" in kernels:  # engine in the message-passing launch
         step = [k for k in step if k not in ("gine_mp_bwd", "gine_mlp_bwd1_wgrad")]
         step += ["gine_mlp_bwd1", "gine_mp_bwd_mlp_wgrad"]
+    if "gine_mp_fwd_layer" in kernels:  # the whole layer forward in one launch
+        step = [k for k in step if k not in ("gine_mp_fwd_mlp1", "gine_mlp_fwd2")]
+        step += ["gine_mp_fwd_layer"]
+    if "gine_mlp_bwd_pair_acc" in kernels:  # (two launches: a pair, not a roofline line)
+        step = [k for k in step if k not in ("gine_mlp_bwd2", "gine_mlp_bwd1")]
     timed = [k for k in step if k in kernels]
     dominant = max(timed, key=lambda k: kernels[k]["us"])
-    return roof_of(dominant, kernels[dominant], layers, work, config)
+    out = roof_of(dominant, kernels[dominant], layers, work, config)
+    # the other per-layer launches of the step against their own 8(d) floors, for context
+    out["per_layer_launches"] = {
+        k: {"avg_us": kernels[k]["us"],
+            "frac": roof_of(k, kernels[k], layers, work, config)["frac"]}
+        for k in timed + [k for k in ("gine_mlp_bwd_pair_acc",) if k in kernels]}
+    return out
 
 
 def roof_of(name: str, rec: dict, layers: int, work: dict, config: str = "cfg2") -> dict:
@@ -504,6 +553,7 @@ def copy_ceiling_gbps(device, nbytes=1 << 30, reps=10):
 PMC_KERNELS = {
     "gine_mp_fwd": ["gine::k_mp_fwd<32, 1, "],
     "gine_mp_fwd_mlp1": ["gine::k_mp_fwd_mlp1<"],
+    "gine_mp_fwd_layer": ["gine::k_mp_fwd_layer<false, 5>"],
     # (the GPU box's host rounds the edge Linear mul-then-add: FMA = false)
     "gine_mp_bwd_mlp_wgrad": ["gine::k_mp_bwd_win<32, false, true, 5>"],
     "gine_mp_bwd": [("gine::k_mp_bwd_win<32, ", "gine::k_mp_bwd<32, 1, ")],
@@ -669,6 +719,7 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    Fn.check_grid_barriers()  # a layer launch whose grid was not co-resident raises here
     per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
     pct = {q: round(per_step[min(len(per_step) - 1, int(q / 100 * len(per_step)))], 4)
            for q in (10, 50, 90)}
@@ -935,6 +986,9 @@ def main():
                          f"visible; RCCL needs one GPU per rank")
     device = torch.device("cuda", local_rank % max(1, ndev))
     torch.cuda.set_device(device)
+    # ranks sharing one GPU (gloo rehearsals) keep the one-launch layer forward off: its grid
+    # barrier needs the whole chip (raincast_gnn.functional.layer_forward_ok)
+    note_device_sharing()
     cfg = BENCH_CONFIGS[args.config].with_hidden(args.hidden)
     if args.dropin:
         if world > 1:

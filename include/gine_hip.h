@@ -30,9 +30,11 @@
 extern "C" {
 #endif
 
-#define GINE_ABI_VERSION 4  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
+#define GINE_ABI_VERSION 5  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
                               3: gine_deepset_bwd_num_partials takes the hidden width;
-                              4: bn_acc grows two grid-barrier words (gine_mp_fwd_layer) */
+                              4: bn_acc grows two grid-barrier words (gine_mp_fwd_layer);
+                              5: grid-barrier failure count (gine_bn_acc_barrier_failures_index),
+                                 gine_mlp_bwd_layer removed */
 
 #define GINE_OK 0
 #define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
@@ -331,6 +333,13 @@ int gine_mp_fwd_mlp1(const float* x, const int32_t* in_rowptr, const int32_t* in
  * The statistics agree with the partials path to ~1e-15 relative (sums are rounded to
  * 2^-64 per workgroup), so bn_save can differ from it in the last fp32 bit. */
 int gine_bn_acc_words(int32_t channels, int64_t* words);
+/* Index (int64 words into bn_acc) of the grid-barrier failure count: gine_mp_fwd_layer adds 1
+ * there for every workgroup whose grid barrier timed out (~2 s: the grid was not resident at
+ * once -- other work held CUs).  Such a launch's outputs are NaN in those workgroups' rows,
+ * bn_save is NaN if workgroup 0 failed, and the running statistics are left as they were.
+ * The caller reads the word at its synchronisation points and raises on a non-zero value;
+ * re-zero the buffer afterwards (raincast_gnn.functional.check_grid_barriers). */
+int gine_bn_acc_barrier_failures_index(int32_t channels, int64_t* index);
 /* Backward, same scheme (a second accumulator per BatchNorm): gine_mlp_bwd2_acc = gine_mlp_bwd2
  * with the [sum dbn | sum dbn*xhat] sums into bn_acc (partials may be NULL);
  * gine_mlp_bwd1_bn = gine_bn_bwd_finalize (training) + gine_mlp_bwd1 in one launch (writes
@@ -343,19 +352,6 @@ int gine_mlp_bwd1_bn(const float* dbn, const float* a1, const float* bn_save, in
                      const float* gamma, float* dgamma, float* dbeta, float* coef,
                      const float* w1, float* dz, int64_t num_nodes, int32_t channels,
                      void* stream);
-/* gine_mlp_bwd2_acc + gine_mlp_bwd1_bn in ONE launch (models/gnn.py:21-26 backward of
- * Linear2 -> ReLU -> BatchNorm1d -> Linear1's input gradient): the two halves separated by a
- * grid barrier (csrc/gine_mlp.hip k_mlp_bwd_layer), each workgroup's dbn and a1 tiles kept in
- * LDS between them, W1 loaded under the barrier's wait.  Same outputs, bit for bit (dbn, coef,
- * dgamma, dbeta, dz), same pairing protocol on bn_acc.  Applies where gine_mlp_bwd_layer_ok
- * says so: channels 64 or 128, at most 2 row tiles per workgroup and the whole grid resident
- * at once (occupancy query, cached per device); GINE_ERR_INVALID otherwise. */
-int gine_mlp_bwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t* ok);
-int gine_mlp_bwd_layer(const float* dy, const float* y, const uint8_t* mask, const float* a1,
-                       const float* bn_save, const float* w2, const float* w1, float* dbn,
-                       int64_t* bn_acc, const float* gamma, float* dgamma, float* dbeta,
-                       float* coef, float* dz, int64_t num_nodes, int32_t channels,
-                       int32_t epilogue, void* stream);
 int gine_mlp_fwd1_acc(const float* z, const float* w1, const float* b1, float* a1,
                       double* partials, int64_t* bn_acc, int64_t num_nodes, int32_t channels,
                       void* stream);
@@ -369,11 +365,16 @@ int gine_mp_fwd_mlp1_acc(const float* x, const int32_t* in_rowptr, const int32_t
  * workgroups, separated by a grid barrier (csrc/gine_mpmlp.hip k_mp_fwd_layer) -- every a1
  * tile stays in LDS between the halves, W2 is staged under the barrier's wait.  Same
  * outputs, bit for bit, as the pair (z, a1, bn_save, running statistics, y, mask), same
- * pairing protocol on bn_acc (the two barrier words at its end, gine_bn_acc_words).
+ * pairing protocol on bn_acc (the barrier words at its end, gine_bn_acc_words; a barrier that
+ * cannot complete is counted there, gine_bn_acc_barrier_failures_index).
  * Applies where gine_mp_fwd_layer_ok says so: channels = 128, max_in_degree <=
  * GINE_MP_FUSED_MAX_DEGREE, at most 2 row tiles per workgroup and the whole grid resident
  * on the device at once (occupancy query, cached per device); GINE_ERR_INVALID otherwise. */
 int gine_mp_fwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_degree, int32_t* ok);
+/* Testing only: `extra` workgroups added to every later gine_mp_fwd_layer grid (0 restores
+ * production), so a test can launch a grid the device cannot hold at once and check that the
+ * barrier's failure reaches the host (gine_bn_acc_barrier_failures_index). */
+int gine_testing_layer_extra_workgroups(int32_t extra);
 int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                       const float* in_attr, const float* lin_w, const float* lin_b,
                       const float* eps, const float* w1, const float* b1, float* z, float* a1,

@@ -30,9 +30,9 @@
 // backward sum dbn | sum dbn * xhat):
 //   [replica: R][hi | mid | lo: W]   [count: W]
 //   [snapshot: 2][hi | mid | lo | count: W]   phase   consumed[2]   barrier[kBarWords]
-// The barrier words (zero at allocation) belong to the one-launch layer kernels
-// (gine_mp_fwd_layer, gine_mlp_bwd_layer), whose producer and consumer halves are separated
-// by a grid barrier instead of a launch boundary (grid_barrier below).
+// The barrier words (zero at allocation) belong to the one-launch layer forward
+// (gine_mp_fwd_layer), whose producer and consumer halves are separated by a grid barrier
+// instead of a launch boundary (grid_barrier below); one of them counts barrier failures.
 #pragma once
 
 #include "gine_common.hpp"
@@ -52,8 +52,8 @@ constexpr int kBnAccWords = 3;   // hi, mid, lo
 constexpr int kBnAccCounts = 1;  // nan | +inf << 21 | -inf << 42
 constexpr int kBnAccCountBits = 21;
 constexpr int kBnAccSnap = kBnAccWords + kBnAccCounts;
-// grid barrier: one 128-byte line each for the global arrival count, the 8 per-XCD arrival
-// counts and the 8 per-XCD generations
+// grid barrier: one 128-byte line each for the global arrival count, the failure count, the
+// 8 per-XCD arrival counts and the 8 per-XCD generations
 constexpr int kBarLine = 16;  // int64 words per line
 constexpr int kBarWords = (2 + 2 * kNumXcd) * kBarLine;
 
@@ -176,10 +176,19 @@ __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool
 // atomics: the barrier orders only the producer's fixed-point atomics (performed at the
 // memory side; the arriving thread waited for every one of its workgroup's before the
 // __syncthreads, see the callers) against the consumer's atomic loads -- no L2 write-back or
-// invalidate.  A watchdog on the constant 100 MHz clock gives up after ~2 s (a grid that was
-// not co-resident after all) rather than hanging the device: that launch's results are then
-// wrong, which the parity tests see.
-__device__ __forceinline__ void grid_barrier(long long* bar, int nblocks) {
+// invalidate.
+// A grid that was not co-resident after all (other work holding CUs: another process on the
+// device, a kernel on another stream) cannot complete: a watchdog on the constant 100 MHz
+// clock gives up after ~2 s rather than hanging the device, adds 1 to the launch's failure
+// word (kBarFailWord, line 1 of the barrier area) and returns false.  The caller then
+// poisons what it computes from the incomplete totals (NaN BatchNorm statistics, no running
+// statistics update), and the host turns a non-zero failure word into GineError
+// (gine_bn_acc_barrier_failures, raincast_gnn.functional.check_grid_barriers).  The late
+// workgroups of such a launch complete the barrier among themselves (their arrival completes
+// the counts) and see complete totals.
+constexpr int kBarFailWord = kBarLine;  // (barrier-area word index)
+
+__device__ __forceinline__ bool grid_barrier(long long* bar, int nblocks) {
   const int b = blockIdx.x, x = b % kNumXcd;
   long long* glob = bar;
   long long* cnt = bar + (2 + x) * kBarLine;
@@ -198,14 +207,20 @@ __device__ __forceinline__ void grid_barrier(long long* bar, int nblocks) {
       for (int y = 0; y < xcds; ++y)
         __hip_atomic_fetch_add(bar + (2 + kNumXcd + y) * kBarLine, 1ll, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-      return;
+      return true;
     }
   }
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
     __builtin_amdgcn_s_sleep(2);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;  // ~2 s: give up
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // ~2 s: give up, loudly
+      __hip_atomic_fetch_add(bar + kBarFailWord, 1ll, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      return false;
+    }
   }
+  return true;
 }
 
 // Record the consumed phase (one thread of workgroup 0 of the consumer).

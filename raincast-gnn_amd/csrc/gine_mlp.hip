@@ -1025,306 +1025,6 @@ __global__ __launch_bounds__(256) void k_bwd1_wgrad(const float* __restrict__ w1
   }
 }
 
-// ----------------------------------------------------------------------------------------
-// The node-MLP backward of a GINE layer in ONE launch (gine_mlp_bwd_layer): the pair
-// gine_mlp_bwd2_acc (dbn = relu'(BN) . (do W2) + the BatchNorm backward sums into the
-// fixed-point accumulator) and gine_mlp_bwd1_bn (BatchNorm backward finish + dz = da1 W1) on
-// the same workgroups, separated by a grid barrier (every workgroup resident, host-checked).
-// Each workgroup keeps its dbn and a1 tiles in LDS across the barrier and loads W1's
-// fragments under the barrier's wait.  Same tile -> workgroup map, thread -> item map, MFMA
-// chains and epilogue arithmetic as the two row-GEMM launches: bit-identical dbn, coef,
-// dgamma, dbeta and dz.
-// ----------------------------------------------------------------------------------------
-constexpr int kBwdLayerTiles = 2;
-
-template <int D>
-struct BwdLayerLds {
-  float a[kRowTile * (D + 4)];                    // staged A tile, then the output tile
-  float kd[kBwdLayerTiles][kRowTile * (D + 4)];   // this workgroup's dbn tiles
-  float ka[kBwdLayerTiles][kRowTile * (D + 4)];   // its a1 tiles
-  float coef[3 * D];
-  double tot[2 * D];
-};
-
-template <int D, int KS>
-__device__ __forceinline__ void load_wk(const float* __restrict__ W, int col, int h,
-                                        float (&bf)[KS]) {  // B[k][j] = W[k][j]
-#pragma unroll
-  for (int s = 0; s < KS; ++s) bf[s] = W[(size_t)(h * KS + s) * D + col];
-}
-
-template <int D, int KS>
-__device__ __forceinline__ floatx16 chain_tile(const float* arow, const BPlanes<KS>& bp,
-                                               const float (&bf)[KS],
-                                               const float* __restrict__ W, int col, int h) {
-  floatx16 acc = zero16();
-  if constexpr (GINE_GEMM_BF16X3 && KS <= 64) {
-#pragma unroll
-    for (int s = 0; s < KS / 8; ++s) {
-      const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);
-      const float4 a1 = *reinterpret_cast<const float4*>(&arow[8 * s + 4]);
-      acc = mfma_bf16x3(split8(a0, a1), bp.f[s], acc);
-    }
-    if (wave_any_nan(acc)) acc = redo_fp32<D, KS, false>(arow, W, col, h);
-  } else {
-    acc = mfma_f32_row<KS>(arow, bf, acc);
-  }
-  return acc;
-}
-
-template <int D, int PDO>
-__global__ __launch_bounds__(2 * D) void k_mlp_bwd_layer(const float* __restrict__ W2,
-                                                         const float* __restrict__ W1,
-                                                         ProArgs pa, const float* __restrict__ a1,
-                                                         float* __restrict__ dbn,
-                                                         float* __restrict__ dz,
-                                                         const float* gamma, float* dgamma,
-                                                         float* dbeta, float* coef,
-                                                         long long* acc, int64_t N,
-                                                         int num_tiles) {
-  constexpr int NT = 2 * D, KS = D / 2, LD = D + 4, D4 = D / 4;
-  constexpr int ITEMS = kRowTile * D4 / NT, RSTEP = NT / D4;
-  __shared__ __attribute__((aligned(16))) BwdLayerLds<D> L;
-  const int tid = threadIdx.x;
-  const int wave = tid / kWave, lane = tid % kWave;
-  const int h = lane >> 5, c32 = lane & 31, col = wave * 32 + c32;
-  const int q_me = tid % D4, r_me = tid / D4;
-  long long* phw = bnacc_phase(acc, 2 * D);
-  // written by earlier launches only (workgroup 0 moves them after the barrier)
-  const long long ph = phw[0] + 1, consumed = phw[1 + ((ph - 1) & 1)];
-  const TileRange tr = xcd_tile_range(num_tiles, blockIdx.x, gridDim.x);
-  const int nt = tr.first < tr.end ? (tr.end - tr.first + tr.step - 1) / tr.step : 0;
-  // rgprof build (tools/layer_prof.py): workgroup 0's phase stamps
-  [[maybe_unused]] const int vb = blockIdx.x;
-  RG_DECL;
-  RG_MARK(10);
-
-  // ---- phase A: dbn = relu'(BN) . (do W2), BatchNorm backward sums ----
-  // tile k+1's inputs are in flight during tile k's chain (tile 0's under the W2 loads); the
-  // a1 rows go to LDS at staging and the epilogue reads them from there
-  RawItem raw[ITEMS];
-  float4 ep[ITEMS];
-  auto load_tile = [&](int k) {
-    const int64_t n0 = (int64_t)(tr.first + k * tr.step) * kRowTile;
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      int64_t n = n0 + r_me + i * RSTEP;
-      n = n < N ? n : N - 1;
-      raw[i] = raw_load<PDO>(pa, D, n, q_me);
-      ep[i] = *reinterpret_cast<const float4*>(a1 + n * D + 4 * q_me);
-    }
-  };
-  if (nt > 0) load_tile(0);
-  float bf[KS];
-  load_wk<D, KS>(W2, col, h, bf);
-  BPlanes<KS> bp;
-  if constexpr (GINE_GEMM_BF16X3 && KS <= 64) bp.from(bf);
-  RG_MARK(11);
-  const ColConst kc = col_const<PDO>(pa, D, q_me);
-  const BnView bv = bn_view(pa.bn, D);
-  const float4 al4 = *reinterpret_cast<const float4*>(bv.alpha + 4 * q_me);
-  const float4 sh4 = *reinterpret_cast<const float4*>(bv.shift + 4 * q_me);
-  const float4 mu4 = *reinterpret_cast<const float4*>(bv.mean + 4 * q_me);
-  const float4 is4 = *reinterpret_cast<const float4*>(bv.invstd + 4 * q_me);
-  double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int k = 0; k < nt; ++k) {
-    const int64_t n0 = (int64_t)(tr.first + k * tr.step) * kRowTile;
-    __syncthreads();  // the previous tile's epilogue reads of L.a are done
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const int r = r_me + i * RSTEP;
-      float4 v = transform<PDO>(pa, raw[i], kc);
-      if (n0 + r >= N) v = f4_zero();
-      *reinterpret_cast<float4*>(&L.a[r * LD + 4 * q_me]) = v;
-      *reinterpret_cast<float4*>(&L.ka[k][r * LD + 4 * q_me]) = ep[i];
-    }
-    __syncthreads();
-    RG_MARK(12);
-    if (k + 1 < nt) load_tile(k + 1);
-    const floatx16 c = chain_tile<D, KS>(&L.a[c32 * LD + h * KS], bp, bf, W2, col, h);
-#ifdef GINE_RG_PROFILE
-    if (c[0] == 1.2345e-30f) L.a[0] = 0.f;  // the stamp below waits for the chain
-#endif
-    RG_MARK(13);
-    __syncthreads();  // every wave's A-fragment reads of L.a are done
-#pragma unroll
-    for (int r = 0; r < 16; ++r) L.a[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + col] = c[r];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {  // EPI_DBN of the row-tile GEMM
-      const int r = r_me + i * RSTEP;
-      const int64_t n = n0 + r;
-      const float4 v = *reinterpret_cast<const float4*>(&L.a[r * LD + 4 * q_me]);
-      const float4 av = *reinterpret_cast<const float4*>(&L.ka[k][r * LD + 4 * q_me]);
-      if (n >= N) continue;
-      const float vv[4] = {v.x, v.y, v.z, v.w};
-      const float a[4] = {av.x, av.y, av.z, av.w};
-      const float al[4] = {al4.x, al4.y, al4.z, al4.w}, sh[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
-      const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
-      float o4[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float bn = bn_apply(a[j], al[j], sh[j]);
-        o4[j] = (bn > 0.f) ? vv[j] : 0.f;
-        const double xhat = (double)((a[j] - mu[j]) * is[j]);
-        st1[j] += (double)o4[j];
-        st2[j] += (double)o4[j] * xhat;
-      }
-      const float4 o = make_float4(o4[0], o4[1], o4[2], o4[3]);
-      *reinterpret_cast<float4*>(dbn + n * D + 4 * q_me) = o;
-      *reinterpret_cast<float4*>(&L.kd[k][r * LD + 4 * q_me]) = o;
-    }
-    RG_MARK(14);
-  }
-  {  // per-column sums of the workgroup: the RSTEP row groups added in fixed order
-    __syncthreads();
-    double* sr = reinterpret_cast<double*>(L.a);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sr[(0 * RSTEP + r_me) * D + 4 * q_me + j] = st1[j];
-      sr[(1 * RSTEP + r_me) * D + 4 * q_me + j] = st2[j];
-    }
-    __syncthreads();
-    for (int c = tid; c < 2 * D; c += NT) {
-      const int which = c / D, cc = c % D;
-      double t = 0.0;
-#pragma unroll
-      for (int g = 0; g < RSTEP; ++g) t += sr[(which * RSTEP + g) * D + cc];
-      bnacc_add<false>(acc, 2 * D, c, t);
-    }
-    // the atomics are performed before this workgroup arrives at the grid barrier
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  RG_MARK(15);
-  // ---- W1 fragments, then the grid barrier ----
-  load_wk<D, KS>(W1, col, h, bf);
-  if constexpr (GINE_GEMM_BF16X3 && KS <= 64) bp.from(bf);
-  RG_MARK(16);
-  __syncthreads();
-  if (tid == 0) grid_barrier(bnacc_barrier(acc, 2 * D), gridDim.x);
-  __syncthreads();
-  RG_MARK(17);
-
-  // ---- phase B: BatchNorm backward finish (k_bwd1_bnacc's arithmetic), dz = da1 W1 ----
-  L.tot[tid] = bnacc_total<true>(acc, 2 * D, tid, blockIdx.x == 0, ph, consumed);
-  __syncthreads();
-  if (tid < D) {
-    const double sd = L.tot[tid], sx = L.tot[D + tid];
-    const double g = gamma ? (double)gamma[tid] : 1.0;
-    const double c1 = g * (double)bv.invstd[tid];
-    const float k1 = (float)c1, k2 = (float)(-c1 * sx / (double)N),
-                k3 = (float)(-c1 * sd / (double)N);
-    L.coef[tid] = k1;
-    L.coef[D + tid] = k2;
-    L.coef[2 * D + tid] = k3;
-    if (blockIdx.x == 0) {
-      if (dgamma) dgamma[tid] = (float)sx;
-      if (dbeta) dbeta[tid] = (float)sd;
-      coef[tid] = k1;
-      coef[D + tid] = k2;
-      coef[2 * D + tid] = k3;
-    }
-  }
-  if (blockIdx.x == 0 && tid == 0) {
-    phw[0] = ph;
-    phw[1 + (ph & 1)] = ph;  // bnacc_mark_consumed
-  }
-  __syncthreads();
-  ProArgs p2 = pa;
-  p2.coef = L.coef;
-  const ColConst kb = col_const<PRO_DA1>(p2, D, q_me);
-  RG_MARK(18);
-  for (int k = 0; k < nt; ++k) {
-    const int64_t n0 = (int64_t)(tr.first + k * tr.step) * kRowTile;
-    __syncthreads();  // the previous tile's output reads of L.a are done
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const int r = r_me + i * RSTEP;
-      RawItem rr;
-      rr.v = *reinterpret_cast<const float4*>(&L.kd[k][r * LD + 4 * q_me]);
-      rr.aux = *reinterpret_cast<const float4*>(&L.ka[k][r * LD + 4 * q_me]);
-      rr.m = make_uchar4(1, 1, 1, 1);
-      float4 v = transform<PRO_DA1>(p2, rr, kb);
-      if (n0 + r >= N) v = f4_zero();
-      *reinterpret_cast<float4*>(&L.a[r * LD + 4 * q_me]) = v;
-    }
-    __syncthreads();
-    const floatx16 c = chain_tile<D, KS>(&L.a[c32 * LD + h * KS], bp, bf, W1, col, h);
-#ifdef GINE_RG_PROFILE
-    if (c[0] == 1.2345e-30f) L.a[0] = 0.f;
-#endif
-    RG_MARK(19);
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) L.a[((r & 3) + 8 * (r >> 2) + 4 * h) * LD + col] = c[r];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-      const int r = r_me + i * RSTEP;
-      const int64_t n = n0 + r;
-      if (n < N)
-        *reinterpret_cast<float4*>(dz + n * D + 4 * q_me) =
-            *reinterpret_cast<const float4*>(&L.a[r * LD + 4 * q_me]);
-    }
-    RG_MARK(20);
-  }
-  RG_FLUSH();
-}
-
-template <int D, int PDO>
-void* bwd_layer_kernel() {
-  return reinterpret_cast<void*>(&k_mlp_bwd_layer<D, PDO>);
-}
-
-// Workgroups of k_mlp_bwd_layer<D, *> the device holds at once (its grid barrier needs every
-// workgroup resident).  Queried once per device and width.
-int bwd_layer_capacity(int D) {
-  static std::mutex mu;
-  static int cap[64][2];
-  static bool known[64][2];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  const int w = D == 64 ? 0 : 1;
-  std::lock_guard<std::mutex> lock(mu);
-  if (!known[dev][w]) {
-    int cus = 0, c = 1 << 30;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 0;
-    void* ks[3];
-    if (D == 64) {
-      ks[0] = bwd_layer_kernel<64, PRO_PLAIN>();
-      ks[1] = bwd_layer_kernel<64, PRO_DOR>();
-      ks[2] = bwd_layer_kernel<64, PRO_DOM>();
-    } else {
-      ks[0] = bwd_layer_kernel<128, PRO_PLAIN>();
-      ks[1] = bwd_layer_kernel<128, PRO_DOR>();
-      ks[2] = bwd_layer_kernel<128, PRO_DOM>();
-    }
-    for (void* k : ks) {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 2 * D, 0) != hipSuccess)
-        return 0;
-      c = std::min(c, nb * cus);
-    }
-    cap[dev][w] = c;
-    known[dev][w] = true;
-  }
-  return cap[dev][w];
-}
-
-int max_tiles_per_block(int tiles, int grid) {  // xcd_tile_range's longest walk
-  const int span = (tiles + kNumXcd - 1) / kNumXcd;
-  int worst = 0;
-  for (int xcd = 0; xcd < kNumXcd; ++xcd) {
-    const int here = grid / kNumXcd + (xcd < grid % kNumXcd ? 1 : 0);
-    const int range = std::max(0, std::min(tiles, (xcd + 1) * span) - xcd * span);
-    if (range > 0 && here == 0) return 1 << 30;
-    if (range > 0) worst = std::max(worst, (range + here - 1) / here);
-  }
-  return worst;
-}
-
-bool bwd_layer_ok(int64_t N, int D);
 
 inline bool mlp_dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
@@ -1358,6 +1058,14 @@ extern "C" int gine_mlp_fwd1(const float* z, const float* w1, const float* b1, f
 extern "C" int gine_bn_acc_words(int32_t channels, int64_t* words) {
   if (!words || channels <= 0) return GINE_ERR_INVALID;
   *words = bnacc_words(channels);
+  return GINE_OK;
+}
+
+extern "C" int gine_bn_acc_barrier_failures_index(int32_t channels, int64_t* index) {
+  if (!index || channels <= 0) return GINE_ERR_INVALID;
+  // the barrier area follows the phase word and the two consumed words (gine_bnacc.hpp)
+  *index = (int64_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * 2 *
+               channels + 3 + kBarFailWord;
   return GINE_OK;
 }
 
@@ -1566,61 +1274,6 @@ extern "C" int gine_mlp_bwd1_bn(const float* dbn, const float* a1, const float* 
                          dgamma, dbeta, coef, acc, num_nodes, tiles);
       break;
   }
-  GINE_LAUNCH_STATUS();
-  return GINE_OK;
-}
-
-namespace gine {
-namespace {
-bool bwd_layer_ok(int64_t N, int D) {
-  if ((D != 64 && D != 128) || N <= 0 || N >= (int64_t(1) << 31)) return false;
-  const int grid = rowgemm_grid(N, D);
-  const int tiles = (int)ceil_div(N, kRowTile);
-  return grid <= bwd_layer_capacity(D) && max_tiles_per_block(tiles, grid) <= kBwdLayerTiles;
-}
-}  // namespace
-}  // namespace gine
-
-extern "C" int gine_mlp_bwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t* ok) {
-  if (!ok) return GINE_ERR_INVALID;
-  *ok = bwd_layer_ok(num_nodes, channels) ? 1 : 0;
-  return GINE_OK;
-}
-
-extern "C" int gine_mlp_bwd_layer(const float* dy, const float* y, const uint8_t* mask,
-                                  const float* a1, const float* bn_save, const float* w2,
-                                  const float* w1, float* dbn, int64_t* bn_acc,
-                                  const float* gamma, float* dgamma, float* dbeta, float* coef,
-                                  float* dz, int64_t num_nodes, int32_t channels,
-                                  int32_t epilogue, void* stream) {
-  if (channels != 64 && channels != 128) return GINE_ERR_DIM;
-  if (!dy || !a1 || !bn_save || !w2 || !w1 || !dbn || !bn_acc || !coef || !dz)
-    return GINE_ERR_INVALID;
-  if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
-  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
-  if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
-  if (!bwd_layer_ok(num_nodes, channels)) return GINE_ERR_INVALID;
-  ProArgs pa{dy, y, mask, bn_save, nullptr};
-  long long* acc = reinterpret_cast<long long*>(bn_acc);
-  const int grid = rowgemm_grid(num_nodes, channels);
-  const int tiles = (int)ceil_div(num_nodes, kRowTile);
-  hipStream_t s = as_stream(stream);
-#define BWD_LAYER(D_, P_)                                                                   \
-  hipLaunchKernelGGL((k_mlp_bwd_layer<D_, P_>), dim3(grid), dim3(2 * D_), 0, s, w2, w1, pa, \
-                     a1, dbn, dz, gamma, dgamma, dbeta, coef, acc, num_nodes, tiles)
-#define BWD_LAYER_D(D_)                                                     \
-  switch (epilogue) {                                                       \
-    case GINE_EPI_NONE: BWD_LAYER(D_, PRO_PLAIN); break;                    \
-    case GINE_EPI_RELU: BWD_LAYER(D_, PRO_DOR); break;                      \
-    default: BWD_LAYER(D_, PRO_DOM); break;                                 \
-  }
-  if (channels == 64) {
-    BWD_LAYER_D(64);
-  } else {
-    BWD_LAYER_D(128);
-  }
-#undef BWD_LAYER_D
-#undef BWD_LAYER
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

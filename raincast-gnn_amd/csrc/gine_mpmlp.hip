@@ -32,6 +32,7 @@
 #include "gine_mlpsrc.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 namespace gine {
@@ -390,6 +391,7 @@ struct LayerLds {
   float a1k[kLayerTiles][kTileRows * kLD];
   float bn[2 * kD];  // alpha | shift
   double tot[2 * kD];
+  int barrier_failed;  // this workgroup's grid barrier timed out (gine_bnacc.hpp)
 };
 
 template <bool FMA, int EPI>
@@ -443,8 +445,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
     }
     if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
   }
-  if (tid == 0) grid_barrier(bnacc_barrier(A.bnacc, 2 * kD), gridDim.x);
+  if (tid == 0) L.barrier_failed = grid_barrier(bnacc_barrier(A.bnacc, 2 * kD), gridDim.x) ? 0 : 1;
   __syncthreads();
+  // a timed-out barrier (the grid was not co-resident): the totals are incomplete, so this
+  // workgroup's statistics and outputs are NaN and the running statistics stay as they were;
+  // the failure word tells the host
+  const bool failed = L.barrier_failed != 0;
   // the gather waves' epilogue operands, in flight under the BatchNorm finish
   float4 xres[kLayerTiles][2];
   float4 bias2 = f4_zero();
@@ -464,14 +470,19 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   }
 
   // ---- phase B: BatchNorm finish (the arithmetic of k_fwd2_bnacc's prologue) ----
-  if (tid < 2 * kD) L.tot[tid] = bnacc_total<true>(A.bnacc, 2 * kD, tid, blockIdx.x == 0, ph,
-                                                  consumed);
+  if (tid < 2 * kD) {
+    const double t = bnacc_total<true>(A.bnacc, 2 * kD, tid, blockIdx.x == 0, ph, consumed);
+    L.tot[tid] = failed ? __builtin_nan("") : t;
+  }
   __syncthreads();
-  if (tid < kD)
-    bn_finish_channel(B.q, kD, tid, L.tot[tid], L.tot[kD + tid], blockIdx.x == 0, &L.bn[tid],
+  if (tid < kD) {
+    BnFwdParams q = B.q;
+    if (failed) q.update_running = 0;
+    bn_finish_channel(q, kD, tid, L.tot[tid], L.tot[kD + tid], blockIdx.x == 0, &L.bn[tid],
                       &L.bn[kD + tid]);
+  }
   if (blockIdx.x == 0 && tid == 0) {
-    if (B.q.update_running && B.q.nbt != nullptr) B.q.nbt[0] = B.q.nbt[0] + 1;
+    if (B.q.update_running && B.q.nbt != nullptr && !failed) B.q.nbt[0] = B.q.nbt[0] + 1;
     phw[0] = ph;
     phw[1 + (ph & 1)] = ph;  // bnacc_mark_consumed
   }
@@ -631,6 +642,11 @@ int max_tiles_per_block(int tiles, int grid) {
   return worst;
 }
 
+// gine_testing_layer_extra_workgroups: workgroups added to k_mp_fwd_layer's grid (0 in
+// production) -- a grid the device cannot hold at once, for the test of the grid barrier's
+// failure path
+std::atomic<int> g_layer_extra{0};
+
 bool layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_degree) {
   if (channels != kD || num_nodes <= 0 || max_in_degree < 0 ||
       max_in_degree > GINE_MP_FUSED_MAX_DEGREE || num_nodes * channels * 4 >= (int64_t(1) << 32))
@@ -641,6 +657,12 @@ bool layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_degree) {
   return grid <= layer_capacity() && max_tiles_per_block(tiles, grid) <= kLayerTiles;
 }
 }  // namespace
+
+extern "C" int gine_testing_layer_extra_workgroups(int32_t extra) {
+  if (extra < 0 || extra > 4096) return GINE_ERR_INVALID;
+  g_layer_extra.store(extra);
+  return GINE_OK;
+}
 
 extern "C" int gine_mp_fwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_degree,
                                     int32_t* ok) {
@@ -672,6 +694,7 @@ extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const
   int32_t grid = 0;
   const int st = gine_mlp_num_partials(num_nodes, channels, &grid);
   if (st != GINE_OK) return st;
+  grid += g_layer_extra.load();
   const int tiles = (int)ceil_div(num_nodes, kTileRows);
   hipStream_t s = as_stream(stream);
   const FusedArgs A{x,  in_rowptr, in_src, in_attr, lin_w, lin_b,

@@ -322,10 +322,29 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
       float* sP = reinterpret_cast<float*>(s_dyn);
       float* sQ = sP + kWgRows * (64 + 4);
       const int e = xcd_remap(blockIdx.x, eng.nblocks);
+#ifdef GINE_WIN_VGPR128
+      // probe build only: the engine path touches v127, so the launch allocates 128 VGPRs
+      // per wave (four waves per SIMD fill the register file) whatever the engine's chain
+      asm volatile("v_mov_b32 v127, 0" ::: "v127");
+#endif
       wgrad_block<MlpWgradSrc<PDO>, 64, 8, GINE_WIN_ENG_X3 != 0>(eng.src, eng.N, eng.D, eng.D,
                                                                  e / eng.tiles,
                                            e % eng.tiles, eng.rows_per_chunk, eng.zstride,
                                            eng.cstride, eng.slab, sP, sQ);
+#ifdef GINE_WIN_LDS_TOUCH_LO
+      // probe build only: keep writing a sentinel into bytes [LO, HI) of this workgroup's own
+      // dynamic LDS for a while (does it reach a co-resident workgroup's allocation?)
+      {
+        float4* pt = reinterpret_cast<float4*>(reinterpret_cast<char*>(s_dyn) +
+                                               GINE_WIN_LDS_TOUCH_LO);
+        constexpr int n = (GINE_WIN_LDS_TOUCH_HI - GINE_WIN_LDS_TOUCH_LO) / 16;
+        for (int it = 0; it < 4000; ++it) {
+          for (int i = threadIdx.x; i < n; i += kWinThreads)
+            pt[i] = make_float4(3.0e38f, 3.0e38f, 3.0e38f, 3.0e38f);
+          asm volatile("s_sleep 1" ::: "memory");
+        }
+      }
+#endif
       return;
     }
     eb = eng.nblocks;

@@ -50,10 +50,39 @@ enum IntOpt {
   kFused,          // gine_mp_fwd_mlp1 applies
   kLayer,          // gine_mp_fwd_layer applies
   kMaxInDegree,
-  kPlanIn,         // address of the forward gine_window_plan (0: none)
-  kPlanOut,        // address of the backward gine_window_plan (0: none)
-  kIntOpts
+  // the window plans' scalars, kPlanFields each: num_tiles (0: no plan), slice_channels,
+  // max_rows, max_edges, max_nodes -- the plan's device arrays come in the graph list, so the
+  // autograd node holds them (a plan's addresses alone would dangle once the graph cache
+  // evicts the graph between forward and backward)
+  kPlanIn,
+  kPlanOut = kPlanIn + 5,
+  kIntOpts = kPlanOut + 5
 };
+constexpr int kPlanFields = 5;
+// graph list: the two CSRs, then per plan (in, out) its device arrays
+enum GraphArg { kInRowptr = 0, kInSrc, kInAttr, kOutRowptr, kOutDst, kOutAttr, kGraphCsr };
+enum PlanArray { kTileBegin = 0, kWinLo, kWinRows, kSlot, kEdgeBegin, kPlanArrays };
+constexpr int kGraphArgs = kGraphCsr + 2 * kPlanArrays;
+
+// The window plan of side `which` (0: in, 1: out) rebuilt from its scalars and its arrays
+// (a struct on the caller's stack: the library reads it only during the call).
+bool plan_of(const std::vector<int64_t>& io, const Tensor* arrays, int which,
+             gine_window_plan* out) {
+  const int64_t* f = io.data() + (which == 0 ? kPlanIn : kPlanOut);
+  if (f[0] <= 0) return false;
+  auto p32 = [&](int k) { return static_cast<const int32_t*>(arrays[k].defined() ? arrays[k].data_ptr() : nullptr); };
+  out->tile_begin = p32(kTileBegin);
+  out->win_lo = p32(kWinLo);
+  out->win_rows = p32(kWinRows);
+  out->num_tiles = (int32_t)f[0];
+  out->slice_channels = (int32_t)f[1];
+  out->max_rows = (int32_t)f[2];
+  out->max_edges = (int32_t)f[3];
+  out->max_nodes = (int32_t)f[4];
+  out->slot = static_cast<const int16_t*>(arrays[kSlot].defined() ? arrays[kSlot].data_ptr() : nullptr);
+  out->edge_begin = p32(kEdgeBegin);
+  return true;
+}
 enum FloatOpt { kMomentum = 0, kBnEps, kFloatOpts };
 
 // Several tensors from ONE allocation (each 256-byte aligned): the caching allocator's
@@ -94,7 +123,7 @@ struct ZeroOnError {  // csrc/gine_bnacc.hpp pairing: re-zero the accumulator if
 
 class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
  public:
-  // graph: in_rowptr, in_src, in_attr, out_rowptr, out_dst, out_attr
+  // graph: in_rowptr, in_src, in_attr, out_rowptr, out_dst, out_attr, the two plans' arrays
   // bn: running_mean, running_var, num_batches_tracked, accumulator (undefined: partials)
   static Tensor forward(AutogradContext* ctx, Tensor x, Tensor lin_w, Tensor lin_b, Tensor eps,
                         Tensor w1, Tensor b1, Tensor gamma, Tensor beta, Tensor w2, Tensor b2,
@@ -115,8 +144,10 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
     const int update_running = (int)io[kUpdateRunning];
     const bool fused = io[kFused] != 0, layer = io[kLayer] != 0;
     const int32_t max_deg = (int32_t)io[kMaxInDegree];
-    const auto* plan_in = reinterpret_cast<const gine_window_plan*>(io[kPlanIn]);
-    const Tensor &in_rowptr = graph[0], &in_src = graph[1], &in_attr = graph[2];
+    gine_window_plan plan_in_v{};
+    const gine_window_plan* plan_in =
+        plan_of(io, graph.data() + kGraphCsr, 0, &plan_in_v) ? &plan_in_v : nullptr;
+    const Tensor &in_rowptr = graph[kInRowptr], &in_src = graph[kInSrc], &in_attr = graph[kInAttr];
     const Tensor &rmean = bn[0], &rvar = bn[1], &nbt = bn[2], &acc = bn[3];
     TORCH_CHECK_VALUE(!(batch_stats && N <= 1), "Expected more than 1 value per channel when "
                 "training, got input size [", N, ", ", D, "]");
@@ -210,8 +241,10 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
       }
       guard.armed = false;
     }
+    const Tensor* po = graph.data() + kGraphCsr + kPlanArrays;  // the backward's plan arrays
     ctx->save_for_backward({x, z, a1, epi == GINE_EPI_RELU ? y : Tensor(), mask, bn_save, lw,
-                            lb, ep, w1c, w2c, g, graph[3], graph[4], graph[5]});
+                            lb, ep, w1c, w2c, g, graph[kOutRowptr], graph[kOutDst],
+                            graph[kOutAttr], po[0], po[1], po[2], po[3], po[4]});
     ctx->saved_data["io"] = io;
     ctx->saved_data["beta"] = beta.defined();
     ctx->saved_data["lin_w_shape"] = lin_w.sizes().vec();
@@ -231,7 +264,9 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
     const int32_t D = (int32_t)x.size(1);
     void* s = stream_of(x);
     const int epi = (int)io[kEpi], lin_flag = (int)io[kLinFlag];
-    const auto* plan_out = reinterpret_cast<const gine_window_plan*>(io[kPlanOut]);
+    gine_window_plan plan_out_v{};
+    const gine_window_plan* plan_out =
+        plan_of(io, sv.data() + 15, 1, &plan_out_v) ? &plan_out_v : nullptr;
     auto fo = x.options();
     const int32_t C = query(gine_mlp_wgrad_num_chunks, N, D, "gine_mlp_wgrad_num_chunks");
     const int32_t Pn = query(gine_mlp_num_partials, N, D, "gine_mlp_num_partials");
@@ -310,10 +345,14 @@ Tensor opt(const c10::optional<Tensor>& t) { return t.has_value() ? *t : Tensor(
 // The Python entry point: one call per layer forward.
 Tensor gine_layer(Tensor x, Tensor lin_w, Tensor lin_b, Tensor eps, Tensor w1, Tensor b1,
                   c10::optional<Tensor> gamma, c10::optional<Tensor> beta, Tensor w2, Tensor b2,
-                  std::vector<Tensor> graph, std::vector<c10::optional<Tensor>> bn,
-                  std::vector<int64_t> io, std::vector<double> fo) {
-  TORCH_CHECK(graph.size() == 6, "graph: in_rowptr, in_src, in_attr, out_rowptr, out_dst, "
-              "out_attr");
+                  std::vector<c10::optional<Tensor>> graph_opt,
+                  std::vector<c10::optional<Tensor>> bn, std::vector<int64_t> io,
+                  std::vector<double> fo) {
+  std::vector<Tensor> graph;
+  for (const auto& t : graph_opt) graph.push_back(opt(t));
+  TORCH_CHECK(graph.size() == kGraphArgs, "graph: in_rowptr, in_src, in_attr, out_rowptr, "
+              "out_dst, out_attr, then the in and out window plans' tile_begin, win_lo, "
+              "win_rows, slot, edge_begin");
   TORCH_CHECK(bn.size() == 4, "bn: running_mean, running_var, num_batches_tracked, acc");
   TORCH_CHECK(io.size() == kIntOpts && fo.size() == kFloatOpts, "option vectors");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.dim() == 2,

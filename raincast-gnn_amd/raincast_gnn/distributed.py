@@ -18,6 +18,33 @@ import torch
 import torch.distributed as dist
 
 
+_SHARED_DEVICE = False
+
+
+def device_shared() -> bool:
+    """True when another rank of the process group uses this process's GPU as well (set by
+    note_device_sharing).  Their kernels can then hold CUs whenever ours launch, so launches
+    that need their whole grid resident at once (the one-launch layer forward's grid
+    barrier: raincast_gnn.functional.layer_forward_ok) are not used."""
+    return _SHARED_DEVICE
+
+
+def note_device_sharing(group=None) -> bool:
+    """Find out (collectively: every rank of ``group`` calls this) whether ranks share a
+    device -- the same host and device index -- and remember it for device_shared()."""
+    global _SHARED_DEVICE
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        _SHARED_DEVICE = False
+        return False
+    import socket
+    me = (socket.gethostname(),
+          torch.cuda.current_device() if torch.cuda.is_available() else -1)
+    every = [None] * dist.get_world_size(group)
+    dist.all_gather_object(every, me, group=group)
+    _SHARED_DEVICE = me[1] >= 0 and every.count(me) > 1
+    return _SHARED_DEVICE
+
+
 def env_rank() -> tuple[int, int, int]:
     """(rank, local_rank, world_size) from the torchrun environment (1-process defaults)."""
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),

@@ -69,11 +69,12 @@ def edge_linear_flag() -> int:
     return _LIN_FLAG
 
 
-_COUNTS: dict = {}  # size queries of the library (pure functions of their arguments)
+_COUNTS: dict = {}  # size queries of the library (functions of their arguments and the device)
 
 
 def _count(fn: str, n: int, d: int) -> int:
-    key = (fn, n, d)
+    # some counts follow the device's CU count (grid sizes), so the device is part of the key
+    key = (fn, n, d, torch.cuda.current_device() if torch.cuda.is_available() else -1)
     v = _COUNTS.get(key)
     if v is None:
         out = ctypes.c_int32(0)
@@ -245,10 +246,21 @@ def engine_in_mp_ok(graph, D: int) -> bool:
 _LAYER_OK = {}
 
 
+def layer_policy_key():
+    """What besides the sizes decides layer_forward_ok: whether other processes share this
+    device (then part of the chip may be held by their kernels whenever ours launch)."""
+    from . import distributed
+    return distributed.device_shared()
+
+
 def layer_forward_ok(N: int, D: int, max_in_degree) -> bool:
     """gine_mp_fwd_layer applies (include/gine_hip.h: D = 128, in-degree <= 32, at most two row
-    tiles per workgroup and the whole grid resident at once on this device)."""
-    if max_in_degree is None or not options.LAYER_FWD:
+    tiles per workgroup and the whole grid resident at once on this device).  Its grid
+    barrier needs every workgroup resident at once, which the occupancy query promises only
+    for an otherwise idle device: when other ranks share this GPU (distributed.device_shared)
+    the pair of launches runs instead.  A barrier that still cannot complete (another
+    process's kernels) fails loudly: check_grid_barriers."""
+    if max_in_degree is None or not options.LAYER_FWD or layer_policy_key():
         return False
     dev = torch.cuda.current_device()
     key = (dev, N, D, int(max_in_degree))
@@ -256,20 +268,6 @@ def layer_forward_ok(N: int, D: int, max_in_degree) -> bool:
     if ok is None:
         out = ctypes.c_int32(0)
         call("gine_mp_fwd_layer_ok", N, D, int(max_in_degree), ctypes.byref(out))
-        ok = _LAYER_OK[key] = bool(out.value)
-    return ok
-
-
-def layer_backward_ok(N: int, D: int) -> bool:
-    """gine_mlp_bwd_layer applies (include/gine_hip.h: D = 64 or 128, at most two row tiles
-    per workgroup and the whole grid resident at once on this device)."""
-    if not options.LAYER_BWD:
-        return False
-    key = (torch.cuda.current_device(), N, D, "bwd")
-    ok = _LAYER_OK.get(key)
-    if ok is None:
-        out = ctypes.c_int32(0)
-        call("gine_mlp_bwd_layer_ok", N, D, ctypes.byref(out))
         ok = _LAYER_OK[key] = bool(out.value)
     return ok
 
@@ -291,6 +289,38 @@ def bn_accumulator(bn: "BnConfig", D: int, dev, kind: str = "fwd") -> "torch.Ten
         acc = torch.zeros(words, dtype=torch.int64, device=dev)
         per_dev[(dev, kind)] = acc
     return acc
+
+
+_FAIL_INDEX: dict = {}
+
+
+def check_grid_barriers() -> None:
+    """Raise GineError if a one-launch layer forward's grid barrier timed out since the last
+    check (gine_bn_acc_barrier_failures_index: the grid was not resident at once, so that
+    launch's outputs are NaN in the failed workgroups' rows).  The affected accumulators are
+    re-zeroed, so the next step starts a fresh pairing.  Reads device memory: call it where
+    the caller synchronises anyway (end of an epoch, after a benchmark's timed steps)."""
+    failed = []
+    for mod, per_dev in list(_BN_ACC.items()):
+        for (dev, kind), acc in list(per_dev.items()):
+            if kind != "fwd":
+                continue
+            D = mod.num_features
+            idx = _FAIL_INDEX.get(D)
+            if idx is None:
+                out = ctypes.c_int64(0)
+                call("gine_bn_acc_barrier_failures_index", D, ctypes.byref(out))
+                idx = _FAIL_INDEX[D] = int(out.value)
+            n = int(acc[idx].item())
+            if n:
+                failed.append((type(mod).__name__, str(dev), n))
+                acc.zero_()
+    if failed:
+        raise _lib.GineError(
+            "gine_mp_fwd_layer: the grid barrier timed out (the launch's workgroups were not "
+            f"all resident at once: other work held CUs) -- {failed} (module, device, "
+            "workgroups); those launches' outputs are NaN in the failed workgroups' rows and "
+            "the running statistics were not updated; the accumulators were reset")
 
 
 class _paired:
@@ -441,17 +471,11 @@ class GineLayer(torch.autograd.Function):
                      ptr(dz), N, D, stream)
             else:
                 with _paired(acc):  # producer + consumer back to back
-                    if layer_backward_ok(N, D):  # both in one launch (grid barrier)
-                        call("gine_mlp_bwd_layer", ptr(dy), ptr(y), ptr(mask), ptr(a1),
-                             ptr(bn_save), ptr(w2c), ptr(w1c), ptr(dbn), ptr(acc), ptr(g),
-                             ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dz), N, D, epi, stream)
-                    else:
-                        call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1),
-                             ptr(bn_save), ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi,
-                             stream)
-                        call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc),
-                             ptr(g), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz),
-                             N, D, stream)
+                    call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1),
+                         ptr(bn_save), ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi, stream)
+                    call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc),
+                         ptr(g), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz), N, D,
+                         stream)
             engine = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epi)
         else:
             # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch

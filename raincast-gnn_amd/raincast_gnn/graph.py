@@ -164,9 +164,9 @@ class GineGraph:
                                             self.device, max_nodes, staged, slots=True)
         self._windows["min_wg"] = 0 if mode == "all" else WINDOW_MIN_WORKGROUPS
 
-    def window_plan(self, side: str, channels: int):
-        """The widest-slice window plan usable at this channel count (``side`` "in" for the
-        forward, "out" for the backward), or None -> gather kernels."""
+    def window_plan_entry(self, side: str, channels: int):
+        """(plan, device arrays) of the widest-slice window plan usable at this channel count
+        (``side`` "in" for the forward, "out" for the backward), or None -> gather kernels."""
         if self._windows is None:
             return None
         for cs, entry in self._windows[side].items():
@@ -174,8 +174,14 @@ class GineGraph:
                 plan = entry[0]
                 if plan.num_tiles * (channels // cs) < self._windows.get("min_wg", 0):
                     return None
-                return plan
+                return entry
         return None
+
+    def window_plan(self, side: str, channels: int):
+        """The plan of :meth:`window_plan_entry` (a ctypes struct whose device arrays this
+        graph owns: callers keep the graph alive while a launch may still use it)."""
+        entry = self.window_plan_entry(side, channels)
+        return None if entry is None else entry[0]
 
     def check(self) -> None:
         """Raise IndexError (like torch.index_select) when an index was out of range."""

@@ -94,20 +94,22 @@ class GINEConv(torch.nn.Module):
         mods = tuple(nn._modules.values())
         l1, bn, act, l2 = mods
         D = x.size(1)
-        # the module structure part is cached per (D, child modules): the drop-in path calls
+        # the module-type part is cached per (D, the child modules themselves -- held, not
+        # their ids, so a replaced child can never match a stale entry): the drop-in path calls
         # this every layer and step (host time; profiles/r04_s03_dropin_prof_cpp.txt)
-        key = (D,) + tuple(map(id, mods))
-        if self.__dict__.get("_fuse_key") != key:
+        cached = self.__dict__.get("_fuse_key")
+        if cached is None or cached[0] != D or any(a is not b for a, b in zip(cached[1], mods)):
             self.__dict__["_fuse_ok"] = (
                 type(l1) is Linear and type(bn) is BatchNorm1d and type(act) is ReLU
-                and type(l2) is Linear and l1.bias is not None and l2.bias is not None
-                and l1.in_features == D and l1.out_features == D and l2.in_features == D
-                and l2.out_features == D and bn.num_features == D and D in FUSED_CHANNELS)
-            self.__dict__["_fuse_key"] = key
+                and type(l2) is Linear and bn.num_features == D and D in FUSED_CHANNELS)
+            self.__dict__["_fuse_key"] = (D, mods)
         if not self.__dict__["_fuse_ok"]:
             return False
+        # attributes a cached child can change in place: re-checked on every call
         w1, w2 = l1.weight, l2.weight
-        return (w1.dtype == torch.float32 and w2.dtype == torch.float32
+        return (l1.bias is not None and l2.bias is not None
+                and w1.shape == (D, D) and w2.shape == (D, D)
+                and w1.dtype == torch.float32 and w2.dtype == torch.float32
                 and w1.device == x.device and w2.device == x.device)
 
     def _check_inputs(self, x, edge_index, edge_attr, size):

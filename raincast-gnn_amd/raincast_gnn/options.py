@@ -20,11 +20,6 @@ BN_ACC_BWD   the same for the BatchNorm backward sums.
 LAYER_FWD    True: where the fused forward and the accumulator apply and the grid fits the
              device at once, the whole layer forward in one launch (gine_mp_fwd_layer: the
              fused forward and the second GEMM separated by a grid barrier); False: the pair.
-LAYER_BWD    True: the BatchNorm-accumulator backward pair (dbn GEMM + BN finish + dz GEMM)
-             in one launch where its grid fits the device at once (gine_mlp_bwd_layer).
-             Off by default: measured slower at cfg2 (36.1 us against 22.6 us for the
-             pair, profiles/r04_s03_layer_prof.txt; workgroup 0 spends 13.5 us at the grid
-             barrier waiting for the slowest phase A, r04_s03_layer_stamps.txt).
 """
 from __future__ import annotations
 
@@ -35,4 +30,3 @@ ENGINE_IN_MP = True
 BN_ACC = True
 BN_ACC_BWD = True
 LAYER_FWD = True
-LAYER_BWD = False

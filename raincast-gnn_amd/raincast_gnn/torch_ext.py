@@ -63,31 +63,45 @@ def get():
     return _ext
 
 
-# io option order of gine_torch.cpp (IntOpt)
-IO_EPI, IO_LIN, IO_BATCH, IO_UPDATE, IO_FUSED, IO_LAYER, IO_DEG, IO_PLAN_IN, IO_PLAN_OUT = range(9)
+# io option order of gine_torch.cpp (IntOpt): then 5 scalars per window plan (in, out)
+IO_EPI, IO_LIN, IO_BATCH, IO_UPDATE, IO_FUSED, IO_LAYER, IO_DEG, IO_PLAN_IN = range(8)
+IO_PLAN_OUT = IO_PLAN_IN + 5
 
 
-def plan_address(plan) -> int:
-    import ctypes
-    return 0 if plan is None else ctypes.addressof(plan)
+def _plan_args(graph, side: str, D: int):
+    """(5 scalars, 5 device arrays) of a window plan for gine_torch.cpp: num_tiles (0: no
+    plan), slice_channels, max_rows, max_edges, max_nodes; tile_begin, win_lo, win_rows, slot,
+    edge_begin (None where absent).  The arrays travel as tensors, so the C++ autograd node
+    holds them between forward and backward whatever the graph cache does meanwhile."""
+    entry = graph.window_plan_entry(side, D)
+    if entry is None:
+        return [0, 0, 0, 0, 0], [None] * 5
+    plan, arrays = entry
+    tb, lo, rows, edge_begin = arrays[:4]
+    slot = arrays[4] if len(arrays) > 4 else None
+    return ([plan.num_tiles, plan.slice_channels, plan.max_rows, plan.max_edges,
+             plan.max_nodes], [tb, lo, rows, slot, edge_begin])
 
 
-def _graph_opts(graph, N: int, D: int, has_acc: bool) -> list:
-    """The io options that depend only on the graph, the sizes and the path switches, cached
-    on the graph object (one dict lookup per layer call instead of the plan and occupancy
-    queries)."""
+def _graph_opts(graph, N: int, D: int, has_acc: bool) -> tuple:
+    """(io options, graph tensor list) that depend only on the graph, the sizes and the path
+    switches, cached on the graph object (one dict lookup per layer call instead of the plan
+    and occupancy queries)."""
     from . import functional as Fn
     from . import options
-    key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD)
+    key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD, Fn.layer_policy_key())
     cache = graph._ext_opts
     got = cache.get(key)
     if got is None:
         fused = Fn.fused_forward_ok(graph, N, D)
         lay = fused and has_acc and Fn.layer_forward_ok(N, D, graph.max_in_degree)
-        got = cache[key] = [int(fused), int(lay),
-                            int(graph.max_in_degree if graph.max_in_degree is not None else -1),
-                            plan_address(graph.window_plan("in", D)),
-                            plan_address(graph.window_plan("out", D))]
+        pin, ain = _plan_args(graph, "in", D)
+        pout, aout = _plan_args(graph, "out", D)
+        io = [int(fused), int(lay),
+              int(graph.max_in_degree if graph.max_in_degree is not None else -1)] + pin + pout
+        tensors = [graph.in_rowptr, graph.in_src, graph.in_attr, graph.out_rowptr,
+                   graph.out_dst, graph.out_attr] + ain + aout
+        got = cache[key] = (io, tensors)
     return got
 
 
@@ -100,12 +114,11 @@ def layer(ext, x, conv, graph, epilogue: int) -> torch.Tensor:
     N, D = x.shape
     bn = Fn.BnConfig(bn_mod)
     acc = Fn.bn_accumulator(bn, D, x.device)
+    gio, tensors = _graph_opts(graph, N, D, acc is not None)
     io = [epilogue, Fn.edge_linear_flag(), int(bn.use_batch_stats),
-          int(bn.update_running)] + _graph_opts(graph, N, D, acc is not None)
+          int(bn.update_running)] + gio
     fo = [bn.momentum, bn.eps]
     return ext.gine_layer(x, conv.lin.weight, conv.lin.bias, conv.eps, l1.weight, l1.bias,
-                          bn_mod.weight, bn_mod.bias, l2.weight, l2.bias,
-                          [graph.in_rowptr, graph.in_src, graph.in_attr, graph.out_rowptr,
-                           graph.out_dst, graph.out_attr],
+                          bn_mod.weight, bn_mod.bias, l2.weight, l2.bias, tensors,
                           [bn.running_mean, bn.running_var,
                            bn.num_batches_tracked if bn.update_running else None, acc], io, fo)

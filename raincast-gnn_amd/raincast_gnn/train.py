@@ -202,6 +202,8 @@ def train_one_epoch(model, loader, optimizer, device, logger=None, runner=None) 
     total = 0.0
     for v in torch.stack(losses).double().cpu().tolist():  # train.py:72 order, one readback
         total += v
+    from .functional import check_grid_barriers
+    check_grid_barriers()  # (synchronised by the readback above)
     avg = _mean_over_ranks(total / len(losses), losses[0].device)
     (logger or log).info(f"  [Train] Loss: {avg:.6f}")
     return avg
@@ -271,7 +273,8 @@ def fit(model, optimizer, train_loader, val_loader, device, max_epochs: int,
 # ---------------------------------------------------------------------------------------
 def main(argv=None) -> dict:
     from .data import synthetic_samples
-    from .distributed import FlatGradReducer, broadcast_parameters, env_rank
+    from .distributed import (FlatGradReducer, broadcast_parameters, env_rank,
+                              note_device_sharing)
     from .models import gnn_from_params
     from .optim import FlatAdamW
     from .params import load_params
@@ -311,6 +314,7 @@ def main(argv=None) -> dict:
     set_seed(args.seed)
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
+    note_device_sharing()
     samples = synthetic_samples(args.stations, args.samples, k=args.k, seed=args.seed,
                                 max_dist=config.get("max_dist", 100.0) if args.radius else None)
     full = DeviceDataset(samples, device)

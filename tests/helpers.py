@@ -441,15 +441,27 @@ def engine_order_batch(batch):
     return relabel_stations(batch, station_order(batch.edge_index[:, :e1], n))
 
 
-def branch_grad_table(grads, rb, r32, r64, tol):
+# The plain normwise bound every gradient except the two ill-conditioned reductions must meet:
+# 3x the largest plain error the engine showed over every configuration and station order of
+# round 4 (1.75e-5: deepset.rho.2.bias at cfg2-D64, profiles/r04_s13_parity_*), so that a
+# regression of the engine's arithmetic fails here even where the condition scale is large.
+PLAIN_TOL = 3e-5
+# d eps = sum dz*x (cancelling sum over N x D terms) and Linear1's bias behind train-mode BN
+# (analytically zero): no plain relative bound exists for these, the condition-scaled one holds
+ILL_CONDITIONED = (".eps", "nn.0.bias")
+
+
+def branch_grad_table(grads, rb, r32, r64, tol, plain_tol=PLAIN_TOL):
     """Every gradient in ``grads`` (name -> tensor) against the fp64 branch oracle ``rb``
-    (check_training_step, recorded: ``rb.scales``), condition-scaled:
-    max |g - g64| / max S  and  ||g - g64|| / ||S||  with S the parameter's componentwise
-    condition scale (condition_scales; for eps, sum |dz * x|).  Both must be <= ``tol``.
-    Listed for context: the plain normwise error ||g - g64|| / ||g64||, the condition
-    number ||S|| / ||g64||, and the fp32 oracle's own plain normwise error against the
-    plain fp64 oracle.
-    Returns (worst scaled max-norm error, table, names above ``tol``)."""
+    (check_training_step, recorded: ``rb.scales``):
+    * condition-scaled, every parameter: max |g - g64| / max S  and  ||g - g64|| / ||S||
+      with S the parameter's componentwise condition scale (condition_scales; for eps,
+      sum |dz * x|), both <= ``tol``;
+    * plain normwise, every parameter but the ILL_CONDITIONED ones: ||g - g64|| / ||g64||
+      <= ``plain_tol``.
+    Listed for context: the condition number ||S|| / ||g64|| and the fp32 oracle's own plain
+    normwise error against the plain fp64 oracle.
+    Returns (worst scaled max-norm error, table, names above their bounds)."""
     p32, p64 = dict(r32.named_parameters()), dict(r64.named_parameters())
     pb = dict(rb.named_parameters())
     rows, fails = [], []
@@ -472,14 +484,16 @@ def branch_grad_table(grads, rb, r32, r64, tol):
         plain = fro_rel(g, exact)
         kappa = (S.norm() / exact.norm()).item() if exact.norm() > 0 else float("inf")
         own32 = fro_rel(p32[name].grad, p64[name].grad)
-        ok = e_max <= tol and e_fro <= tol
-        rows.append(f"{name:<36} {e_max:>9.2e} {e_fro:>9.2e} {plain:>9.2e} {kappa:>9.2e} "
+        ill = name.endswith(ILL_CONDITIONED)
+        ok = e_max <= tol and e_fro <= tol and (ill or plain <= plain_tol)
+        rows.append(f"{name:<36} {e_max:>9.2e} {e_fro:>9.2e} {plain:>9.2e} "
+                    f"{'-' if ill else format(plain_tol, '.0e'):>6} {kappa:>9.2e} "
                     f"{own32:>9.2e} {'ok' if ok else 'FAIL'}")
         if not ok:
             fails.append(name)
         worst = max(worst, e_max)
     table = "\n".join([f"{'parameter':<36} {'max/S':>9} {'norm/S':>9} {'plain':>9} "
-                        f"{'kappa':>9} {'fp32 own':>9}"] + rows)
+                        f"{'bound':>6} {'kappa':>9} {'fp32 own':>9}"] + rows)
     return worst, table, fails
 
 
@@ -490,19 +504,21 @@ def check_training_step(params, batch, dev, tol=1e-5, seed=42, relabel=False, re
     Predictions, loss and the BatchNorm running statistics: within ``tol`` (max-norm
     relative) of the fp32 oracle, fp64 oracle as tie-break.
 
-    Gradients: every parameter gradient within ``tol`` of the fp64 oracle ON THE ENGINE'S
-    BRANCH, both max-norm relative (max |g - g64| / max |g64|) and normwise (||g - g64|| /
-    ||g64||).  A ReLU decision whose pre-activation lies within fp32 rounding of zero can go
+    Gradients: against the fp64 oracle ON THE ENGINE'S BRANCH (branch_grad_table), every
+    parameter within ``tol`` of its condition scale S (max |g - g64| / max S and ||g - g64|| /
+    ||S||: S = |dY|^T |X| for weights, sum |dY| for biases, sum |dz*x| for eps), and every
+    parameter but eps and Linear1's bias also within PLAIN_TOL (3e-5) plain normwise
+    (||g - g64|| / ||g64||).  A ReLU decision whose pre-activation lies within fp32 rounding of zero can go
     either way in any fp32 implementation, and each such decision moves one gradient entry by
     the whole upstream gradient -- at 10^4-10^5 nodes a step makes ~10^8 decisions and the
     reference restatement itself, at 1 vs all threads, differs from the exact gradient by
     1e-4..5e-3.  So the fp64 oracle follows the engine's decisions (EngineTies), each
     differing one checked against the engine's forward error bound computed from the saved
     operands, and the engine's gradients are then held to ``tol`` against that exact
-    branch gradient.  Two reductions are ill-conditioned in any fp32 implementation and get
-    their condition scale: ``d eps = sum dz*x`` (|err| <= tol * sum |dz*x|) and Linear1's
-    bias gradient, analytically zero behind train-mode BN (|err| <= tol * sum_n |d a1|,
-    normwise over channels).
+    branch gradient.  Two reductions are ill-conditioned in any fp32 implementation and are
+    held to their condition scale only: ``d eps = sum dz*x`` (|err| <= tol * sum |dz*x|) and
+    Linear1's bias gradient, analytically zero behind train-mode BN (|err| <= tol *
+    sum_n |d a1|, normwise over channels).
     ``relabel``: the engine runs the batch in its locality order (engine_order_batch) and
     its tensors are mapped back to the collated order; the oracle runs the reference order.
     ``report``: a list the per-parameter error table and the decision table are appended to.

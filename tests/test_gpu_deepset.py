@@ -2,9 +2,10 @@
 models/gnn.py:48-68's ``relu(phi[0](ens)).sum(dim=1)`` and its weight gradients.
 
 Tolerances are condition-scaled (fp32 accumulation vs an exact fp64 sum): elementwise
-``|gpu - exact| <= 1e-5 * sum|terms|``.  A row whose pre-activation lies within fp32
-rounding of 0 may take either ReLU branch in any fp32 implementation (the reference's CPU
-path included); its whole contribution is added to the bound for the weight gradients.
+``|gpu - exact| <= 1e-5 * sum|terms|``.  The weight gradients are held against the exact
+gradients of the branch the kernel took: its ReLU decisions are read from the bit mask its
+forward saved, and each one that differs from the fp64 sign must lie within that decision's
+forward rounding bound (tests/helpers.EngineTies' phi[0] bound, 2 gamma_F (|ens||W|^T + |b|)).
 """
 import ctypes
 
@@ -13,6 +14,8 @@ import torch
 
 from raincast_gnn import _lib, deepset
 from raincast_gnn.models import DeepSetEncoder
+
+from helpers import ctypes_int, decode_deepset_mask, gamma_dot
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -51,17 +54,23 @@ def test_phi_sum_forward_and_weight_grads(N, M, F, H):
     r64 = pre.clamp_min(0).sum(1)
     assert ((r.double() - r64).abs() <= TOL * mag.sum(1) + 1e-30).all()
 
+    # the kernel's ReLU decisions (its saved bit mask) against the fp64 signs: a differing
+    # decision must lie within its own forward rounding bound
+    words = r.grad_fn.saved_tensors[1].detach().cpu().numpy().view("uint16")
+    G = ctypes_int(lambda out: _lib.call("gine_deepset_mask_layout", N, H, out))
+    on = torch.from_numpy(decode_deepset_mask(words, N, M, H, G)).to(DEV)
+    diff = on != (pre > 0)
+    beta = 2 * gamma_dot(F) * mag
+    assert (pre.abs()[diff] <= beta[diff]).all(), "a ReLU decision outside its rounding bound"
+
     dr = torch.randn(N, H, device=DEV)
     r.backward(dr)
-    ambiguous = pre.abs() <= TOL * mag                           # either branch is valid
-    live = (pre > 0).double() * dr.double()[:, None, :]          # [N, M, H]
+    live = on.double() * dr.double()[:, None, :]                 # [N, M, H], kernel's branch
     e64 = ens.double()
     dw64 = torch.einsum("nmh,nmf->hf", live, e64)
     db64 = live.sum((0, 1))
-    amb = ambiguous.double() * dr.double().abs()[:, None, :]
-    bound_w = TOL * torch.einsum("nmh,nmf->hf", live.abs(), e64.abs()) + \
-        torch.einsum("nmh,nmf->hf", amb, e64.abs()) + 1e-30
-    bound_b = TOL * live.abs().sum((0, 1)) + amb.sum((0, 1)) + 1e-30
+    bound_w = TOL * torch.einsum("nmh,nmf->hf", live.abs(), e64.abs()) + 1e-30
+    bound_b = TOL * live.abs().sum((0, 1)) + 1e-30
     assert ((lin.weight.grad.double() - dw64).abs() <= bound_w).all()
     assert ((lin.bias.grad.double() - db64).abs() <= bound_b).all()
 

@@ -175,3 +175,50 @@ def test_dropin_cpp_binding_same_bits_as_python_function(order, monkeypatch):
     for a_step, b_step in zip(cpp, py):
         for a, b in zip(a_step, b_step):
             assert torch.equal(a, b)
+
+
+def test_cpp_binding_backward_after_graph_eviction():
+    """the C++ autograd node must hold the window plan it ran the forward with.
+    Forward through the C++ binding, evict every graph from the cache and collect it, fill
+    the caching allocator's freed blocks with garbage, then backward: the gradients are the
+    same bits as with the graph alive."""
+    import gc
+    from raincast_gnn import GINEConv, torch_ext
+    from raincast_gnn.graph import graph_cache
+    from helpers import engine_order_batch
+    assert torch_ext.get() is not None, "the C++ binding was not built / did not load"
+    # cfg2's batch (32 x 500 stations, locality order): the window backward applies
+    batch = engine_order_batch(collate(synthetic_samples(500, 32, k=10, seed=6))).to(DEV)
+    D = 128
+    torch.manual_seed(8)
+    mlp = torch.nn.Sequential(torch.nn.Linear(D, D), torch.nn.BatchNorm1d(D), torch.nn.ReLU(),
+                              torch.nn.Linear(D, D))
+    conv = GINEConv(nn=mlp, train_eps=True, edge_dim=1).to(DEV).train()
+    state = {k: v.clone() for k, v in conv.state_dict().items()}
+    x0 = torch.randn(batch.num_nodes, D, device=DEV)
+    gy = torch.randn(batch.num_nodes, D, device=DEV)
+
+    def run(evict):
+        conv.load_state_dict(state)
+        conv.zero_grad(set_to_none=True)
+        graph_cache.clear()
+        x = x0.clone().requires_grad_()
+        ei, ea = batch.edge_index.clone(), batch.edge_attr.clone()
+        g = graph_cache.get(ei, ea.float(), batch.num_nodes)
+        assert g.window_plan("out", D) is not None, "the window backward must apply"
+        y = conv.forward_residual_relu(x, ei, ea)
+        assert type(y.grad_fn).__name__ != "GineLayerBackward", "C++ binding expected"
+        if evict:
+            del g, ei, ea
+            graph_cache.clear()
+            gc.collect()
+            junk = [torch.full((1 << 20,), float("nan"), device=DEV) for _ in range(64)]
+            del junk
+        y.backward(gy)
+        torch.cuda.synchronize()
+        return [x.grad.clone()] + [p.grad.clone() for p in conv.parameters()]
+
+    ref = run(False)
+    got = run(True)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)

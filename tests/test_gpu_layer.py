@@ -122,9 +122,8 @@ def test_model_step_same_bits_with_and_without_layer_launches(hidden, monkeypatc
     torch.manual_seed(5)
     base = gnn_from_params(c.params()).to(DEV).train()
 
-    def run(fwd, bwd):
+    def run(fwd):
         monkeypatch.setattr(options, "LAYER_FWD", fwd)
-        monkeypatch.setattr(options, "LAYER_BWD", bwd)
         m = copy.deepcopy(base)
         out = []
         for _ in range(2):
@@ -139,14 +138,58 @@ def test_model_step_same_bits_with_and_without_layer_launches(hidden, monkeypatc
         return out
 
     n = batch.num_nodes
-    monkeypatch.setattr(options, "LAYER_FWD", True)   # (LAYER_BWD is off by default)
-    monkeypatch.setattr(options, "LAYER_BWD", True)
-    assert F.layer_backward_ok(n, hidden)
+    monkeypatch.setattr(options, "LAYER_FWD", True)
     if hidden == 128:
         assert F.layer_forward_ok(n, hidden, c.k + 1)
-    ref = run(False, False)
-    for fwd, bwd in ((True, False), (False, True), (True, True)):
-        got = run(fwd, bwd)
-        for a_step, b_step in zip(got, ref):
-            for a, b in zip(a_step, b_step):
-                assert torch.equal(a, b), (fwd, bwd)
+    ref = run(False)
+    got = run(True)
+    for a_step, b_step in zip(got, ref):
+        for a, b in zip(a_step, b_step):
+            assert torch.equal(a, b)
+
+
+def test_layer_barrier_failure_is_loud(monkeypatch):
+    """A grid the device cannot hold at once (gine_testing_layer_extra_workgroups adds one
+    workgroup per CU beyond the resident limit): the resident workgroups' barrier times out
+    (~2 s), their rows come out NaN, the running statistics stay untouched, and
+    check_grid_barriers raises GineError and resets the accumulator -- after which the
+    production grid gives the pair's bits again."""
+    ei, ea, n = knn_batch_graph(500, 10, 32, seed=510)
+    conv = _conv(seed=3)
+    state = {kk: v.clone() for kk, v in conv.state_dict().items()}
+    x = torch.randn(n, 128, device=DEV) * 1.5 + 0.2
+    eid, ead = ei.to(DEV), ea.to(DEV)
+    monkeypatch.setattr(options, "LAYER_FWD", True)
+    assert Fn.layer_forward_ok(n, 128, 11)
+    Fn.check_grid_barriers()  # nothing pending from earlier tests
+    bn = conv.nn[1]
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    _lib.call("gine_testing_layer_extra_workgroups", cus)
+    try:
+        with torch.no_grad():
+            y = conv.forward_residual_relu(x, eid, ead)
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("gine_testing_layer_extra_workgroups", 0)
+    assert torch.isnan(y).any(), "the workgroups whose barrier failed must poison their rows"
+    with pytest.raises(_lib.GineError, match="grid barrier timed out"):
+        Fn.check_grid_barriers()
+    acc = Fn._BN_ACC[bn][(DEV, "fwd")]
+    assert int(acc.abs().sum()) == 0                      # reset for a fresh pairing
+    assert torch.equal(bn.running_mean, rm0) and torch.equal(bn.running_var, rv0)
+    Fn.check_grid_barriers()                              # reported once
+    # the production grid afterwards: the layer launch and the pair agree bit for bit again
+    got = _steps(conv, state, x, eid, ead, "residual", [True], monkeypatch)
+    ref = _steps(conv, state, x, eid, ead, "residual", [False], monkeypatch)
+    for a, b in zip(got[0][0], ref[0][0]):
+        assert torch.equal(a, b)
+    Fn.check_grid_barriers()
+
+
+def test_layer_forward_refused_when_ranks_share_the_device(monkeypatch):
+    from raincast_gnn import distributed
+    monkeypatch.setattr(options, "LAYER_FWD", True)
+    assert Fn.layer_forward_ok(16000, 128, 11)
+    monkeypatch.setattr(distributed, "_SHARED_DEVICE", True)
+    assert not Fn.layer_forward_ok(16000, 128, 11)
