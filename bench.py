@@ -77,8 +77,10 @@ def parse():
                          "the collective-capture path, which has never run with more than "
                          "one rank; costs the two cross-stream hops of an eager collective "
                          "(0.548 vs 0.534 ms per cfg2 step at world 1, profiles/r03_s08); "
-                         "graph: the all-reduce captured inside the step's HIP graph (RCCL "
-                         "only; a failed capture exits non-zero)")
+                         "graph: the all-reduce captured inside the step's HIP graph, the "
+                         "GINE stack's and head's gradients reduced on a side stream under "
+                         "the rest of the backward (RCCL only; a failed capture exits "
+                         "non-zero)")
     ap.add_argument("--station-order", choices=("locality", "dataset"), default="locality",
                     help="locality: the batch in the engine's station order (reverse "
                          "Cuthill-McKee, raincast_gnn.data.station_order -- the device "
@@ -125,7 +127,16 @@ class Trainer:
         # the same flat gradient buffer is what the data-parallel all-reduce reduces
         self.opt = FlatAdamW(self.model.parameters(), lr=params["lr"])
         self.reducer = FlatGradReducer(self.model.parameters(), flat=self.opt.flat_grad,
-                                       force=force_allreduce)
+                                       force=force_allreduce, offsets=self.opt._offsets)
+        self.overlap = False
+        if (self.collective and allreduce == "graph" and dist.is_initialized()
+                and dist.get_backend() == "nccl"):
+            # the GINE stack's and the head's gradients (the tail of the flat buffer) are
+            # all-reduced on a side stream as soon as the stack's backward is done, under
+            # the dense chain's and the DeepSet's backward (captured as a fork of the graph)
+            self.reducer.overlap_after(self.model.conv, list(self.model.conv.parameters())
+                                       + list(self.model.aggr.parameters()))
+            self.overlap = True
         self.graph_fb = self.graph_opt = None
         self.loss = None
         self.allreduce_in_graph = False
@@ -191,9 +202,11 @@ class Trainer:
                 stream = torch.cuda.current_stream(self.device)
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record(stream)
+                t0 = time.perf_counter()
                 self.reducer.all_reduce_()
+                host_ms = (time.perf_counter() - t0) * 1e3  # the call's host time (gloo: whole)
                 ev[1].record(stream)
-                self.ar_events.append(ev)
+                self.ar_events.append(ev + (host_ms,))
             else:
                 self.reducer.all_reduce_()
             self.graph_opt.replay()
@@ -720,31 +733,66 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     Fn.check_grid_barriers()  # a layer launch whose grid was not co-resident raises here
-    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    in_order = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    per_step = sorted(in_order)
     pct = {q: round(per_step[min(len(per_step) - 1, int(q / 100 * len(per_step)))], 4)
            for q in (10, 50, 90)}
-    # the split all-reduce alone (between the fwd+bwd and AdamW graphs), per step
-    ar = sorted(a.elapsed_time(b) for a, b in tr.ar_events)
+    # the split all-reduce alone (between the fwd+bwd and AdamW graphs), per step: on the
+    # stream (HIP events) and on the host (the collective call itself)
+    ar_steps = [(a.elapsed_time(b), h) for a, b, h in tr.ar_events]
+    ar = sorted(t for t, _ in ar_steps)
     tr.ar_events = None
     pct["allreduce_p50"] = round(ar[len(ar) // 2], 4) if ar else None
+    pct["stalls"] = stalled_steps(in_order, ar_steps)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-        pct["per_rank"] = gather_per_rank(pct[50], pct["allreduce_p50"], world, device)
+        st = pct["stalls"]
+        pct["per_rank"] = gather_per_rank(pct[50], pct["allreduce_p50"], world, device,
+                                          step_max=per_step[-1],
+                                          stalls=st["count"] if st else 0)
     return tr, elapsed, pct
 
 
-def gather_per_rank(step_p50, allreduce_p50, world, device):
-    """Every rank's p50 step time and p50 all-reduce time (ms), for the N > 1 line's
-    decomposition (a tensor all_gather: on the GPU over RCCL, on the CPU over gloo)."""
-    mine = torch.tensor([step_p50, -1.0 if allreduce_p50 is None else allreduce_p50],
+def stalled_steps(in_order, ar_steps):
+    """Steps that took more than 10x the median (and over 1 ms): their index, time, and the
+    all-reduce's stream / host time in that step -- so that one stall (seen with two ranks
+    sharing one GPU over gloo) is reported beside the wall-clock value instead of silently
+    defining it.  None when there is none."""
+    if not in_order:
+        return None
+    med = sorted(in_order)[len(in_order) // 2]
+    bad = [i for i, t in enumerate(in_order) if t > max(10 * med, 1.0)]
+    if not bad:
+        return None
+    out = {"threshold_ms": round(max(10 * med, 1.0), 4), "count": len(bad),
+           "total_ms": round(sum(in_order[i] for i in bad), 3), "steps": []}
+    for i in bad[:8]:
+        rec = {"step": i, "ms": round(in_order[i], 3)}
+        if i < len(ar_steps):
+            rec["allreduce_stream_ms"] = round(ar_steps[i][0], 3)
+            rec["allreduce_host_ms"] = round(ar_steps[i][1], 3)
+        out["steps"].append(rec)
+    rest = [t for i, t in enumerate(in_order) if i not in set(bad)]
+    out["ms_per_step_other_steps"] = round(sum(rest) / len(rest), 4) if rest else None
+    return out
+
+
+def gather_per_rank(step_p50, allreduce_p50, world, device, step_max=None, stalls=0):
+    """Every rank's p50 step time, p50 all-reduce time, slowest step (ms) and stalled-step
+    count, for the N > 1 line's decomposition (a tensor all_gather: on the GPU over RCCL, on
+    the CPU over gloo)."""
+    mine = torch.tensor([step_p50, -1.0 if allreduce_p50 is None else allreduce_p50,
+                         -1.0 if step_max is None else step_max, float(stalls)],
                         device=device if dist.get_backend() == "nccl" else "cpu",
                         dtype=torch.float64)
     every = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(every, mine)
     return [{"rank": r, "step_ms_p50": round(v[0].item(), 4),
-             "allreduce_ms_p50": round(v[1].item(), 4) if v[1].item() >= 0 else None}
+             "allreduce_ms_p50": round(v[1].item(), 4) if v[1].item() >= 0 else None,
+             "step_ms_max": round(v[2].item(), 4) if v[2].item() >= 0 else None,
+             "stalled_steps": int(v[3].item())}
             for r, v in enumerate(every)]
 
 
@@ -1070,7 +1118,8 @@ def main():
                        "nodes_per_gpu": tr.batch.num_nodes, "edges_per_gpu": E_rank,
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
                        "station_order": args.station_order,
-                       "allreduce_in_graph": tr.allreduce_in_graph},
+                       "allreduce_in_graph": tr.allreduce_in_graph,
+                       "allreduce_overlap": tr.overlap},
             "edges_aggregated_per_s": round(edges_per_s, 1),
             "step_ms_p10_p50_p90": [pct[10], pct[50], pct[90]],
             # N > 1 decomposition: the gradient all-reduce between the fwd+bwd and AdamW
@@ -1078,6 +1127,8 @@ def main():
             # graph or there is no collective), and every rank's p50 step
             "allreduce_ms_p50": pct.get("allreduce_p50"),
             "per_rank": pct.get("per_rank"),
+            # steps > 10x the median on rank 0 (flagged, still inside `value`)
+            "stalled_steps": pct.get("stalls"),
             "roofline": roof, "roofline_step": roof_step,
             "roofline_message_passing": roof_mp,
             "strong_scaling_cfg4": strong,

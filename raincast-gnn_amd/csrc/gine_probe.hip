@@ -8,22 +8,28 @@ namespace gine {
 namespace {
 
 constexpr int kCopyThreads = 256;
-constexpr int kCopyUnroll = 4;
+constexpr int kCopyUnroll = 8;
 
-// Each thread moves kCopyUnroll float4 per pass, all loads issued before the stores; the
-// passes stride the whole grid, so consecutive lanes touch consecutive 16-byte chunks.
-__global__ __launch_bounds__(kCopyThreads) void k_copy_f4(const float4* __restrict__ src,
-                                                           float4* __restrict__ dst, int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * kCopyThreads;
-  int64_t i = (int64_t)blockIdx.x * kCopyThreads + threadIdx.x;
-  for (; i + (kCopyUnroll - 1) * stride < n; i += kCopyUnroll * stride) {
-    float4 v[kCopyUnroll];
+// One workgroup moves one contiguous 32 KiB block (kCopyUnroll float4 per thread, lane-
+// consecutive 16-byte chunks, every load issued before the first store); non-temporal loads
+// and stores, since every byte is touched once.  One block per 32 KiB gives the dispatcher
+// tens of thousands of short workgroups to balance over the 256 CUs (a grid-stride loop over
+// 8 workgroups per CU measured 4.4-4.7 TB/s on the same boxes).
+typedef float f4n __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(kCopyThreads) void k_copy_f4(const f4n* __restrict__ src,
+                                                           f4n* __restrict__ dst, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * kCopyThreads * kCopyUnroll + threadIdx.x;
+  f4n v[kCopyUnroll];
 #pragma unroll
-    for (int u = 0; u < kCopyUnroll; ++u) v[u] = src[i + u * stride];
-#pragma unroll
-    for (int u = 0; u < kCopyUnroll; ++u) dst[i + u * stride] = v[u];
+  for (int u = 0; u < kCopyUnroll; ++u) {
+    const int64_t i = base + (int64_t)u * kCopyThreads;
+    v[u] = i < n ? __builtin_nontemporal_load(src + i) : f4n{0.f, 0.f, 0.f, 0.f};
   }
-  for (; i < n; i += stride) dst[i] = src[i];
+#pragma unroll
+  for (int u = 0; u < kCopyUnroll; ++u) {
+    const int64_t i = base + (int64_t)u * kCopyThreads;
+    if (i < n) __builtin_nontemporal_store(v[u], dst + i);
+  }
 }
 
 }  // namespace
@@ -35,10 +41,10 @@ extern "C" int gine_copy_f4(const void* src, void* dst, int64_t bytes, void* str
   if (!src || !dst || bytes < 0 || bytes % 16 != 0) return GINE_ERR_INVALID;
   const int64_t n = bytes / 16;
   if (n == 0) return GINE_OK;
-  const int64_t want = ceil_div(n, (int64_t)kCopyThreads * kCopyUnroll);
-  const int grid = (int)(want < 8 * kNumCu ? want : 8 * kNumCu);
+  const int64_t grid = ceil_div(n, (int64_t)kCopyThreads * kCopyUnroll);
+  if (grid >= (int64_t(1) << 31)) return GINE_ERR_TOO_LARGE;
   hipLaunchKernelGGL(k_copy_f4, dim3(grid), dim3(kCopyThreads), 0, as_stream(stream),
-                     reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst), n);
+                     reinterpret_cast<const f4n*>(src), reinterpret_cast<f4n*>(dst), n);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }

@@ -60,7 +60,7 @@ class FlatGradReducer:
     """
 
     def __init__(self, params, group=None, flat: torch.Tensor | None = None,
-                 force: bool = False):
+                 force: bool = False, offsets=None):
         self.force = force  # all-reduce even in a 1-rank group (rehearsing the collective)
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
@@ -68,19 +68,27 @@ class FlatGradReducer:
         dev = self.params[0].device
         total = sum(p.numel() for p in self.params)
         self.group = group
+        self._tail_lo = None       # overlap_after: where the early-reduced tail starts
+        self._tail_started = False
+        self._tail_work = None
+        self._side = None
         if flat is not None:  # gradients already live in this buffer (e.g. FlatAdamW's,
-            # whose parameter slices are aligned: it may hold zero gaps between them)
+            # whose parameter slices are aligned: it may hold zero gaps between them;
+            # ``offsets``: each parameter's slice offset, FlatAdamW._offsets)
             if flat.numel() < total:
                 raise ValueError("flat gradient buffer does not match the parameters")
             self.flat = flat
+            self.offsets = list(offsets) if offsets is not None else None
             return
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         off = 0
+        self.offsets = []
         for p in self.params:
             if p.dtype != torch.float32:
                 raise TypeError("FlatGradReducer expects fp32 parameters")
             n = p.numel()
             p.grad = self.flat[off:off + n].view_as(p)
+            self.offsets.append(off)
             off += n
 
     @property
@@ -90,14 +98,92 @@ class FlatGradReducer:
     def zero_(self) -> None:
         self.flat.zero_()
 
-    def all_reduce_(self) -> None:
+    def _collective(self) -> bool:
         if not (dist.is_available() and dist.is_initialized()):
+            return False
+        return dist.get_world_size(self.group) > 1 or self.force
+
+    def all_reduce_(self) -> None:
+        if not self._collective():
             return
         world = dist.get_world_size(self.group)
-        if world == 1 and not self.force:
+        if not self._tail_started:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+            self.flat.div_(world)
             return
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.div_(world)
+        # the tail's collective is in flight (overlap_after): the rest of the buffer now,
+        # then join the tail's stream (or wait for its work object on CPU tensors)
+        self._tail_started = False
+        head = self.flat[:self._tail_lo]
+        dist.all_reduce(head, op=dist.ReduceOp.SUM, group=self.group)
+        head.div_(world)
+        if self._tail_work is not None:
+            self._tail_work.wait()
+            self._tail_work = None
+            self.flat[self._tail_lo:].div_(world)
+        else:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
+
+    # -- overlap of the tail's all-reduce with the rest of the backward --------------------
+    def overlap_after(self, module: torch.nn.Module, tail_params) -> None:
+        """Start the all-reduce of ``tail_params``' gradients -- which must fill the END of
+        the flat buffer, e.g. the GINE stack and the head behind it (models/gnn.py:136-139)
+        -- as soon as autograd has differentiated ``module``'s input (``module`` = the GINE
+        stack: by then the backward has produced every gradient behind it), on a side stream,
+        so that it overlaps the rest of the backward (dense chain, DeepSet).  all_reduce_()
+        then reduces the front of the buffer and joins.  Deferred HIP reductions queued so
+        far are launched first (raincast_gnn.gradbuf.flush), so the tail is final.  Works
+        eagerly and inside HIP-graph capture (RCCL: the tail's collective and the join are
+        captured as a fork of the step graph); on CPU tensors (gloo) the tail's collective
+        is an async work object."""
+        tail = [p for p in tail_params if p.requires_grad]
+        if self.offsets is None:
+            raise ValueError("overlap_after needs the parameters' offsets in the flat buffer")
+        pos = {id(p): off for p, off in zip(self.params, self.offsets)}
+        if any(id(p) not in pos for p in tail):
+            raise ValueError("overlap_after: a tail parameter is not reduced by this reducer")
+        lo = min(pos[id(p)] for p in tail)
+        tail_ids = {id(p) for p in tail}
+        if any(off >= lo and id(p) not in tail_ids for p, off in zip(self.params, self.offsets)):
+            raise ValueError("overlap_after: the tail parameters must fill the end of the "
+                             "flat buffer")
+        self._tail_lo = lo
+        self._tail_params = tail
+        if self.flat.is_cuda and self._side is None:
+            self._side = torch.cuda.Stream(self.flat.device)
+        module.register_forward_pre_hook(self._arm)
+
+    def _arm(self, module, inputs):
+        x = inputs[0] if inputs else None
+        if (isinstance(x, torch.Tensor) and x.requires_grad and torch.is_grad_enabled()
+                and self._collective()):
+            x.register_hook(self._start_tail)
+
+    def _start_tail(self, grad):
+        # every tail gradient must already sit in its slice (adopted flat views); otherwise
+        # the end-of-backward gather copies it in and the whole buffer is reduced then
+        base, flat = self.flat.data_ptr(), self.flat
+        for p in self._tail_params:
+            g = p.grad
+            if g is None or not (base <= g.data_ptr() < base + 4 * flat.numel()):
+                return None
+        from . import gradbuf
+        gradbuf.flush()  # the deferred reductions of the tail (their kernels precede ours)
+        tail = flat[self._tail_lo:]
+        world = dist.get_world_size(self.group)
+        if flat.is_cuda:
+            cur = torch.cuda.current_stream(flat.device)
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                dist.all_reduce(tail, op=dist.ReduceOp.SUM, group=self.group)
+                tail.div_(world)
+            # (the backward keeps writing the front of the buffer on ``cur`` meanwhile; the
+            # flat buffer outlives the step, so no allocator bookkeeping is needed)
+        else:
+            self._tail_work = dist.all_reduce(tail, op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True)
+        self._tail_started = True
+        return None
 
     def check_views(self) -> bool:
         """True while every .grad still aliases the flat buffer (nobody replaced it)."""

@@ -105,6 +105,13 @@ class StepRunner:
             raise ValueError(f"allreduce={allreduce!r}: expected 'split' or 'graph'")
         self.model, self.opt, self.reducer = model, optimizer, reducer
         self.graphed, self.warmup, self.allreduce = graphed, warmup, allreduce
+        if (reducer is not None and allreduce == "graph" and dist.is_initialized()
+                and dist.get_backend() == "nccl" and reducer.offsets is not None
+                and hasattr(model, "conv") and hasattr(model, "aggr")):
+            # the GINE stack's and the head's gradients reduced on a side stream under the
+            # rest of the backward (distributed.FlatGradReducer.overlap_after)
+            reducer.overlap_after(model.conv, list(model.conv.parameters())
+                                  + list(model.aggr.parameters()))
         self._seen: dict[int, int] = {}
         self._graphs: dict[int, tuple] = {}
 
@@ -326,7 +333,8 @@ def main(argv=None) -> dict:
     model = gnn_from_params(config, in_channels=samples[0].x.size(1)).to(device)
     broadcast_parameters(model)
     opt = FlatAdamW(model.parameters(), lr=config["lr"])
-    reducer = FlatGradReducer(model.parameters(), flat=opt.flat_grad) if world > 1 else None
+    reducer = (FlatGradReducer(model.parameters(), flat=opt.flat_grad, offsets=opt._offsets)
+               if world > 1 else None)
     runner = StepRunner(model, opt, graphed=not args.eager, reducer=reducer,
                         allreduce=args.allreduce)
     out = fit(model, opt, train_loader, val_loader, device,

@@ -86,3 +86,66 @@ def test_shard_range_covers_batch():
             assert got[0][0] == 0 and got[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
             assert max(h - l for l, h in got) - min(h - l for l, h in got) <= 1
+
+
+def _overlap_worker(rank, world, port, result_dir):
+    """The overlapped form: the GINE stack's and the head's gradients (the tail of the flat
+    buffer) are all-reduced as soon as autograd has differentiated the stack's input, while
+    the backward of the dense front continues; all_reduce_() reduces the front and joins."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import gine_cpu as O
+    from raincast_gnn.data import collate, synthetic_samples
+    torch.manual_seed(100 + rank)
+    model = O.OracleGNN(35, 32, 2, "MixedLoss", "False", 1.71, 0.5)
+    broadcast_parameters(model)
+    samples = synthetic_samples(40, 6, k=5, seed=11)
+    lo, hi = shard_range(len(samples), rank, world)
+    batch = collate(samples[lo:hi])
+    red = FlatGradReducer(model.parameters())
+    tail = list(model.conv.parameters()) + list(model.aggr.parameters())
+    red.overlap_after(model.conv, tail)
+    fired = []
+    model.conv.register_forward_pre_hook(lambda m, i: fired.append(i[0].requires_grad))
+    outs = []
+    for _ in range(2):                     # two steps: the hook re-arms every forward
+        red.zero_()
+        loss = model.crps(model(batch), batch.y)
+        loss.backward()
+        started = red._tail_started
+        red.all_reduce_()
+        assert not red._tail_started
+        outs.append((started, red.flat.clone()))
+    # a plain (non-overlapped) reduction of the same step for comparison
+    red2 = FlatGradReducer(model.parameters())
+    red2.zero_()
+    model.crps(model(batch), batch.y).backward()
+    red2.all_reduce_()
+    torch.save({"outs": outs, "plain": red2.flat.clone(), "fired": fired},
+               os.path.join(result_dir, f"ov{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_overlapped_tail_allreduce_equals_plain(tmp_path):
+    world = 2
+    mp.spawn(_overlap_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+             join=True)
+    res = [torch.load(tmp_path / f"ov{r}.pt", weights_only=True) for r in range(world)]
+    for r in res:
+        for started, flat in r["outs"]:
+            assert started, "the tail's collective must start inside the backward"
+            assert torch.equal(flat, r["plain"])   # same sums, same division
+        assert all(r["fired"])
+    assert torch.equal(res[0]["plain"], res[1]["plain"])
+
+
+def test_overlap_after_rejects_a_tail_that_is_not_the_end():
+    from oracle import gine_cpu as O
+    model = O.OracleGNN(35, 16, 2, "MixedLoss", "False", 1.71, 0.5)
+    red = FlatGradReducer(model.parameters())
+    with pytest.raises(ValueError, match="end of the flat buffer"):
+        red.overlap_after(model.conv, list(model.conv.parameters()))   # aggr follows it
+    red.overlap_after(model.conv, list(model.conv.parameters()) + list(model.aggr.parameters()))

@@ -113,13 +113,16 @@ def _free_port():
     return port
 
 
-def _dp_worker(rank, world, port, out_dir):
+def _dp_worker(rank, world, port, out_dir, overlap=False):
     import torch.distributed as dist
     from raincast_gnn.data import collate
     from raincast_gnn.distributed import FlatGradReducer, broadcast_parameters, shard_range
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    from raincast_gnn.distributed import note_device_sharing
+    assert note_device_sharing()   # both ranks on cuda:0: the grid-barrier layer stays off
     params = dict(EXPERIMENTS["24h_mixed"])
     torch.manual_seed(100 + rank)               # different init per rank: broadcast fixes it
     model = gnn_from_params(params).to(dev).train()
@@ -129,14 +132,18 @@ def _dp_worker(rank, world, port, out_dir):
     lo, hi = shard_range(len(samples), rank, world)
     batch = collate(samples[lo:hi]).to(dev)
     opt = FlatAdamW(model.parameters(), lr=params["lr"])
-    red = FlatGradReducer(model.parameters(), flat=opt.flat_grad)
+    red = FlatGradReducer(model.parameters(), flat=opt.flat_grad, offsets=opt._offsets)
+    if overlap:  # the GINE stack's + head's tail reduced from inside the backward
+        red.overlap_after(model.conv, list(model.conv.parameters())
+                          + list(model.aggr.parameters()))
     runner = T.StepRunner(model, opt, graphed=False, reducer=red)
     runner._fwd_bwd(batch)
+    assert red._tail_started == overlap
     red.all_reduce_()
     torch.cuda.synchronize()
     torch.save({"flat": opt.flat_grad.cpu(), "start": start, "offsets": list(opt._offsets),
                 "names": [n for n, _ in model.named_parameters()]},
-               os.path.join(out_dir, f"rank{rank}.pt"))
+               os.path.join(out_dir, f"rank{rank}{'_ov' if overlap else ''}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -183,3 +190,18 @@ def test_engine_data_parallel_gradient_is_mean_of_shards(tmp_path):
     for shp, foff in zip(shapes, res[0]["offsets"]):
         covered[foff:foff + int(torch.Size(shp).numel())] = True
     assert not res[0]["flat"][~covered].any()  # the alignment gaps hold no gradient
+
+
+@pytest.mark.timeout(300)
+def test_engine_data_parallel_overlapped_tail_same_bits(tmp_path):
+    """The overlapped reduction (distributed.FlatGradReducer.overlap_after: the deferred GINE
+    and head reductions launched from inside the backward, their tail of the flat buffer
+    reduced on a side stream) gives the same bits as the plain one, 2 gloo ranks."""
+    world = 2
+    for ov in (False, True):
+        mp.spawn(_dp_worker, args=(world, _free_port(), str(tmp_path), ov), nprocs=world,
+                 join=True)
+    for r in range(world):
+        a = torch.load(tmp_path / f"rank{r}.pt", weights_only=True)["flat"]
+        b = torch.load(tmp_path / f"rank{r}_ov.pt", weights_only=True)["flat"]
+        assert torch.equal(a, b)
