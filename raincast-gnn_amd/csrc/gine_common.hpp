@@ -16,6 +16,19 @@
     if (gine_e_ != hipSuccess) return GINE_ERR_HIP_BASE + (int)gine_e_; \
   } while (0)
 
+// Every kernel of the library is compiled without the packed-FP32 VALU instructions
+// (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32; Makefile: -target-feature -packed-fp32-ops,
+// so the compiler emits two-lane VOP3 ops instead).  Measured on MI355X (DESIGN.md 4,
+// profiles/r05_s01-s03): in the combined window backward, the low halves of the
+// message-passing waves' packed-FP32 results came out wrong and varied from run to run (even
+// float columns of dx, ~100 of 16,000 rows) whenever the co-resident engine workgroups ran
+// v_mfma_f32_32x32x16_bf16 -- with the message-passing code byte-identical, and correct with
+// the fp32 MFMA, without the bf16 MFMAs (at 120 and at 128 VGPRs) and without packed FP32.
+// The unpacked form is also as fast or faster here (gather backward at cfg5 87-90 -> 77-79
+// us; window backward 13.1 -> 12.3 us at cfg2).  (A `target("no-packed-fp32-ops")` function
+// attribute does the same per kernel, but measured 176 instead of 12 bytes of spill in the
+// combined window backward, so the switch is the command-line feature.)
+
 #define GINE_LAUNCH_STATUS() \
   do {                                                            \
     hipError_t gine_e_ = hipGetLastError();                       \

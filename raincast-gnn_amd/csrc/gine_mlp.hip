@@ -1009,15 +1009,19 @@ __global__ __launch_bounds__(256) void k_bwd1_wgrad(const float* __restrict__ w1
                                                     int chunks, int rows_per_chunk,
                                                     size_t zstride, size_t cstride,
                                                     float* __restrict__ slab, int eng_blocks) {
-  __shared__ __attribute__((aligned(16))) float sP[kWgRows * (kMlpWgTO + 4)];
-  __shared__ __attribute__((aligned(16))) float sQ[kWgRows * kWgLdQ];
+  // one region: the engine's operand images (fp32 tiles or split planes, wg_lds_bytes),
+  // or the row GEMM's A tile in its sQ part
+  __shared__ __attribute__((aligned(16))) float s_eng[wg_lds_bytes<kMlpWgTO>() / sizeof(float)];
+  float* sP = s_eng;
+  float* sQ = s_eng + kWgRows * (kMlpWgTO + 4);
   const int b = blockIdx.x;
   if (b < eng_blocks) {
     // the output tiles of one row chunk run back to back on ONE XCD: they read the same
     // rows (a1 by all four, z by the two dW1 tiles), which that XCD's L2 then serves
     const int lb = xcd_remap(b, eng_blocks), tiles = eng_blocks / chunks;
-    wgrad_block<MlpWgradSrc<PDO>, kMlpWgTO, 4, false>(src, N, 128, 128, lb / tiles, lb % tiles,
-                                         rows_per_chunk, zstride, cstride, slab, sP, sQ);
+    wgrad_block<MlpWgradSrc<PDO>, kMlpWgTO, 4, kMlpEngX3>(src, N, 128, 128, lb / tiles,
+                                                          lb % tiles, rows_per_chunk, zstride,
+                                                          cstride, slab, sP, sQ);
   } else {
     static_assert(kRowTile * (128 + 4) <= kWgRows * kWgLdQ, "row tile fits in sQ");
     rowgemm_body<128, PRO_DA1, EPI_PLAIN, false>(w1, pa, ea, N, num_tiles, sQ,
@@ -1307,15 +1311,15 @@ extern "C" int gine_mlp_wgrad(const float* dy, const float* y, const uint8_t* ma
   int st;
   if (epilogue == GINE_EPI_NONE) {
     const MlpWgradSrc<PRO_PLAIN> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<kMlpWgTO, MlpWgradSrc<PRO_PLAIN>, false>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
+    st = launch_wgrad_engine<kMlpWgTO, MlpWgradSrc<PRO_PLAIN>, kMlpEngX3>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
                                        per * p.chunks, per, slab, s);
   } else if (epilogue == GINE_EPI_RELU) {
     const MlpWgradSrc<PRO_DOR> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<kMlpWgTO, MlpWgradSrc<PRO_DOR>, false>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
+    st = launch_wgrad_engine<kMlpWgTO, MlpWgradSrc<PRO_DOR>, kMlpEngX3>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
                                        per * p.chunks, per, slab, s);
   } else {
     const MlpWgradSrc<PRO_DOM> src{p_do, q_r, p_da1, q_z, D};
-    st = launch_wgrad_engine<kMlpWgTO, MlpWgradSrc<PRO_DOM>, false>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
+    st = launch_wgrad_engine<kMlpWgTO, MlpWgradSrc<PRO_DOM>, kMlpEngX3>(src, num_nodes, D, D, 2 * p.tiles_o * p.tiles_i, p,
                                        per * p.chunks, per, slab, s);
   }
   if (st != GINE_OK) return st;

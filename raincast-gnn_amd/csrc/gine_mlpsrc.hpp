@@ -170,6 +170,14 @@ __device__ __forceinline__ float4 transform(const ProArgs& p, const RawItem& r,
 #define GINE_MLP_WG_TO 64
 #endif
 constexpr int kMlpWgTO = GINE_MLP_WG_TO;
+// The node-MLP weight-gradient engines -- stand-alone (gine_mlp_wgrad), beside the dz GEMM
+// (gine_mlp_bwd1_wgrad) and inside the window backward (gine_mp_bwd_win_mlp_wgrad) -- all run
+// the split-bf16 chain (gine_wgrad.hpp wgrad_body_x3), so the three give the same bits
+// (tests/test_gpu_fuzz.py, test_gpu_training.py).  0: the fp32 chain everywhere (A/B builds).
+#ifndef GINE_MLP_ENG_X3
+#define GINE_MLP_ENG_X3 1
+#endif
+constexpr bool kMlpEngX3 = GINE_MLP_ENG_X3 != 0;
 
 template <int PDO>  // PRO_PLAIN | PRO_DOR | PRO_DOM: how do is formed from dy
 struct MlpWgradSrc {

@@ -241,20 +241,19 @@ struct WinEngine {
   int nblocks, tiles, rows_per_chunk;
   int D;  // node-MLP width (64 or 128): the engine's O = I
 };
-// The engine in this launch runs the fp32 chain (wgrad_body), not the split one the
-// stand-alone engines use: with the split chain the launch needs 132 registers, i.e. one
-// workgroup per CU, and measured 30.3 against 26.8 us per launch (profiles/r04_s13); capped to
-// 128 registers for two workgroups per CU, its message-passing half came out wrong and varied
-// from run to run (even float columns of dx; tools/determinism_layer.py --flat, r04_s09 /
-// r04_s11) with no spill and no state shared between the roles -- not diagnosed further.
-#ifndef GINE_WIN_ENG_X3
-#define GINE_WIN_ENG_X3 0
-#endif
+// The engine in this launch runs the split-bf16 chain, as the stand-alone node-MLP engines do
+// (kMlpEngX3: the same bits), at two workgroups per CU (128 registers).  Round 4 found this
+// build's message-passing half wrong and varying from run to run (even float columns of dx);
+// round 5 traced it to the packed-FP32 VALU instructions of the message-passing waves beside
+// the engine's v_mfma_f32_32x32x16_bf16 waves (gine_common.hpp __global__):
+// every kernel is now compiled without packed FP32, and the split chain here is bit-exact
+// run after run (tools/determinism_layer.py --flat, tests/test_gpu_layer.py).  Measured
+// 26.5-27.0 -> 24.1-24.2 us per launch at cfg2 (profiles/r05_s05).
 #ifndef GINE_WIN_ENG_LDS  // (experiments: a larger floor limits workgroups per CU)
 #define GINE_WIN_ENG_LDS 0
 #endif
 constexpr size_t kWinEngineLdsNeed =
-    GINE_WIN_ENG_X3 ? wg_lds_bytes<64>() : sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
+    kMlpEngX3 ? wg_lds_bytes<64>() : sizeof(float) * kWgRows * ((64 + 4) + kWgLdQ);
 constexpr size_t kWinEngineLds =
     kWinEngineLdsNeed > GINE_WIN_ENG_LDS ? kWinEngineLdsNeed : GINE_WIN_ENG_LDS;
 
@@ -322,29 +321,10 @@ __global__ __launch_bounds__(kWinThreads, ENG ? GINE_WIN_ENG_OCC : 2) void k_mp_
       float* sP = reinterpret_cast<float*>(s_dyn);
       float* sQ = sP + kWgRows * (64 + 4);
       const int e = xcd_remap(blockIdx.x, eng.nblocks);
-#ifdef GINE_WIN_VGPR128
-      // probe build only: the engine path touches v127, so the launch allocates 128 VGPRs
-      // per wave (four waves per SIMD fill the register file) whatever the engine's chain
-      asm volatile("v_mov_b32 v127, 0" ::: "v127");
-#endif
-      wgrad_block<MlpWgradSrc<PDO>, 64, 8, GINE_WIN_ENG_X3 != 0>(eng.src, eng.N, eng.D, eng.D,
-                                                                 e / eng.tiles,
-                                           e % eng.tiles, eng.rows_per_chunk, eng.zstride,
-                                           eng.cstride, eng.slab, sP, sQ);
-#ifdef GINE_WIN_LDS_TOUCH_LO
-      // probe build only: keep writing a sentinel into bytes [LO, HI) of this workgroup's own
-      // dynamic LDS for a while (does it reach a co-resident workgroup's allocation?)
-      {
-        float4* pt = reinterpret_cast<float4*>(reinterpret_cast<char*>(s_dyn) +
-                                               GINE_WIN_LDS_TOUCH_LO);
-        constexpr int n = (GINE_WIN_LDS_TOUCH_HI - GINE_WIN_LDS_TOUCH_LO) / 16;
-        for (int it = 0; it < 4000; ++it) {
-          for (int i = threadIdx.x; i < n; i += kWinThreads)
-            pt[i] = make_float4(3.0e38f, 3.0e38f, 3.0e38f, 3.0e38f);
-          asm volatile("s_sleep 1" ::: "memory");
-        }
-      }
-#endif
+      wgrad_block<MlpWgradSrc<PDO>, 64, 8, kMlpEngX3>(eng.src, eng.N, eng.D, eng.D,
+                                                      e / eng.tiles, e % eng.tiles,
+                                                      eng.rows_per_chunk, eng.zstride,
+                                                      eng.cstride, eng.slab, sP, sQ);
       return;
     }
     eb = eng.nblocks;

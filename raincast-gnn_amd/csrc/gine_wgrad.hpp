@@ -362,7 +362,6 @@ __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, 
   using Raw = typename Src::Raw;
   using Col = typename Src::Col;
   using IP = WgImg<TO>;
-  using IQ = WgImg<kWgTI>;
   char* imgP = reinterpret_cast<char*>(sP);  // sP.. is one region (wg_lds_bytes)
   char* imgQ = imgP + IP::kBytes;
   constexpr int NT = 64 * NW;
@@ -463,16 +462,7 @@ __device__ __forceinline__ void wgrad_body_x3(const Src& src, int64_t R, int O, 
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int k = 0; k < NI; ++k) {
-#ifdef GINE_WG_X3_NOMFMA  // probe build only: the fragments consumed by VALU, no MFMA
-          typedef uint32_t u32x4p __attribute__((ext_vector_type(4)));
-          const u32x4p u = __builtin_bit_cast(u32x4p, fa[j].h) ^ __builtin_bit_cast(u32x4p, fb[k].h) ^
-                           __builtin_bit_cast(u32x4p, fa[j].m) ^ __builtin_bit_cast(u32x4p, fb[k].l);
-          acc[j][k][0] += __builtin_bit_cast(float, (u[0] ^ u[1] ^ u[2] ^ u[3]) & 0x3f7fffffu);
-#else
-          acc[j][k] = mfma_bf16x3(fa[j], fb[k], acc[j][k]);
-#endif
-        }
+        for (int k = 0; k < NI; ++k) acc[j][k] = mfma_bf16x3(fa[j], fb[k], acc[j][k]);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();

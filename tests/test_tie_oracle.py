@@ -37,7 +37,8 @@ def test_fp32_oracle_within_tol_of_its_branch_oracle(graphs):
     r64 = _oracle_step(ref, batch, torch.float64)[0]
     rb = _oracle_step(ref, batch, torch.float64, record=True, hooks=ties.hooks)[0]
     grads = {n: p.grad for n, p in r32.named_parameters()}
-    worst, table, fails = branch_grad_table(grads, rb, r32, r64, TOL)
+    # (the plain bound is the HIP engine's; this "engine" is the fp32 CPU oracle itself)
+    worst, table, fails = branch_grad_table(grads, rb, r32, r64, TOL, plain_tol=None)
     print(table)
     print(ties.table())
     assert not fails, table

@@ -25,7 +25,8 @@ run() {  # run <name> <seconds> cmd...
 
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 660 python -u -m pytest tests -m gpu -q -rf --durations=15 --timeout 120 --timeout-method thread ;;
+    tests) GINE_PARITY_REPORT=$OUT/parity run pytest_gpu 660 python -u -m pytest tests -m gpu -q -rf --durations=15 --timeout 200 --timeout-method thread ;;
+    det)   run determinism_layer 200 python tools/determinism_layer.py --flat ;;
     ntests) run pytest_new 300 python -u -m pytest ${NTESTS:-tests/test_gpu_dropin.py} -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     btests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/bounds/libgine_hip.so \
             run pytest_bounds 300 python -u -m pytest tests/test_gpu_bnacc.py tests/test_gpu_deepset.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
@@ -54,6 +55,25 @@ for s in $STEPS; do
                "$OUT"/pmc_write_$P/run_counter_collection.csv --config $P \
                --tree-hash "$(python -c 'import bench; print(bench.source_tree_hash())')" \
                --traffic-json "$OUT/${P}_pmc_traffic.json" > "$OUT/${P}_pmc_summary.txt" 2>&1 ;;
+    libtests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/${LIBVAR}/libgine_hip.so \
+            run pytest_${LIBVAR} 660 python -u -m pytest tests -m gpu -q -rf --timeout 200 --timeout-method thread ;;
+    overlap1)  # world-1 RCCL rehearsal: the captured step with the overlapped tail all-reduce
+           # against the split form -- the same final loss bits (an all-reduce over one rank
+           # is exact) and both lines' timings
+           for m in graph split; do
+             run rccl1_$m 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                 --master-addr 127.0.0.1 --master-port $((29500 + RANDOM % 1000)) bench.py --gpus 1 \
+                 --force-allreduce --allreduce $m --no-cpu --no-strong --steps 30 --kernel-reps 5
+           done
+           python - "$OUT" <<'PY' | tee -a "$OUT/session.log"
+import json, sys
+o = sys.argv[1]
+d = {m: json.loads([l for l in open(f"{o}/rccl1_{m}.log") if l.startswith("{")][-1]) for m in ("graph", "split")}
+for m, v in d.items():
+    print(m, v["ms_per_step"], v["config"].get("allreduce_in_graph"), v["config"].get("allreduce_overlap"), v["final_loss"])
+print("same final loss bits:", d["graph"]["final_loss"] == d["split"]["final_loss"])
+PY
+           ;;
     dist2) run bench_dist2_gloo 600 python bench.py --gpus 2 --dist-backend gloo --steps 10 \
                --warmup 3 --no-cpu ;;
     rgprof) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/rgprof/libgine_hip.so run rg_prof 300 python tools/rg_prof.py ;;
