@@ -3,9 +3,12 @@
 //
 // The same launches as raincast_gnn/functional.py's GineLayer (forward: the one-launch layer,
 // the fused gather + Linear1 or the unfused pair, BatchNorm sums through the fixed-point
-// accumulator or fp64 partials; backward: the non-deferred form -- dbn GEMM, BatchNorm
-// backward finish, dz GEMM beside the node-MLP weight-gradient engine, message-passing
-// backward reducing that slab in the same launch, then its own finish), issued from a C++
+// accumulator or fp64 partials; backward, the non-deferred form: where a 32-channel window
+// plan exists, dbn GEMM + BatchNorm sums and BatchNorm finish + dz GEMM (accumulator pair),
+// the window message passing with the node-MLP weight-gradient engine in one launch, and
+// one batch launch for the engine's slab and the message passing's partials; otherwise dbn
+// GEMM, BatchNorm backward finish, dz GEMM beside the engine, message-passing backward
+// reducing that slab in the same launch, then its own finish), issued from a C++
 // torch::autograd::Function: one Python call per layer forward and none in backward, where
 // the Python Function spends ~50 us and ~190 us of host time per layer on argument
 // marshalling, allocations and per-launch ctypes calls (profiles/r04_s02_dropin_prof.txt).
@@ -50,6 +53,7 @@ enum IntOpt {
   kFused,          // gine_mp_fwd_mlp1 applies
   kLayer,          // gine_mp_fwd_layer applies
   kMaxInDegree,
+  kEngine,         // gine_mp_bwd_win_mlp_wgrad applies (functional.engine_in_mp_ok)
   // the window plans' scalars, kPlanFields each: num_tiles (0: no plan), slice_channels,
   // max_rows, max_edges, max_nodes -- the plan's device arrays come in the graph list, so the
   // autograd node holds them (a plan's addresses alone would dangle once the graph cache
@@ -124,7 +128,8 @@ struct ZeroOnError {  // csrc/gine_bnacc.hpp pairing: re-zero the accumulator if
 class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
  public:
   // graph: in_rowptr, in_src, in_attr, out_rowptr, out_dst, out_attr, the two plans' arrays
-  // bn: running_mean, running_var, num_batches_tracked, accumulator (undefined: partials)
+  // bn: running_mean, running_var, num_batches_tracked, accumulator, backward accumulator
+  // (undefined: partials)
   static Tensor forward(AutogradContext* ctx, Tensor x, Tensor lin_w, Tensor lin_b, Tensor eps,
                         Tensor w1, Tensor b1, Tensor gamma, Tensor beta, Tensor w2, Tensor b2,
                         std::vector<Tensor> graph, std::vector<Tensor> bn,
@@ -244,7 +249,7 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
     const Tensor* po = graph.data() + kGraphCsr + kPlanArrays;  // the backward's plan arrays
     ctx->save_for_backward({x, z, a1, epi == GINE_EPI_RELU ? y : Tensor(), mask, bn_save, lw,
                             lb, ep, w1c, w2c, g, graph[kOutRowptr], graph[kOutDst],
-                            graph[kOutAttr], po[0], po[1], po[2], po[3], po[4]});
+                            graph[kOutAttr], po[0], po[1], po[2], po[3], po[4], bn[4]});
     ctx->saved_data["io"] = io;
     ctx->saved_data["beta"] = beta.defined();
     ctx->saved_data["lin_w_shape"] = lin_w.sizes().vec();
@@ -291,6 +296,76 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
                                        {{Pn, 2, D}, torch::kFloat64, true},
                                        {{P2, 3, D}, torch::kFloat64, true}});
     Tensor dbn = sc[0], coef = sc[1], dz = sc[2], slab = sc[3], partials = sc[4], part2 = sc[5];
+    Tensor dres = epi == GINE_EPI_RESIDUAL_RELU ? dy : Tensor();
+    Tensor dx = torch::empty_like(x);
+    const int32_t flags = GINE_MP_BWD_SELF | lin_flag;
+    if (plan_out && io[kEngine]) {
+      const Tensor& bacc = sv[20];  // the BatchNorm-backward accumulator (undefined: partials)
+      if (bacc.defined()) {
+        ZeroOnError guard{bacc};
+        ok(gine_mlp_bwd2_acc((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
+                             (const float*)P(a1), (const float*)P(bn_save), (const float*)P(w2c),
+                             (float*)P(dbn), nullptr, (int64_t*)P(bacc), N, D, epi, s),
+           "gine_mlp_bwd2_acc");
+        ok(gine_mlp_bwd1_bn((const float*)P(dbn), (const float*)P(a1), (const float*)P(bn_save),
+                            (int64_t*)P(bacc), (const float*)P(g), (float*)P(dgamma),
+                            (float*)P(dbeta), (float*)P(coef), (const float*)P(w1c),
+                            (float*)P(dz), N, D, s),
+           "gine_mlp_bwd1_bn");
+        guard.armed = false;
+      } else {
+        ok(gine_mlp_bwd2((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
+                         (const float*)P(a1), (const float*)P(bn_save), (const float*)P(w2c),
+                         (float*)P(dbn), (double*)P(partials), N, D, epi, s),
+           "gine_mlp_bwd2");
+        ok(gine_bn_bwd_finalize((const double*)P(partials), Pn, (const float*)P(g),
+                                (const float*)P(bn_save), (float*)P(dgamma), (float*)P(dbeta),
+                                (float*)P(coef), N, D, io[kBatchStats] ? 1 : 0, s),
+           "gine_bn_bwd_finalize");
+        ok(gine_mlp_bwd1((const float*)P(dbn), (const float*)P(a1), (const float*)P(bn_save),
+                         (const float*)P(coef), (const float*)P(w1c), (float*)P(dz), N, D, s),
+           "gine_mlp_bwd1");
+      }
+      // message passing + the dW1 / dW2 engine in one launch, then both reductions in one
+      ok(gine_mp_bwd_win_mlp_wgrad((const float*)P(dz), (const float*)P(x),
+                                   (const int32_t*)P(out_rowptr), (const int32_t*)P(out_dst),
+                                   (const float*)P(out_attr), (const float*)P(lw),
+                                   (const float*)P(lb), (const float*)P(ep), (const float*)P(dres),
+                                   (float*)P(dx), (double*)P(part2), N, D, flags, plan_out,
+                                   (const float*)P(dy), (const float*)P(y),
+                                   (const uint8_t*)P(mask), (const float*)P(a1),
+                                   (const float*)P(bn_save), (const float*)P(dbn),
+                                   (const float*)P(coef), (const float*)P(z), (float*)P(slab), epi,
+                                   s),
+         "gine_mp_bwd_win_mlp_wgrad");
+      gine_grad_job jobs[2] = {};
+      const int64_t per = (int64_t)D * D + D;
+      jobs[0].kind = GINE_GRAD_JOB_SLAB;  // [dW2 | db2], [dW1 | db1] (MlpWgradOut order)
+      jobs[0].src = P(slab);
+      jobs[0].rows = C;
+      jobs[0].nz = 2;
+      jobs[0].cstride = per;
+      jobs[0].zstride = per * C;
+      float* wz[2][2] = {{(float*)P(dw2), (float*)P(db2)}, {(float*)P(dw1), (float*)P(db1)}};
+      for (int zi = 0; zi < 2; ++zi) {
+        jobs[0].per[zi] = per;
+        jobs[0].wsize[zi] = (int64_t)D * D;
+        jobs[0].bscale[zi] = 1.f;
+        jobs[0].w[zi] = wz[zi][0];
+        jobs[0].b[zi] = wz[zi][1];
+      }
+      jobs[1].kind = GINE_GRAD_JOB_MP;   // dW_e, db_e, eps from the window partials
+      jobs[1].src = P(part2);
+      jobs[1].rows = P2;
+      jobs[1].channels = D;
+      jobs[1].eps_cols = D / plan_out->slice_channels;
+      jobs[1].w[0] = (float*)P(dlw);
+      jobs[1].w[1] = (float*)P(dlb);
+      jobs[1].w[2] = (float*)P(deps);
+      ok(gine_grad_finalize_batch(jobs, 2, s), "gine_grad_finalize_batch");
+      return {dx,    dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1,      db1,     dgamma,
+              dbeta, dw2,                   db2, Tensor(),          Tensor(), Tensor(), Tensor()};
+    }
     ok(gine_mlp_bwd2((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
                      (const float*)P(a1), (const float*)P(bn_save), (const float*)P(w2c),
                      (float*)P(dbn), (double*)P(partials), N, D, epi, s),
@@ -307,9 +382,6 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
                            N, D, epi, s),
        "gine_mlp_bwd1_wgrad");
     // message-passing backward; its extra workgroups reduce the slab
-    Tensor dres = epi == GINE_EPI_RESIDUAL_RELU ? dy : Tensor();
-    Tensor dx = torch::empty_like(x);
-    const int32_t flags = GINE_MP_BWD_SELF | lin_flag;
     if (plan_out) {
       ok(gine_mp_bwd_win_side((const float*)P(dz), (const float*)P(x),
                               (const int32_t*)P(out_rowptr), (const int32_t*)P(out_dst),
@@ -353,7 +425,8 @@ Tensor gine_layer(Tensor x, Tensor lin_w, Tensor lin_b, Tensor eps, Tensor w1, T
   TORCH_CHECK(graph.size() == kGraphArgs, "graph: in_rowptr, in_src, in_attr, out_rowptr, "
               "out_dst, out_attr, then the in and out window plans' tile_begin, win_lo, "
               "win_rows, slot, edge_begin");
-  TORCH_CHECK(bn.size() == 4, "bn: running_mean, running_var, num_batches_tracked, acc");
+  TORCH_CHECK(bn.size() == 5, "bn: running_mean, running_var, num_batches_tracked, acc, "
+              "backward acc");
   TORCH_CHECK(io.size() == kIntOpts && fo.size() == kFloatOpts, "option vectors");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.dim() == 2,
               "x: fp32 [N, D] on a HIP device");

@@ -116,14 +116,16 @@ def mp_forward(x, graph, lin_w, lin_b, eps, lin_flag=None):
 
 
 def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_flag=None,
-                params=(None, None, None), side=None, engine=None):
+                params=(None, None, None), side=None, engine=None, jobs=None):
     """Returns (dx, dlin_w, dlin_b, deps); ``params`` = the (lin.weight, lin.bias, eps)
     Parameters, whose gradients then go straight to their flat-buffer slices if any.
     ``side`` = (slab, chunks, D, dw1, db1, dw2, db2): a node-MLP weight-gradient slab left
     by gine_mlp_bwd1_wgrad, reduced by extra workgroups of the same launch.
     ``engine`` = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epilogue): the node-MLP
     weight-gradient engine run by extra workgroups of the window launch (the caller checked
-    engine_in_mp_ok)."""
+    engine_in_mp_ok).  ``jobs``: a list the window form's finish job is appended to (the
+    caller launches it with its own in one gine_grad_finalize_batch) instead of its own
+    finish launch, when the reduction is not deferred to the end of the backward."""
     N, D = x.shape
     dev = x.device
     dx = torch.empty_like(x)
@@ -157,6 +159,9 @@ def mp_backward(dz, x, graph, lin_w, lin_b, eps, dres=None, self_term=True, lin_
         if gradbuf.deferrable(dlw, dlb, deps):  # in the end-of-backward batch
             gradbuf.defer(gradbuf.mp_job(partials, P, D, D // plan.slice_channels, dlw, dlb,
                                          deps), dev, (partials,))
+        elif jobs is not None:  # in the caller's batch (it keeps ``partials`` alive)
+            jobs.append((gradbuf.mp_job(partials, P, D, D // plan.slice_channels, dlw, dlb,
+                                        deps), partials))
         else:
             call("gine_mp_bwd_win_finalize", ptr(partials), P, D, plan.slice_channels,
                  ptr(dlw), ptr(dlb), ptr(deps), stream)
@@ -446,7 +451,10 @@ class GineLayer(torch.autograd.Function):
         dw1, db1 = grad_out(p_w1, (D, D), dev), grad_out(p_b1, (D,), dev)
         dw2, db2 = grad_out(p_w2, (D, D), dev), grad_out(p_b2, (D,), dev)
         deferrable = gradbuf.deferrable(dw1, db1, dw2, db2)
-        use_engine = deferrable and engine_in_mp_ok(ctx.graph, D)
+        # the node-MLP weight-gradient engine inside the window backward launch wherever a
+        # 32-channel plan exists: its slab joins the end-of-backward batch (deferred), or
+        # this layer's own batch launch with the message passing's finish (drop-in path)
+        use_engine = engine_in_mp_ok(ctx.graph, D)
         # BatchNorm backward sums as fixed-point atomics, finished in the dz GEMM
         acc = ctx.bn_acc_bwd if use_engine else None
 
@@ -483,9 +491,10 @@ class GineLayer(torch.autograd.Function):
                  ptr(dbn), ptr(coef), ptr(z), ptr(w1c), ptr(dz), ptr(slab), None, None, None,
                  None, N, D, epi, stream)
         dres = dy if epi == EPI_RESIDUAL_RELU else None
-        if deferrable:
-            # only the optimizer reads dW1/db1/dW2/db2: the slab joins the end-of-backward
-            # batch, off the critical path of the message-passing backward
+        jobs = None
+        if deferrable or use_engine:
+            # only the optimizer reads dW1/db1/dW2/db2: the slab is reduced by a batch launch
+            # (the end-of-backward one when deferrable), off the message passing's path
             per = D * D + D
             job = _lib.GradJob()
             job.kind, job.src, job.rows, job.nz = _lib.GRAD_JOB_SLAB, slab.data_ptr(), C, 2
@@ -493,12 +502,19 @@ class GineLayer(torch.autograd.Function):
             for zi, (wg, bg) in enumerate(((dw2, db2), (dw1, db1))):  # MlpWgradOut order
                 job.per[zi], job.wsize[zi], job.bscale[zi] = per, D * D, 1.0
                 job.w[zi], job.b[zi] = wg.data_ptr(), bg.data_ptr()
-            gradbuf.defer(job, dev, (slab,))
+            if deferrable:
+                gradbuf.defer(job, dev, (slab,))
+            else:
+                jobs = [(job, slab)]
             side = None
         else:  # reduced by extra workgroups of the message-passing backward launch
             side = (slab, C, D, dw1, db1, dw2, db2)
         dx, dlw, dlb, deps = mp_backward(dz, x, ctx.graph, lw, lb, ep, dres=dres,
-                                         params=(p_lw, p_lb, p_eps), side=side, engine=engine)
+                                         params=(p_lw, p_lb, p_eps), side=side, engine=engine,
+                                         jobs=jobs)
+        if jobs:  # this layer's slab and message-passing finish in one launch
+            arr = (_lib.GradJob * len(jobs))(*[j for j, _ in jobs])
+            call("gine_grad_finalize_batch", arr, len(jobs), stream)
         lin_w_shape, affine = ctx.shapes
         return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1, dgamma, dbeta,
                 dw2, db2, None, None, None)

@@ -64,7 +64,7 @@ def get():
 
 
 # io option order of gine_torch.cpp (IntOpt): then 5 scalars per window plan (in, out)
-IO_EPI, IO_LIN, IO_BATCH, IO_UPDATE, IO_FUSED, IO_LAYER, IO_DEG, IO_PLAN_IN = range(8)
+IO_EPI, IO_LIN, IO_BATCH, IO_UPDATE, IO_FUSED, IO_LAYER, IO_DEG, IO_ENGINE, IO_PLAN_IN = range(9)
 IO_PLAN_OUT = IO_PLAN_IN + 5
 
 
@@ -89,7 +89,8 @@ def _graph_opts(graph, N: int, D: int, has_acc: bool) -> tuple:
     and occupancy queries)."""
     from . import functional as Fn
     from . import options
-    key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD, Fn.layer_policy_key())
+    key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD, options.ENGINE_IN_MP,
+           Fn.layer_policy_key())
     cache = graph._ext_opts
     got = cache.get(key)
     if got is None:
@@ -98,7 +99,8 @@ def _graph_opts(graph, N: int, D: int, has_acc: bool) -> tuple:
         pin, ain = _plan_args(graph, "in", D)
         pout, aout = _plan_args(graph, "out", D)
         io = [int(fused), int(lay),
-              int(graph.max_in_degree if graph.max_in_degree is not None else -1)] + pin + pout
+              int(graph.max_in_degree if graph.max_in_degree is not None else -1),
+              int(Fn.engine_in_mp_ok(graph, D))] + pin + pout
         tensors = [graph.in_rowptr, graph.in_src, graph.in_attr, graph.out_rowptr,
                    graph.out_dst, graph.out_attr] + ain + aout
         got = cache[key] = (io, tensors)
@@ -110,10 +112,12 @@ def layer(ext, x, conv, graph, epilogue: int) -> torch.Tensor:
     layer's parameters are not flat-buffer slices, i.e. its backward is the non-deferred
     form)."""
     from . import functional as Fn
+    from . import options
     l1, bn_mod, _, l2 = conv.nn
     N, D = x.shape
     bn = Fn.BnConfig(bn_mod)
     acc = Fn.bn_accumulator(bn, D, x.device)
+    bacc = Fn.bn_accumulator(bn, D, x.device, "bwd") if options.BN_ACC_BWD else None
     gio, tensors = _graph_opts(graph, N, D, acc is not None)
     io = [epilogue, Fn.edge_linear_flag(), int(bn.use_batch_stats),
           int(bn.update_running)] + gio
@@ -121,4 +125,5 @@ def layer(ext, x, conv, graph, epilogue: int) -> torch.Tensor:
     return ext.gine_layer(x, conv.lin.weight, conv.lin.bias, conv.eps, l1.weight, l1.bias,
                           bn_mod.weight, bn_mod.bias, l2.weight, l2.bias, tensors,
                           [bn.running_mean, bn.running_var,
-                           bn.num_batches_tracked if bn.update_running else None, acc], io, fo)
+                           bn.num_batches_tracked if bn.update_running else None, acc, bacc],
+                          io, fo)

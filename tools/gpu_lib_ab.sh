@@ -15,7 +15,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 k = d["kernels"]
 print(f"{sys.argv[2]:14s} {d['config']['workload'][:6]} {d['ms_per_step']:.4f} ms  p50 {d['step_ms_p10_p50_p90'][1]:.4f}  {d['value']:.0f} graphs/s  "
-      + "  ".join(f"{n} {k[n]['us']}" for n in ("gine_mp_bwd_mlp_wgrad", "gine_mp_fwd_layer", "gine_mp_bwd") if n in k))
+      + "  ".join(f"{n} {k[n]['us']}" for n in ("gine_mp_bwd_mlp_wgrad", "gine_mp_fwd_layer", "gine_mp_fwd", "gine_mp_bwd") if n in k))
 PY
   done
 done | tee $O/ab_c$C.txt

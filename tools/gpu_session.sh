@@ -27,6 +27,7 @@ for s in $STEPS; do
   case $s in
     tests) GINE_PARITY_REPORT=$OUT/parity run pytest_gpu 660 python -u -m pytest tests -m gpu -q -rf --durations=15 --timeout 200 --timeout-method thread ;;
     det)   run determinism_layer 200 python tools/determinism_layer.py --flat ;;
+    copy)  run copy_probe 200 python tools/copy_probe.py ;;
     ntests) run pytest_new 300 python -u -m pytest ${NTESTS:-tests/test_gpu_dropin.py} -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     btests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/bounds/libgine_hip.so \
             run pytest_bounds 300 python -u -m pytest tests/test_gpu_bnacc.py tests/test_gpu_deepset.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
