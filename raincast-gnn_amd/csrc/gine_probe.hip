@@ -8,13 +8,14 @@ namespace gine {
 namespace {
 
 constexpr int kCopyThreads = 256;
-constexpr int kCopyUnroll = 8;
+constexpr int kCopyUnroll = 4;
 
-// One workgroup moves one contiguous 32 KiB block (kCopyUnroll float4 per thread, lane-
-// consecutive 16-byte chunks, every load issued before the first store); non-temporal loads
-// and stores, since every byte is touched once.  One block per 32 KiB gives the dispatcher
-// tens of thousands of short workgroups to balance over the 256 CUs (a grid-stride loop over
-// 8 workgroups per CU measured 4.4-4.7 TB/s on the same boxes).
+// One workgroup moves one contiguous 16 KiB block (kCopyUnroll float4 per thread, lane-
+// consecutive 16-byte chunks, every load issued before the first store): the fastest of the
+// forms measured with tools/copy_probe.py (profiles/r05_s06_copy_forms.txt, 1 and 4 GiB):
+// 5.75-5.79 TB/s, against 5.0-5.5 for 32-64 KiB blocks, non-temporal loads / stores, 512-1024
+// threads, and 4.4-4.9 for grid-stride loops (the round-4 form) and 4.6-4.8 for torch's
+// copy_.  None reached the guide's 6.29 TB/s float4-copy figure on these boxes.
 typedef float f4n __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(kCopyThreads) void k_copy_f4(const f4n* __restrict__ src,
                                                            f4n* __restrict__ dst, int64_t n) {
@@ -23,12 +24,12 @@ __global__ __launch_bounds__(kCopyThreads) void k_copy_f4(const f4n* __restrict_
 #pragma unroll
   for (int u = 0; u < kCopyUnroll; ++u) {
     const int64_t i = base + (int64_t)u * kCopyThreads;
-    v[u] = i < n ? __builtin_nontemporal_load(src + i) : f4n{0.f, 0.f, 0.f, 0.f};
+    v[u] = i < n ? src[i] : f4n{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
   for (int u = 0; u < kCopyUnroll; ++u) {
     const int64_t i = base + (int64_t)u * kCopyThreads;
-    if (i < n) __builtin_nontemporal_store(v[u], dst + i);
+    if (i < n) dst[i] = v[u];
   }
 }
 

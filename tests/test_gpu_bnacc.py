@@ -353,6 +353,12 @@ def test_bn_acc_backward_small_gradients(monkeypatch):
         conv.forward_residual_relu(x, eid, ead).backward(dy)
         torch.cuda.synchronize()
         grads[mode] = [x.grad.clone()] + [p.grad.clone() for p in conv.parameters()]
-    for a, b in zip(grads["1"], grads["0"]):
+    names = ["x"] + [n for n, _ in conv.named_parameters()]
+    w1 = dict(zip(names, grads["0"]))["nn.0.weight"]
+    for name, a, b in zip(names, grads["1"], grads["0"]):
         den = float(b.abs().max())
-        assert float((a - b).abs().max()) <= TOL * den + 1e-30
+        if name == "nn.0.bias":
+            # analytically zero behind train-mode BatchNorm: rounding noise of sum_n d a1,
+            # whose scale is that of the weight gradient sum_n d a1 z (z ~ 1)
+            den = max(den, float(w1.abs().max()))
+        assert float((a - b).abs().max()) <= TOL * den + 1e-30, name
