@@ -196,17 +196,27 @@ class Trainer:
     def step(self):
         if self.graph_fb is None:
             return self.eager_step()
+        timed = self.ar_events is not None and self.collective and self.graph_opt is not None
+        if timed:
+            stream = torch.cuda.current_stream(self.device)
+            ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
+            ev[0].record(stream)
         self.graph_fb.replay()
         if self.graph_opt is not None:
-            if self.ar_events is not None and self.collective:
-                stream = torch.cuda.current_stream(self.device)
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record(stream)
+            if timed:
+                ev[1].record(stream)
+                sync_ms = None
+                if dist.get_backend(self.reducer.group) != "nccl":
+                    # gloo reduces host copies: the wait for the fwd+bwd graph, timed apart
+                    # from the collective itself
+                    t0 = time.perf_counter()
+                    stream.synchronize()
+                    sync_ms = (time.perf_counter() - t0) * 1e3
                 t0 = time.perf_counter()
                 self.reducer.all_reduce_()
                 host_ms = (time.perf_counter() - t0) * 1e3  # the call's host time (gloo: whole)
-                ev[1].record(stream)
-                self.ar_events.append(ev + (host_ms,))
+                ev[2].record(stream)
+                self.ar_events.append(ev + (host_ms, sync_ms))
             else:
                 self.reducer.all_reduce_()
             self.graph_opt.replay()
@@ -739,8 +749,9 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
            for q in (10, 50, 90)}
     # the split all-reduce alone (between the fwd+bwd and AdamW graphs), per step: on the
     # stream (HIP events) and on the host (the collective call itself)
-    ar_steps = [(a.elapsed_time(b), h) for a, b, h in tr.ar_events]
-    ar = sorted(t for t, _ in ar_steps)
+    ar_steps = [(b.elapsed_time(c), h, sy, a.elapsed_time(b))
+                for a, b, c, h, sy in tr.ar_events]
+    ar = sorted(t[0] for t in ar_steps)
     tr.ar_events = None
     pct["allreduce_p50"] = round(ar[len(ar) // 2], 4) if ar else None
     pct["stalls"] = stalled_steps(in_order, ar_steps)
@@ -771,8 +782,12 @@ def stalled_steps(in_order, ar_steps):
     for i in bad[:8]:
         rec = {"step": i, "ms": round(in_order[i], 3)}
         if i < len(ar_steps):
-            rec["allreduce_stream_ms"] = round(ar_steps[i][0], 3)
-            rec["allreduce_host_ms"] = round(ar_steps[i][1], 3)
+            ar_ms, host_ms, sync_ms, fb_ms = ar_steps[i]
+            rec["fwd_bwd_stream_ms"] = round(fb_ms, 3)  # the fwd+bwd graph on the stream
+            if sync_ms is not None:  # host wait for it before the gloo collective
+                rec["fwd_bwd_host_wait_ms"] = round(sync_ms, 3)
+            rec["allreduce_stream_ms"] = round(ar_ms, 3)
+            rec["allreduce_host_ms"] = round(host_ms, 3)
         out["steps"].append(rec)
     rest = [t for i, t in enumerate(in_order) if i not in set(bad)]
     out["ms_per_step_other_steps"] = round(sum(rest) / len(rest), 4) if rest else None

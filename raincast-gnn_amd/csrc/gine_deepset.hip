@@ -114,11 +114,30 @@ __device__ __forceinline__ int staged_row(int i) {
 // (scalar) tile base plus a 32-bit lane offset.
 // X3: the staged tile is three bf16 planes (dst in bf16 elements): DsImg<KP>'s (the
 // forward, KI = 0) or DsBwdImg<KI>'s (the backward)
-template <int NT, int KP, bool PAD, bool X3 = false, int KI = 0>  // PAD: G*M % 16 != 0 possible
+// Stores of the stagers without a branch per element (bit 0: the backward's, bit 1: the
+// forward's): backward 40.4 -> 39.3 us, forward 27.8 -> 27.3 us at 16,000 nodes
+// (profiles/r05_s08_ds_ab_branchless.txt)
+#ifndef GINE_DS_BRANCHLESS
+#define GINE_DS_BRANCHLESS 3
+#endif
+// PAD: G*M % 16 != 0 possible; BWD: the backward's stager
+template <int NT, int KP, bool PAD, bool X3 = false, int KI = 0, bool BWD = false>
 struct Stager {
   static constexpr int PER = (32 * KP + NT - 1) / NT;  // >= 32*F / NT
   static constexpr int LD = stager_ld<KP, X3, KI>();
   static constexpr int kPlane = stager_plane<KP, X3, KI>();
+  // A thread without an element stores its zero to a padding slot no chain reads instead
+  // of branching around the store (GINE_DS_BRANCHLESS bit 0: the backward's stager, bit 1:
+  // the forward's): row t % 32 past the k range of the row-major images (columns KX.. /
+  // KP..), rows 32.. of feature t % 32 in the column-major ones -- a slot per thread, so no
+  // two lanes of a store share an address
+  static constexpr bool kBranchless = (GINE_DS_BRANCHLESS & (BWD ? 1 : 2)) != 0;
+  __device__ static int dummy_slot() {
+    const int r = threadIdx.x & 31, u = threadIdx.x >> 5;
+    if constexpr (X3 && KI != 0) return r * LD + 32 + (u & 7);
+    else if constexpr (X3) return r * LD + DsImg<KP>::KX + (u & 7);
+    else return r * LD + KP + (u & 3);
+  }
   int src[PER];  // float offset from the tile's first row (0 if the thread has no element)
   int row[PER];  // group-row offset from the tile's first row (INT_MAX: no element)
   int dst[PER];  // LDS offset (-1: no element)
@@ -134,9 +153,9 @@ struct Stager {
       src[i] = has ? c * G * M * F + off : 0;
       row[i] = has ? c * G * M + j : 0x7fffffff;
       if constexpr (X3 && KI != 0)
-        dst[i] = has ? f * LD + (16 * c + j) : -1;  // the backward's column-major planes
+        dst[i] = has ? f * LD + (16 * c + j) : (kBranchless ? dummy_slot() : -1);  // col-major
       else
-        dst[i] = has ? (16 * c + j) * LD + f : -1;
+        dst[i] = has ? (16 * c + j) * LD + f : (kBranchless ? dummy_slot() : -1);
       if constexpr (PAD) jrow[i] = has ? (uint32_t)j : 0u;
     }
   }
@@ -185,12 +204,12 @@ struct Stager {
         const float b = ((ok >> i1) & 1u) ? v[i1] : 0.f;
         uint32_t ph, pm, pl;
         split2(a, b, ph, pm, pl);
-        if (dst[i] >= 0) {
+        if (kBranchless || dst[i] >= 0) {
           img[dst[i]] = (uint16_t)ph;
           img[PL + dst[i]] = (uint16_t)pm;
           img[2 * PL + dst[i]] = (uint16_t)pl;
         }
-        if (i + 1 < PER && dst[i1] >= 0) {
+        if (i + 1 < PER && (kBranchless || dst[i1] >= 0)) {
           img[dst[i1]] = (uint16_t)(ph >> 16);
           img[PL + dst[i1]] = (uint16_t)(pm >> 16);
           img[2 * PL + dst[i1]] = (uint16_t)(pl >> 16);
@@ -199,7 +218,7 @@ struct Stager {
     } else {
 #pragma unroll
       for (int i = 0; i < PER; ++i)
-        if (dst[i] >= 0) s_e[dst[i]] = ((ok >> i) & 1u) ? v[i] : 0.f;
+        if (kBranchless || dst[i] >= 0) s_e[dst[i]] = ((ok >> i) & 1u) ? v[i] : 0.f;
     }
   }
 };
@@ -356,20 +375,25 @@ struct Cursor {
 // (never consumed) instead of being skipped, so no register merge at the loop's back edge
 // waits for them (backward 41.4 -> 39.0 us at 16,000 nodes; the forward, whose ring holds
 // no mask word, runs 0.9 us slower that way: profiles/r03_s35).
-template <bool UNCOND, int NT, int KP, bool PAD, bool X3, int KI, class Body>
+template <bool UNCOND, bool MASKIN, int NT, int KP, bool PAD, bool X3, int KI, bool BWD,
+          class Body>
 __device__ __forceinline__ void walk_tiles(const Groups& gr, int GM, int tpg,
-                                           const Stager<NT, KP, PAD, X3, KI>& st,
+                                           const Stager<NT, KP, PAD, X3, KI, BWD>& st,
                                            const float* __restrict__ ens, int64_t rows_total,
                                            int F, float* buf0, float* buf1,
                                            const uint16_t* __restrict__ mask_in, Body&& tile) {
-  constexpr int PER = Stager<NT, KP, PAD, X3, KI>::PER;
+  constexpr int PER = Stager<NT, KP, PAD, X3, KI, BWD>::PER;
   if (gr.first >= gr.end) return;
   const int count = ((gr.end - gr.first + gr.step - 1) / gr.step) * tpg;
   Cursor cur, pf;  // tile being computed, tile being loaded
   cur.start(gr.first, GM);
   pf = cur;
+  // the mask ring is a compile-time property of the walk: a run-time null test made the
+  // mask load conditional, and the s_waitcnt at the staging store below then assumed the
+  // path without it -- waiting for the first load of tile k+2, i.e. a one-deep ring
   auto mload = [&](const Cursor& c) -> uint32_t {
-    return mask_in ? (uint32_t)mask_in[((int64_t)c.g * tpg + c.t) * NT + threadIdx.x] : 0u;
+    if constexpr (MASKIN) return (uint32_t)mask_in[((int64_t)c.g * tpg + c.t) * NT + threadIdx.x];
+    else return 0u;
   };
   auto sload = [&](float (&v)[PER], const Cursor& c) -> uint32_t {
     return st.load(v, ens, c.row, rows_total, F, GM - 16 * c.t);
@@ -428,6 +452,12 @@ __device__ __forceinline__ void walk_tiles(const Groups& gr, int GM, int tpg,
 // forward that follows.  They are dealt first (so they never wait for a free slot behind the
 // walk) and share one LDS buffer with the walk's tiles (so the walk's occupancy is that of
 // the larger of the two, not of their sum).
+// (experiments) the forward's ring loads unconditional, as the backward's: the compiler then
+// waits for the ring at the loop head instead (register reuse), 27.5 vs 27.8 us at 16,000
+// nodes and 14.7 vs 13.9 at 4,000 (profiles/r05_s07_ds_ab_ring_branchless.txt): off
+#ifndef GINE_DS_FWD_UNCOND
+#define GINE_DS_FWD_UNCOND 0
+#endif
 template <int H, int KP, int G, bool MASK, bool FOLD = false>
 __global__ __launch_bounds__(2 * H, 4) void k_deepset_fwd(const float* __restrict__ ens,
                                                        const float* __restrict__ w1,
@@ -486,7 +516,8 @@ __global__ __launch_bounds__(2 * H, 4) void k_deepset_fwd(const float* __restric
   float* s_mine = s_r + (G * h) * H + col;  // this lane's column of its half's G nodes
   // uniform walk state: node (0..G-1 within each half's G; G: padding) and rows left in it
   int node = 0, rem = M;
-  walk_tiles<false>(gr, GM, tpg, st, ens, N * M, F, s_e[0], s_e[1], nullptr,
+  walk_tiles<GINE_DS_FWD_UNCOND != 0, false>(gr, GM, tpg, st, ens, N * M, F, s_e[0], s_e[1],
+                                             nullptr,
              [&](const Cursor& c, const float* buf, uint32_t) {
     if (c.t == 0) {
       node = 0;
@@ -508,6 +539,8 @@ __global__ __launch_bounds__(2 * H, 4) void k_deepset_fwd(const float* __restric
       const float v = acc[q] + bias;
       bits |= (v > 0.f ? 1u : 0u) << q;
       run += relu_nan(v);
+      // (a branch-free form -- every row storing the running sum to its node's slot --
+      // measured 4.4 us slower at 16,000 nodes: profiles/r05_s07_ds_ab_ring_branchless.txt)
       if (--rem == 0) {  // last member of this node: keep its sum
         if (node < G) s_mine[node * H] = run;
         run = 0.f;
@@ -584,13 +617,13 @@ __device__ __forceinline__ bool ds_bwd_body(const float* __restrict__ ens,
   for (int j = 0; j < TAIL; ++j) tw[j] = 0.f;
   double gb = 0.0;
 
-  Stager<NT, KP, G != 16, X3, KI> st;
+  Stager<NT, KP, G != 16, X3, KI, true> st;
   st.init(F, M, G);
   const Groups gr(num_groups, gridDim.x);
   const int GM = G * M, tpg = tiles_per_group(G, M);
   const float* my_dr = s_dr + G * h * H + col;  // this lane: node j of its half at j*H
   int node = 0, rem = M;
-  walk_tiles<true>(gr, GM, tpg, st, ens, N * M, F, s_e0, s_e1, mask,
+  walk_tiles<true, true>(gr, GM, tpg, st, ens, N * M, F, s_e0, s_e1, mask,
              [&](const Cursor& c, const float* buf, uint32_t bits) {
     if (c.t == 0) {  // dr of this group, this wave's columns (read by this wave only)
       const int64_t node0 = (int64_t)c.g * 2 * G;

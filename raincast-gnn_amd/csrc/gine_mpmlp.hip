@@ -63,6 +63,25 @@ constexpr uint32_t kRowBytes = kD * 4;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+#ifdef GINE_LAYER_PROFILE
+// Debug build only (make layerprof): thread 0 of every workgroup of the one-launch layer
+// forward stamps s_memtime at its phase boundaries (tools/layer_prof.py):
+// 0 entry, 1 matrix role done, 2 phase A done (block), 3 W2 fragments ready, 4 grid barrier
+// passed, 5 BatchNorm finish done, 6 r = relu(bn(a1)) done, 7 last Linear2 chain done.
+// Phase A detail: 8 W1 planes ready, 9 / 11 tile 1 / 2 chain done, 10 / 12 tile 1 / 2
+// epilogue done, 13 statistics in the accumulator (matrix role, thread 0); 14 / 15 tile 1 /
+// 2 gathered (gather role, thread 256).
+__device__ long long g_layer_prof[1024][16];
+#define LAYER_MARK_T(t, i)                                                       \
+  do {                                                                           \
+    if (threadIdx.x == (t) && blockIdx.x < 1024)                                 \
+      g_layer_prof[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memtime();    \
+  } while (0)
+#else
+#define LAYER_MARK_T(t, i) do {} while (0)
+#endif
+#define LAYER_MARK(i) LAYER_MARK_T(0, i)
+
 struct TileSeq {
   int first, end, step;
   __device__ int count() const { return first < end ? (end - first + step - 1) / step : 0; }
@@ -169,6 +188,7 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
   BPlanes<kKS> bp;
   if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
   __syncthreads();  // (iteration 0: the gather role stages the first tile)
+  if constexpr (LAYER) LAYER_MARK(8);
   double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
   const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
   float* tt = &L.w[wave * 32 * kTLD];
@@ -201,6 +221,12 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bf[4 * q + 3], acc, 0, 0, 0);
       }
     }
+#ifdef GINE_LAYER_PROFILE
+    if constexpr (LAYER) {
+      if (it <= 2 && acc[0] == 1.2345e-30f) tt[0] = 0.f;  // the stamp waits for the chain
+      if (it <= 2) LAYER_MARK(7 + 2 * it);
+    }
+#endif
     // this wave's 32x32 block -> row-major through its own LDS tile
 #pragma unroll
     for (int r = 0; r < 16; ++r) tt[((r & 3) + 8 * (r >> 2) + 4 * h) * kTLD + c32] = acc[r];
@@ -226,6 +252,9 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
                                         4 * cq]) = make_float4(o4[0], o4[1], o4[2], o4[3]);
     }
     __builtin_amdgcn_wave_barrier();  // the next tile's transposition writes come after
+    if constexpr (LAYER) {
+      if (it <= 2) LAYER_MARK(8 + 2 * it);
+    }
     __syncthreads();
   }
   // per-column partials: the 8 row groups added in fixed order (row-tile GEMM order)
@@ -246,6 +275,7 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
     bnacc_add<false>(A.bnacc, 2 * kD, which * kD + cc, s);
     // the atomics are performed before this workgroup arrives at the grid barrier
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LAYER_MARK(13);
   } else if (A.bnacc) {
     bnacc_add(A.bnacc, 2 * kD, which * kD + cc, s);
   }
@@ -347,6 +377,7 @@ __device__ __forceinline__ void gather_role(const FusedArgs& A, FusedLds& L, con
       *reinterpret_cast<f4v*>(&sz[r * kLD + 4 * t]) = zv;
       if (n < N) *reinterpret_cast<f4v*>(A.z + n * kD + 4 * t) = zv;
     }
+    if (it < 2) LAYER_MARK_T(kMatThreads, 14 + it);
     __builtin_amdgcn_wave_barrier();  // edge-list reads done before the next tile's writes
     __syncthreads();
   }
@@ -407,9 +438,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   const long long ph = phw[0] + 1, consumed = phw[1 + ((ph - 1) & 1)];
 
   // ---- phase A ----
+  LAYER_MARK(0);
   if (mat) matrix_role<true>(A, L.f, ts, nt, &L.a1k[0][0]);
   else gather_role<FMA>(A, L.f, ts, nt);
+  LAYER_MARK(1);
   __syncthreads();  // phase A's LDS use is over (L.f.w is free)
+  LAYER_MARK(2);
 
   // ---- W2 fragments and the residual rows, before the barrier ----
   const int lane = tid % kWave;
@@ -445,8 +479,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
     }
     if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
   }
+  LAYER_MARK(3);
   if (tid == 0) L.barrier_failed = grid_barrier(bnacc_barrier(A.bnacc, 2 * kD), gridDim.x) ? 0 : 1;
   __syncthreads();
+  LAYER_MARK(4);
   // a timed-out barrier (the grid was not co-resident): the totals are incomplete, so this
   // workgroup's statistics and outputs are NaN and the running statistics stay as they were;
   // the failure word tells the host
@@ -487,6 +523,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
     phw[1 + (ph & 1)] = ph;  // bnacc_mark_consumed
   }
   __syncthreads();
+  LAYER_MARK(5);
   // r = relu(bn(a1)) in place; rows past N are zero (the row GEMM stages them as zero)
   for (int e = tid; e < nt * kTileRows * kD4; e += kThreads) {
     const int k = e / (kTileRows * kD4), r = (e / kD4) % kTileRows, q4 = e % kD4;
@@ -500,6 +537,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
     *reinterpret_cast<float4*>(a) = v;
   }
   __syncthreads();
+  LAYER_MARK(6);
   for (int k = 0; k < nt; ++k) {
     float* sO = L.f.z[k & 1];
     if (mat) {  // Linear2 chain of tile k (the row GEMM's split-bf16 chain and k order)
@@ -560,6 +598,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
       }
     }
   }
+  LAYER_MARK(7);
 }
 
 }  // namespace
@@ -743,3 +782,11 @@ extern "C" int gine_mp_fwd_mlp1_acc(const float* x, const int32_t* in_rowptr,
   return mp_fwd_mlp1(x, in_rowptr, in_src, in_attr, lin_w, lin_b, eps, w1, b1, z, a1, partials,
                      bn_acc, num_nodes, channels, max_in_degree, flags, stream);
 }
+
+#ifdef GINE_LAYER_PROFILE
+extern "C" int gine_debug_layer_prof(long long* out) {  // [1024][16] host buffer
+  GINE_RETURN_IF_HIP(hipDeviceSynchronize());
+  GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_layer_prof), sizeof(g_layer_prof)));
+  return GINE_OK;
+}
+#endif

@@ -71,3 +71,20 @@ def test_world_size_must_match_gpus():
     p = _run(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert p.returncode != 0
     assert "must agree" in p.stderr
+
+
+def test_stalled_steps_decomposition():
+    """A stalled step is reported with its fwd+bwd stream time, the host wait for it (gloo)
+    and the collective's own times; steps within 10x the median are not."""
+    sys.path.insert(0, ROOT)
+    import importlib
+    bench = importlib.import_module("bench")
+    steps = [2.0, 2.1, 600.0, 2.05, 1.9]
+    ar = [(0.7, 0.8, 1.0, 1.2), (0.7, 0.9, 1.1, 1.3), (0.8, 1.0, 598.0, 1.25),
+          (0.7, 0.8, 1.0, 1.2), (0.7, 0.8, 1.0, 1.2)]
+    out = bench.stalled_steps(steps, ar)
+    assert out["count"] == 1 and out["steps"][0]["step"] == 2
+    rec = out["steps"][0]
+    assert rec["fwd_bwd_host_wait_ms"] == 598.0 and rec["fwd_bwd_stream_ms"] == 1.25
+    assert rec["allreduce_stream_ms"] == 0.8 and rec["allreduce_host_ms"] == 1.0
+    assert bench.stalled_steps([2.0, 2.1, 1.9], ar[:3]) is None

@@ -32,6 +32,11 @@ for s in $STEPS; do
     btests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/bounds/libgine_hip.so \
             run pytest_bounds 300 python -u -m pytest tests/test_gpu_bnacc.py tests/test_gpu_deepset.py -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     ktests) run pytest_k 600 python -u -m pytest tests -m gpu -q -rf -k "${KTESTS:-window}" --timeout 120 --timeout-method thread ;;
+    layerprof) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/layerprof/libgine_hip.so \
+            run layer_prof 200 python tools/layer_prof.py --config ${LPCFG:-2} ;;
+    dsab)  run ds_ab 900 bash tools/gpu_ds_ab.sh $TAG/dsab ${DSVARS:-main} ;;
+    kvtests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/${LIBVAR}/libgine_hip.so \
+            run pytest_k_${LIBVAR} 600 python -u -m pytest tests -m gpu -q -rf -k "${KTESTS:-deepset}" --timeout 120 --timeout-method thread ;;
     smoke) run smoke 150 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     benchnc) run bench_nocpu 600 python bench.py --no-cpu ;;
