@@ -66,12 +66,20 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 #ifdef GINE_LAYER_PROFILE
 // Debug build only (make layerprof): thread 0 of every workgroup of the one-launch layer
 // forward stamps s_memtime at its phase boundaries (tools/layer_prof.py):
-// 0 entry, 1 matrix role done, 2 phase A done (block), 3 W2 fragments ready, 4 grid barrier
-// passed, 5 BatchNorm finish done, 6 r = relu(bn(a1)) done, 7 last Linear2 chain done.
+// 0 entry, 1 matrix role done, 2 phase A done (block), 3 barrier arrival, 4 grid barrier
+// passed, 5 BatchNorm finish + W2 fragments done, 6 r = relu(bn(a1)) done, 7 last Linear2
+// chain done.
 // Phase A detail: 8 W1 planes ready, 9 / 11 tile 1 / 2 chain done, 10 / 12 tile 1 / 2
 // epilogue done, 13 statistics in the accumulator (matrix role, thread 0); 14 / 15 tile 1 /
 // 2 gathered (gather role, thread 256).
-__device__ long long g_layer_prof[1024][16];
+// 16-19: s_memrealtime (the 100 MHz clock every XCD shares) at entry, barrier arrival,
+// barrier release and the end, for the arrival skew across workgroups.
+__device__ long long g_layer_prof[1024][24];
+#define LAYER_RT(i)                                                              \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 1024)                                   \
+      g_layer_prof[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define LAYER_MARK_T(t, i)                                                       \
   do {                                                                           \
     if (threadIdx.x == (t) && blockIdx.x < 1024)                                 \
@@ -79,6 +87,7 @@ __device__ long long g_layer_prof[1024][16];
   } while (0)
 #else
 #define LAYER_MARK_T(t, i) do {} while (0)
+#define LAYER_RT(i) do {} while (0)
 #endif
 #define LAYER_MARK(i) LAYER_MARK_T(0, i)
 
@@ -194,6 +203,9 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
   float* tt = &L.w[wave * 32 * kTLD];
   for (int it = 1; it <= nt; ++it) {
     const int T = ts.at(it - 1);
+    if constexpr (LAYER) {
+      if (it <= 2) LAYER_MARK(19 + it);  // (profile builds) tile it's z is in LDS
+    }
     const float* arow = &L.z[(it - 1) & 1][c32 * kLD + h * kKS];
     floatx16 acc;
 #pragma unroll
@@ -281,8 +293,9 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
   }
 }
 
-// Gather role (waves 4-11).  Barriers: 1 + (nt + 1), as the matrix role.
-template <bool FMA>
+// Gather role (waves 4-11).  Barriers: 1 + (nt + 1), as the matrix role; without LAST_SYNC
+// the caller runs the last one (after work of its own beside the matrix role's last tile).
+template <bool FMA, bool LAST_SYNC = true>
 __device__ __forceinline__ void gather_role(const FusedArgs& A, FusedLds& L, const TileSeq& ts,
                                             int nt) {
   const int p = threadIdx.x - kMatThreads;
@@ -362,6 +375,8 @@ __device__ __forceinline__ void gather_role(const FusedArgs& A, FusedLds& L, con
           a0[u] = L.attr[hw][pr][j];
           a1v[u] = L.attr[hw][pr + 1][j];
         }
+        // (an unmasked copy of this loop for full batches -- the common case -- spilled: 292 B of
+        // scratch in k_mp_fwd_mlp1, which then ran 34 instead of 14 us; profiles/r05_s15)
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           edge_acc<FMA>(acc[pr], r0[u], a0[u], lw, lb, j0 + u < cnt[pr]);
@@ -381,7 +396,7 @@ __device__ __forceinline__ void gather_role(const FusedArgs& A, FusedLds& L, con
     __builtin_amdgcn_wave_barrier();  // edge-list reads done before the next tile's writes
     __syncthreads();
   }
-  __syncthreads();  // (iteration nt: the matrix role multiplies the last tile)
+  if constexpr (LAST_SYNC) __syncthreads();  // (iteration nt: the matrix role multiplies the last tile)
 }
 
 template <bool FMA>
@@ -403,11 +418,33 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_mlp1(FusedArgs A) {
 //   phase B = k_fwd2_bnacc on the workgroup's own tiles: BatchNorm finish from the
 //             accumulator totals, r = relu(bn(a1)) from the LDS tiles, Linear2 on the matrix
 //             waves, epilogue (bias, ResGnn ReLU / residual + mask) on the gather waves.
-// W2's fragments and the residual rows are loaded before the barrier, under its wait.
+// W2 is loaded by the gather waves under the matrix role's last chain and staged in LDS
+// before the barrier; its fragments are read after it, beside the BatchNorm totals (gather
+// waves), so a workgroup arrives as soon as its phase A is done; the residual rows are
+// loaded under the BatchNorm finish.
 // Same tile -> workgroup map, same arithmetic and order as the two-launch pair (bit-identical:
 // the BatchNorm totals are integer sums, the MFMA chains and epilogues are the row GEMM's).
 // ---------------------------------------------------------------------------------------
 constexpr int kLayerTiles = 2;  // a1 tiles a workgroup keeps in LDS
+
+// W2 in flight in the gather waves' registers: 8 float4 per thread (element idx = t + n*j,
+// row idx / kD4, column chunk idx % kD4), staged into the padded LDS image.
+template <int PER>
+struct W2Regs {
+  static_assert(PER == 8, "eight float4 per gather thread");
+  float4 v0, v1, v2, v3, v4, v5, v6, v7;
+  __device__ __forceinline__ void load(const float4* __restrict__ w4, int t, int n) {
+    v0 = w4[t]; v1 = w4[t + n]; v2 = w4[t + 2 * n]; v3 = w4[t + 3 * n];
+    v4 = w4[t + 4 * n]; v5 = w4[t + 5 * n]; v6 = w4[t + 6 * n]; v7 = w4[t + 7 * n];
+  }
+  __device__ __forceinline__ void put(float* w, int idx, float4 v) const {
+    *reinterpret_cast<float4*>(&w[(idx / kD4) * kLD + 4 * (idx % kD4)]) = v;
+  }
+  __device__ __forceinline__ void store(float* w, int t, int n) const {
+    put(w, t, v0); put(w, t + n, v1); put(w, t + 2 * n, v2); put(w, t + 3 * n, v3);
+    put(w, t + 4 * n, v4); put(w, t + 5 * n, v5); put(w, t + 6 * n, v6); put(w, t + 7 * n, v7);
+  }
+};
 
 struct LayerArgs {
   const float* W2;
@@ -439,50 +476,43 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
 
   // ---- phase A ----
   LAYER_MARK(0);
-  if (mat) matrix_role<true>(A, L.f, ts, nt, &L.a1k[0][0]);
-  else gather_role<FMA>(A, L.f, ts, nt);
-  LAYER_MARK(1);
-  __syncthreads();  // phase A's LDS use is over (L.f.w is free)
-  LAYER_MARK(2);
+  LAYER_RT(16);
+  // W2 for the second half: the gather waves load it (coalesced, 8 float4 per thread) once
+  // their last tile is gathered, so its latency hides under the matrix role's last chain
+  // and statistics, and stage it in LDS when phase A's use of L.f.w is over
+  constexpr int kW2Per = kD * kD4 / (kThreads - kMatThreads);
+  static_assert(kD * kD4 % (kThreads - kMatThreads) == 0, "W2 in whole float4 per thread");
+  if (mat) {
+    matrix_role<true>(A, L.f, ts, nt, &L.a1k[0][0]);
+    LAYER_MARK(1);
+    __syncthreads();  // phase A's LDS use is over (L.f.w is free)
+    LAYER_MARK(2);
+  } else {
+    // (W2Regs is confined to this branch -- live across the matrix role it would spill --
+    // and a struct of scalars: an array held across the barriers went to scratch)
+    gather_role<FMA, false>(A, L.f, ts, nt);
+    W2Regs<kW2Per> w2r;
+    w2r.load(reinterpret_cast<const float4*>(B.W2), tid - kMatThreads, kThreads - kMatThreads);
+    __syncthreads();  // gather_role's last barrier (the matrix role multiplies the last tile)
+    __syncthreads();  // phase A's LDS use is over (L.f.w is free)
+    w2r.store(L.f.w, tid - kMatThreads, kThreads - kMatThreads);
+  }
 
-  // ---- W2 fragments and the residual rows, before the barrier ----
   const int lane = tid % kWave;
   const int h = lane >> 5, c32 = lane & 31;
   const int col = 32 * wave + c32;  // (matrix waves)
-  if (mat) {
-    const float4* w4 = reinterpret_cast<const float4*>(B.W2);
-    float4 wt[kD * kD4 / kMatThreads];
-#pragma unroll
-    for (int j = 0; j < kD * kD4 / kMatThreads; ++j) wt[j] = w4[tid + kMatThreads * j];
-#pragma unroll
-    for (int j = 0; j < kD * kD4 / kMatThreads; ++j) {
-      const int idx = tid + kMatThreads * j;
-      *reinterpret_cast<float4*>(&L.f.w[(idx / kD4) * kLD + 4 * (idx % kD4)]) = wt[j];
-    }
-  }
   // epilogue items of the gather waves: rows p / 32 and p / 32 + 16 of a tile, column chunk
   // p % 32 (p = tid - 256 < 512)
   const int p = tid - kMatThreads;
   const int eq = p & 31, er = p >> 5;
-  __syncthreads();  // W2 staged
-  float bf[kKS];
-  BPlanes<kKS> bp;
-  if (mat) {
-    const float* wr = &L.f.w[col * kLD + h * kKS];
-#pragma unroll
-    for (int q = 0; q < kKS / 4; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(&wr[4 * q]);
-      bf[4 * q] = v.x;
-      bf[4 * q + 1] = v.y;
-      bf[4 * q + 2] = v.z;
-      bf[4 * q + 3] = v.w;
-    }
-    if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
-  }
   LAYER_MARK(3);
+  LAYER_RT(17);
+  // the workgroup arrives as soon as phase A is done; W2's fragments are read after the
+  // barrier, beside the BatchNorm totals
   if (tid == 0) L.barrier_failed = grid_barrier(bnacc_barrier(A.bnacc, 2 * kD), gridDim.x) ? 0 : 1;
-  __syncthreads();
+  __syncthreads();  // (also: W2 staged by the gather waves)
   LAYER_MARK(4);
+  LAYER_RT(18);
   // a timed-out barrier (the grid was not co-resident): the totals are incomplete, so this
   // workgroup's statistics and outputs are NaN and the running statistics stay as they were;
   // the failure word tells the host
@@ -505,17 +535,31 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
       }
   }
 
-  // ---- phase B: BatchNorm finish (the arithmetic of k_fwd2_bnacc's prologue) ----
-  if (tid < 2 * kD) {
-    const double t = bnacc_total<true>(A.bnacc, 2 * kD, tid, blockIdx.x == 0, ph, consumed);
-    L.tot[tid] = failed ? __builtin_nan("") : t;
+  // ---- phase B: BatchNorm finish (the arithmetic of k_fwd2_bnacc's prologue) on the
+  // gather waves, W2's fragments on the matrix waves ----
+  float bf[kKS];
+  BPlanes<kKS> bp;
+  if (mat) {
+    const float* wr = &L.f.w[col * kLD + h * kKS];
+#pragma unroll
+    for (int q = 0; q < kKS / 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(&wr[4 * q]);
+      bf[4 * q] = v.x;
+      bf[4 * q + 1] = v.y;
+      bf[4 * q + 2] = v.z;
+      bf[4 * q + 3] = v.w;
+    }
+    if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
+  } else if (p < 2 * kD) {
+    const double t = bnacc_total<true>(A.bnacc, 2 * kD, p, blockIdx.x == 0, ph, consumed);
+    L.tot[p] = failed ? __builtin_nan("") : t;
   }
   __syncthreads();
-  if (tid < kD) {
+  if (!mat && p < kD) {
     BnFwdParams q = B.q;
     if (failed) q.update_running = 0;
-    bn_finish_channel(q, kD, tid, L.tot[tid], L.tot[kD + tid], blockIdx.x == 0, &L.bn[tid],
-                      &L.bn[kD + tid]);
+    bn_finish_channel(q, kD, p, L.tot[p], L.tot[kD + p], blockIdx.x == 0, &L.bn[p],
+                      &L.bn[kD + p]);
   }
   if (blockIdx.x == 0 && tid == 0) {
     if (B.q.update_running && B.q.nbt != nullptr && !failed) B.q.nbt[0] = B.q.nbt[0] + 1;
@@ -599,6 +643,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
     }
   }
   LAYER_MARK(7);
+  LAYER_RT(19);
 }
 
 }  // namespace
@@ -784,7 +829,7 @@ extern "C" int gine_mp_fwd_mlp1_acc(const float* x, const int32_t* in_rowptr,
 }
 
 #ifdef GINE_LAYER_PROFILE
-extern "C" int gine_debug_layer_prof(long long* out) {  // [1024][16] host buffer
+extern "C" int gine_debug_layer_prof(long long* out) {  // [1024][24] host buffer
   GINE_RETURN_IF_HIP(hipDeviceSynchronize());
   GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_layer_prof), sizeof(g_layer_prof)));
   return GINE_OK;

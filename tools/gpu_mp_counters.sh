@@ -4,6 +4,7 @@
 # counter group within the per-block limits (8 SQ, 4 TCP, 2 TA, 2 TD, 2 GRBM, 4 TCC); names
 # missing from this device's `rocprofv3 -L` list are dropped before a pass runs.
 #   tools/gpu_mp_counters.sh <tag> [config]
+#   LAYER=1 FILTER=gine::k_mp_fwd_layer tools/gpu_mp_counters.sh <tag> 2   (the layer forward)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -22,8 +23,13 @@ pass_run() {  # pass_run <name> counters...
   local c; c=$(have "$@")
   [ -n "$c" ] || { echo "pass $name: no listed counters"; return 0; }
   echo "pass $name: $c"
-  timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/$name -o run -- \
-    python3 tools/mp_micro.py --configs $CFG --tiles "" --rcm --eager --reps 5 > $O/$name.log 2>&1
+  if [ "${LAYER:-0}" = 1 ]; then  # the one-launch layer forward (tools/layer_prof.py)
+    timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/$name -o run -- \
+      python3 tools/layer_prof.py --config $CFG --reps 5 --no-stamps > $O/$name.log 2>&1
+  else
+    timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/$name -o run -- \
+      python3 tools/mp_micro.py --configs $CFG --tiles "" --rcm --eager --reps 5 > $O/$name.log 2>&1
+  fi
   local rc=$?
   [ $rc -eq 0 ] || { echo "pass $name rc=$rc"; tail -3 $O/$name.log; exit $rc; }
 }
@@ -37,5 +43,5 @@ pass_run td TD_BUSY_avr TD_TC_STALL_sum
 pass_run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum
 pass_run grbm GRBM_GUI_ACTIVE GRBM_COUNT
 for f in $O/*/run_counter_collection.csv; do echo "$f"; done > $O/passes.txt
-python tools/pmc_summary.py $O/*/run_counter_collection.csv --filter "gine::k_mp_" > $O/summary.txt 2>&1
+python tools/pmc_summary.py $O/*/run_counter_collection.csv --filter "${FILTER:-gine::k_mp_}" > $O/summary.txt 2>&1
 cat $O/summary.txt

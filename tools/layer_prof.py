@@ -1,8 +1,8 @@
 """Phase profile of the one-launch GINE layer forward (every workgroup's s_memtime stamps).
     GINE_HIP_LIB=.../var/layerprof/libgine_hip.so python tools/layer_prof.py [--config 2]
 Stamps of thread 0 per workgroup (gine_mpmlp.hip GINE_LAYER_PROFILE): 0 entry -> 1 matrix
-role done -> 2 phase A done (block) -> 3 W2 fragments ready -> 4 grid barrier passed -> 5
-BatchNorm finish -> 6 relu(bn(a1)) in LDS -> 7 last Linear2 chain done."""
+role done -> 2 phase A done (block) -> 3 barrier arrival -> 4 grid barrier passed -> 5
+BatchNorm finish + W2 fragments -> 6 relu(bn(a1)) in LDS -> 7 last Linear2 chain done."""
 import argparse
 import ctypes
 import os
@@ -26,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-stamps", action="store_true", help="plain library: time only")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     D = 128
@@ -59,21 +60,26 @@ def main():
              ptr(y), ptr(mask), N, D, g.max_in_degree, lin, 2, s)
 
     lib = _lib.load()
-    buf = (ctypes.c_longlong * (1024 * 16))()
+    buf = (ctypes.c_longlong * (1024 * 24))()
     P = Fn._count("gine_mlp_num_partials", N, D)
-    names = ["matrix role", "phase A sync", "W2 ready", "grid barrier", "BN finish",
+    names = ["matrix role", "phase A sync", "to arrival", "grid barrier", "BN finish + W2",
              "relu pass", "Linear2 chains"]
-    for rep in range(a.reps):
+    for rep in range(0 if a.no_stamps else a.reps):
         run()
         torch.cuda.synchronize()
         lib.gine_debug_layer_prof(buf)
-        full = np.frombuffer(buf, dtype=np.int64).reshape(1024, 16)[:P].astype(np.float64)
+        full = np.frombuffer(buf, dtype=np.int64).reshape(1024, 24).astype(np.float64)
+        # the workgroups of this launch: realtime entry stamps (one clock for all XCDs)
+        # within 1 ms of the latest (the grid can be below P; older rows hold older runs)
+        live = (full[:, 16] > 0) & (full[:, 16] > full[:, 16].max() - 1e5)
+        full = full[live]
         t = full[:, :8]
         rel = t - t[:, 0].min()
         ph = np.diff(t, axis=1)
         if rep < a.reps - 1:
             continue
-        print(f"cfg{a.config}: N={N}, {P} workgroups; s_memtime ticks (last of {a.reps} runs)")
+        print(f"cfg{a.config}: N={N}, {len(full)} workgroups (P = {P}); {TICK_NOTE} (last of "
+              f"{a.reps} runs)")
         print(f"  span entry->last end {rel[:, 7].max():.0f}; entry: median "
               f"{np.median(rel[:, 0]):.0f} max {rel[:, 0].max():.0f}")
         print(f"  barrier arrival (mark 3): median {np.median(rel[:, 3]):.0f} max "
@@ -82,15 +88,26 @@ def main():
         for i, nm in enumerate(names):
             print(f"  {nm:15s} median {np.median(ph[:, i]):8.0f}  p90 "
                   f"{np.percentile(ph[:, i], 90):8.0f}  max {ph[:, i].max():8.0f}")
+        rt = (full[:, 16:20] - full[:, 16].min()) * 10.0  # 100 MHz ticks -> ns
+        print(f"  realtime (ns after the first entry): entry median {np.median(rt[:, 0]):.0f} "
+              f"p90 {np.percentile(rt[:, 0], 90):.0f} max {rt[:, 0].max():.0f}; barrier arrival "
+              f"median {np.median(rt[:, 1]):.0f} max {rt[:, 1].max():.0f}; release min "
+              f"{rt[:, 2].min():.0f} max {rt[:, 2].max():.0f}; end median {np.median(rt[:, 3]):.0f}"
+              f" max {rt[:, 3].max():.0f}")
+        arr = rt[:, 1] - rt[:, 0]
+        print(f"  entry -> arrival (ns): median {np.median(arr):.0f} p90 "
+              f"{np.percentile(arr, 90):.0f} max {arr.max():.0f}; latest-arriving workgroup "
+              f"entered at {rt[np.argmax(rt[:, 1]), 0]:.0f}")
         # phase A detail, relative to each workgroup's entry (mark 0); workgroups with two
         # tiles only for the tile-2 marks
         two = full[:, 11] > full[:, 0]
         print(f"  phase A detail (ticks after entry, median over workgroups; {int(two.sum())} "
               f"with two tiles):")
-        for i, nm in ((8, "W1 planes ready"), (14, "tile 1 gathered"), (9, "tile 1 chain"),
-                      (10, "tile 1 epilogue"), (15, "tile 2 gathered"), (11, "tile 2 chain"),
+        for i, nm in ((8, "W1 planes ready"), (14, "tile 1 gathered"), (20, "tile 1 z ready"),
+                      (9, "tile 1 chain"), (10, "tile 1 epilogue"), (15, "tile 2 gathered"),
+                      (21, "tile 2 z ready"), (11, "tile 2 chain"),
                       (12, "tile 2 epilogue"), (13, "stats in acc"), (1, "matrix role end")):
-            sel = two if i in (11, 12, 15) else np.ones_like(two)
+            sel = two if i in (11, 12, 15, 21) else np.ones_like(two)
             d = full[sel, i] - full[sel, 0]
             print(f"    {nm:16s} median {np.median(d):8.0f}  p90 {np.percentile(d, 90):8.0f}")
     # a reference: HIP-event time of the launch
