@@ -388,6 +388,17 @@ def time_kernels(tr: Trainer, reps: int):
         kernels["gine_mlp_bwd_pair_acc"] = (mlp_bwd_pair_acc, {
             "flops": 4 * N * D * D, "bytes": 25 * N * D})
 
+        if Fn.layer_backward_ok(N, D):  # the pair in one launch, as the step runs it
+            lbacc = torch.zeros(Fn._count64("gine_bn_acc_words", D), dtype=torch.int64,
+                                device=dev)
+
+            def mlp_bwd_layer():
+                call("gine_mlp_bwd_layer", ptr(dz), None, ptr(mask), ptr(a1), ptr(bn_save),
+                     ptr(w2), ptr(dbn), ptr(lbacc), ptr(bn.weight), ptr(dg), ptr(dbt),
+                     ptr(coef), ptr(w1), ptr(dx), N, D, 2, S[0])
+            kernels["gine_mlp_bwd_layer"] = (mlp_bwd_layer, {
+                "flops": 4 * N * D * D, "bytes": 25 * N * D})
+
     if Fn.engine_in_mp_ok(g, D):  # what the training step's backward runs at this size
         # bytes: the message-passing backward's B_b (dz, x, dx, CSR, dres = dy) + the
         # engine's other operands read once (mask u8, dbn, a1, z) + its fp32 slab
@@ -462,6 +473,7 @@ def sec8d_launch_work(name: str, w: dict) -> dict:
         "gine_mp_fwd_mlp1": {"bytes": w["B_f"], "flops": half_fwd},
         "gine_mp_fwd_layer": {"bytes": w["B_f"], "flops": 2 * half_fwd},
         "gine_mlp_bwd_pair_acc": {"flops": 2 * half_bwd},
+        "gine_mlp_bwd_layer": {"flops": 2 * half_bwd},
         "gine_mp_bwd_mlp_wgrad": {"bytes": w["B_b"], "flops": 2 * half_bwd},
         "gine_mlp_fwd1": {"flops": half_fwd}, "gine_mlp_fwd2": {"flops": half_fwd},
         "gine_mlp_bwd2": {"flops": half_bwd}, "gine_mlp_bwd1": {"flops": half_bwd},
@@ -487,6 +499,8 @@ def roofline_for(kernels: dict, layers: int, work: dict, config: str = "cfg2"):
         step += ["gine_mp_fwd_layer"]
     if "gine_mlp_bwd_pair_acc" in kernels:  # (two launches: a pair, not a roofline line)
         step = [k for k in step if k not in ("gine_mlp_bwd2", "gine_mlp_bwd1")]
+    if "gine_mlp_bwd_layer" in kernels:  # the pair in one launch
+        step += ["gine_mlp_bwd_layer"]
     timed = [k for k in step if k in kernels]
     dominant = max(timed, key=lambda k: kernels[k]["us"])
     out = roof_of(dominant, kernels[dominant], layers, work, config)

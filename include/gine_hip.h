@@ -30,11 +30,12 @@
 extern "C" {
 #endif
 
-#define GINE_ABI_VERSION 5  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
+#define GINE_ABI_VERSION 6  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
                               3: gine_deepset_bwd_num_partials takes the hidden width;
                               4: bn_acc grows two grid-barrier words (gine_mp_fwd_layer);
                               5: grid-barrier failure count (gine_bn_acc_barrier_failures_index),
-                                 gine_mlp_bwd_layer removed */
+                                 gine_mlp_bwd_layer removed;
+                              6: gine_mlp_bwd_layer again, in the forward layer's role-split form */
 
 #define GINE_OK 0
 #define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
@@ -352,6 +353,26 @@ int gine_mlp_bwd1_bn(const float* dbn, const float* a1, const float* bn_save, in
                      const float* gamma, float* dgamma, float* dbeta, float* coef,
                      const float* w1, float* dz, int64_t num_nodes, int32_t channels,
                      void* stream);
+/* The backward pair in ONE launch (csrc/gine_mlpbwd.hip k_mlp_bwd_layer; replaces
+ * gine_mlp_bwd2_acc followed by gine_mlp_bwd1_bn, models/gnn.py:21-26 autograd): phase A =
+ * dbn and the BatchNorm-backward sums, grid barrier, phase B = coef (workgroup 0 also writes
+ * coef, dgamma, dbeta) and dz = da1 W1 -- both row tiles of a workgroup stay in LDS, W1 is
+ * loaded under phase A.  Same outputs, bit for bit, as the pair (dbn, dz, coef, dgamma,
+ * dbeta) and the same pairing protocol on bn_acc (the backward accumulator); a barrier that
+ * cannot complete is counted at gine_bn_acc_barrier_failures_index and makes that launch's
+ * coef / dz NaN.  Applies where gine_mlp_bwd_layer_ok says so: channels = 128, at most 2
+ * row tiles per workgroup and the whole grid resident at once (occupancy query, cached per
+ * device); GINE_ERR_INVALID otherwise.  gamma, dgamma, dbeta may be NULL; y (GINE_EPI_RELU)
+ * and mask (GINE_EPI_RESIDUAL_RELU) as for gine_mlp_bwd2. */
+int gine_mlp_bwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t* ok);
+int gine_mlp_bwd_layer(const float* dy, const float* y, const uint8_t* mask, const float* a1,
+                       const float* bn_save, const float* w2, float* dbn, int64_t* bn_acc,
+                       const float* gamma, float* dgamma, float* dbeta, float* coef,
+                       const float* w1, float* dz, int64_t num_nodes, int32_t channels,
+                       int32_t epilogue, void* stream);
+/* Testing only: `extra` workgroups added to every later gine_mlp_bwd_layer grid (0 restores
+ * production), for the barrier-failure test. */
+int gine_testing_bwd_layer_extra_workgroups(int32_t extra);
 int gine_mlp_fwd1_acc(const float* z, const float* w1, const float* b1, float* a1,
                       double* partials, int64_t* bn_acc, int64_t num_nodes, int32_t channels,
                       void* stream);

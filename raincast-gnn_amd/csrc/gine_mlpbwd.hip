@@ -1,0 +1,476 @@
+// The node-MLP backward of a GINE layer in one launch (gine_mlp_bwd_layer), D = 128:
+//   phase A = gine_mlp_bwd2_acc: do = PRO(dy) (residual mask / ReLU of y / none),
+//             dbn = (do W2) * 1[bn(a1) > 0], the BatchNorm-backward sums
+//             [sum dbn | sum dbn * xhat] into the fixed-point accumulator (gine_bnacc.hpp);
+//   grid barrier (every workgroup resident: one per CU, host-checked);
+//   phase B = gine_mlp_bwd1_bn: coef = [c1 | c2 | c3] from the totals (workgroup 0 also
+//             writes coef, dgamma, dbeta and the consumed phase), da1 = c1 dbn + c2 xhat + c3,
+//             dz = da1 W1.
+// Replaces models/gnn.py:21-26's autograd through Linear2 -> ReLU -> BatchNorm1d -> Linear1
+// (torch: addmm backward, threshold_backward, native_batch_norm_backward, addmm backward),
+// which the two launches above run with a launch boundary where this one has a barrier.
+// Same layout as the one-launch forward (gine_mpmlp.hip): 768 threads, waves 0-3 multiply
+// ("matrix"), waves 4-11 stage ("helpers"):
+//   * the helpers stage both of the workgroup's tiles at once -- do into x[t], the a1 rows
+//     into o[t] -- and W2 (then W1, loaded under phase A's chains) through the padded LDS
+//     image w;
+//   * the matrix waves keep the weight planes in registers (split-bf16 chain of the row GEMM,
+//     gine_bf16x3.hpp), transpose each 32x32 accumulator block through a tile of their own
+//     and finish the EPI_DBN epilogue in place: dbn overwrites the a1 rows in o[t] (and goes
+//     to HBM for the weight-gradient engine);
+//   * after the barrier the helpers read the totals beside the matrix waves' W1 fragments,
+//     then stage da1 into x[t].
+// Bit-identical to the pair: same tile -> workgroup map (xcd tile ranges, grid =
+// gine_mlp_num_partials), the same chains (k order, NaN redo on the fp32 chain), the same
+// epilogue and prologue arithmetic, the per-workgroup sums in the row GEMM's order (row groups
+// r % 8, then the 8 groups in order), integer totals.
+#include "gine_common.hpp"
+#include "gine_mlpsrc.hpp"
+#include "gine_bnacc.hpp"
+#include "gine_bf16x3.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+
+namespace gine {
+namespace {
+
+constexpr int kD = 128, kD4 = kD / 4, kLD = kD + 4, kKS = kD / 2;
+constexpr int kRows = 32;                 // rows per tile
+constexpr int kMat = 256;                 // waves 0-3
+constexpr int kThreads = 768;             // + waves 4-11
+constexpr int kHelp = kThreads - kMat;    // 512 helper threads
+constexpr int kTiles = 2;                 // tiles a workgroup holds
+constexpr int kTLD = 36;                  // per-wave transposition tile row (floats)
+constexpr int kItems = kRows * kD4 / kHelp;  // float4 items per helper thread per tile (2)
+constexpr int kWPer = kD * kD4 / kHelp;      // float4 of a weight per helper thread (8)
+static_assert(kItems == 2 && kWPer == 8 && kTiles == 2, "staging shares");
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct BwdLayerArgs {
+  const float* dy;
+  const float* y;        // PRO_DOR
+  const uint8_t* mask;   // PRO_DOM
+  const float* a1;
+  const float* bn_save;  // [mean | invstd | alpha | shift]
+  const float* W2;
+  const float* W1;
+  const float* gamma;
+  float* dbn;
+  float* dz;
+  float* coef;
+  float* dgamma;
+  float* dbeta;
+  long long* acc;
+  int N, num_tiles;
+};
+
+struct BwdLayerLds {
+  float w[kD * kLD];              // W2 image; per-wave transposition tiles + sums; W1 image
+  float x[kTiles][kRows * kLD];   // staged A operands: do (phase A), da1 (phase B)
+  float o[kTiles][kRows * kLD];   // a1 rows, overwritten in place by dbn
+  float bnp[4 * kD];              // bn_save: mean | invstd | alpha | shift
+  double tot[2 * kD];
+  float coef[3 * kD];
+  int barrier_failed;
+};
+static_assert(4 * 32 * kTLD * 4 + 2 * 8 * kD * 8 <= kD * kLD * 4, "scratch fits in w");
+
+// The row GEMM's tile -> workgroup assignment (gine_mlp.hip xcd_tile_range).
+struct Tiles {
+  int first, end, step;
+  __device__ int count() const { return first < end ? (end - first + step - 1) / step : 0; }
+  __device__ int at(int k) const { return first + k * step; }
+};
+__device__ __forceinline__ Tiles tiles_of(int num_tiles, int vb, int nb) {
+  const int xcd = vb % kNumXcd, pos = vb / kNumXcd;
+  const int here = nb / kNumXcd + (xcd < nb % kNumXcd ? 1 : 0);
+  const int span = (num_tiles + kNumXcd - 1) / kNumXcd;
+  const int b = xcd * span;
+  return Tiles{b + pos, min(num_tiles, b + span), here};
+}
+
+// A weight (row-major [D][D], 16 KB-float image) staged by the helpers: 8 float4 per thread.
+struct WRegs {
+  float4 v0, v1, v2, v3, v4, v5, v6, v7;
+  __device__ __forceinline__ void load(const float4* __restrict__ w4, int p) {
+    v0 = w4[p]; v1 = w4[p + kHelp]; v2 = w4[p + 2 * kHelp]; v3 = w4[p + 3 * kHelp];
+    v4 = w4[p + 4 * kHelp]; v5 = w4[p + 5 * kHelp]; v6 = w4[p + 6 * kHelp];
+    v7 = w4[p + 7 * kHelp];
+  }
+  __device__ __forceinline__ void put(float* w, int idx, float4 v) const {
+    *reinterpret_cast<float4*>(&w[(idx / kD4) * kLD + 4 * (idx % kD4)]) = v;
+  }
+  __device__ __forceinline__ void store(float* w, int p) const {
+    put(w, p, v0); put(w, p + kHelp, v1); put(w, p + 2 * kHelp, v2); put(w, p + 3 * kHelp, v3);
+    put(w, p + 4 * kHelp, v4); put(w, p + 5 * kHelp, v5); put(w, p + 6 * kHelp, v6);
+    put(w, p + 7 * kHelp, v7);
+  }
+};
+
+// dX = dY W fragments (B[k][j] = W[k][j]): lane half h takes k in [h*64, h*64 + 64) of
+// column col, read down the staged image (the row GEMM's BT = false fragment).
+__device__ __forceinline__ void w_fragments(const float* w, int col, int h, float (&bf)[kKS]) {
+#pragma unroll
+  for (int s = 0; s < kKS; ++s) bf[s] = w[(h * kKS + s) * kLD + col];
+}
+
+// One 32x32 block of a tile: A = the staged rows, B = the lane's weight planes; a wave whose
+// accumulators see a NaN redoes it on the fp32 chain from W in global memory.
+__device__ __forceinline__ floatx16 chain(const float* x, const BPlanes<kKS>& bp,
+                                          const float* __restrict__ W, int col, int h, int c32) {
+  const float* arow = x + c32 * kLD + h * kKS;
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int s = 0; s < kKS / 8; ++s) {
+    const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);
+    const float4 a1 = *reinterpret_cast<const float4*>(&arow[8 * s + 4]);
+    acc = mfma_bf16x3(split8(a0, a1), bp.f[s], acc);
+  }
+  if (wave_any_nan(acc)) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    acc = mfma_f32_row_mem<kKS>(arow, W + (size_t)h * kKS * kD + col, kD, acc);
+  }
+  return acc;
+}
+
+// this wave's 32x32 block -> row-major through its own LDS tile
+__device__ __forceinline__ void transpose_in(float* tt, const floatx16& acc, int h, int c32) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tt[((r & 3) + 8 * (r >> 2) + 4 * h) * kTLD + c32] = acc[r];
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int PRO>
+__global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
+  __shared__ __attribute__((aligned(16))) BwdLayerLds L;
+  const Tiles ts = tiles_of(A.num_tiles, blockIdx.x, gridDim.x);
+  const int nt = ts.count();
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const bool mat = wave < kMat / kWave;
+  const int lane = tid % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int cq = lane & 7, grp = lane >> 3;  // transposed epilogue: 4-column chunk, row group
+  const int col = 32 * wave + c32;           // (matrix waves)
+  const int p = tid - kMat;                   // (helpers)
+  long long* phw = bnacc_phase(A.acc, 2 * kD);
+  // written by earlier launches only (workgroup 0 moves them after the barrier)
+  const long long ph = phw[0] + 1, consumed = phw[1 + ((ph - 1) & 1)];
+  const BnView bv = bn_view(A.bn_save, kD);
+  float* tt = &L.w[wave * 32 * kTLD];
+
+  // ---- phase A staging: W2 and both tiles (helpers) ----
+  if (!mat) {
+    WRegs w2;
+    w2.load(reinterpret_cast<const float4*>(A.W2), p);
+    ProArgs pa{A.dy, A.y, A.mask, nullptr, nullptr};
+    RawItem raw[kTiles][kItems];
+    float4 a1v[kTiles][kItems];
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+      for (int j = 0; j < kItems; ++j) {
+        const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
+        int64_t n = (int64_t)ts.at(t < nt ? t : 0) * kRows + r;
+        n = n < A.N ? n : A.N - 1;
+        raw[t][j] = raw_load<PRO>(pa, kD, n, q);
+        a1v[t][j] = *reinterpret_cast<const float4*>(A.a1 + n * kD + 4 * q);
+      }
+    w2.store(L.w, p);
+    if (p < kD) *reinterpret_cast<float4*>(&L.bnp[4 * p]) =
+        *reinterpret_cast<const float4*>(A.bn_save + 4 * p);
+    const ColConst kc{};
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+      for (int j = 0; j < kItems; ++j) {
+        const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
+        float4 v = transform<PRO>(pa, raw[t][j], kc);
+        if (t >= nt || (int64_t)ts.at(t) * kRows + r >= A.N) v = f4_zero();
+        *reinterpret_cast<float4*>(&L.x[t][r * kLD + 4 * q]) = v;
+        *reinterpret_cast<float4*>(&L.o[t][r * kLD + 4 * q]) = a1v[t][j];
+      }
+  }
+  __syncthreads();  // S1: W2 and the tiles staged
+
+  if (mat) {
+    // ---- phase A: dbn = (do W2) * 1[bn(a1) > 0], BatchNorm-backward sums ----
+    float bf[kKS];
+    w_fragments(L.w, col, h, bf);
+    BPlanes<kKS> bp;
+    bp.from(bf);
+    __syncthreads();  // S2: every wave's fragment reads of w are done (transposition tiles)
+    const int c0 = 32 * wave + 4 * cq;
+    double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < nt; ++t) {
+      const floatx16 acc = chain(L.x[t], bp, A.W2, col, h, c32);
+      transpose_in(tt, acc, h, c32);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = grp + 8 * i;
+        const int64_t n = (int64_t)ts.at(t) * kRows + row;
+        const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * cq]);
+        if (n >= A.N) continue;
+        float* slot = &L.o[t][row * kLD + c0];
+        const float4 a14 = *reinterpret_cast<const float4*>(slot);
+        // the BatchNorm constants of these columns from LDS each row (in registers they
+        // pushed the weight planes into scratch)
+        const float4 mu4 = *reinterpret_cast<const float4*>(&L.bnp[c0]);
+        const float4 is4 = *reinterpret_cast<const float4*>(&L.bnp[kD + c0]);
+        const float4 al4 = *reinterpret_cast<const float4*>(&L.bnp[2 * kD + c0]);
+        const float4 sh4 = *reinterpret_cast<const float4*>(&L.bnp[3 * kD + c0]);
+        const float al[4] = {al4.x, al4.y, al4.z, al4.w}, sh[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+        const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        const float a1[4] = {a14.x, a14.y, a14.z, a14.w};
+        float o4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // EPI_DBN of the row GEMM
+          const float bn = bn_apply(a1[k], al[k], sh[k]);
+          o4[k] = (bn > 0.f) ? vv[k] : 0.f;
+          const double xhat = (double)((a1[k] - mu[k]) * is[k]);
+          st1[k] += (double)o4[k];
+          st2[k] += (double)o4[k] * xhat;
+        }
+        const float4 ov = make_float4(o4[0], o4[1], o4[2], o4[3]);
+        *reinterpret_cast<float4*>(slot) = ov;
+        *reinterpret_cast<float4*>(A.dbn + n * kD + c0) = ov;
+      }
+      __builtin_amdgcn_wave_barrier();  // the next tile's transposition writes come after
+    }
+    // per-column sums: the 8 row groups added in fixed order (row-tile GEMM order)
+    double* sr = reinterpret_cast<double*>(&L.w[4 * 32 * kTLD]);  // [2][8][kD]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sr[(0 * 8 + grp) * kD + c0 + k] = st1[k];
+      sr[(1 * 8 + grp) * kD + c0 + k] = st2[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int which = lane >> 5, cc = 32 * wave + (lane & 31);
+    double s = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += sr[(which * 8 + g) * kD + cc];
+    bnacc_add<false>(A.acc, 2 * kD, which * kD + cc, s);
+    // the atomics are performed before this workgroup arrives at the grid barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // S3: phase A's use of w is over
+  } else {
+    __syncthreads();  // S2
+    // W1 and phase B's a1 rows, in flight under phase A's chains
+    WRegs w1;
+    w1.load(reinterpret_cast<const float4*>(A.W1), p);
+    // (named registers: an array held across the barrier went to scratch)
+    auto a1_at = [&](int t, int j) {
+      const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
+      int64_t n = (int64_t)ts.at(t < nt ? t : 0) * kRows + r;
+      n = n < A.N ? n : A.N - 1;
+      return *reinterpret_cast<const float4*>(A.a1 + n * kD + 4 * q);
+    };
+    const float4 a1b00 = a1_at(0, 0), a1b01 = a1_at(0, 1), a1b10 = a1_at(1, 0),
+                 a1b11 = a1_at(1, 1);
+    __syncthreads();  // S3
+    w1.store(L.w, p);
+    // a1 for phase B's prologue goes to the x tiles' slots it will be combined with: x[t] is
+    // free (phase A's chains are done) and each helper later reads back exactly the items it
+    // wrote
+    auto stash = [&](int t, int j, float4 v) {
+      const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
+      *reinterpret_cast<float4*>(&L.x[t][r * kLD + 4 * q]) = v;
+    };
+    stash(0, 0, a1b00);
+    stash(0, 1, a1b01);
+    stash(1, 0, a1b10);
+    stash(1, 1, a1b11);
+  }
+
+  if (tid == 0)
+    L.barrier_failed = grid_barrier(bnacc_barrier(A.acc, 2 * kD), gridDim.x) ? 0 : 1;
+  __syncthreads();  // S4: barrier passed; W1 staged
+  // a timed-out barrier (the grid was not co-resident): the totals are incomplete, so this
+  // workgroup's coefficients and outputs are NaN; the failure word tells the host
+  const bool failed = L.barrier_failed != 0;
+
+  // ---- phase B: coef from the totals (helpers) beside W1's fragments (matrix) ----
+  float bf1[kKS];
+  BPlanes<kKS> bp1;
+  if (mat) {
+    w_fragments(L.w, col, h, bf1);
+    bp1.from(bf1);
+  } else if (p < 2 * kD) {
+    const double t = bnacc_total<true>(A.acc, 2 * kD, p, blockIdx.x == 0, ph, consumed);
+    L.tot[p] = failed ? __builtin_nan("") : t;
+  }
+  __syncthreads();  // S5
+  if (!mat && p < kD) {  // the arithmetic of k_bwd1_bnacc's prologue
+    const double sd = L.tot[p], sx = L.tot[kD + p];
+    const double g = A.gamma ? (double)A.gamma[p] : 1.0;
+    const double c1 = g * (double)bv.invstd[p];
+    const float k1 = (float)c1, k2 = (float)(-c1 * sx / (double)A.N),
+                k3 = (float)(-c1 * sd / (double)A.N);
+    L.coef[p] = k1;
+    L.coef[kD + p] = k2;
+    L.coef[2 * kD + p] = k3;
+    if (blockIdx.x == 0) {
+      if (A.dgamma) A.dgamma[p] = (float)sx;
+      if (A.dbeta) A.dbeta[p] = (float)sd;
+      A.coef[p] = k1;
+      A.coef[kD + p] = k2;
+      A.coef[2 * kD + p] = k3;
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    phw[0] = ph;
+    phw[1 + (ph & 1)] = ph;  // bnacc_mark_consumed
+  }
+  __syncthreads();  // S6: coef in LDS
+  if (!mat) {  // da1 = PRO_DA1(dbn) into x[t] (rows past N zero, as the row GEMM stages them)
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t)
+#pragma unroll
+      for (int j = 0; j < kItems; ++j) {
+        const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
+        float* xs = &L.x[t][r * kLD + 4 * q];
+        RawItem ri;
+        ri.v = *reinterpret_cast<const float4*>(&L.o[t][r * kLD + 4 * q]);
+        ri.aux = *reinterpret_cast<const float4*>(xs);
+        ri.m = make_uchar4(1, 1, 1, 1);
+        ColConst kc;
+        kc.a = *reinterpret_cast<const float4*>(&L.coef[4 * q]);
+        kc.b = *reinterpret_cast<const float4*>(&L.coef[kD + 4 * q]);
+        kc.c = *reinterpret_cast<const float4*>(&L.coef[2 * kD + 4 * q]);
+        kc.d = *reinterpret_cast<const float4*>(&L.bnp[4 * q]);
+        kc.e = *reinterpret_cast<const float4*>(&L.bnp[kD + 4 * q]);
+        const ProArgs pa{};
+        float4 v = transform<PRO_DA1>(pa, ri, kc);
+        if (t >= nt || (int64_t)ts.at(t) * kRows + r >= A.N) v = f4_zero();
+        *reinterpret_cast<float4*>(xs) = v;
+      }
+  }
+  __syncthreads();  // S7: da1 staged
+  if (mat) {  // dz = da1 W1 (EPI_PLAIN)
+    const int c0 = 32 * wave + 4 * cq;
+    for (int t = 0; t < nt; ++t) {
+      const floatx16 acc = chain(L.x[t], bp1, A.W1, col, h, c32);
+      transpose_in(tt, acc, h, c32);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = grp + 8 * i;
+        const int64_t n = (int64_t)ts.at(t) * kRows + row;
+        const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * cq]);
+        if (n < A.N) *reinterpret_cast<float4*>(A.dz + n * kD + c0) = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+int bwd_layer_capacity() {
+  static std::mutex mu;
+  static int cap[64];
+  static bool known[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!known[dev]) {
+    int cus = 0, c = 1 << 30;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    const void* ks[] = {(const void*)k_mlp_bwd_layer<PRO_PLAIN>,
+                        (const void*)k_mlp_bwd_layer<PRO_DOR>,
+                        (const void*)k_mlp_bwd_layer<PRO_DOM>};
+    for (const void* k : ks) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess)
+        return 0;
+      c = std::min(c, nb * cus);
+    }
+    cap[dev] = c;
+    known[dev] = true;
+  }
+  return cap[dev];
+}
+
+// Largest number of tiles one workgroup walks (tiles_of).
+int max_tiles(int tiles, int grid) {
+  const int span = (tiles + kNumXcd - 1) / kNumXcd;
+  int worst = 0;
+  for (int xcd = 0; xcd < kNumXcd; ++xcd) {
+    const int here = grid / kNumXcd + (xcd < grid % kNumXcd ? 1 : 0);
+    const int range = std::max(0, std::min(tiles, (xcd + 1) * span) - xcd * span);
+    if (range > 0 && here == 0) return 1 << 30;
+    if (range > 0) worst = std::max(worst, (range + here - 1) / here);
+  }
+  return worst;
+}
+
+// gine_testing_bwd_layer_extra_workgroups: workgroups added to the grid (0 in production),
+// for the test of the grid barrier's failure path
+std::atomic<int> g_bwd_layer_extra{0};
+
+bool bwd_layer_ok(int64_t num_nodes, int32_t channels) {
+  if (channels != kD || num_nodes <= 0 || num_nodes * channels * 4 >= (int64_t(1) << 32))
+    return false;
+  int32_t grid = 0;
+  if (gine_mlp_num_partials(num_nodes, channels, &grid) != GINE_OK) return false;
+  const int tiles = (int)ceil_div(num_nodes, kRows);
+  return grid <= bwd_layer_capacity() && max_tiles(tiles, grid) <= kTiles;
+}
+
+}  // namespace
+}  // namespace gine
+
+using namespace gine;
+
+extern "C" int gine_testing_bwd_layer_extra_workgroups(int32_t extra) {
+  if (extra < 0 || extra > 4096) return GINE_ERR_INVALID;
+  g_bwd_layer_extra.store(extra);
+  return GINE_OK;
+}
+
+extern "C" int gine_mlp_bwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t* ok) {
+  if (!ok) return GINE_ERR_INVALID;
+  *ok = bwd_layer_ok(num_nodes, channels) ? 1 : 0;
+  return GINE_OK;
+}
+
+extern "C" int gine_mlp_bwd_layer(const float* dy, const float* y, const uint8_t* mask,
+                                  const float* a1, const float* bn_save, const float* w2,
+                                  float* dbn, int64_t* bn_acc, const float* gamma,
+                                  float* dgamma, float* dbeta, float* coef, const float* w1,
+                                  float* dz, int64_t num_nodes, int32_t channels,
+                                  int32_t epilogue, void* stream) {
+  if (channels != kD) return GINE_ERR_DIM;
+  if (!dy || !a1 || !bn_save || !w2 || !dbn || !bn_acc || !coef || !w1 || !dz)
+    return GINE_ERR_INVALID;
+  if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RELU && !y) return GINE_ERR_INVALID;
+  if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
+  if (!bwd_layer_ok(num_nodes, channels)) return GINE_ERR_INVALID;
+  int32_t grid = 0;
+  const int st = gine_mlp_num_partials(num_nodes, channels, &grid);
+  if (st != GINE_OK) return st;
+  grid += g_bwd_layer_extra.load();
+  const BwdLayerArgs A{dy,  y,    mask,  a1,     bn_save, w2, w1, gamma,
+                       dbn, dz,   coef,  dgamma, dbeta,   reinterpret_cast<long long*>(bn_acc),
+                       (int)num_nodes, (int)ceil_div(num_nodes, kRows)};
+  hipStream_t s = as_stream(stream);
+  switch (epilogue) {
+    case GINE_EPI_NONE:
+      hipLaunchKernelGGL(k_mlp_bwd_layer<PRO_PLAIN>, dim3((unsigned)grid), dim3(kThreads), 0, s,
+                         A);
+      break;
+    case GINE_EPI_RELU:
+      hipLaunchKernelGGL(k_mlp_bwd_layer<PRO_DOR>, dim3((unsigned)grid), dim3(kThreads), 0, s, A);
+      break;
+    default:
+      hipLaunchKernelGGL(k_mlp_bwd_layer<PRO_DOM>, dim3((unsigned)grid), dim3(kThreads), 0, s, A);
+  }
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}

@@ -54,6 +54,7 @@ enum IntOpt {
   kLayer,          // gine_mp_fwd_layer applies
   kMaxInDegree,
   kEngine,         // gine_mp_bwd_win_mlp_wgrad applies (functional.engine_in_mp_ok)
+  kLayerBwd,       // gine_mlp_bwd_layer applies (functional.layer_backward_ok)
   // the window plans' scalars, kPlanFields each: num_tiles (0: no plan), slice_channels,
   // max_rows, max_edges, max_nodes -- the plan's device arrays come in the graph list, so the
   // autograd node holds them (a plan's addresses alone would dangle once the graph cache
@@ -303,15 +304,26 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
       const Tensor& bacc = sv[20];  // the BatchNorm-backward accumulator (undefined: partials)
       if (bacc.defined()) {
         ZeroOnError guard{bacc};
-        ok(gine_mlp_bwd2_acc((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
-                             (const float*)P(a1), (const float*)P(bn_save), (const float*)P(w2c),
-                             (float*)P(dbn), nullptr, (int64_t*)P(bacc), N, D, epi, s),
-           "gine_mlp_bwd2_acc");
-        ok(gine_mlp_bwd1_bn((const float*)P(dbn), (const float*)P(a1), (const float*)P(bn_save),
-                            (int64_t*)P(bacc), (const float*)P(g), (float*)P(dgamma),
-                            (float*)P(dbeta), (float*)P(coef), (const float*)P(w1c),
-                            (float*)P(dz), N, D, s),
-           "gine_mlp_bwd1_bn");
+        if (io[kLayerBwd]) {  // the pair in one launch (grid barrier)
+          ok(gine_mlp_bwd_layer((const float*)P(dy), (const float*)P(y),
+                                (const uint8_t*)P(mask), (const float*)P(a1),
+                                (const float*)P(bn_save), (const float*)P(w2c), (float*)P(dbn),
+                                (int64_t*)P(bacc), (const float*)P(g), (float*)P(dgamma),
+                                (float*)P(dbeta), (float*)P(coef), (const float*)P(w1c),
+                                (float*)P(dz), N, D, epi, s),
+             "gine_mlp_bwd_layer");
+        } else {
+          ok(gine_mlp_bwd2_acc((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),
+                               (const float*)P(a1), (const float*)P(bn_save),
+                               (const float*)P(w2c), (float*)P(dbn), nullptr, (int64_t*)P(bacc),
+                               N, D, epi, s),
+             "gine_mlp_bwd2_acc");
+          ok(gine_mlp_bwd1_bn((const float*)P(dbn), (const float*)P(a1),
+                              (const float*)P(bn_save), (int64_t*)P(bacc), (const float*)P(g),
+                              (float*)P(dgamma), (float*)P(dbeta), (float*)P(coef),
+                              (const float*)P(w1c), (float*)P(dz), N, D, s),
+             "gine_mlp_bwd1_bn");
+        }
         guard.armed = false;
       } else {
         ok(gine_mlp_bwd2((const float*)P(dy), (const float*)P(y), (const uint8_t*)P(mask),

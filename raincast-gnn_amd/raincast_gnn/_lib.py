@@ -23,7 +23,7 @@ GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
-ABI_VERSION = 5
+ABI_VERSION = 6
 COUNT_PARTS = 64  # GINE_COUNT_PARTS
 
 _c_void_p = ctypes.c_void_p
@@ -100,6 +100,9 @@ _SIGNATURES = {
     "gine_testing_layer_extra_workgroups": [_i32],
     "gine_mlp_bwd2_acc": [_c_void_p] * 9 + [_i64, _i32, _i32, _c_void_p],
     "gine_mlp_bwd1_bn": [_c_void_p] * 10 + [_i64, _i32, _c_void_p],
+    "gine_mlp_bwd_layer_ok": [_i64, _i32, ctypes.POINTER(_i32)],
+    "gine_mlp_bwd_layer": [_c_void_p] * 14 + [_i64, _i32, _i32, _c_void_p],
+    "gine_testing_bwd_layer_extra_workgroups": [_i32],
     "gine_bn_fwd_finalize": [_c_void_p, _i32] + [_c_void_p] * 6 + [_i64, _i32, _f32, _f32, _i32,
                                                                    _i32, _c_void_p],
     "gine_mlp_fwd2": [_c_void_p] * 7 + [_i64, _i32, _i32, _c_void_p],

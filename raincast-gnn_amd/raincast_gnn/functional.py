@@ -277,6 +277,25 @@ def layer_forward_ok(N: int, D: int, max_in_degree) -> bool:
     return ok
 
 
+_LAYER_BWD_OK = {}
+
+
+def layer_backward_ok(N: int, D: int) -> bool:
+    """gine_mlp_bwd_layer applies (include/gine_hip.h: D = 128, at most two row tiles per
+    workgroup, the whole grid resident at once); off when other ranks share this GPU, for
+    the reason layer_forward_ok gives."""
+    if not options.LAYER_BWD or layer_policy_key():
+        return False
+    dev = torch.cuda.current_device()
+    key = (dev, N, D)
+    ok = _LAYER_BWD_OK.get(key)
+    if ok is None:
+        out = ctypes.c_int32(0)
+        call("gine_mlp_bwd_layer_ok", N, D, ctypes.byref(out))
+        ok = _LAYER_BWD_OK[key] = bool(out.value)
+    return ok
+
+
 _BN_ACC = weakref.WeakKeyDictionary()
 
 
@@ -300,16 +319,15 @@ _FAIL_INDEX: dict = {}
 
 
 def check_grid_barriers() -> None:
-    """Raise GineError if a one-launch layer forward's grid barrier timed out since the last
-    check (gine_bn_acc_barrier_failures_index: the grid was not resident at once, so that
-    launch's outputs are NaN in the failed workgroups' rows).  The affected accumulators are
-    re-zeroed, so the next step starts a fresh pairing.  Reads device memory: call it where
-    the caller synchronises anyway (end of an epoch, after a benchmark's timed steps)."""
+    """Raise GineError if a one-launch layer forward's or backward's grid barrier timed out
+    since the last check (gine_bn_acc_barrier_failures_index: the grid was not resident at
+    once, so that launch's outputs are NaN in the failed workgroups' rows).  The affected
+    accumulators are re-zeroed, so the next step starts a fresh pairing.  Reads device
+    memory: call it where the caller synchronises anyway (end of an epoch, after a
+    benchmark's timed steps)."""
     failed = []
     for mod, per_dev in list(_BN_ACC.items()):
         for (dev, kind), acc in list(per_dev.items()):
-            if kind != "fwd":
-                continue
             D = mod.num_features
             idx = _FAIL_INDEX.get(D)
             if idx is None:
@@ -318,14 +336,15 @@ def check_grid_barriers() -> None:
                 idx = _FAIL_INDEX[D] = int(out.value)
             n = int(acc[idx].item())
             if n:
-                failed.append((type(mod).__name__, str(dev), n))
+                failed.append((type(mod).__name__, kind, str(dev), n))
                 acc.zero_()
     if failed:
         raise _lib.GineError(
-            "gine_mp_fwd_layer: the grid barrier timed out (the launch's workgroups were not "
-            f"all resident at once: other work held CUs) -- {failed} (module, device, "
-            "workgroups); those launches' outputs are NaN in the failed workgroups' rows and "
-            "the running statistics were not updated; the accumulators were reset")
+            "gine_mp_fwd_layer / gine_mlp_bwd_layer: the grid barrier timed out (the launch's "
+            f"workgroups were not all resident at once: other work held CUs) -- {failed} "
+            "(module, fwd|bwd, device, workgroups); those launches' outputs are NaN in the "
+            "failed workgroups' rows and the running statistics were not updated; the "
+            "accumulators were reset")
 
 
 class _paired:
@@ -479,11 +498,17 @@ class GineLayer(torch.autograd.Function):
                      ptr(dz), N, D, stream)
             else:
                 with _paired(acc):  # producer + consumer back to back
-                    call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1),
-                         ptr(bn_save), ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi, stream)
-                    call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc),
-                         ptr(g), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz), N, D,
-                         stream)
+                    if layer_backward_ok(N, D):  # the pair in one launch (grid barrier)
+                        call("gine_mlp_bwd_layer", ptr(dy), ptr(y), ptr(mask), ptr(a1),
+                             ptr(bn_save), ptr(w2c), ptr(dbn), ptr(acc), ptr(g), ptr(dgamma),
+                             ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz), N, D, epi, stream)
+                    else:
+                        call("gine_mlp_bwd2_acc", ptr(dy), ptr(y), ptr(mask), ptr(a1),
+                             ptr(bn_save), ptr(w2c), ptr(dbn), None, ptr(acc), N, D, epi,
+                             stream)
+                        call("gine_mlp_bwd1_bn", ptr(dbn), ptr(a1), ptr(bn_save), ptr(acc),
+                             ptr(g), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(w1c), ptr(dz),
+                             N, D, stream)
             engine = (dy, y, mask, a1, bn_save, dbn, coef, z, slab, epi)
         else:
             # dz = da1 W1 and the dW1, dW2 partial slabs side by side in one launch

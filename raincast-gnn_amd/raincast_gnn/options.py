@@ -20,6 +20,9 @@ BN_ACC_BWD   the same for the BatchNorm backward sums.
 LAYER_FWD    True: where the fused forward and the accumulator apply and the grid fits the
              device at once, the whole layer forward in one launch (gine_mp_fwd_layer: the
              fused forward and the second GEMM separated by a grid barrier); False: the pair.
+LAYER_BWD    True: where the backward accumulator applies and the grid fits the device at
+             once, the node-MLP backward in one launch (gine_mlp_bwd_layer: the dbn GEMM and
+             the dz GEMM separated by a grid barrier); False: the pair.
 """
 from __future__ import annotations
 
@@ -30,3 +33,4 @@ ENGINE_IN_MP = True
 BN_ACC = True
 BN_ACC_BWD = True
 LAYER_FWD = True
+LAYER_BWD = True

@@ -64,7 +64,8 @@ def get():
 
 
 # io option order of gine_torch.cpp (IntOpt): then 5 scalars per window plan (in, out)
-IO_EPI, IO_LIN, IO_BATCH, IO_UPDATE, IO_FUSED, IO_LAYER, IO_DEG, IO_ENGINE, IO_PLAN_IN = range(9)
+(IO_EPI, IO_LIN, IO_BATCH, IO_UPDATE, IO_FUSED, IO_LAYER, IO_DEG, IO_ENGINE, IO_LAYER_BWD,
+ IO_PLAN_IN) = range(10)
 IO_PLAN_OUT = IO_PLAN_IN + 5
 
 
@@ -89,8 +90,8 @@ def _graph_opts(graph, N: int, D: int, has_acc: bool) -> tuple:
     and occupancy queries)."""
     from . import functional as Fn
     from . import options
-    key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD, options.ENGINE_IN_MP,
-           Fn.layer_policy_key())
+    key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD, options.LAYER_BWD,
+           options.ENGINE_IN_MP, Fn.layer_policy_key())
     cache = graph._ext_opts
     got = cache.get(key)
     if got is None:
@@ -100,7 +101,7 @@ def _graph_opts(graph, N: int, D: int, has_acc: bool) -> tuple:
         pout, aout = _plan_args(graph, "out", D)
         io = [int(fused), int(lay),
               int(graph.max_in_degree if graph.max_in_degree is not None else -1),
-              int(Fn.engine_in_mp_ok(graph, D))] + pin + pout
+              int(Fn.engine_in_mp_ok(graph, D)), int(Fn.layer_backward_ok(N, D))] + pin + pout
         tensors = [graph.in_rowptr, graph.in_src, graph.in_attr, graph.out_rowptr,
                    graph.out_dst, graph.out_attr] + ain + aout
         got = cache[key] = (io, tensors)
