@@ -709,6 +709,12 @@ int gine_chain_unfold_grads2(const float* gfold, const float* wr1, const float* 
  * with 16-byte-per-lane streaming loads and stores -- the HBM copy ceiling bench.py prices
  * the message-passing kernels against (csrc/gine_probe.hip). */
 int gine_copy_f4(const void* src, void* dst, int64_t bytes, void* stream);
+/* Measurement utility (tools/chain_micro.py): `reps` 32x32 blocks of the split-bf16 row-GEMM
+ * chain (K = 128) per wave in `blocks` 256-thread workgroups, in form `variant` (0: A split
+ * in the loop, 1: pre-split A planes from LDS, 2: MFMAs only, 3: two chains interleaved);
+ * ticks[block * 4 + wave] = shader-clock ticks of the loop, sink = [blocks * 256] sums. */
+int gine_probe_chain(int32_t variant, int32_t reps, int32_t blocks, float* sink,
+                     long long* ticks, void* stream);
 
 #ifdef __cplusplus
 }

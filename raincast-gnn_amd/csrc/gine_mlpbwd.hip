@@ -49,6 +49,28 @@ static_assert(kItems == 2 && kWPer == 8 && kTiles == 2, "staging shares");
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+#ifdef GINE_LAYER_PROFILE
+// Debug build only (make variant VDEFS=-DGINE_LAYER_PROFILE): thread 0 of every workgroup
+// stamps s_memtime at its phase boundaries (tools/layer_bwd_prof.py): 0 entry, 1 tiles
+// staged, 2 W2 planes ready, 3 / 4 tile 1 / 2 epilogue done, 5 sums in the accumulator,
+// 6 barrier passed, 7 W1 planes ready, 8 totals read, 9 coef ready, 10 da1 staged, 11 end;
+// 16-19 s_memrealtime at entry, arrival, release and the end.
+__device__ long long g_bwd_layer_prof[1024][24];
+#define BL_MARK(i)                                                                  \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 1024)                                      \
+      g_bwd_layer_prof[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memtime();     \
+  } while (0)
+#define BL_RT(i)                                                                    \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 1024)                                      \
+      g_bwd_layer_prof[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define BL_MARK(i) do {} while (0)
+#define BL_RT(i) do {} while (0)
+#endif
+
 struct BwdLayerArgs {
   const float* dy;
   const float* y;        // PRO_DOR
@@ -67,16 +89,22 @@ struct BwdLayerArgs {
   int N, num_tiles;
 };
 
+constexpr int kPS = kD + 8;  // plane row stride (bf16): 272-byte rows, conflict-free b128 reads
 struct BwdLayerLds {
   float w[kD * kLD];              // W2 image; per-wave transposition tiles + sums; W1 image
-  float x[kTiles][kRows * kLD];   // staged A operands: do (phase A), da1 (phase B)
+  // the staged A operands -- do (phase A), da1 (phase B) -- as split-bf16 planes hi | mid | lo
+  // (gine_bf16x3.hpp split2), split once by the helpers: a matrix wave's chain then reads
+  // them (2,046 instead of 3,081 shader ticks per 32x32 block at one wave per SIMD, where
+  // the in-loop split's VALU work adds to the MFMA chain instead of hiding under it;
+  // tools/chain_micro.py, profiles/r05_s18_chain_micro.txt)
+  uint16_t xp[kTiles][3][kRows * kPS];
   float o[kTiles][kRows * kLD];   // a1 rows, overwritten in place by dbn
   float bnp[4 * kD];              // bn_save: mean | invstd | alpha | shift
   double tot[2 * kD];
   float coef[3 * kD];
   int barrier_failed;
 };
-static_assert(4 * 32 * kTLD * 4 + 2 * 8 * kD * 8 <= kD * kLD * 4, "scratch fits in w");
+static_assert(kTiles * 4 * 32 * kTLD * 4 + 2 * 8 * kD * 8 <= kD * kLD * 4, "scratch fits in w");
 
 // The row GEMM's tile -> workgroup assignment (gine_mlp.hip xcd_tile_range).
 struct Tiles {
@@ -117,26 +145,62 @@ __device__ __forceinline__ void w_fragments(const float* w, int col, int h, floa
   for (int s = 0; s < kKS; ++s) bf[s] = w[(h * kKS + s) * kLD + col];
 }
 
-// One 32x32 block of a tile: A = the staged rows, B = the lane's weight planes; a wave whose
-// accumulators see a NaN redoes it on the fp32 chain from W in global memory.
-__device__ __forceinline__ floatx16 chain(const float* x, const BPlanes<kKS>& bp,
-                                          const float* __restrict__ W, int col, int h, int c32) {
-  const float* arow = x + c32 * kLD + h * kKS;
+// Split a staged float4 item (row r, k = 4q .. 4q + 3) into the three planes of tile t.
+__device__ __forceinline__ void put_planes(uint16_t (*xp)[kRows * kPS], int r, int q, float4 v) {
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split2(v.x, v.y, h0, m0, l0);
+  split2(v.z, v.w, h1, m1, l1);
+  const int e = r * kPS + 4 * q;
+  *reinterpret_cast<uint2*>(&xp[0][e]) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(&xp[1][e]) = make_uint2(m0, m1);
+  *reinterpret_cast<uint2*>(&xp[2][e]) = make_uint2(l0, l1);
+}
+
+// One 32x32 block of a tile: A = the staged planes, B = the lane's weight planes (the row
+// GEMM's split chain, the same k order and products).  A wave whose accumulators see a NaN
+// redoes the block on the fp32 chain of the row GEMM's redo (mfma_f32_row_mem's order), with
+// A[row c32][h*64 + k] from `aval(k)` -- the staged values recomputed from their sources.
+template <class AVal>
+__device__ __forceinline__ floatx16 chain(const uint16_t (*xp)[kRows * kPS],
+                                          const BPlanes<kKS>& bp, const float* __restrict__ W,
+                                          int col, int h, int c32, const AVal& aval) {
+  const int e = c32 * kPS + h * kKS;
   floatx16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
   for (int s = 0; s < kKS / 8; ++s) {
-    const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);
-    const float4 a1 = *reinterpret_cast<const float4*>(&arow[8 * s + 4]);
-    acc = mfma_bf16x3(split8(a0, a1), bp.f[s], acc);
+    Bf16x3 a;
+    a.h = *reinterpret_cast<const bf16x8_t*>(&xp[0][e + 8 * s]);
+    a.m = *reinterpret_cast<const bf16x8_t*>(&xp[1][e + 8 * s]);
+    a.l = *reinterpret_cast<const bf16x8_t*>(&xp[2][e + 8 * s]);
+    acc = mfma_bf16x3(a, bp.f[s], acc);
   }
   if (wave_any_nan(acc)) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    acc = mfma_f32_row_mem<kKS>(arow, W + (size_t)h * kKS * kD + col, kD, acc);
+    const float* wp = W + (size_t)h * kKS * kD + col;
+#pragma unroll 1
+    for (int q = 0; q < kKS / 4; ++q) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aval(4 * q), wp[(4 * q) * kD], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aval(4 * q + 1), wp[(4 * q + 1) * kD], acc, 0,
+                                                 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aval(4 * q + 2), wp[(4 * q + 2) * kD], acc, 0,
+                                                 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aval(4 * q + 3), wp[(4 * q + 3) * kD], acc, 0,
+                                                 0, 0);
+    }
   }
   return acc;
+}
+
+// Transposition tiles in w, one per (tile, matrix wave): the helpers finish tile t while the
+// matrix waves chain tile t + 1.  Then the epilogue's sums scratch.
+__device__ __forceinline__ float* tt_of(float* w, int t, int wave) {
+  return w + (t * 4 + wave) * 32 * kTLD;
+}
+__device__ __forceinline__ double* sums_of(float* w) {
+  return reinterpret_cast<double*>(w + kTiles * 4 * 32 * kTLD);
 }
 
 // this wave's 32x32 block -> row-major through its own LDS tile
@@ -156,14 +220,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
   const bool mat = wave < kMat / kWave;
   const int lane = tid % kWave;
   const int h = lane >> 5, c32 = lane & 31;
-  const int cq = lane & 7, grp = lane >> 3;  // transposed epilogue: 4-column chunk, row group
   const int col = 32 * wave + c32;           // (matrix waves)
   const int p = tid - kMat;                   // (helpers)
   long long* phw = bnacc_phase(A.acc, 2 * kD);
   // written by earlier launches only (workgroup 0 moves them after the barrier)
   const long long ph = phw[0] + 1, consumed = phw[1 + ((ph - 1) & 1)];
   const BnView bv = bn_view(A.bn_save, kD);
-  float* tt = &L.w[wave * 32 * kTLD];
+  BL_MARK(0);
+  BL_RT(16);
 
   // ---- phase A staging: W2 and both tiles (helpers) ----
   if (!mat) {
@@ -193,11 +257,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
         const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
         float4 v = transform<PRO>(pa, raw[t][j], kc);
         if (t >= nt || (int64_t)ts.at(t) * kRows + r >= A.N) v = f4_zero();
-        *reinterpret_cast<float4*>(&L.x[t][r * kLD + 4 * q]) = v;
+        put_planes(L.xp[t], r, q, v);
         *reinterpret_cast<float4*>(&L.o[t][r * kLD + 4 * q]) = a1v[t][j];
       }
   }
   __syncthreads();  // S1: W2 and the tiles staged
+  BL_MARK(1);
 
   if (mat) {
     // ---- phase A: dbn = (do W2) * 1[bn(a1) > 0], BatchNorm-backward sums ----
@@ -206,27 +271,57 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
     BPlanes<kKS> bp;
     bp.from(bf);
     __syncthreads();  // S2: every wave's fragment reads of w are done (transposition tiles)
-    const int c0 = 32 * wave + 4 * cq;
+    BL_MARK(2);
+    for (int t = 0; t < kTiles; ++t) {  // (the barriers are uniform: kTiles of them)
+      if (t < nt) {
+        const int64_t nrow = (int64_t)ts.at(t) * kRows + c32;  // this lane's A row
+        const floatx16 acc = chain(L.xp[t], bp, A.W2, col, h, c32, [&](int k) -> float {
+          if (nrow >= A.N) return 0.f;  // (rows past N are staged as zero)
+          const int64_t off = nrow * kD + h * kKS + k;
+          const float v = A.dy[off];
+          if constexpr (PRO == PRO_DOM) return A.mask[off] ? v : 0.f;
+          else if constexpr (PRO == PRO_DOR) return A.y[off] > 0.f ? v : 0.f;
+          else return v;
+        });
+        transpose_in(tt_of(L.w, t, wave), acc, h, c32);
+      }
+      __syncthreads();  // E_t: tile t's blocks transposed (the helpers' epilogue follows)
+      BL_MARK(3 + t);
+    }
+    __syncthreads();  // X: the epilogue's sums in sr
+    BL_MARK(5);
+    __syncthreads();  // S3: phase A's use of w is over (the accumulator holds the sums)
+  } else {
+    __syncthreads();  // S2
+    // W1, in flight under phase A's chains
+    WRegs w1;
+    w1.load(reinterpret_cast<const float4*>(A.W1), p);
+    // The EPI_DBN epilogue of tile t beside the matrix waves' chain of tile t + 1: thread
+    // p < 256 takes the (row group, column chunk) slot of lane p % 64 of matrix wave p / 64
+    // -- the row GEMM's thread mapping, so the BatchNorm-backward sums accumulate in its order
+    const bool epi = p < kMat;
+    const int ew = p >> 6, el = p & 63;
+    const int eg = el >> 3, ecq = el & 7;
+    const int c0 = 32 * ew + 4 * ecq;
     double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int t = 0; t < nt; ++t) {
-      const floatx16 acc = chain(L.x[t], bp, A.W2, col, h, c32);
-      transpose_in(tt, acc, h, c32);
+    for (int t = 0; t < kTiles; ++t) {
+      __syncthreads();  // E_t
+      if (!epi || t >= nt) continue;
+      const float* tt = tt_of(L.w, t, ew);
+      const float4 mu4 = *reinterpret_cast<const float4*>(&L.bnp[c0]);
+      const float4 is4 = *reinterpret_cast<const float4*>(&L.bnp[kD + c0]);
+      const float4 al4 = *reinterpret_cast<const float4*>(&L.bnp[2 * kD + c0]);
+      const float4 sh4 = *reinterpret_cast<const float4*>(&L.bnp[3 * kD + c0]);
+      const float al[4] = {al4.x, al4.y, al4.z, al4.w}, sh[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+      const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = grp + 8 * i;
+        const int row = eg + 8 * i;
         const int64_t n = (int64_t)ts.at(t) * kRows + row;
-        const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * cq]);
+        const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * ecq]);
         if (n >= A.N) continue;
         float* slot = &L.o[t][row * kLD + c0];
         const float4 a14 = *reinterpret_cast<const float4*>(slot);
-        // the BatchNorm constants of these columns from LDS each row (in registers they
-        // pushed the weight planes into scratch)
-        const float4 mu4 = *reinterpret_cast<const float4*>(&L.bnp[c0]);
-        const float4 is4 = *reinterpret_cast<const float4*>(&L.bnp[kD + c0]);
-        const float4 al4 = *reinterpret_cast<const float4*>(&L.bnp[2 * kD + c0]);
-        const float4 sh4 = *reinterpret_cast<const float4*>(&L.bnp[3 * kD + c0]);
-        const float al[4] = {al4.x, al4.y, al4.z, al4.w}, sh[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
-        const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
         const float vv[4] = {v.x, v.y, v.z, v.w};
         const float a1[4] = {a14.x, a14.y, a14.z, a14.w};
         float o4[4];
@@ -242,30 +337,76 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
         *reinterpret_cast<float4*>(slot) = ov;
         *reinterpret_cast<float4*>(A.dbn + n * kD + c0) = ov;
       }
-      __builtin_amdgcn_wave_barrier();  // the next tile's transposition writes come after
     }
     // per-column sums: the 8 row groups added in fixed order (row-tile GEMM order)
-    double* sr = reinterpret_cast<double*>(&L.w[4 * 32 * kTLD]);  // [2][8][kD]
+    double* sr = sums_of(L.w);  // [2][8][kD]
+    if (epi) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      sr[(0 * 8 + grp) * kD + c0 + k] = st1[k];
-      sr[(1 * 8 + grp) * kD + c0 + k] = st2[k];
+      for (int k = 0; k < 4; ++k) {
+        sr[(0 * 8 + eg) * kD + c0 + k] = st1[k];
+        sr[(1 * 8 + eg) * kD + c0 + k] = st2[k];
+      }
     }
-    __builtin_amdgcn_wave_barrier();
-    const int which = lane >> 5, cc = 32 * wave + (lane & 31);
-    double s = 0.0;
+    __syncthreads();  // X
+    if (epi) {
+      const int which = el >> 5, cc = 32 * ew + (el & 31);
+      double sum = 0.0;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) s += sr[(which * 8 + g) * kD + cc];
-    bnacc_add<false>(A.acc, 2 * kD, which * kD + cc, s);
-    // the atomics are performed before this workgroup arrives at the grid barrier
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // S3: phase A's use of w is over
+      for (int g = 0; g < 8; ++g) sum += sr[(which * 8 + g) * kD + cc];
+      bnacc_add<false>(A.acc, 2 * kD, which * kD + cc, sum);
+      // the atomics are performed before this workgroup arrives at the grid barrier
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();  // S3
+    w1.store(L.w, p);
+  }
+
+  BL_RT(17);
+  if (tid == 0)
+    L.barrier_failed = grid_barrier(bnacc_barrier(A.acc, 2 * kD), gridDim.x) ? 0 : 1;
+  __syncthreads();  // S4: barrier passed; W1 staged
+  BL_MARK(6);
+  BL_RT(18);
+  // a timed-out barrier (the grid was not co-resident): the totals are incomplete, so this
+  // workgroup's coefficients and outputs are NaN; the failure word tells the host
+  const bool failed = L.barrier_failed != 0;
+
+  // ---- phase B: W1's fragments (matrix) beside the totals, coef and the da1 planes
+  // (helpers); each role in a branch of its own, so that neither holds the other's registers
+  if (mat) {
+    float bf1[kKS];
+    w_fragments(L.w, col, h, bf1);
+    BPlanes<kKS> bp1;
+    bp1.from(bf1);
+    BL_MARK(7);
+    __syncthreads();  // S5: totals in LDS
+    BL_MARK(8);
+    if (blockIdx.x == 0 && tid == 0) {
+      phw[0] = ph;
+      phw[1 + (ph & 1)] = ph;  // bnacc_mark_consumed
+    }
+    __syncthreads();  // S6: coef in LDS
+    BL_MARK(9);
+    __syncthreads();  // S7: da1 staged
+    BL_MARK(10);
+    for (int t = 0; t < kTiles; ++t) {  // dz = da1 W1 (EPI_PLAIN: stored by the helpers)
+      if (t < nt) {
+        const int64_t nrow = (int64_t)ts.at(t) * kRows + c32;
+        const floatx16 acc = chain(L.xp[t], bp1, A.W1, col, h, c32, [&](int k) -> float {
+          if (nrow >= A.N) return 0.f;
+          const int kk = h * kKS + k;
+          const float v = L.o[t][c32 * kLD + kk];
+          const float a1 = A.a1[nrow * kD + kk];
+          return L.coef[kk] * v + L.coef[kD + kk] * ((a1 - L.bnp[kk]) * L.bnp[kD + kk]) +
+                 L.coef[2 * kD + kk];  // transform<PRO_DA1>'s expression
+        });
+        transpose_in(tt_of(L.w, t, wave), acc, h, c32);
+      }
+      __syncthreads();  // F_t: tile t's dz blocks transposed
+    }
   } else {
-    __syncthreads();  // S2
-    // W1 and phase B's a1 rows, in flight under phase A's chains
-    WRegs w1;
-    w1.load(reinterpret_cast<const float4*>(A.W1), p);
-    // (named registers: an array held across the barrier went to scratch)
+    // the a1 rows of this thread's items, in flight under the totals (named registers: an
+    // array held across the barriers went to scratch)
     auto a1_at = [&](int t, int j) {
       const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
       int64_t n = (int64_t)ts.at(t < nt ? t : 0) * kRows + r;
@@ -274,100 +415,68 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
     };
     const float4 a1b00 = a1_at(0, 0), a1b01 = a1_at(0, 1), a1b10 = a1_at(1, 0),
                  a1b11 = a1_at(1, 1);
-    __syncthreads();  // S3
-    w1.store(L.w, p);
-    // a1 for phase B's prologue goes to the x tiles' slots it will be combined with: x[t] is
-    // free (phase A's chains are done) and each helper later reads back exactly the items it
-    // wrote
-    auto stash = [&](int t, int j, float4 v) {
-      const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
-      *reinterpret_cast<float4*>(&L.x[t][r * kLD + 4 * q]) = v;
-    };
-    stash(0, 0, a1b00);
-    stash(0, 1, a1b01);
-    stash(1, 0, a1b10);
-    stash(1, 1, a1b11);
-  }
-
-  if (tid == 0)
-    L.barrier_failed = grid_barrier(bnacc_barrier(A.acc, 2 * kD), gridDim.x) ? 0 : 1;
-  __syncthreads();  // S4: barrier passed; W1 staged
-  // a timed-out barrier (the grid was not co-resident): the totals are incomplete, so this
-  // workgroup's coefficients and outputs are NaN; the failure word tells the host
-  const bool failed = L.barrier_failed != 0;
-
-  // ---- phase B: coef from the totals (helpers) beside W1's fragments (matrix) ----
-  float bf1[kKS];
-  BPlanes<kKS> bp1;
-  if (mat) {
-    w_fragments(L.w, col, h, bf1);
-    bp1.from(bf1);
-  } else if (p < 2 * kD) {
-    const double t = bnacc_total<true>(A.acc, 2 * kD, p, blockIdx.x == 0, ph, consumed);
-    L.tot[p] = failed ? __builtin_nan("") : t;
-  }
-  __syncthreads();  // S5
-  if (!mat && p < kD) {  // the arithmetic of k_bwd1_bnacc's prologue
-    const double sd = L.tot[p], sx = L.tot[kD + p];
-    const double g = A.gamma ? (double)A.gamma[p] : 1.0;
-    const double c1 = g * (double)bv.invstd[p];
-    const float k1 = (float)c1, k2 = (float)(-c1 * sx / (double)A.N),
-                k3 = (float)(-c1 * sd / (double)A.N);
-    L.coef[p] = k1;
-    L.coef[kD + p] = k2;
-    L.coef[2 * kD + p] = k3;
-    if (blockIdx.x == 0) {
-      if (A.dgamma) A.dgamma[p] = (float)sx;
-      if (A.dbeta) A.dbeta[p] = (float)sd;
-      A.coef[p] = k1;
-      A.coef[kD + p] = k2;
-      A.coef[2 * kD + p] = k3;
+    if (p < 2 * kD) {
+      const double t = bnacc_total<true>(A.acc, 2 * kD, p, blockIdx.x == 0, ph, consumed);
+      L.tot[p] = failed ? __builtin_nan("") : t;
     }
-  }
-  if (blockIdx.x == 0 && tid == 0) {
-    phw[0] = ph;
-    phw[1 + (ph & 1)] = ph;  // bnacc_mark_consumed
-  }
-  __syncthreads();  // S6: coef in LDS
-  if (!mat) {  // da1 = PRO_DA1(dbn) into x[t] (rows past N zero, as the row GEMM stages them)
-#pragma unroll
-    for (int t = 0; t < kTiles; ++t)
-#pragma unroll
-      for (int j = 0; j < kItems; ++j) {
-        const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
-        float* xs = &L.x[t][r * kLD + 4 * q];
-        RawItem ri;
-        ri.v = *reinterpret_cast<const float4*>(&L.o[t][r * kLD + 4 * q]);
-        ri.aux = *reinterpret_cast<const float4*>(xs);
-        ri.m = make_uchar4(1, 1, 1, 1);
-        ColConst kc;
-        kc.a = *reinterpret_cast<const float4*>(&L.coef[4 * q]);
-        kc.b = *reinterpret_cast<const float4*>(&L.coef[kD + 4 * q]);
-        kc.c = *reinterpret_cast<const float4*>(&L.coef[2 * kD + 4 * q]);
-        kc.d = *reinterpret_cast<const float4*>(&L.bnp[4 * q]);
-        kc.e = *reinterpret_cast<const float4*>(&L.bnp[kD + 4 * q]);
-        const ProArgs pa{};
-        float4 v = transform<PRO_DA1>(pa, ri, kc);
-        if (t >= nt || (int64_t)ts.at(t) * kRows + r >= A.N) v = f4_zero();
-        *reinterpret_cast<float4*>(xs) = v;
+    __syncthreads();  // S5
+    if (p < kD) {  // the arithmetic of k_bwd1_bnacc's prologue
+      const double sd = L.tot[p], sx = L.tot[kD + p];
+      const double g = A.gamma ? (double)A.gamma[p] : 1.0;
+      const double c1 = g * (double)bv.invstd[p];
+      const float k1 = (float)c1, k2 = (float)(-c1 * sx / (double)A.N),
+                  k3 = (float)(-c1 * sd / (double)A.N);
+      L.coef[p] = k1;
+      L.coef[kD + p] = k2;
+      L.coef[2 * kD + p] = k3;
+      if (blockIdx.x == 0) {
+        if (A.dgamma) A.dgamma[p] = (float)sx;
+        if (A.dbeta) A.dbeta[p] = (float)sd;
+        A.coef[p] = k1;
+        A.coef[kD + p] = k2;
+        A.coef[2 * kD + p] = k3;
       }
-  }
-  __syncthreads();  // S7: da1 staged
-  if (mat) {  // dz = da1 W1 (EPI_PLAIN)
-    const int c0 = 32 * wave + 4 * cq;
-    for (int t = 0; t < nt; ++t) {
-      const floatx16 acc = chain(L.x[t], bp1, A.W1, col, h, c32);
-      transpose_in(tt, acc, h, c32);
+    }
+    __syncthreads();  // S6
+    // da1 = PRO_DA1(dbn) as split planes (rows past N zero, as the row GEMM stages them)
+    auto stage = [&](int t, int j, float4 a1v) {
+      const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
+      RawItem ri;
+      ri.v = *reinterpret_cast<const float4*>(&L.o[t][r * kLD + 4 * q]);
+      ri.aux = a1v;
+      ri.m = make_uchar4(1, 1, 1, 1);
+      ColConst kc;
+      kc.a = *reinterpret_cast<const float4*>(&L.coef[4 * q]);
+      kc.b = *reinterpret_cast<const float4*>(&L.coef[kD + 4 * q]);
+      kc.c = *reinterpret_cast<const float4*>(&L.coef[2 * kD + 4 * q]);
+      kc.d = *reinterpret_cast<const float4*>(&L.bnp[4 * q]);
+      kc.e = *reinterpret_cast<const float4*>(&L.bnp[kD + 4 * q]);
+      const ProArgs pa{};
+      float4 v = transform<PRO_DA1>(pa, ri, kc);
+      if (t >= nt || (int64_t)ts.at(t) * kRows + r >= A.N) v = f4_zero();
+      put_planes(L.xp[t], r, q, v);
+    };
+    stage(0, 0, a1b00);
+    stage(0, 1, a1b01);
+    stage(1, 0, a1b10);
+    stage(1, 1, a1b11);
+    __syncthreads();  // S7
+    for (int t = 0; t < kTiles; ++t) {  // dz rows of tile t beside the chain of tile t + 1
+      __syncthreads();  // F_t
+      if (p >= kMat || t >= nt) continue;
+      const int ew = p >> 6, el = p & 63, eg = el >> 3, ecq = el & 7;
+      const float* tt = tt_of(L.w, t, ew);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int row = grp + 8 * i;
+        const int row = eg + 8 * i;
         const int64_t n = (int64_t)ts.at(t) * kRows + row;
-        const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * cq]);
-        if (n < A.N) *reinterpret_cast<float4*>(A.dz + n * kD + c0) = v;
+        const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * ecq]);
+        if (n < A.N) *reinterpret_cast<float4*>(A.dz + n * kD + 32 * ew + 4 * ecq) = v;
       }
-      __builtin_amdgcn_wave_barrier();
     }
   }
+  BL_MARK(11);
+  BL_RT(19);
 }
 
 int bwd_layer_capacity() {
@@ -474,3 +583,12 @@ extern "C" int gine_mlp_bwd_layer(const float* dy, const float* y, const uint8_t
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
+
+#ifdef GINE_LAYER_PROFILE
+extern "C" int gine_debug_bwd_layer_prof(long long* out) {  // [1024][24] host buffer
+  GINE_RETURN_IF_HIP(hipDeviceSynchronize());
+  GINE_RETURN_IF_HIP(
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_layer_prof), sizeof(g_bwd_layer_prof)));
+  return GINE_OK;
+}
+#endif

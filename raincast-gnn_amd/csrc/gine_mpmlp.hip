@@ -426,6 +426,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_mlp1(FusedArgs A) {
 // the BatchNorm totals are integer sums, the MFMA chains and epilogues are the row GEMM's).
 // ---------------------------------------------------------------------------------------
 constexpr int kLayerTiles = 2;  // a1 tiles a workgroup keeps in LDS
+constexpr int kPS = kD + 8;     // split-plane row stride (bf16): conflict-free 16-byte reads
+static_assert(kLayerTiles * 3 * kTileRows * kPS * 2 <= kD * kLD * 4, "planes fit in w");
 
 // W2 in flight in the gather waves' registers: 8 float4 per thread (element idx = t + n*j,
 // row idx / kD4, column chunk idx % kD4), staged into the padded LDS image.
@@ -568,41 +570,66 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   }
   __syncthreads();
   LAYER_MARK(5);
-  // r = relu(bn(a1)) in place; rows past N are zero (the row GEMM stages them as zero)
+  // r = relu(bn(a1)) as split-bf16 planes (hi | mid | lo, gine_bf16x3.hpp split2) in the
+  // w region (free since W2's fragments were read): split once here by all 12 waves, the
+  // matrix waves' chains then only read them (a wave's in-loop split adds to its MFMA chain:
+  // 3,081 against 2,046 shader ticks per 32x32 block, tools/chain_micro.py).  a1k keeps a1
+  // for the rare fp32 redo.  Rows past N are zero (the row GEMM stages them as zero).
+  uint16_t* rp = reinterpret_cast<uint16_t*>(L.f.w);  // [kLayerTiles][3][kTileRows * kPS]
   for (int e = tid; e < nt * kTileRows * kD4; e += kThreads) {
     const int k = e / (kTileRows * kD4), r = (e / kD4) % kTileRows, q4 = e % kD4;
-    float* a = &L.a1k[k][r * kLD + 4 * q4];
-    float4 v = *reinterpret_cast<const float4*>(a);
+    float4 v = *reinterpret_cast<const float4*>(&L.a1k[k][r * kLD + 4 * q4]);
     const float4 al = *reinterpret_cast<const float4*>(&L.bn[4 * q4]);
     const float4 sh = *reinterpret_cast<const float4*>(&L.bn[kD + 4 * q4]);
     v = make_float4(relu_nan(bn_apply(v.x, al.x, sh.x)), relu_nan(bn_apply(v.y, al.y, sh.y)),
                     relu_nan(bn_apply(v.z, al.z, sh.z)), relu_nan(bn_apply(v.w, al.w, sh.w)));
     if ((int64_t)ts.at(k) * kTileRows + r >= A.N) v = f4_zero();
-    *reinterpret_cast<float4*>(a) = v;
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split2(v.x, v.y, h0, m0, l0);
+    split2(v.z, v.w, h1, m1, l1);
+    uint16_t* pl = rp + k * 3 * kTileRows * kPS + r * kPS + 4 * q4;
+    *reinterpret_cast<uint2*>(pl) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(pl + kTileRows * kPS) = make_uint2(m0, m1);
+    *reinterpret_cast<uint2*>(pl + 2 * kTileRows * kPS) = make_uint2(l0, l1);
   }
   __syncthreads();
   LAYER_MARK(6);
   for (int k = 0; k < nt; ++k) {
     float* sO = L.f.z[k & 1];
     if (mat) {  // Linear2 chain of tile k (the row GEMM's split-bf16 chain and k order)
-      const float* arow = &L.a1k[k][c32 * kLD + h * kKS];
       floatx16 acc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0.f;
       if constexpr (GINE_GEMM_BF16X3) {
+        const uint16_t* pa = rp + k * 3 * kTileRows * kPS + c32 * kPS + h * kKS;
 #pragma unroll
         for (int s8 = 0; s8 < kKS / 8; ++s8) {
-          const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s8]);
-          const float4 a1v = *reinterpret_cast<const float4*>(&arow[8 * s8 + 4]);
-          acc = mfma_bf16x3(split8(a0, a1v), bp.f[s8], acc);
+          Bf16x3 a;
+          a.h = *reinterpret_cast<const bf16x8_t*>(pa + 8 * s8);
+          a.m = *reinterpret_cast<const bf16x8_t*>(pa + kTileRows * kPS + 8 * s8);
+          a.l = *reinterpret_cast<const bf16x8_t*>(pa + 2 * kTileRows * kPS + 8 * s8);
+          acc = mfma_bf16x3(a, bp.f[s8], acc);
         }
-        if (wave_any_nan(acc)) {
+        if (wave_any_nan(acc)) {  // the fp32 chain, r recomputed from a1 (mfma_f32_row_mem's order)
 #pragma unroll
           for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-          acc = mfma_f32_row_mem<kKS>(arow, B.W2 + (size_t)col * kD + h * kKS, 1, acc);
+          const bool live = (int64_t)ts.at(k) * kTileRows + c32 < A.N;
+          const float* arow = &L.a1k[k][c32 * kLD + h * kKS];
+          const float* wp = B.W2 + (size_t)col * kD + h * kKS;
+          auto rv = [&](int kk) -> float {
+            const int c = h * kKS + kk;
+            return live ? relu_nan(bn_apply(arow[kk], L.bn[c], L.bn[kD + c])) : 0.f;
+          };
+#pragma unroll 1
+          for (int q = 0; q < kKS / 4; ++q) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(rv(4 * q), wp[4 * q], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(rv(4 * q + 1), wp[4 * q + 1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(rv(4 * q + 2), wp[4 * q + 2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(rv(4 * q + 3), wp[4 * q + 3], acc, 0, 0, 0);
+          }
         }
       } else {
-        acc = mfma_f32_row<kKS>(arow, bf, acc);
+        static_assert(GINE_GEMM_BF16X3, "the layer forward's second half reads split planes");
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) sO[((r & 3) + 8 * (r >> 2) + 4 * h) * kLD + col] = acc[r];

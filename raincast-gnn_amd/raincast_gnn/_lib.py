@@ -134,6 +134,7 @@ _SIGNATURES = {
     "gine_deepset_mask_bytes": [_i64, _i32, _i32, ctypes.POINTER(_size)],
     "gine_deepset_mask_layout": [_i64, _i32, ctypes.POINTER(_i32)],
     "gine_copy_f4": [_c_void_p, _c_void_p, _i64, _c_void_p],
+    "gine_probe_chain": [_i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p],
     "gine_deepset_fwd":[_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
                          _i32, _i32, _c_void_p],
     "gine_deepset_bwd_num_partials": [_i64, _i32, ctypes.POINTER(_i32)],

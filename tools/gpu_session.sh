@@ -34,6 +34,9 @@ for s in $STEPS; do
     ktests) run pytest_k 600 python -u -m pytest tests -m gpu -q -rf -k "${KTESTS:-window}" --timeout 120 --timeout-method thread ;;
     layerprof) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/layerprof/libgine_hip.so \
             run layer_prof 200 python tools/layer_prof.py --config ${LPCFG:-2} ;;
+    lbprof) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/layerbwdprof/libgine_hip.so \
+            run layer_bwd_prof 200 python tools/layer_bwd_prof.py ;;
+    chain) run chain_micro 200 python tools/chain_micro.py ;;
     dsab)  run ds_ab 900 bash tools/gpu_ds_ab.sh $TAG/dsab ${DSVARS:-main} ;;
     kvtests) GINE_HIP_LIB=raincast-gnn_amd/raincast_gnn/_native/var/${LIBVAR}/libgine_hip.so \
             run pytest_k_${LIBVAR} 600 python -u -m pytest tests -m gpu -q -rf -k "${KTESTS:-deepset}" --timeout 120 --timeout-method thread ;;
