@@ -387,7 +387,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
     }
     __syncthreads();  // S6: coef in LDS
     BL_MARK(9);
-    __syncthreads();  // S7: da1 staged
+    __syncthreads();  // S7: tile 0's da1 staged (tile 1's follows beside chain 0)
     BL_MARK(10);
     for (int t = 0; t < kTiles; ++t) {  // dz = da1 W1 (EPI_PLAIN: stored by the helpers)
       if (t < nt) {
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
         });
         transpose_in(tt_of(L.w, t, wave), acc, h, c32);
       }
-      __syncthreads();  // F_t: tile t's dz blocks transposed
+      __syncthreads();  // F_t: tile t's dz blocks transposed (F_0: tile 1's da1 staged)
     }
   } else {
     // the a1 rows of this thread's items, in flight under the totals (named registers: an
@@ -413,8 +413,17 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
       n = n < A.N ? n : A.N - 1;
       return *reinterpret_cast<const float4*>(A.a1 + n * kD + 4 * q);
     };
-    const float4 a1b00 = a1_at(0, 0), a1b01 = a1_at(0, 1), a1b10 = a1_at(1, 0),
-                 a1b11 = a1_at(1, 1);
+    // xhat = (a1 - mean) * invstd of these items now (transform<PRO_DA1>'s inner product,
+    // the same operations), so that the staging behind the totals is three FMAs' worth
+    auto xhat_of = [&](int j, float4 a) {
+      const int q = (p + kHelp * j) % kD4;
+      const float4 mu = *reinterpret_cast<const float4*>(&L.bnp[4 * q]);
+      const float4 is = *reinterpret_cast<const float4*>(&L.bnp[kD + 4 * q]);
+      return make_float4((a.x - mu.x) * is.x, (a.y - mu.y) * is.y, (a.z - mu.z) * is.z,
+                         (a.w - mu.w) * is.w);
+    };
+    const float4 xh00 = xhat_of(0, a1_at(0, 0)), xh01 = xhat_of(1, a1_at(0, 1)),
+                 xh10 = xhat_of(0, a1_at(1, 0)), xh11 = xhat_of(1, a1_at(1, 1));
     if (p < 2 * kD) {
       const double t = bnacc_total<true>(A.acc, 2 * kD, p, blockIdx.x == 0, ph, consumed);
       L.tot[p] = failed ? __builtin_nan("") : t;
@@ -438,29 +447,25 @@ __global__ __launch_bounds__(kThreads, 1) void k_mlp_bwd_layer(BwdLayerArgs A) {
       }
     }
     __syncthreads();  // S6
-    // da1 = PRO_DA1(dbn) as split planes (rows past N zero, as the row GEMM stages them)
-    auto stage = [&](int t, int j, float4 a1v) {
+    // da1 = PRO_DA1(dbn) as split planes (rows past N zero, as the row GEMM stages them):
+    // c1 dbn + c2 xhat + c3, transform<PRO_DA1>'s expression.  Tile 0 first; tile 1 beside
+    // the matrix waves' chain of tile 0.
+    auto stage = [&](int t, int j, float4 xh) {
       const int e = p + kHelp * j, r = e / kD4, q = e % kD4;
-      RawItem ri;
-      ri.v = *reinterpret_cast<const float4*>(&L.o[t][r * kLD + 4 * q]);
-      ri.aux = a1v;
-      ri.m = make_uchar4(1, 1, 1, 1);
-      ColConst kc;
-      kc.a = *reinterpret_cast<const float4*>(&L.coef[4 * q]);
-      kc.b = *reinterpret_cast<const float4*>(&L.coef[kD + 4 * q]);
-      kc.c = *reinterpret_cast<const float4*>(&L.coef[2 * kD + 4 * q]);
-      kc.d = *reinterpret_cast<const float4*>(&L.bnp[4 * q]);
-      kc.e = *reinterpret_cast<const float4*>(&L.bnp[kD + 4 * q]);
-      const ProArgs pa{};
-      float4 v = transform<PRO_DA1>(pa, ri, kc);
+      const float4 v0 = *reinterpret_cast<const float4*>(&L.o[t][r * kLD + 4 * q]);
+      const float4 c1 = *reinterpret_cast<const float4*>(&L.coef[4 * q]);
+      const float4 c2 = *reinterpret_cast<const float4*>(&L.coef[kD + 4 * q]);
+      const float4 c3 = *reinterpret_cast<const float4*>(&L.coef[2 * kD + 4 * q]);
+      float4 v = make_float4(c1.x * v0.x + c2.x * xh.x + c3.x, c1.y * v0.y + c2.y * xh.y + c3.y,
+                             c1.z * v0.z + c2.z * xh.z + c3.z, c1.w * v0.w + c2.w * xh.w + c3.w);
       if (t >= nt || (int64_t)ts.at(t) * kRows + r >= A.N) v = f4_zero();
       put_planes(L.xp[t], r, q, v);
     };
-    stage(0, 0, a1b00);
-    stage(0, 1, a1b01);
-    stage(1, 0, a1b10);
-    stage(1, 1, a1b11);
+    stage(0, 0, xh00);
+    stage(0, 1, xh01);
     __syncthreads();  // S7
+    stage(1, 0, xh10);
+    stage(1, 1, xh11);
     for (int t = 0; t < kTiles; ++t) {  // dz rows of tile t beside the chain of tile t + 1
       __syncthreads();  // F_t
       if (p >= kMat || t >= nt) continue;

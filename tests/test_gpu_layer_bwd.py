@@ -174,3 +174,42 @@ def test_model_step_same_bits_with_and_without_layer_backward(monkeypatch):
             for a, b in zip(a_step, b_step):
                 assert torch.equal(a, b), ext
     Fn.check_grid_barriers()
+
+
+@pytest.mark.parametrize("bad", [float("inf"), float("nan"), float("-inf")],
+                         ids=["inf", "nan", "-inf"])
+def test_layer_kernels_nonfinite_follow_oracle(bad, monkeypatch):
+    """D = 128 train-mode layer with a non-finite input value through the one-launch forward
+    and backward (their split-plane chains redo a non-finite tile on the fp32 chain): the
+    NaN / Inf pattern of y, of the running statistics and of every gradient equals the CPU
+    oracle's."""
+    import copy
+    from oracle import gine_cpu as O
+    from helpers import knn_batch_graph
+    from test_gpu_bnacc import _cls, _conv
+    from raincast_gnn import nn as rnn
+    monkeypatch.setattr(rnn, "USE_TORCH_EXT", False)
+    ei, ea, n = knn_batch_graph(500, 10, 4, seed=21)
+    assert Fn.layer_forward_ok(n, D, 11) and Fn.layer_backward_ok(n, D)
+    conv = _conv(D, seed=4)
+    ref = O.OracleGINEConv(copy.deepcopy(conv.nn).cpu(), train_eps=True, edge_dim=1)
+    ref.load_state_dict({k: v.cpu() for k, v in conv.state_dict().items()})
+    ref.train()
+    x = torch.randn(n, D)
+    x[321, 17] = bad
+    xg = x.to(DEV).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    y = conv.forward_residual_relu(xg, ei.to(DEV), ea.to(DEV))
+    yr = xr + torch.relu(ref(xr, ei, ea))
+    w = torch.linspace(-1, 1, y.numel()).view_as(yr)
+    (y * w.to(DEV)).sum().backward()
+    (yr * w).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(_cls(y.detach().cpu()), _cls(yr.detach()))
+    for buf in ("running_mean", "running_var"):
+        assert torch.equal(_cls(getattr(conv.nn[1], buf).cpu()), _cls(getattr(ref.nn[1], buf)))
+    assert torch.equal(_cls(xg.grad.cpu()), _cls(xr.grad))
+    refp = dict(ref.named_parameters())
+    for name, p in conv.named_parameters():
+        assert torch.equal(_cls(p.grad.cpu()), _cls(refp[name].grad)), name
+    Fn.check_grid_barriers()
