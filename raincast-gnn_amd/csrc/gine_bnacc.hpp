@@ -85,10 +85,15 @@ __device__ __forceinline__ void bnacc_add(long long* acc, int W, int c, double v
     const double f = (v - h) * 4294967296.0;  // exact: |v - h| <= 1/2, power-of-2 scale
     const double m = __builtin_rint(f);
     const double l = __builtin_rint((f - m) * 4294967296.0);
-    __hip_atomic_fetch_add(r + c, (long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(r + W + c, (long long)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(r + 2 * W + c, (long long)l, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    // a zero word is not added (the identity; the backward's sums of small gradients mostly
+    // have hi == 0): fewer same-address atomics for the memory side to serialise
+    if (h != 0.0)
+      __hip_atomic_fetch_add(r + c, (long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m != 0.0)
+      __hip_atomic_fetch_add(r + W + c, (long long)m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l != 0.0)
+      __hip_atomic_fetch_add(r + 2 * W + c, (long long)l, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   } else {  // NaN, +-Inf, or out of range (counted as NaN)
     const int k = (v == __builtin_inf()) ? 1 : (v == -__builtin_inf()) ? 2 : 0;
     __hip_atomic_fetch_add(bnacc_counts(acc, W) + c, 1ll << (kBnAccCountBits * k),
