@@ -62,19 +62,35 @@ __device__ __forceinline__ float post_bwd(int role, float x, float g) {
   }
 }
 
+// The slab row of a workgroup: LDS partial rows [0, rows) summed in fixed order (fp64), by
+// all kThreads threads (after the __syncthreads that published the rows).
+template <int K>
+__device__ __forceinline__ void reduce_rows(float* __restrict__ out, int D,
+                                            const float (*s_part)[kMaxK * 256 + kMaxK],
+                                            int rows) {
+  const int per = K * D + K;
+  for (int e = threadIdx.x; e < per; e += kThreads) {
+    double s = 0.0;
+    for (int r = 0; r < rows; ++r) s += (double)s_part[r][e];
+    out[e] = (float)s;
+  }
+}
+
 // One workgroup's share of the head backward: half-wave hw takes the nodes n = first + hw +
 // stride j (n < N), U rows per batch of loads; d raw = graw(n) [K floats] -> dh[n] = d raw W
 // (written), and the K x D dW / K db partials of these nodes, summed over the 8 half-waves
 // in fixed order (fp64) into the slab row `out` (K*D + K floats).  256 threads; s_part:
 // kRowsPerBlock * (kMaxK*256 + kMaxK) floats of LDS.  load() issues a batch's row loads and
 // step() consumes them, so a caller can put other work between the two (the CRPS pass
-// evaluates the loss while its rows arrive).
-template <int K, int U>
+// evaluates the loss while its rows arrive).  C: float4 column chunks per lane (1 when
+// D <= 128; the registers of a second chunk are not held for nothing).
+template <int K, int U, int C = kMaxChunks>
 struct HeadRows {
-  float4 wk[kMaxChunks][K];
-  float4 aw[kMaxChunks][K];  // sum over this half-wave's nodes of d raw[k] * h[n, cols]
+  static_assert(C >= 1 && C <= kMaxChunks, "column chunks per lane");
+  float4 wk[C][K];
+  float4 aw[C][K];  // sum over this half-wave's nodes of d raw[k] * h[n, cols]
   float ab[K];
-  float4 x[U][kMaxChunks];
+  float4 x[U][C];
   int t, hw, D4;
 
   __device__ __forceinline__ void init(const float* __restrict__ w, int D) {
@@ -85,10 +101,10 @@ struct HeadRows {
     for (int k = 0; k < K; ++k) {
       ab[k] = 0.f;
 #pragma unroll
-      for (int c = 0; c < kMaxChunks; ++c) aw[c][k] = f4_zero();
+      for (int c = 0; c < C; ++c) aw[c][k] = f4_zero();
     }
 #pragma unroll
-    for (int c = 0; c < kMaxChunks; ++c) {
+    for (int c = 0; c < C; ++c) {
       const int q = min(t + 32 * c, D4 - 1);
 #pragma unroll
       for (int k = 0; k < K; ++k)
@@ -102,7 +118,7 @@ struct HeadRows {
     for (int u = 0; u < U; ++u) {
       const int64_t n = n0 + u * stride;
 #pragma unroll
-      for (int c = 0; c < kMaxChunks; ++c) {
+      for (int c = 0; c < C; ++c) {
         const int q = t + 32 * c;
         x[u][c] = (n < N && q < D4) ? reinterpret_cast<const float4*>(h + n * D)[q] : f4_zero();
       }
@@ -129,7 +145,7 @@ struct HeadRows {
 #pragma unroll
       for (int k = 0; k < K; ++k) ab[k] += g[u][k];
 #pragma unroll
-      for (int c = 0; c < kMaxChunks; ++c) {
+      for (int c = 0; c < C; ++c) {
         const int q = t + 32 * c;
         if (q < D4) {
           float4 o = f4_zero();
@@ -149,32 +165,30 @@ struct HeadRows {
       }
     }
   }
-  // workgroup partial: the 8 half-waves summed in fixed order (fp64) -> one slab row
-  __device__ __forceinline__ void flush(float* __restrict__ out, int D,
-                                        float (*s_part)[kMaxK * 256 + kMaxK]) {
+  // this half-wave's partial into LDS row `row`
+  __device__ __forceinline__ void put(float (*s_part)[kMaxK * 256 + kMaxK], int row, int D) {
 #pragma unroll
-    for (int c = 0; c < kMaxChunks; ++c) {
+    for (int c = 0; c < C; ++c) {
       const int q = t + 32 * c;
       if (q < D4) {
 #pragma unroll
         for (int k = 0; k < K; ++k)
-          *reinterpret_cast<float4*>(&s_part[hw][k * D + 4 * q]) = aw[c][k];
+          *reinterpret_cast<float4*>(&s_part[row][k * D + 4 * q]) = aw[c][k];
       }
     }
     if (t < K) {
       float v = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) v = (t == k) ? ab[k] : v;
-      s_part[hw][K * D + t] = v;
+      s_part[row][K * D + t] = v;
     }
+  }
+  // workgroup partial: the 8 half-waves summed in fixed order (fp64) -> one slab row
+  __device__ __forceinline__ void flush(float* __restrict__ out, int D,
+                                        float (*s_part)[kMaxK * 256 + kMaxK]) {
+    put(s_part, hw, D);
     __syncthreads();
-    const int per = K * D + K;
-    for (int e = threadIdx.x; e < per; e += kThreads) {
-      double s = 0.0;
-#pragma unroll
-      for (int r = 0; r < kRowsPerBlock; ++r) s += (double)s_part[r][e];
-      out[e] = (float)s;
-    }
+    reduce_rows<K>(out, D, s_part, kRowsPerBlock);
   }
 };
 

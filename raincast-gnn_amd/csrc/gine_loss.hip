@@ -239,11 +239,14 @@ struct HeadBwdArgs {
 
 // One thread per node.  Writes d crps_n / d pred_n (0 for NaN targets) and per-block
 // [sum crps, count] partials; the workgroup that finishes last (ticket) reduces the partials
-// into the loss -- no separate finalize launch.  HEAD: kHeadNodes nodes per workgroup (the
-// CRPS evaluation is latency-bound: one busy wave per CU costs what four do), then the head
-// backward of those nodes from grad_unit, one batch of 8 rows per half-wave
-// (gine_headrow.hpp) -- with 256 nodes per workgroup each half-wave would walk 32 rows.
-template <int KIND, bool HEAD = false>
+// into the loss -- no separate finalize launch.  HC > 0 (the head backward of these nodes
+// from grad_unit, HC float4 column chunks per lane): kHeadNodes nodes per workgroup (the
+// CRPS evaluation is latency-bound: one busy wave per CU costs what four do), evaluated by
+// wave 0 alone, while the other waves load the head's weight and the nodes' h rows; after
+// one barrier those waves run the head backward, the nodes spread over their half-waves
+// (gine_headrow.hpp).  The roles stay in branches of their own: h rows held through the
+// loss evaluation had pushed it past 256 registers into scratch.
+template <int KIND, int HC = 0>
 __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pred,
                                                    const float* __restrict__ y, int64_t n,
                                                    double u_fixed, double xi, double c,
@@ -255,10 +258,15 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
                                                    const uint32_t* __restrict__ count_parts,
                                                    float* __restrict__ grad_unit,
                                                    HeadBwdArgs hb) {
+  constexpr bool HEAD = HC > 0;
   constexpr int K = LossK<KIND>::value;
   static_assert(kThreads == head::kThreads, "one CRPS node per head-backward thread");
+  // the head backward's half-waves (waves 1..3) and the rows each walks
+  constexpr int kHelpHW = (kThreads - kHeadNodes) / 32;
+  constexpr int kHelpU = (kHeadNodes + kHelpHW - 1) / kHelpHW;
+  static_assert(kHeadNodes % kWave == 0 && kHelpHW > 0, "wave 0 evaluates the loss");
   __shared__ float s_graw[HEAD ? kHeadNodes : 1][K];
-  __shared__ float s_part[HEAD ? head::kRowsPerBlock : 1][head::kMaxK * 256 + head::kMaxK];
+  __shared__ float s_part[HEAD ? kHelpHW : 1][head::kMaxK * 256 + head::kMaxK];
   __shared__ double s_sum[kThreads];
   __shared__ double s_cnt[kThreads];
   __shared__ int s_last;
@@ -273,64 +281,70 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
     }
     __syncthreads();
   }
-  static_assert(kHeadNodes == 8 * head::kRowsPerBlock, "one batch of 8 rows per half-wave");
   const int64_t i = blockIdx.x * (int64_t)NPB + threadIdx.x;
   const int64_t first = blockIdx.x * (int64_t)NPB;
   const int64_t n_blk = min<int64_t>(n, first + NPB);
-  head::HeadRows<K, HEAD ? 8 : 1> rows;
-  if constexpr (HEAD) {  // the head's weight and h rows arrive while the loss is evaluated
-    rows.init(hb.w, hb.D);
-    rows.load(first + threadIdx.x / 32, head::kRowsPerBlock, n_blk, hb.h, hb.D);
-  }
   double val = 0.0, cnt = 0.0;
-  if ((NPB == kThreads || (int)threadIdx.x < NPB) && i < n) {
-    const float yf = y[i];
-    double g[K];
+  if (!HEAD || (int)threadIdx.x < NPB) {  // the loss (wave 0 when HEAD)
+    if (i < n) {
+      const float yf = y[i];
+      double g[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) g[k] = 0.0;
-    if (yf == yf) {  // NaN targets are masked out (loss.py:22,220)
-      const double yy = (double)yf;
-      Dual<K> v[K];
+      for (int k = 0; k < K; ++k) g[k] = 0.0;
+      if (yf == yf) {  // NaN targets are masked out (loss.py:22,220)
+        const double yy = (double)yf;
+        Dual<K> v[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) v[k] = var<K>((double)pred[i * K + k], k);
-      Dual<K> r;
-      if constexpr (KIND == GINE_LOSS_NORMAL) {
-        r = crps_normal(v[0], v[1], yy);
-      } else if constexpr (KIND == GINE_LOSS_MIXED_NORMAL) {
-        r = crps_mixed_normal(v[0], v[1], v[2], yy, c);
-      } else if constexpr (KIND == GINE_LOSS_MIXED) {
-        r = crps_mixed<K, false>(v[0], v[1], v[2], v[3], cst<K>(u_fixed), yy, c, xi, t);
-      } else {
-        r = crps_mixed<K, true>(v[0], v[1], v[2], v[3], v[4], yy, c, xi, t);
+        for (int k = 0; k < K; ++k) v[k] = var<K>((double)pred[i * K + k], k);
+        Dual<K> r;
+        if constexpr (KIND == GINE_LOSS_NORMAL) {
+          r = crps_normal(v[0], v[1], yy);
+        } else if constexpr (KIND == GINE_LOSS_MIXED_NORMAL) {
+          r = crps_mixed_normal(v[0], v[1], v[2], yy, c);
+        } else if constexpr (KIND == GINE_LOSS_MIXED) {
+          r = crps_mixed<K, false>(v[0], v[1], v[2], v[3], cst<K>(u_fixed), yy, c, xi, t);
+        } else {
+          r = crps_mixed<K, true>(v[0], v[1], v[2], v[3], v[4], yy, c, xi, t);
+        }
+        val = r.v;
+        cnt = 1.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) g[k] = r.d[k];
       }
-      val = r.v;
-      cnt = 1.0;
 #pragma unroll
-      for (int k = 0; k < K; ++k) g[k] = r.d[k];
-    }
+      for (int k = 0; k < K; ++k) dpred[i * K + k] = g[k];
+      if (grad_unit != nullptr) {  // d loss / d pred for gloss = 1, as k_crps_bwd rounds it
+        const double cnt_all = s_count;
 #pragma unroll
-    for (int k = 0; k < K; ++k) dpred[i * K + k] = g[k];
-    if (grad_unit != nullptr) {  // d loss / d pred for gloss = 1, as k_crps_bwd rounds it
-      const double cnt_all = s_count;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const float gu = (float)(1.0 * g[k] / cnt_all);
-        grad_unit[i * K + k] = gu;
-        if constexpr (HEAD)  // d raw, as k_head_bwd forms it from grad_pred
-          s_graw[threadIdx.x][k] =
-              head::post_bwd(head::role_of(KIND, k), hb.raw[i * K + k], gu);
+        for (int k = 0; k < K; ++k) {
+          const float gu = (float)(1.0 * g[k] / cnt_all);
+          grad_unit[i * K + k] = gu;
+          if constexpr (HEAD)  // d raw, as k_head_bwd forms it from grad_pred
+            s_graw[threadIdx.x][k] =
+                head::post_bwd(head::role_of(KIND, k), hb.raw[i * K + k], gu);
+        }
       }
     }
-  }
-  if constexpr (HEAD) {
-    __syncthreads();
+    if constexpr (HEAD) {
+      __syncthreads();  // d raw in LDS
+      __syncthreads();  // the helpers' partial rows in LDS
+    }
+  } else if constexpr (HEAD) {  // waves 1..3: the head backward of the workgroup's nodes
+    head::HeadRows<K, kHelpU, HC> rows;
+    const int hw = threadIdx.x / 32 - NPB / 32;
+    rows.init(hb.w, hb.D);
+    rows.load(first + hw, kHelpHW, n_blk, hb.h, hb.D);  // arriving under the evaluation
+    __syncthreads();  // d raw in LDS
     rows.step([&](int64_t nd, float (&gr)[K]) {
 #pragma unroll
                 for (int k = 0; k < K; ++k) gr[k] = s_graw[nd - first][k];
               },
-              first + threadIdx.x / 32, head::kRowsPerBlock, n_blk, hb.dh, hb.D);
-    rows.flush(hb.slab + (size_t)blockIdx.x * (K * hb.D + K), hb.D, s_part);
+              first + hw, kHelpHW, n_blk, hb.dh, hb.D);
+    rows.put(s_part, hw, hb.D);
+    __syncthreads();  // the partial rows in LDS
   }
+  if constexpr (HEAD)
+    head::reduce_rows<K>(hb.slab + (size_t)blockIdx.x * (K * hb.D + K), hb.D, s_part, kHelpHW);
   s_sum[threadIdx.x] = val;
   s_cnt[threadIdx.x] = cnt;
   __syncthreads();
@@ -341,13 +355,16 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
     }
     __syncthreads();
   }
-  // publish the partial, then draw a ticket (MI355X_MICROARCH.md hand-off recipe: drain,
-  // agent-scope release, drain, relaxed agent-scope add; the last arriver acquires)
+  // publish the partial, then draw a ticket.  The partial goes out as agent-scope atomic
+  // exchanges (performed at the memory side, like the BatchNorm accumulator's adds) and the
+  // last arriver reads the partials with agent-scope atomic loads: no release / acquire
+  // fence -- an agent-scope release writes the XCD's whole L2 back, and with the head
+  // backward's dh rows just written that write-back sat in every workgroup's tail.
   if (threadIdx.x == 0) {
-    partials[2 * blockIdx.x] = s_sum[0];
-    partials[2 * blockIdx.x + 1] = s_cnt[0];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_exchange(&partials[2 * blockIdx.x], s_sum[0], __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(&partials[2 * blockIdx.x + 1], s_cnt[0], __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned int prev =
         __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -355,17 +372,12 @@ __global__ __launch_bounds__(kThreads) void k_crps(const float* __restrict__ pre
   }
   __syncthreads();
   if (!s_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   // fixed order: thread j sums partial rows j, j + 256, ... then the same tree as above
   const int P = gridDim.x;
   double a = 0.0, b = 0.0;
   for (int p = threadIdx.x; p < P; p += kThreads) {
-    a += partials[2 * p];
-    b += partials[2 * p + 1];
+    a += __hip_atomic_load(&partials[2 * p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b += __hip_atomic_load(&partials[2 * p + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   s_sum[threadIdx.x] = a;
   s_cnt[threadIdx.x] = b;
@@ -433,10 +445,11 @@ int crps_fwd_launch(const float* pred, const float* y, int64_t num_nodes, int32_
   hipLaunchKernelGGL((k_crps<KIND_, H_>), dim3((unsigned)blocks), dim3(kThreads), 0, s, pred, y, \
                      num_nodes, u, xi, c, t, dpred, partials, loss_out, count_out, ticket,      \
                      count_parts, grad_unit, hb ? *hb : HeadBwdArgs{})
-#define LAUNCH_CRPS(KIND_)                        \
-  do {                                            \
-    if (hb) LAUNCH_CRPS_H(KIND_, true);           \
-    else LAUNCH_CRPS_H(KIND_, false);             \
+#define LAUNCH_CRPS(KIND_)                                 \
+  do {                                                     \
+    if (!hb) LAUNCH_CRPS_H(KIND_, 0);                      \
+    else if (hb->D <= 128) LAUNCH_CRPS_H(KIND_, 1);        \
+    else LAUNCH_CRPS_H(KIND_, 2);                          \
   } while (0)
   switch (kind) {
     case GINE_LOSS_NORMAL: LAUNCH_CRPS(GINE_LOSS_NORMAL); break;
