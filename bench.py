@@ -591,6 +591,7 @@ PMC_KERNELS = {
     "gine_mp_fwd": ["gine::k_mp_fwd<32, 1, "],
     "gine_mp_fwd_mlp1": ["gine::k_mp_fwd_mlp1<"],
     "gine_mp_fwd_layer": ["gine::k_mp_fwd_layer<false, 5>"],
+    "gine_mlp_bwd_layer": ["gine::k_mlp_bwd_layer<5>"],
     # (the GPU box's host rounds the edge Linear mul-then-add: FMA = false)
     "gine_mp_bwd_mlp_wgrad": ["gine::k_mp_bwd_win<32, false, true, 5>"],
     "gine_mp_bwd": [("gine::k_mp_bwd_win<32, ", "gine::k_mp_bwd<32, 1, ")],
