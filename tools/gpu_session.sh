@@ -94,6 +94,9 @@ PY
     mpvar) for v in raincast-gnn_amd/csrc/build/var/*/; do n=$(basename "$v")
              GINE_HIP_LIB=${v}libgine_hip.so run mp_micro_${n} 300 python tools/mp_micro.py ${MPARGS:-}
            done ;;
+    mpnvar) for v in raincast-gnn_amd/raincast_gnn/_native/var/mp_*/; do n=$(basename "$v")
+             GINE_HIP_LIB=${v}libgine_hip.so run mp_micro_${n} 300 python tools/mp_micro.py ${MPARGS:-}
+           done ;;
     mpsq)  run mp_sq1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d "$OUT/mp_sq1" -o run -- \
                python3 tools/mp_micro.py --eager --reps 5 ${MPARGS:-}
            run mp_sq2 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/mp_sq2" -o run -- \
