@@ -11,15 +11,18 @@
 // which the two launches above run with a launch boundary where this one has a barrier.
 // Same layout as the one-launch forward (gine_mpmlp.hip): 768 threads, waves 0-3 multiply
 // ("matrix"), waves 4-11 stage ("helpers"):
-//   * the helpers stage both of the workgroup's tiles at once -- do into x[t], the a1 rows
-//     into o[t] -- and W2 (then W1, loaded under phase A's chains) through the padded LDS
-//     image w;
-//   * the matrix waves keep the weight planes in registers (split-bf16 chain of the row GEMM,
-//     gine_bf16x3.hpp), transpose each 32x32 accumulator block through a tile of their own
-//     and finish the EPI_DBN epilogue in place: dbn overwrites the a1 rows in o[t] (and goes
-//     to HBM for the weight-gradient engine);
-//   * after the barrier the helpers read the totals beside the matrix waves' W1 fragments,
-//     then stage da1 into x[t].
+//   * the helpers stage both of the workgroup's tiles at once -- do as split-bf16 planes
+//     into xp[t] (split once here, not inside the chains), the a1 rows into o[t] -- and W2
+//     (then W1, loaded under phase A's chains) through the padded LDS image w;
+//   * the matrix waves keep the weight planes in registers (the row GEMM's split-bf16 chain,
+//     gine_bf16x3.hpp) and transpose each 32x32 accumulator block through a tile of their
+//     own; the helpers run the EPI_DBN epilogue of tile t beside the chain of tile t + 1
+//     (double-buffered transposition tiles): dbn overwrites the a1 rows in o[t] and goes to
+//     HBM for the weight-gradient engine, and the BatchNorm-backward sums accumulate in the
+//     row GEMM's thread mapping;
+//   * after the barrier the helpers read the totals beside the matrix waves' W1 fragments
+//     (x-hat of their items computed before the totals arrive), then stage da1 as planes --
+//     tile 1's beside the chain of tile 0 -- and store the dz rows the matrix waves transpose.
 // Bit-identical to the pair: same tile -> workgroup map (xcd tile ranges, grid =
 // gine_mlp_num_partials), the same chains (k order, NaN redo on the fp32 chain), the same
 // epilogue and prologue arithmetic, the per-workgroup sums in the row GEMM's order (row groups

@@ -416,8 +416,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_mlp1(FusedArgs A) {
 //             accumulator), a1 tiles also kept in LDS;
 //   grid barrier (every workgroup resident: one per CU, host-checked);
 //   phase B = k_fwd2_bnacc on the workgroup's own tiles: BatchNorm finish from the
-//             accumulator totals, r = relu(bn(a1)) from the LDS tiles, Linear2 on the matrix
-//             waves, epilogue (bias, ResGnn ReLU / residual + mask) on the gather waves.
+//             accumulator totals, r = relu(bn(a1)) from the LDS tiles, split once into
+//             split-bf16 planes by the gather waves (the matrix waves' Linear2 chains read
+//             them instead of splitting inside the chain), epilogue (bias, ResGnn ReLU /
+//             residual + mask) on the gather waves.
 // W2 is loaded by the gather waves under the matrix role's last chain and staged in LDS
 // before the barrier; its fragments are read after it, beside the BatchNorm totals (gather
 // waves), so a workgroup arrives as soon as its phase A is done; the residual rows are
