@@ -748,6 +748,7 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     stream = torch.cuda.current_stream(device)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     tr.ar_events = []
+    thr0 = cpu_throttle()
     t0 = time.perf_counter()
     evs[0].record(stream)
     for i in range(args.steps):
@@ -757,6 +758,7 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    thr = throttle_delta(thr0, cpu_throttle())
     Fn.check_grid_barriers()  # a layer launch whose grid was not co-resident raises here
     in_order = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     per_step = sorted(in_order)
@@ -770,15 +772,31 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
     tr.ar_events = None
     pct["allreduce_p50"] = round(ar[len(ar) // 2], 4) if ar else None
     pct["stalls"] = stalled_steps(in_order, ar_steps)
+    pct["cpu_throttle"] = thr
     if world > 1:
+        own = elapsed
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
         st = pct["stalls"]
         pct["per_rank"] = gather_per_rank(pct[50], pct["allreduce_p50"], world, device,
                                           step_max=per_step[-1],
-                                          stalls=st["count"] if st else 0)
+                                          stalls=st["count"] if st else 0,
+                                          wall_ms=own / args.steps * 1e3,
+                                          events_ms=sum(in_order) / len(in_order),
+                                          gpu=device.index if device.type == "cuda" else -1)
+        check_rank_devices(pct["per_rank"], args)
     return tr, elapsed, pct
+
+
+def check_rank_devices(per_rank, args) -> None:
+    """RCCL runs one rank per GPU: every rank's device must differ (LOCAL_RANK -> GPU), and
+    the group must hold exactly --gpus ranks.  gloo rehearsals may put
+    several ranks on one GPU."""
+    assert len(per_rank) == args.gpus, (len(per_rank), args.gpus)
+    if args.dist_backend == "nccl" and not args.dry_run:
+        gpus = [r["gpu"] for r in per_rank]
+        assert len(set(gpus)) == len(gpus), f"ranks share a GPU under RCCL: {gpus}"
 
 
 def stalled_steps(in_order, ar_steps):
@@ -809,20 +827,83 @@ def stalled_steps(in_order, ar_steps):
     return out
 
 
-def gather_per_rank(step_p50, allreduce_p50, world, device, step_max=None, stalls=0):
+def _cgroup_file(name: str):
+    for d in ("/sys/fs/cgroup", "/sys/fs/cgroup/cpu", "/sys/fs/cgroup/cpu,cpuacct"):
+        f = os.path.join(d, name)
+        if os.path.exists(f):
+            return f
+    return None
+
+
+def cpu_share() -> int:
+    """CPUs this job may use: the cgroup quota (cpu.max or cpu.cfs_quota_us / period), else
+    OMP_NUM_THREADS, else the affinity mask (os.cpu_count() on the GPU boxes shows the whole
+    machine, many times the job's share)."""
+    try:
+        f = _cgroup_file("cpu.max")
+        if f:
+            q, per = open(f).read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) / int(per)))
+        fq, fp = _cgroup_file("cpu.cfs_quota_us"), _cgroup_file("cpu.cfs_period_us")
+        if fq and fp and int(open(fq).read()) > 0:
+            return max(1, int(int(open(fq).read()) / int(open(fp).read())))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        return int(omp)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_throttle():
+    """The cgroup's CPU-throttling counters {nr_throttled, throttled_usec} (None when the
+    cgroup does not expose them): read before and after the timed steps, their difference
+    says whether the job's CPU quota was throttled while it ran."""
+    f = _cgroup_file("cpu.stat")
+    if not f:
+        return None
+    out = {}
+    try:
+        for line in open(f):
+            k, v = line.split()[:2]
+            if k in ("nr_throttled", "throttled_usec", "throttled_time", "nr_periods"):
+                out[k] = int(v)
+    except (OSError, ValueError):
+        return None
+    return out or None
+
+
+def throttle_delta(a, b):
+    if not a or not b:
+        return None
+    return {k: b[k] - a[k] for k in b if k in a}
+
+
+def gather_per_rank(step_p50, allreduce_p50, world, device, step_max=None, stalls=0,
+                    wall_ms=None, events_ms=None, gpu=-1):
     """Every rank's p50 step time, p50 all-reduce time, slowest step (ms) and stalled-step
     count, for the N > 1 line's decomposition (a tensor all_gather: on the GPU over RCCL, on
     the CPU over gloo)."""
-    mine = torch.tensor([step_p50, -1.0 if allreduce_p50 is None else allreduce_p50,
-                         -1.0 if step_max is None else step_max, float(stalls)],
+    def opt(v):
+        return -1.0 if v is None else float(v)
+    mine = torch.tensor([step_p50, opt(allreduce_p50), opt(step_max), float(stalls),
+                         opt(wall_ms), opt(events_ms), float(gpu)],
                         device=device if dist.get_backend() == "nccl" else "cpu",
                         dtype=torch.float64)
     every = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(every, mine)
+
+    def val(x, nd=4):
+        return round(x.item(), nd) if x.item() >= 0 else None
+    # wall_ms_per_step: this rank's own wall clock between the synchronised barriers (the
+    # line's ms_per_step is the max over ranks); events_ms_per_step: the mean of its HIP-event
+    # step times -- the two reconcile when the host kept the stream fed
     return [{"rank": r, "step_ms_p50": round(v[0].item(), 4),
-             "allreduce_ms_p50": round(v[1].item(), 4) if v[1].item() >= 0 else None,
-             "step_ms_max": round(v[2].item(), 4) if v[2].item() >= 0 else None,
-             "stalled_steps": int(v[3].item())}
+             "allreduce_ms_p50": val(v[1]), "step_ms_max": val(v[2]),
+             "stalled_steps": int(v[3].item()),
+             "wall_ms_per_step": val(v[4]), "events_ms_per_step": val(v[5]),
+             "gpu": int(v[6].item()) if v[6].item() >= 0 else None}
             for r, v in enumerate(every)]
 
 
@@ -953,6 +1034,7 @@ def dry_run(args, rank: int, world: int) -> None:
                        "allreduce_floats": reducer.numel, "parameters": n_params,
                        "parallelism": f"dp{world}"},
             "allreduce_ms_p50": round(ar_p50, 4) if ar_p50 is not None else None,
+            "host_threads_per_rank": torch.get_num_threads(), "cpu_share": cpu_share(),
             "per_rank": per_rank}), flush=True)
     if dist.is_initialized():
         dist.barrier()
@@ -1053,6 +1135,12 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} rank(s) "
                          f"(WORLD_SIZE); they must agree")
+    # the host's CPU share split over the ranks on it, before any GPU call: N ranks x
+    # OMP_NUM_THREADS intra-op threads on one share oversubscribe it (the
+    # N > 1 rehearsals' host-side stalls inside the collective)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world) or world)
+    threads = max(1, cpu_share() // max(1, local_world))
+    torch.set_num_threads(threads)
     if args.dry_run:
         return dry_run(args, rank, world)
     if world > 1 or args.force_allreduce:
@@ -1111,6 +1199,10 @@ def main():
         del tr4
         torch.cuda.empty_cache()
 
+    rccl_world = (dist.get_world_size() if dist.is_initialized()
+                  and dist.get_backend() == "nccl" else None)
+    if world > 1 and args.dist_backend == "nccl":
+        assert rccl_world == args.gpus, (rccl_world, args.gpus)
     kernels = time_kernels(tr, args.kernel_reps) if rank == 0 else {}
     result = None
     if rank == 0:
@@ -1136,8 +1228,7 @@ def main():
             "dtype": "f32 (split-bf16x3 GEMM products, fp32 accumulate)",
             "data": "synthetic (k-NN station graphs, random-init weights)",
             "backend": dist.get_backend() if dist.is_initialized() else None,
-            "rccl_world_size": (dist.get_world_size() if dist.is_initialized()
-                                and dist.get_backend() == "nccl" else None),
+            "rccl_world_size": rccl_world,
             "launcher": ("bench.py --gpus (one child process per GPU)"
                          if os.environ.get(LAUNCH_ENV) == "1" else
                          "torch.distributed.run" if world > 1 else "single process"),
@@ -1159,6 +1250,10 @@ def main():
             "per_rank": pct.get("per_rank"),
             # steps > 10x the median on rank 0 (flagged, still inside `value`)
             "stalled_steps": pct.get("stalls"),
+            # host side of the N > 1 line: intra-op threads per rank (the CPU share over the
+            # local ranks) and the cgroup's throttling counters over the timed steps
+            "host_threads_per_rank": threads, "cpu_share": cpu_share(),
+            "cpu_throttle_timed": pct.get("cpu_throttle"),
             "roofline": roof, "roofline_step": roof_step,
             "roofline_message_passing": roof_mp,
             "strong_scaling_cfg4": strong,

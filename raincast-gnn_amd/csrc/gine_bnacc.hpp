@@ -56,6 +56,7 @@ constexpr int kBnAccSnap = kBnAccWords + kBnAccCounts;
 // 8 per-XCD arrival counts and the 8 per-XCD generations
 constexpr int kBarLine = 16;  // int64 words per line
 constexpr int kBarWords = (2 + 2 * kNumXcd) * kBarLine;
+constexpr int kBarFailWord = kBarLine;  // (barrier-area word index: the failure count)
 
 __host__ __device__ constexpr int64_t bnacc_words(int D) {
   return (int64_t)(kBnAccReplicas * kBnAccWords + kBnAccCounts + 2 * kBnAccSnap) * 2 * D + 3 +
@@ -74,6 +75,17 @@ __device__ __forceinline__ long long* bnacc_phase(long long* acc, int W) {
 
 __device__ __forceinline__ long long* bnacc_barrier(long long* acc, int W) {
   return bnacc_phase(acc, W) + 3;
+}
+
+// A grid barrier of this accumulator has failed (its failure word is non-zero) since the host
+// last zeroed it (raincast_gnn.functional.check_grid_barriers): sticky -- every consumer then
+// finishes NaN statistics and leaves the running statistics alone (see bnacc_total).  LIVE:
+// an agent-scope atomic load (inside the launch whose workgroups may be adding to it).
+template <bool LIVE = false>
+__device__ __forceinline__ bool bnacc_poisoned(long long* acc, int W) {
+  long long* w = bnacc_barrier(acc, W) + kBarFailWord;
+  if constexpr (LIVE) return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  else return *w != 0;
 }
 
 // PHASE = false: the caller (gine_mp_fwd_layer) keeps the phase word itself.
@@ -157,7 +169,13 @@ __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool
   const unsigned long long fm = (1ull << kBnAccCountBits) - 1, cnt_d = (unsigned long long)d[3];
   const bool n_nan = (cnt_d & fm) != 0, n_pinf = ((cnt_d >> kBnAccCountBits) & fm) != 0,
              n_ninf = ((cnt_d >> (2 * kBnAccCountBits)) & fm) != 0;
-  const bool nan = n_nan || (n_pinf && n_ninf) || ph - consumed != 1;
+  // a grid barrier of this accumulator has failed since the host last zeroed it: its
+  // snapshot and phase words may have been written from incomplete totals (workgroup 0 of
+  // the failed launch) while late workgroups' atomics landed after them, so every later
+  // statistic of this accumulator is NaN until the host's reset (check_grid_barriers) --
+  // never finite but wrong
+  const bool poisoned = bnacc_poisoned<LIVE>(acc, W);
+  const bool nan = n_nan || (n_pinf && n_ninf) || ph - consumed != 1 || poisoned;
   double v;
   if (nan) v = __builtin_nan("");
   else if (n_pinf) v = __builtin_inf();
@@ -191,8 +209,6 @@ __device__ __forceinline__ double bnacc_total(long long* acc, int W, int t, bool
 // (gine_bn_acc_barrier_failures, raincast_gnn.functional.check_grid_barriers).  The late
 // workgroups of such a launch complete the barrier among themselves (their arrival completes
 // the counts) and see complete totals.
-constexpr int kBarFailWord = kBarLine;  // (barrier-area word index)
-
 __device__ __forceinline__ bool grid_barrier(long long* bar, int nblocks) {
   const int b = blockIdx.x, x = b % kNumXcd;
   long long* glob = bar;

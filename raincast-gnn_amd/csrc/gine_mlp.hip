@@ -777,12 +777,16 @@ __global__ __launch_bounds__(2 * D) void k_fwd2_bnacc(const float* __restrict__ 
   auto finish = [=]() {  // by value: a reference to a kernel argument puts it in scratch
     const int t = threadIdx.x;  // 2D threads: word t = (sum | sum of squares) of column t % D
     s_tot[t] = bnacc_total(acc, 2 * D, t, blockIdx.x == 0);
+    // a failed grid barrier on this accumulator (sticky until the host's reset): NaN
+    // statistics from bnacc_total, running statistics untouched
+    BnFwdParams qq = q;
+    if (bnacc_poisoned(acc, 2 * D)) qq.update_running = 0;
     __syncthreads();
     if (t < D)
-      bn_finish_channel(q, D, t, s_tot[t], s_tot[D + t], blockIdx.x == 0, &s_bn[2 * D + t],
+      bn_finish_channel(qq, D, t, s_tot[t], s_tot[D + t], blockIdx.x == 0, &s_bn[2 * D + t],
                         &s_bn[3 * D + t]);
     if (blockIdx.x == 0 && t == 0) {
-      if (q.update_running && q.nbt != nullptr) q.nbt[0] = q.nbt[0] + 1;
+      if (qq.update_running && qq.nbt != nullptr) qq.nbt[0] = qq.nbt[0] + 1;
       bnacc_mark_consumed(acc, 2 * D);
     }
     __syncthreads();

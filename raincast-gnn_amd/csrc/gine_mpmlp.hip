@@ -513,7 +513,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   LAYER_RT(17);
   // the workgroup arrives as soon as phase A is done; W2's fragments are read after the
   // barrier, beside the BatchNorm totals
-  if (tid == 0) L.barrier_failed = grid_barrier(bnacc_barrier(A.bnacc, 2 * kD), gridDim.x) ? 0 : 1;
+  // (a barrier that failed earlier on this accumulator, before the host's reset, counts too:
+  // bnacc_poisoned is sticky)
+  if (tid == 0)
+    L.barrier_failed = grid_barrier(bnacc_barrier(A.bnacc, 2 * kD), gridDim.x) &&
+                               !bnacc_poisoned<true>(A.bnacc, 2 * kD)
+                           ? 0
+                           : 1;
   __syncthreads();  // (also: W2 staged by the gather waves)
   LAYER_MARK(4);
   LAYER_RT(18);

@@ -23,10 +23,17 @@ _SHARED_DEVICE = False
 
 def device_shared() -> bool:
     """True when another rank of the process group uses this process's GPU as well (set by
+    note_device_sharing), or when the launcher started more local ranks than this host has
+    visible GPUs (LOCAL_WORLD_SIZE > device count: some ranks must share one -- detected
+    without the caller's help, e.g. for drop-in GINEConv users that never call
     note_device_sharing).  Their kernels can then hold CUs whenever ours launch, so launches
-    that need their whole grid resident at once (the one-launch layer forward's grid
-    barrier: raincast_gnn.functional.layer_forward_ok) are not used."""
-    return _SHARED_DEVICE
+    that need their whole grid resident at once (the one-launch layer forward's and
+    backward's grid barriers: raincast_gnn.functional.layer_forward_ok / layer_backward_ok)
+    are not used."""
+    if _SHARED_DEVICE:
+        return True
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+    return local > 1 and torch.cuda.is_available() and local > torch.cuda.device_count()
 
 
 def note_device_sharing(group=None) -> bool:
@@ -70,6 +77,7 @@ class FlatGradReducer:
         self.group = group
         self._tail_lo = None       # overlap_after: where the early-reduced tail starts
         self._tail_started = False
+        self._armed = False        # this step's hook is registered (tail-then-front order)
         self._tail_work = None
         self._side = None
         if flat is not None:  # gradients already live in this buffer (e.g. FlatAdamW's,
@@ -107,7 +115,17 @@ class FlatGradReducer:
         if not self._collective():
             return
         world = dist.get_world_size(self.group)
+        armed, self._armed = self._armed, False
         if not self._tail_started:
+            if armed:
+                # the hook bailed on this rank (a tail gradient outside the flat buffer) while
+                # other ranks may have started their tail: keep the collective sequence every
+                # rank issues -- tail, then front -- independent of the rank
+                tail, head = self.flat[self._tail_lo:], self.flat[:self._tail_lo]
+                dist.all_reduce(tail, op=dist.ReduceOp.SUM, group=self.group)
+                dist.all_reduce(head, op=dist.ReduceOp.SUM, group=self.group)
+                self.flat.div_(world)
+                return
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
             self.flat.div_(world)
             return
@@ -158,6 +176,7 @@ class FlatGradReducer:
         if (isinstance(x, torch.Tensor) and x.requires_grad and torch.is_grad_enabled()
                 and self._collective()):
             x.register_hook(self._start_tail)
+            self._armed = True
 
     def _start_tail(self, grad):
         # every tail gradient must already sit in its slice (adopted flat views); otherwise

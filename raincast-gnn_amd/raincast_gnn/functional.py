@@ -318,13 +318,17 @@ def bn_accumulator(bn: "BnConfig", D: int, dev, kind: str = "fwd") -> "torch.Ten
 _FAIL_INDEX: dict = {}
 
 
-def check_grid_barriers() -> None:
+def check_grid_barriers(group=None) -> None:
     """Raise GineError if a one-launch layer forward's or backward's grid barrier timed out
     since the last check (gine_bn_acc_barrier_failures_index: the grid was not resident at
-    once, so that launch's outputs are NaN in the failed workgroups' rows).  The affected
-    accumulators are re-zeroed, so the next step starts a fresh pairing.  Reads device
-    memory: call it where the caller synchronises anyway (end of an epoch, after a
-    benchmark's timed steps)."""
+    once, so that launch's outputs are NaN in the failed workgroups' rows; the failure is
+    sticky on the device: every later statistic of that accumulator is NaN until this reset).
+    The affected accumulators are re-zeroed, so the next step starts a fresh pairing.  Reads
+    device memory: call it where the caller synchronises anyway (end of an epoch, after a
+    benchmark's timed steps; drop-in GINEConv users: at their own synchronisation points).
+    Collective under torch.distributed (every rank of ``group`` must call it): the failure
+    counts are all-reduced (MAX) first, so every rank raises together instead of the others
+    blocking in their next collective."""
     failed = []
     for mod, per_dev in list(_BN_ACC.items()):
         for (dev, kind), acc in list(per_dev.items()):
@@ -338,6 +342,17 @@ def check_grid_barriers() -> None:
             if n:
                 failed.append((type(mod).__name__, kind, str(dev), n))
                 acc.zero_()
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        on_gpu = dist.get_backend(group) == "nccl"
+        t = torch.tensor([len(failed)], dtype=torch.int64,
+                         device=torch.device("cuda", torch.cuda.current_device()) if on_gpu
+                         else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        if int(t.item()) and not failed:
+            raise _lib.GineError(
+                "gine_mp_fwd_layer / gine_mlp_bwd_layer: another rank's grid barrier timed out "
+                "(its launch's outputs are NaN); raised on every rank together")
     if failed:
         raise _lib.GineError(
             "gine_mp_fwd_layer / gine_mlp_bwd_layer: the grid barrier timed out (the launch's "

@@ -149,3 +149,92 @@ def test_overlap_after_rejects_a_tail_that_is_not_the_end():
     with pytest.raises(ValueError, match="end of the flat buffer"):
         red.overlap_after(model.conv, list(model.conv.parameters()))   # aggr follows it
     red.overlap_after(model.conv, list(model.conv.parameters()) + list(model.aggr.parameters()))
+
+
+def _bail_worker(rank, world, port, result_dir):
+    """Rank 1's tail hook bails (as when a tail gradient is outside the flat buffer) while
+    rank 0's starts the tail's collective inside the backward: every rank must still issue
+    the same collective sequence (tail, then front), and the sums must equal the plain
+    reduction's (distributed.py _start_tail)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import gine_cpu as O
+    from raincast_gnn.data import collate, synthetic_samples
+    torch.manual_seed(7)
+    model = O.OracleGNN(35, 32, 2, "MixedLoss", "False", 1.71, 0.5)
+    broadcast_parameters(model)
+    samples = synthetic_samples(40, 6, k=5, seed=11)
+    lo, hi = shard_range(len(samples), rank, world)
+    batch = collate(samples[lo:hi])
+    red = FlatGradReducer(model.parameters())
+    red.overlap_after(model.conv, list(model.conv.parameters()) + list(model.aggr.parameters()))
+    if rank == 1:
+        red._start_tail = lambda grad: None  # the hook bails on this rank only
+    red.zero_()
+    model.crps(model(batch), batch.y).backward()
+    started = red._tail_started
+    red.all_reduce_()
+    red2 = FlatGradReducer(model.parameters())
+    red2.zero_()
+    model.crps(model(batch), batch.y).backward()
+    red2.all_reduce_()
+    torch.save({"started": started, "flat": red.flat.clone(), "plain": red2.flat.clone()},
+               os.path.join(result_dir, f"bail{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dp_tail_hook_bailing_on_one_rank_keeps_the_collective_order(tmp_path):
+    world = 2
+    mp.spawn(_bail_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = [torch.load(tmp_path / f"bail{r}.pt", weights_only=True) for r in range(world)]
+    assert res[0]["started"] and not res[1]["started"]
+    for r in res:
+        assert torch.equal(r["flat"], r["plain"])
+    assert torch.equal(res[0]["flat"], res[1]["flat"])
+
+
+def _barrier_check_worker(rank, world, port, result_dir):
+    """check_grid_barriers is collective: a failure word on rank 0 only makes BOTH ranks raise
+    (instead of rank 1 blocking in its next collective while rank 0 raised)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ctypes
+    from raincast_gnn import _lib
+    from raincast_gnn import functional as Fn
+
+    class FakeBn:
+        num_features = 128
+    words = ctypes.c_int64(0)
+    _lib.call("gine_bn_acc_words", 128, ctypes.byref(words))
+    idx = ctypes.c_int64(0)
+    _lib.call("gine_bn_acc_barrier_failures_index", 128, ctypes.byref(idx))
+    acc = torch.zeros(int(words.value), dtype=torch.int64)
+    if rank == 0:
+        acc[int(idx.value)] = 3
+    fake = FakeBn()  # (_BN_ACC holds its modules weakly)
+    Fn._BN_ACC[fake] = {("cpu", "fwd"): acc}
+    raised = None
+    try:
+        Fn.check_grid_barriers()
+    except _lib.GineError as e:
+        raised = str(e)
+    Fn._BN_ACC.clear()
+    Fn.check_grid_barriers()  # reset: nothing pending on any rank
+    torch.save({"raised": raised, "acc_sum": int(acc.abs().sum())},
+               os.path.join(result_dir, f"chk{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_grid_barrier_check_raises_on_every_rank(tmp_path):
+    world = 2
+    mp.spawn(_barrier_check_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+             join=True)
+    res = [torch.load(tmp_path / f"chk{r}.pt", weights_only=True) for r in range(world)]
+    assert "grid barrier timed out" in res[0]["raised"] and res[0]["acc_sum"] == 0
+    assert "another rank" in res[1]["raised"]

@@ -173,6 +173,20 @@ def test_layer_barrier_failure_is_loud(monkeypatch):
     finally:
         _lib.call("gine_testing_layer_extra_workgroups", 0)
     assert torch.isnan(y).any(), "the workgroups whose barrier failed must poison their rows"
+    assert torch.equal(bn.running_mean, rm0) and torch.equal(bn.running_var, rv0)
+    nbt0 = bn.num_batches_tracked.clone()
+    # the failure is sticky on the device: production launches on the same
+    # accumulator before the host's check -- the one-launch layer and the pair -- give NaN
+    # everywhere and leave the running statistics alone, never finite-but-wrong statistics
+    for layer in (True, False):
+        monkeypatch.setattr(options, "LAYER_FWD", layer)
+        with torch.no_grad():
+            y2 = conv.forward_residual_relu(x, eid, ead)
+        torch.cuda.synchronize()
+        assert torch.isnan(y2).all(), layer
+        assert torch.equal(bn.running_mean, rm0) and torch.equal(bn.running_var, rv0), layer
+        assert torch.equal(bn.num_batches_tracked, nbt0), layer
+    monkeypatch.setattr(options, "LAYER_FWD", True)
     with pytest.raises(_lib.GineError, match="grid barrier timed out"):
         Fn.check_grid_barriers()
     acc = Fn._BN_ACC[bn][(DEV, "fwd")]
