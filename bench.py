@@ -48,6 +48,10 @@ from raincast_gnn.params import BENCH_CONFIGS  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix peak (dense)
+# what the node-MLP products actually execute: split-bf16x3 (gine_bf16x3.hpp), six
+# v_mfma_f32_32x32x16_bf16 per fp32-class product on the bf16 rate (16x fp32, dense): the
+# ceiling of an fp32-class flop on the instructions the kernels run
+BF16X3_EXEC_PEAK_TFLOPS = round(16 * FP32_MFMA_PEAK_TFLOPS / 6, 1)
 
 
 def log(*a):
@@ -502,6 +506,10 @@ def roofline_for(kernels: dict, layers: int, work: dict, config: str = "cfg2"):
     if "gine_mlp_bwd_layer" in kernels:  # the pair in one launch
         step += ["gine_mlp_bwd_layer"]
     timed = [k for k in step if k in kernels]
+    # the kernels table also times launches the step does not run (the pair forms, the
+    # stand-alone gather / GEMM / finalize entry points): marked, for context only
+    for k, rec in kernels.items():
+        rec["in_step"] = k in timed
     dominant = max(timed, key=lambda k: kernels[k]["us"])
     out = roof_of(dominant, kernels[dominant], layers, work, config)
     # the other per-layer launches of the step against their own 8(d) floors, for context
@@ -520,7 +528,11 @@ def roof_of(name: str, rec: dict, layers: int, work: dict, config: str = "cfg2")
     sec = rec["us"] * 1e-6
     if t_mfma > t_hbm:
         roof = {"kernel": name, "bound": "mfma", "achieved": round(f / sec * 1e-12, 2),
-                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s"}
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                # the same flops against the split-bf16x3 instructions' own ceiling (the
+                # fp32 peak flatters an MFMA-bound frac by 16/6)
+                "peak_executed": BF16X3_EXEC_PEAK_TFLOPS,
+                "frac_executed": round(f / sec * 1e-12 / BF16X3_EXEC_PEAK_TFLOPS, 4)}
     else:
         roof = {"kernel": name, "bound": "hbm", "achieved": round(b / sec * 1e-9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s"}
@@ -1144,6 +1156,10 @@ def main():
     if args.dry_run:
         return dry_run(args, rank, world)
     if world > 1 or args.force_allreduce:
+        if world == 1:  # a forced 1-rank group outside a launcher: its own rendezvous
+            for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0"),
+                         ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(_free_port()))):
+                os.environ.setdefault(k, v)
         dist.init_process_group(args.dist_backend)
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     ndev = torch.cuda.device_count()

@@ -14,12 +14,15 @@
 // gine_mlp.hip row-tile GEMM) must agree bit for bit: both use these helpers with the same
 // k permutation.
 //
-// Where it is used: the row-tile GEMMs (weights split once per workgroup, the A fragment
-// split as it is read) and the fused forward's matrix chain.  Not in the weight-gradient
-// engine (gine_wgrad.hpp): there both operands stream through LDS, every wave re-splits
-// what it reads, and at one wave per SIMD the split's VALU work serialises with the MFMA
-// chain -- measured slower than the fp32 engine (cfg2 0.5536 / 0.5445 vs 0.5489 / 0.5354 ms
-// even at 4 waves per SIMD; cfg3 2.86 / 2.88 vs 2.84 / 2.84; profiles/r03_s12_*).
+// Where it is used: every node-MLP product.  The row-tile GEMMs split the weights once per
+// workgroup and the A fragment as it is read; the one-launch layers (gine_mpmlp.hip
+// k_mp_fwd_layer, gine_mlpbwd.hip k_mlp_bwd_layer) have their A tiles split ONCE into LDS
+// planes by the waves that produce them; the weight-gradient engines (gine_wgrad.hpp
+// wgrad_body_x3, kMlpEngX3: stand-alone, beside the dz GEMM and inside the window backward)
+// have each staged value split once by its stager into column-major planes.  (Round 3's
+// engine forms that re-split per wave measured slower than the fp32 engine, profiles/
+// r03_s12_*; the stager-split form replaced them in round 4, and round 5 moved the window
+// backward's engine onto it too)
 #pragma once
 
 #include "gine_common.hpp"

@@ -157,6 +157,24 @@ struct FusedLds {
 };
 static_assert(4 * 32 * kTLD * 4 + 2 * 8 * kD * 8 <= kD * kLD * 4, "scratch fits in w");
 
+// The one-launch layer's phase A hands each z tile from the gather waves to the matrix waves
+// as split-bf16 planes (hi | mid | lo, gine_bf16x3.hpp split2), split ONCE by the producers:
+// in the pair form every matrix wave splits the whole 32x128 A tile inside its chain (4x the
+// work, on the SIMDs the gather waves issue from: the 4 matrix waves' in-loop split is ~450
+// VALU instructions each per tile against the gather waves' ~570).  The fp32 z tile is not
+// kept in LDS (the rare non-finite redo reads z back from HBM): tile it's planes live in the
+// z region (it even) or in the w region past the matrix waves' transposition tiles and
+// statistics scratch (it odd; W1's staging there is over by then).
+constexpr int kPS = kD + 8;  // split-plane row stride (bf16): conflict-free 16-byte reads
+constexpr int kPlaneBytes = 3 * kTileRows * kPS * 2;
+constexpr int kPlaneOffW = 4 * 32 * kTLD * 4 + 2 * 8 * kD * 8;  // bytes into w
+static_assert(kPlaneOffW + kPlaneBytes <= kD * kLD * 4, "odd tiles' planes fit in w");
+static_assert(kPlaneBytes <= 2 * kTileRows * kLD * 4, "even tiles' planes fit in the z tiles");
+__device__ __forceinline__ uint16_t* tile_planes(FusedLds& L, int it) {
+  return (it & 1) ? reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(L.w) + kPlaneOffW)
+                  : reinterpret_cast<uint16_t*>(&L.z[0][0]);
+}
+
 // Matrix role (waves 0-3).  Barriers: 1 + (nt + 1), as the gather role.
 // LAYER (gine_mp_fwd_layer): every a1 tile is also kept in LDS (a1k[it], row-major, at most
 // kLayerTiles of them) for the second half of the layer, and the producer's phase word is
@@ -198,7 +216,17 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
   if constexpr (GINE_GEMM_BF16X3) bp.from(bf);
   __syncthreads();  // (iteration 0: the gather role stages the first tile)
   if constexpr (LAYER) LAYER_MARK(8);
-  double st1[4] = {0.0, 0.0, 0.0, 0.0}, st2[4] = {0.0, 0.0, 0.0, 0.0};
+  // per-column BatchNorm sums of this lane's (row group, 4 columns), kept in the statistics
+  // scratch of LDS between tiles rather than in 16 VGPRs beside the B planes (the lane's own
+  // slots, brought into registers for each tile's rows: the same sequential order, the same
+  // bits); W1's staging is over
+  double* sr = reinterpret_cast<double*>(&L.w[4 * 32 * kTLD]);  // [2][8][kD]
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = 32 * wave + 4 * cq + k;
+    sr[(0 * 8 + grp) * kD + c] = 0.0;
+    sr[(1 * 8 + grp) * kD + c] = 0.0;
+  }
   const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
   float* tt = &L.w[wave * 32 * kTLD];
   for (int it = 1; it <= nt; ++it) {
@@ -210,7 +238,36 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
     floatx16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    if constexpr (GINE_GEMM_BF16X3) {  // the row-tile GEMM's split-bf16 chain (gine_mlp.hip)
+    if constexpr (LAYER) {  // the same chain from the gather waves' split planes
+      static_assert(GINE_GEMM_BF16X3, "the layer forward reads split planes");
+      const uint16_t* pa = tile_planes(L, it - 1) + c32 * kPS + h * kKS;
+      auto frag = [&](int s8) {
+        Bf16x3 a;
+        a.h = *reinterpret_cast<const bf16x8_t*>(pa + 8 * s8);
+        a.m = *reinterpret_cast<const bf16x8_t*>(pa + kTileRows * kPS + 8 * s8);
+        a.l = *reinterpret_cast<const bf16x8_t*>(pa + 2 * kTileRows * kPS + 8 * s8);
+        return a;
+      };
+      // one fragment in flight beside the current block's six MFMAs (192 cycles hide the LDS
+      // latency): with all eight hoisted the matrix waves' B planes (96 VGPRs) spilled
+      Bf16x3 a = frag(0);
+#pragma unroll
+      for (int s8 = 0; s8 < (GINE_FUSED_DBG == 2 ? 1 : kKS / 8); ++s8) {
+        Bf16x3 an = a;
+        if (s8 + 1 < kKS / 8) an = frag(s8 + 1);
+        acc = mfma_bf16x3(a, bp.f[s8], acc);
+        __builtin_amdgcn_sched_barrier(0);
+        a = an;
+      }
+      if (wave_any_nan(acc)) {  // non-finite operands: the fp32 chain on z read back from HBM
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the gather waves' z stores
+        const int64_t zr = min((int64_t)T * kTileRows + c32, (int64_t)A.N - 1);
+        acc = mfma_f32_row_mem<kKS>(A.z + zr * kD + h * kKS,
+                                    A.W1 + (size_t)(32 * wave + c32) * kD + h * kKS, 1, acc);
+      }
+    } else if constexpr (GINE_GEMM_BF16X3) {  // the row-tile GEMM's split-bf16 chain (gine_mlp.hip)
 #pragma unroll
       for (int s = 0; s < (GINE_FUSED_DBG == 2 ? 1 : kKS / 8); ++s) {
         const float4 a0 = *reinterpret_cast<const float4*>(&arow[8 * s]);
@@ -243,6 +300,13 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
 #pragma unroll
     for (int r = 0; r < 16; ++r) tt[((r & 3) + 8 * (r >> 2) + 4 * h) * kTLD + c32] = acc[r];
     __builtin_amdgcn_wave_barrier();
+    // the running sums come into registers for the tile's 4 rows (same order, same bits)
+    double st1[4], st2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      st1[k] = sr[(0 * 8 + grp) * kD + 32 * wave + 4 * cq + k];
+      st2[k] = sr[(1 * 8 + grp) * kD + 32 * wave + 4 * cq + k];
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = grp + 8 * i;
@@ -263,6 +327,11 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
         *reinterpret_cast<float4*>(&a1k[(it - 1) * kTileRows * kLD + row * kLD + 32 * wave +
                                         4 * cq]) = make_float4(o4[0], o4[1], o4[2], o4[3]);
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sr[(0 * 8 + grp) * kD + 32 * wave + 4 * cq + k] = st1[k];
+      sr[(1 * 8 + grp) * kD + 32 * wave + 4 * cq + k] = st2[k];
+    }
     __builtin_amdgcn_wave_barrier();  // the next tile's transposition writes come after
     if constexpr (LAYER) {
       if (it <= 2) LAYER_MARK(8 + 2 * it);
@@ -270,13 +339,6 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
     __syncthreads();
   }
   // per-column partials: the 8 row groups added in fixed order (row-tile GEMM order)
-  double* sr = reinterpret_cast<double*>(&L.w[4 * 32 * kTLD]);  // [2][8][kD]
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int c = 32 * wave + 4 * cq + k;
-    sr[(0 * 8 + grp) * kD + c] = st1[k];
-    sr[(1 * 8 + grp) * kD + c] = st2[k];
-  }
   __builtin_amdgcn_wave_barrier();
   const int which = lane >> 5, cc = 32 * wave + (lane & 31);
   double s = 0.0;
@@ -295,7 +357,9 @@ __device__ __forceinline__ void matrix_role(const FusedArgs& A, FusedLds& L, con
 
 // Gather role (waves 4-11).  Barriers: 1 + (nt + 1), as the matrix role; without LAST_SYNC
 // the caller runs the last one (after work of its own beside the matrix role's last tile).
-template <bool FMA, bool LAST_SYNC = true>
+// PLANES (the one-launch layer): the tile goes to the matrix waves as split-bf16 planes
+// (tile_planes) instead of an fp32 LDS tile.
+template <bool FMA, bool LAST_SYNC = true, bool PLANES = false>
 __device__ __forceinline__ void gather_role(const FusedArgs& A, FusedLds& L, const TileSeq& ts,
                                             int nt) {
   const int p = threadIdx.x - kMatThreads;
@@ -389,7 +453,17 @@ __device__ __forceinline__ void gather_role(const FusedArgs& A, FusedLds& L, con
       const int r = hw + kHalves * i;
       const int64_t n = (int64_t)T * kTileRows + r;
       const f4v zv = add_scaled(acc[i], ope, self[i]);
-      *reinterpret_cast<f4v*>(&sz[r * kLD + 4 * t]) = zv;
+      if constexpr (PLANES) {
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split2(zv.x, zv.y, h0, m0, l0);
+        split2(zv.z, zv.w, h1, m1, l1);
+        uint16_t* pl = tile_planes(L, it) + r * kPS + 4 * t;
+        *reinterpret_cast<uint2*>(pl) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(pl + kTileRows * kPS) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(pl + 2 * kTileRows * kPS) = make_uint2(l0, l1);
+      } else {
+        *reinterpret_cast<f4v*>(&sz[r * kLD + 4 * t]) = zv;
+      }
       if (n < N) *reinterpret_cast<f4v*>(A.z + n * kD + 4 * t) = zv;
     }
     if (it < 2) LAYER_MARK_T(kMatThreads, 14 + it);
@@ -428,7 +502,6 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_mlp1(FusedArgs A) {
 // the BatchNorm totals are integer sums, the MFMA chains and epilogues are the row GEMM's).
 // ---------------------------------------------------------------------------------------
 constexpr int kLayerTiles = 2;  // a1 tiles a workgroup keeps in LDS
-constexpr int kPS = kD + 8;     // split-plane row stride (bf16): conflict-free 16-byte reads
 static_assert(kLayerTiles * 3 * kTileRows * kPS * 2 <= kD * kLD * 4, "planes fit in w");
 
 // W2 in flight in the gather waves' registers: 8 float4 per thread (element idx = t + n*j,
@@ -494,7 +567,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   } else {
     // (W2Regs is confined to this branch -- live across the matrix role it would spill --
     // and a struct of scalars: an array held across the barriers went to scratch)
-    gather_role<FMA, false>(A, L.f, ts, nt);
+    gather_role<FMA, false, true>(A, L.f, ts, nt);
     W2Regs<kW2Per> w2r;
     w2r.load(reinterpret_cast<const float4*>(B.W2), tid - kMatThreads, kThreads - kMatThreads);
     __syncthreads();  // gather_role's last barrier (the matrix role multiplies the last tile)
