@@ -30,12 +30,14 @@
 extern "C" {
 #endif
 
-#define GINE_ABI_VERSION 6  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
+#define GINE_ABI_VERSION 7  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
                               3: gine_deepset_bwd_num_partials takes the hidden width;
                               4: bn_acc grows two grid-barrier words (gine_mp_fwd_layer);
                               5: grid-barrier failure count (gine_bn_acc_barrier_failures_index),
                                  gine_mlp_bwd_layer removed;
-                              6: gine_mlp_bwd_layer again, in the forward layer's role-split form */
+                              6: gine_mlp_bwd_layer again, in the forward layer's role-split form;
+                              7: gine_mp_fwd_layer takes the layer window plan
+                                 (gine_graph_plan_layer_windows, gine_mp_fwd_layer_windows_fit) */
 
 #define GINE_OK 0
 #define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
@@ -396,6 +398,12 @@ int gine_mp_fwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_deg
  * production), so a test can launch a grid the device cannot hold at once and check that the
  * barrier's failure reaches the host (gine_bn_acc_barrier_failures_index). */
 int gine_testing_layer_extra_workgroups(int32_t extra);
+/* With a layer window plan (tile_windows != NULL; ABI 7) every workgroup stages each of its
+ * 32-row tiles' neighbour rows -- the tile's window, one contiguous run of rows -- in LDS once
+ * and sums the messages from there (per-destination LDS staging; same bits as the gather);
+ * window_rows is the plan's largest window and (window_rows, max_in_degree) must pass
+ * gine_mp_fwd_layer_windows_fit (GINE_ERR_INVALID otherwise).  NULL: neighbour rows are
+ * gathered from L2 (any graph). */
 int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                       const float* in_attr, const float* lin_w, const float* lin_b,
                       const float* eps, const float* w1, const float* b1, float* z, float* a1,
@@ -404,7 +412,23 @@ int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* i
                       float* bn_save, float momentum, float bn_eps, int32_t update_running,
                       const float* w2, const float* b2, float* y, uint8_t* mask,
                       int64_t num_nodes, int32_t channels, int32_t max_in_degree, int32_t flags,
-                      int32_t epilogue, void* stream);
+                      int32_t epilogue, const int32_t* tile_windows, int32_t window_rows,
+                      void* stream);
+/* The layer window plan of a graph (built once per graph, like its CSRs): for every 32-row
+ * tile of destinations, tile_windows[2T] = first row and tile_windows[2T + 1] = number of rows
+ * of the run [lo, lo + rows) holding the tile's own rows and all their in-neighbours (int32
+ * [ceil(N / 32)][2], device), and maxima[0] / maxima[1] = the largest window and the largest
+ * number of in-edges of a tile (int32[2], device; zeroed by the call).  The caller reads the
+ * maxima back once and asks gine_mp_fwd_layer_windows_fit (largest window, the graph's largest
+ * in-degree) whether the plan fits the launch's LDS: (rows + 1) x 512 B of window rows (a -inf
+ * dummy row last), 32 x round_up(max_in_degree, 4) x 8 B of padded slot table and 33 rowptr
+ * words within 73,712 B, rows <= 144 (cfg2's 500-station k = 10 graphs in the locality order:
+ * about 129 rows, in-degree 11).
+ * Replaces nothing in the reference: the data movement of PyG's x.index_select per tile. */
+int gine_graph_plan_layer_windows(const int32_t* in_rowptr, const int32_t* in_src,
+                                  int64_t num_nodes, int32_t* tile_windows, int32_t* maxima,
+                                  void* stream);
+int gine_mp_fwd_layer_windows_fit(int32_t window_rows, int32_t max_in_degree, int32_t* ok);
 int gine_mlp_fwd2_bn(const float* a1, int64_t* bn_acc, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, int64_t* num_batches_tracked,
                      float* bn_save, float momentum, float bn_eps, int32_t update_running,

@@ -34,6 +34,7 @@
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <type_traits>
 
 namespace gine {
 namespace {
@@ -74,6 +75,8 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // 2 gathered (gather role, thread 256).
 // 16-19: s_memrealtime (the 100 MHz clock every XCD shares) at entry, barrier arrival,
 // barrier release and the end, for the arrival skew across workgroups.
+// 20 / 21: tile 1 / 2's planes in LDS (matrix role); 22 / 23: the window form's tile 1 / 2
+// staged (gather role, thread 256, after G).
 __device__ long long g_layer_prof[1024][24];
 #define LAYER_RT(i)                                                              \
   do {                                                                           \
@@ -529,6 +532,9 @@ struct LayerArgs {
   float* y;
   uint8_t* mask;
   BnFwdParams q;
+  const int2* win;     // WIN: per 32-row tile (first window row, window rows)
+  int win_rows;        // WIN: max window rows over the tiles (the dummy row's index)
+  int win_slots;       // WIN: slots per row of the padded slot table (lw_slots)
 };
 
 struct LayerLds {
@@ -539,9 +545,391 @@ struct LayerLds {
   int barrier_failed;  // this workgroup's grid barrier timed out (gine_bnacc.hpp)
 };
 
-template <bool FMA, int EPI>
+// ---------------------------------------------------------------------------------------
+// WIN: phase A with LDS staging of each tile's neighbour rows (north star: per-destination
+// LDS staging of neighbour features).  A PyG batch is block-diagonal and the stations are in
+// the locality order, so the in-neighbours of a 32-row tile lie in one short run of rows --
+// the tile's window [lo, lo + rows) (gine_graph_plan_layer_windows; cfg2: ~100 rows, at most
+// 129, against 352 neighbour reads).  The gather waves stage the window (coalesced, each row
+// once), the tile's CSR segment (window byte offset | attribute) and its local rowptr in LDS,
+// then sum every destination's messages from LDS in edge order -- the same per-edge rounding
+// sequence as gine_mp_fwd, so z is bit-identical.  Tile k+1's staging loads are in flight in
+// registers while tile k is summed (one window in LDS).  A dummy row of -inf and a dummy edge
+// pointing at it stand in for past-the-degree slots (masked, so any weights give the gather's
+// bits).  The rest of the workgroup's LDS: the matrix waves' transposition tiles and BatchNorm
+// sums, two tiles of split planes; W1's fragments come straight from memory (no staging
+// image) and a1 is read back from memory in phase B (no a1 tiles kept).
+// Barriers: two per tile in both roles (G: window staged | S: tile summed and planes written),
+// for it = 0 .. nt (the matrix role multiplies tile it - 1).
+// ---------------------------------------------------------------------------------------
+#ifndef GINE_LW_U  // (experiments)
+#define GINE_LW_U 4
+#endif
+constexpr int kLwU = GINE_LW_U;             // slots per row and group (LDS reads in flight)
+constexpr int kLwRowLoads = 9;              // float4 per gather thread: windows <= 144 rows
+constexpr int kLwRowsMax = kLwRowLoads * (kThreads - kMatThreads) / kD4;
+constexpr int kLwRegion = 73712;            // window | slot table | rowptr (phase B: W2's image)
+struct LayerWinLds {
+  float tt[4 * 32 * kTLD];                  // transposition tiles | phase B: output tiles
+  double sr[2 * 8 * kD];                    // BatchNorm sums     | (output tiles, cont.)
+  uint16_t planes[2][3 * kTileRows * kPS];  // z planes of tiles it & 1 | phase B: relu planes
+  float4 win[kLwRegion / 16];
+  float bn[2 * kD];
+  double tot[2 * kD];
+  int barrier_failed;
+};
+static_assert(sizeof(LayerWinLds) <= 160 * 1024, "one workgroup per CU");
+static_assert(kD * kLD * 4 <= kLwRegion, "W2's image fits the window region");
+static_assert(2 * kTileRows * kLD * 4 <= sizeof(float) * 4 * 32 * kTLD + sizeof(double) * 2 * 8 * kD,
+              "phase B's output tiles fit the transposition + statistics region");
+// Slots per row of the padded slot table: the in-degree bound rounded up to whole groups.
+__host__ __device__ constexpr int lw_slots(int max_in_degree) {
+  return (max_in_degree + kLwU - 1) / kLwU * kLwU;
+}
+__host__ __device__ constexpr int lw_table_off(int win_rows) { return (win_rows + 1) * kRowBytes; }
+__host__ __device__ constexpr int lw_rowptr_off(int win_rows, int slots) {
+  return lw_table_off(win_rows) + kTileRows * slots * 8;
+}
+__host__ __device__ constexpr bool lw_fits(int win_rows, int max_in_degree) {
+  return win_rows >= 1 && win_rows <= kLwRowsMax && max_in_degree >= 0 &&
+         max_in_degree <= GINE_MP_FUSED_MAX_DEGREE &&
+         lw_rowptr_off(win_rows, lw_slots(max_in_degree)) + (kTileRows + 1) * 4 <= kLwRegion;
+}
+static_assert(kTileRows * lw_slots(GINE_MP_FUSED_MAX_DEGREE) <= 2 * (kThreads - kMatThreads),
+              "two slot-table entries per gather thread");
+
+// The gather waves' staging of one tile in two dependent levels, each a tile ahead of its
+// use, so that nothing waits on a load until the tile that consumes it:
+//   level A (tile it + 2): the window (plan), the row pointers of this thread's slot-table
+//            entries (entry e = p, p + 512: row e / SP, slot e % SP) and local rowptr word p;
+//   level B (tile it + 1): the window rows and the entries' edges, from level A's values.
+// Named scalars written out member by member: an array (or an accessor returning references,
+// or HIP's float4 union) held across the barriers stays a private-memory object -- scratch
+// stores right behind the loads, which serialise the prefetch.
+struct LwLevelA {
+  int lo, rows, ra0, rb0, ra1, rb1, rpx;
+  __device__ __forceinline__ void load(const FusedArgs& A, const int2* win, int T, int p,
+                                       int SP, int kG) {
+    const int2 w = win[T];
+    lo = w.x;
+    rows = w.y;
+    const int n0 = T * kTileRows;
+    const int r0 = min(p / SP, kTileRows - 1), r1 = min((p + kG) / SP, kTileRows - 1);
+    ra0 = A.rowptr[min(n0 + r0, A.N)];
+    rb0 = A.rowptr[min(n0 + r0 + 1, A.N)];
+    ra1 = A.rowptr[min(n0 + r1, A.N)];
+    rb1 = A.rowptr[min(n0 + r1 + 1, A.N)];
+    rpx = A.rowptr[min(n0 + min(p, kTileRows), A.N)];
+  }
+};
+struct LwStage {
+  f4v v0, v1, v2, v3, v4, v5, v6, v7, v8;
+  int32_t nb0, nb1;
+  float at0, at1;
+  int lo, rows, ra0, rb0, ra1, rb1, rpx;
+  // window element p + k * 512 (row-major float4 of the window rows): row p / 32 + 16 k,
+  // chunk p % 32 -- one base offset, the rows as immediate steps, and a predicate per k (the
+  // stores below use the same one)
+  __device__ __forceinline__ void load(const FusedArgs& A, const LwLevelA& a, int p, int SP,
+                                       int kG) {
+    static_assert(kLwRowLoads == 9, "the members below");
+    static_assert(kThreads - kMatThreads == 16 * kD4, "16 window rows per load round");
+    lo = a.lo;
+    rows = a.rows;
+    ra0 = a.ra0;
+    rb0 = a.rb0;
+    ra1 = a.ra1;
+    rb1 = a.rb1;
+    rpx = a.rpx;
+    // the edges first: their indices use level A's values, and a wait for those placed
+    // after the window loads would count the window loads too (vmcnt is in issue order)
+    const int j0 = p % SP, j1 = (p + kG) % SP;
+    if (j0 < rb0 - ra0) {
+      nb0 = A.nbr[ra0 + j0];
+      at0 = A.attr[ra0 + j0];
+    }
+    if (j1 < rb1 - ra1) {
+      nb1 = A.nbr[ra1 + j1];
+      at1 = A.attr[ra1 + j1];
+    }
+    const char* xb = reinterpret_cast<const char*>(A.x);
+    const uint32_t off0 = ((uint32_t)(lo + (p >> 5)) * kD4 + (p & 31)) * 16u;
+    const int lim = rows - (p >> 5);
+#define LW_LD(K, V) \
+  if (16 * (K) < lim) V = *reinterpret_cast<const f4v*>(xb + off0 + (K) * 8192u);
+    LW_LD(0, v0) LW_LD(1, v1) LW_LD(2, v2) LW_LD(3, v3) LW_LD(4, v4) LW_LD(5, v5)
+    LW_LD(6, v6) LW_LD(7, v7) LW_LD(8, v8)
+#undef LW_LD
+  }
+  // window rows, the padded slot table (past-the-degree slots: the dummy row R, attribute 0)
+  // and the local rowptr into LDS
+  __device__ __forceinline__ void store(float4* win, int2* tab, int* rpl, int p, int SP, int kG,
+                                        int R) const {
+    f4v* w = reinterpret_cast<f4v*>(win) + p;
+    const int lim = rows - (p >> 5);
+#define LW_ST(K, V) if (16 * (K) < lim) w[(K) * 512] = V;
+    LW_ST(0, v0) LW_ST(1, v1) LW_ST(2, v2) LW_ST(3, v3) LW_ST(4, v4) LW_ST(5, v5)
+    LW_ST(6, v6) LW_ST(7, v7) LW_ST(8, v8)
+#undef LW_ST
+    const int2 dummy = make_int2(R * (int)kRowBytes, 0);
+    if (p < kTileRows * SP)
+      tab[p] = p % SP < rb0 - ra0
+                   ? make_int2((nb0 - lo) * (int)kRowBytes, __float_as_int(at0))
+                   : dummy;
+    if (p + kG < kTileRows * SP)
+      tab[p + kG] = (p + kG) % SP < rb1 - ra1
+                        ? make_int2((nb1 - lo) * (int)kRowBytes, __float_as_int(at1))
+                        : dummy;
+    if (p <= kTileRows) rpl[p] = rpx;  // (absolute: only differences are read)
+  }
+};
+
+// Matrix role of the window form.  Barriers: 2 (nt + 1).
+__device__ __forceinline__ void matrix_role_win(const FusedArgs& A, LayerWinLds& L,
+                                                const TileSeq& ts, int nt) {
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int cq = lane & 7, grp = lane >> 3;
+  // W1^T fragments straight from memory: lane (h, c32) reads W1[32 wave + c32][h*64 ..+64)
+  float bf[kKS];
+  {
+    const float4* wr = reinterpret_cast<const float4*>(A.W1 + (size_t)(32 * wave + c32) * kD +
+                                                       h * kKS);
+#pragma unroll
+    for (int q = 0; q < kKS / 4; ++q) {
+      const float4 v = wr[q];
+      bf[4 * q] = v.x;
+      bf[4 * q + 1] = v.y;
+      bf[4 * q + 2] = v.z;
+      bf[4 * q + 3] = v.w;
+    }
+  }
+  const float4 bias4 = *reinterpret_cast<const float4*>(A.b1 + 32 * wave + 4 * cq);
+  BPlanes<kKS> bp;
+  bp.from(bf);
+  double* sr = L.sr;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    sr[(0 * 8 + grp) * kD + 32 * wave + 4 * cq + k] = 0.0;
+    sr[(1 * 8 + grp) * kD + 32 * wave + 4 * cq + k] = 0.0;
+  }
+  LAYER_MARK(8);
+  const float bb[4] = {bias4.x, bias4.y, bias4.z, bias4.w};
+  float* tt = &L.tt[wave * 32 * kTLD];
+  for (int it = 0; it <= nt; ++it) {
+    __syncthreads();  // G_it
+    if (it >= 1) {
+      const int T = ts.at(it - 1);
+      if (it <= 2) LAYER_MARK(19 + it);
+      floatx16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+      const uint16_t* pa = L.planes[(it - 1) & 1] + c32 * kPS + h * kKS;
+      auto frag = [&](int s8) {
+        Bf16x3 a;
+        a.h = *reinterpret_cast<const bf16x8_t*>(pa + 8 * s8);
+        a.m = *reinterpret_cast<const bf16x8_t*>(pa + kTileRows * kPS + 8 * s8);
+        a.l = *reinterpret_cast<const bf16x8_t*>(pa + 2 * kTileRows * kPS + 8 * s8);
+        return a;
+      };
+      Bf16x3 a = frag(0);
+#pragma unroll
+      for (int s8 = 0; s8 < kKS / 8; ++s8) {
+        Bf16x3 an = a;
+        if (s8 + 1 < kKS / 8) an = frag(s8 + 1);
+        acc = mfma_bf16x3(a, bp.f[s8], acc);
+        __builtin_amdgcn_sched_barrier(0);
+        a = an;
+      }
+      if (wave_any_nan(acc)) {  // non-finite operands: the fp32 chain on z read back from HBM
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the gather waves' z stores
+        const int64_t zr = min((int64_t)T * kTileRows + c32, (int64_t)A.N - 1);
+        acc = mfma_f32_row_mem<kKS>(A.z + zr * kD + h * kKS,
+                                    A.W1 + (size_t)(32 * wave + c32) * kD + h * kKS, 1, acc);
+      }
+#ifdef GINE_LAYER_PROFILE
+      if (it <= 2 && acc[0] == 1.2345e-30f) tt[0] = 0.f;
+      if (it <= 2) LAYER_MARK(7 + 2 * it);
+#endif
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tt[((r & 3) + 8 * (r >> 2) + 4 * h) * kTLD + c32] = acc[r];
+      __builtin_amdgcn_wave_barrier();
+      double st1[4], st2[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        st1[k] = sr[(0 * 8 + grp) * kD + 32 * wave + 4 * cq + k];
+        st2[k] = sr[(1 * 8 + grp) * kD + 32 * wave + 4 * cq + k];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = grp + 8 * i;
+        const int64_t n = (int64_t)T * kTileRows + row;
+        const float4 v = *reinterpret_cast<const float4*>(&tt[row * kTLD + 4 * cq]);
+        if (n >= A.N) continue;
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        float o4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          o4[k] = vv[k] + bb[k];
+          st1[k] += (double)o4[k];
+          st2[k] += (double)o4[k] * (double)o4[k];
+        }
+        *reinterpret_cast<float4*>(A.a1 + n * kD + 32 * wave + 4 * cq) =
+            make_float4(o4[0], o4[1], o4[2], o4[3]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sr[(0 * 8 + grp) * kD + 32 * wave + 4 * cq + k] = st1[k];
+        sr[(1 * 8 + grp) * kD + 32 * wave + 4 * cq + k] = st2[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (it <= 2) LAYER_MARK(8 + 2 * it);
+    }
+    __syncthreads();  // S_it+1
+  }
+  // per-column partials: the 8 row groups added in fixed order (row-tile GEMM order)
+  __builtin_amdgcn_wave_barrier();
+  const int which = lane >> 5, cc = 32 * wave + (lane & 31);
+  double s = 0.0;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) s += sr[(which * 8 + g) * kD + cc];
+  bnacc_add<false>(A.bnacc, 2 * kD, which * kD + cc, s);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // performed before the barrier arrival
+  LAYER_MARK(13);
+}
+
+// Gather role of the window form (waves 4-11).  Barriers: 2 (nt + 1).  In the last round
+// (it = nt) W2 is loaded and staged into the window region under the matrix role's last
+// chain.
+// The sums: a half-wave owns rows hw and hw + 16 of the tile, lane t the 16-byte chunk t, and
+// walks both rows' SP slots in groups of kLwU (slot entry -> neighbour row, both from LDS).
+// Where the edge Linear's weights are finite in every lane (the wave checks) the padded slots
+// need no mask: the dummy row is -inf and its attribute 0, so relu(-inf + lin(0)) = +0 and
+// acc + 0 = acc (acc is never -0); otherwise each slot is masked by its row's in-degree, as
+// the gather does.
+template <bool FMA>
+__device__ __forceinline__ void lw_sum(f4v (&acc)[kRowsPerHalf], const char* wb, const int2* t0,
+                                       const int2* t1, uint32_t qb, int SP, f4v lw, f4v lb,
+                                       bool masked, int c0, int c1) {
+  for (int j0 = 0; j0 < SP; j0 += kLwU) {
+    int2 q0[kLwU], q1[kLwU];
+#pragma unroll
+    for (int u = 0; u < kLwU; ++u) {
+      q0[u] = t0[j0 + u];
+      q1[u] = t1[j0 + u];
+    }
+    f4v r0[kLwU], r1[kLwU];
+#pragma unroll
+    for (int u = 0; u < kLwU; ++u) {
+      r0[u] = *reinterpret_cast<const f4v*>(wb + q0[u].x + qb);
+      r1[u] = *reinterpret_cast<const f4v*>(wb + q1[u].x + qb);
+    }
+    if (masked) {
+#pragma unroll
+      for (int u = 0; u < kLwU; ++u) {
+        edge_acc<FMA>(acc[0], r0[u], __int_as_float(q0[u].y), lw, lb, j0 + u < c0);
+        edge_acc<FMA>(acc[1], r1[u], __int_as_float(q1[u].y), lw, lb, j0 + u < c1);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kLwU; ++u) {
+        fwd_edge<FMA>(acc[0], r0[u], __int_as_float(q0[u].y), lw, lb);
+        fwd_edge<FMA>(acc[1], r1[u], __int_as_float(q1[u].y), lw, lb);
+      }
+    }
+  }
+}
+
+template <bool FMA>
+__device__ __forceinline__ void gather_role_win(const FusedArgs& A, const LayerArgs& B,
+                                                LayerWinLds& L, const TileSeq& ts, int nt) {
+  const int p = threadIdx.x - kMatThreads;  // 0 .. 511
+  constexpr int kG = kThreads - kMatThreads;
+  const int hw = p >> 5, t = p & 31;
+  const int N = A.N;
+  const uint32_t qb = (uint32_t)t * 16u;
+  char* wb = reinterpret_cast<char*>(L.win);
+  const int R = B.win_rows, SP = B.win_slots;
+  int2* tab = reinterpret_cast<int2*>(wb + lw_table_off(R));
+  int* rpl = reinterpret_cast<int*>(wb + lw_rowptr_off(R, SP));
+  // (member functions, not lambdas: a lambda called from two sites is not inlined, and what
+  // it captures by reference then lives in scratch)
+  LwLevelA la;
+  LwStage st;
+  // the dummy row (-inf), once (nothing else writes there in phase A)
+  if (p < kD4) L.win[R * kD4 + p] = make_float4(-__builtin_inff(), -__builtin_inff(),
+                                                -__builtin_inff(), -__builtin_inff());
+  const f4v lw = ld_f4v(reinterpret_cast<const char*>(A.lin_w), qb);
+  const f4v lb = ld_f4v(reinterpret_cast<const char*>(A.lin_b), qb);
+  const float ope = 1.0f + A.eps[0];
+  static_assert(kLayerTiles == 2, "the tile rounds below are unrolled for two tiles");
+  if (nt > 0) la.load(A, B.win, ts.at(0), p, SP, kG);
+  if (nt > 0) st.load(A, la, p, SP, kG);
+  if (nt > 1) la.load(A, B.win, ts.at(1), p, SP, kG);
+  // padded slots unmasked only where every lane's Linear(1, D) weights are finite
+  const bool fin = __builtin_isfinite(lw.x) && __builtin_isfinite(lw.y) &&
+                   __builtin_isfinite(lw.z) && __builtin_isfinite(lw.w) &&
+                   __builtin_isfinite(lb.x) && __builtin_isfinite(lb.y) &&
+                   __builtin_isfinite(lb.z) && __builtin_isfinite(lb.w);
+  const bool masked = __builtin_amdgcn_readfirstlane(__any(!fin) ? 1 : 0) != 0;
+  // the tile rounds unrolled (nt <= kLayerTiles = 2, host-checked): in a rolled loop the
+  // stage registers loaded in round it and stored in round it + 1 are copied at the back
+  // edge, and each copy waits for its load (s_waitcnt vmcnt(0) right behind the issue)
+#pragma unroll
+  for (int it = 0; it < kLayerTiles; ++it) {
+    if (it >= nt) break;
+    const int T = ts.at(it);
+    const int lo = st.lo;
+    st.store(L.win, tab, rpl, p, SP, kG, R);
+    __syncthreads();  // G_it: window, slot table and rowptr of tile it staged
+    LAYER_MARK_T(kMatThreads, 22 + it);
+    if (it + 1 < nt) st.load(A, la, p, SP, kG);             // level B of tile it + 1
+    f4v self[kRowsPerHalf], acc[kRowsPerHalf];
+    int c[kRowsPerHalf];
+#pragma unroll
+    for (int i = 0; i < kRowsPerHalf; ++i) {
+      const int r = hw + kHalves * i;
+      const int n = T * kTileRows + r;
+      c[i] = rpl[r + 1] - rpl[r];
+      self[i] = *reinterpret_cast<const f4v*>(wb + (min(n, N - 1) - lo) * (int)kRowBytes + qb);
+      acc[i] = f4v_zero();
+    }
+    if (GINE_FUSED_DBG != 1)
+      lw_sum<FMA>(acc, wb, tab + hw * SP, tab + (hw + kHalves) * SP, qb, SP, lw, lb, masked,
+                  c[0], c[1]);
+#pragma unroll
+    for (int i = 0; i < kRowsPerHalf; ++i) {
+      const int r = hw + kHalves * i;
+      const int64_t n = (int64_t)T * kTileRows + r;
+      const f4v zv = add_scaled(acc[i], ope, self[i]);
+      uint32_t h0, m0, l0, h1, m1, l1;
+      split2(zv.x, zv.y, h0, m0, l0);
+      split2(zv.z, zv.w, h1, m1, l1);
+      uint16_t* pl = L.planes[it & 1] + r * kPS + 4 * t;
+      *reinterpret_cast<uint2*>(pl) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(pl + kTileRows * kPS) = make_uint2(m0, m1);
+      *reinterpret_cast<uint2*>(pl + 2 * kTileRows * kPS) = make_uint2(l0, l1);
+      if (n < N) *reinterpret_cast<f4v*>(A.z + n * kD + 4 * t) = zv;
+    }
+    LAYER_MARK_T(kMatThreads, 14 + it);
+    __syncthreads();  // S_it+1: tile it summed, its planes written
+  }
+  // round nt: W2 under the matrix role's last chain, into the (free) window region
+  constexpr int kW2Per = kD * kD4 / kG;
+  W2Regs<kW2Per> w2r;
+  w2r.load(reinterpret_cast<const float4*>(B.W2), p, kG);
+  __syncthreads();  // G_nt: every gather wave is done with the last window
+  w2r.store(reinterpret_cast<float*>(L.win), p, kG);
+  __syncthreads();  // S_nt+1
+}
+
+template <bool FMA, int EPI, bool WIN = false>
 __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, LayerArgs B) {
-  __shared__ __attribute__((aligned(16))) LayerLds L;
+  using Lds = std::conditional_t<WIN, LayerWinLds, LayerLds>;
+  __shared__ __attribute__((aligned(16))) Lds L;
   const TileSeq ts = tile_seq(A.num_tiles, blockIdx.x, gridDim.x);
   const int nt = ts.count();
   const int tid = threadIdx.x;
@@ -559,20 +947,41 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   // and statistics, and stage it in LDS when phase A's use of L.f.w is over
   constexpr int kW2Per = kD * kD4 / (kThreads - kMatThreads);
   static_assert(kD * kD4 % (kThreads - kMatThreads) == 0, "W2 in whole float4 per thread");
-  if (mat) {
-    matrix_role<true>(A, L.f, ts, nt, &L.a1k[0][0]);
-    LAYER_MARK(1);
-    __syncthreads();  // phase A's LDS use is over (L.f.w is free)
+  // phase B's LDS: W2's image, the relu planes, the output tiles
+  float* w2img;
+  uint16_t* rp;  // [kLayerTiles][3][kTileRows * kPS]
+  float* sOb;    // [2][kTileRows * kLD]
+  if constexpr (WIN) {
+    w2img = reinterpret_cast<float*>(L.win);
+    rp = &L.planes[0][0];
+    sOb = L.tt;
+    if (mat) {
+      matrix_role_win(A, L, ts, nt);
+      LAYER_MARK(1);
+    } else {
+      gather_role_win<FMA>(A, B, L, ts, nt);
+    }
+    __syncthreads();  // every matrix wave's statistics atomics performed (before the arrival)
     LAYER_MARK(2);
   } else {
-    // (W2Regs is confined to this branch -- live across the matrix role it would spill --
-    // and a struct of scalars: an array held across the barriers went to scratch)
-    gather_role<FMA, false, true>(A, L.f, ts, nt);
-    W2Regs<kW2Per> w2r;
-    w2r.load(reinterpret_cast<const float4*>(B.W2), tid - kMatThreads, kThreads - kMatThreads);
-    __syncthreads();  // gather_role's last barrier (the matrix role multiplies the last tile)
-    __syncthreads();  // phase A's LDS use is over (L.f.w is free)
-    w2r.store(L.f.w, tid - kMatThreads, kThreads - kMatThreads);
+    w2img = L.f.w;
+    rp = reinterpret_cast<uint16_t*>(L.f.w);
+    sOb = &L.f.z[0][0];
+    if (mat) {
+      matrix_role<true>(A, L.f, ts, nt, &L.a1k[0][0]);
+      LAYER_MARK(1);
+      __syncthreads();  // phase A's LDS use is over (L.f.w is free)
+      LAYER_MARK(2);
+    } else {
+      // (W2Regs is confined to this branch -- live across the matrix role it would spill --
+      // and a struct of scalars: an array held across the barriers went to scratch)
+      gather_role<FMA, false, true>(A, L.f, ts, nt);
+      W2Regs<kW2Per> w2r;
+      w2r.load(reinterpret_cast<const float4*>(B.W2), tid - kMatThreads, kThreads - kMatThreads);
+      __syncthreads();  // gather_role's last barrier (the matrix role multiplies the last tile)
+      __syncthreads();  // phase A's LDS use is over (L.f.w is free)
+      w2r.store(L.f.w, tid - kMatThreads, kThreads - kMatThreads);
+    }
   }
 
   const int lane = tid % kWave;
@@ -600,6 +1009,22 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   // workgroup's statistics and outputs are NaN and the running statistics stay as they were;
   // the failure word tells the host
   const bool failed = L.barrier_failed != 0;
+  // WIN: a1 (kept in memory, not in LDS) for the relu pass, in flight under the BatchNorm
+  // finish: element e = tid + kThreads * j of the workgroup's tiles (row-major float4)
+  constexpr int kA1Per = (kLayerTiles * kTileRows * kD4 + kThreads - 1) / kThreads;
+  float4 a1v[WIN ? kA1Per : 1];
+  if constexpr (WIN) {
+#pragma unroll
+    for (int j = 0; j < kA1Per; ++j) {
+      const int e = tid + kThreads * j;
+      const int k = e / (kTileRows * kD4), r = (e / kD4) % kTileRows, q4 = e % kD4;
+      int64_t n = (int64_t)ts.at(k < nt ? k : 0) * kTileRows + r;
+      n = n < A.N ? n : A.N - 1;
+      a1v[j] = e < nt * kTileRows * kD4
+                   ? *reinterpret_cast<const float4*>(A.a1 + n * kD + 4 * q4)
+                   : f4_zero();
+    }
+  }
   // the gather waves' epilogue operands, in flight under the BatchNorm finish
   float4 xres[kLayerTiles][2];
   float4 bias2 = f4_zero();
@@ -623,7 +1048,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   float bf[kKS];
   BPlanes<kKS> bp;
   if (mat) {
-    const float* wr = &L.f.w[col * kLD + h * kKS];
+    const float* wr = &w2img[col * kLD + h * kKS];
 #pragma unroll
     for (int q = 0; q < kKS / 4; ++q) {
       const float4 v = *reinterpret_cast<const float4*>(&wr[4 * q]);
@@ -656,10 +1081,15 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   // matrix waves' chains then only read them (a wave's in-loop split adds to its MFMA chain:
   // 3,081 against 2,046 shader ticks per 32x32 block, tools/chain_micro.py).  a1k keeps a1
   // for the rare fp32 redo.  Rows past N are zero (the row GEMM stages them as zero).
-  uint16_t* rp = reinterpret_cast<uint16_t*>(L.f.w);  // [kLayerTiles][3][kTileRows * kPS]
-  for (int e = tid; e < nt * kTileRows * kD4; e += kThreads) {
+#pragma unroll
+  for (int j = 0; j < (WIN ? kA1Per : (kLayerTiles * kTileRows * kD4 + kThreads - 1) / kThreads);
+       ++j) {
+    const int e = tid + kThreads * j;
+    if (e >= nt * kTileRows * kD4) break;
     const int k = e / (kTileRows * kD4), r = (e / kD4) % kTileRows, q4 = e % kD4;
-    float4 v = *reinterpret_cast<const float4*>(&L.a1k[k][r * kLD + 4 * q4]);
+    float4 v;
+    if constexpr (WIN) v = a1v[j];
+    else v = *reinterpret_cast<const float4*>(&L.a1k[k][r * kLD + 4 * q4]);
     const float4 al = *reinterpret_cast<const float4*>(&L.bn[4 * q4]);
     const float4 sh = *reinterpret_cast<const float4*>(&L.bn[kD + 4 * q4]);
     v = make_float4(relu_nan(bn_apply(v.x, al.x, sh.x)), relu_nan(bn_apply(v.y, al.y, sh.y)),
@@ -676,7 +1106,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   __syncthreads();
   LAYER_MARK(6);
   for (int k = 0; k < nt; ++k) {
-    float* sO = L.f.z[k & 1];
+    float* sO = sOb + (k & 1) * kTileRows * kLD;
     if (mat) {  // Linear2 chain of tile k (the row GEMM's split-bf16 chain and k order)
       floatx16 acc;
 #pragma unroll
@@ -695,7 +1125,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
 #pragma unroll
           for (int i = 0; i < 16; ++i) acc[i] = 0.f;
           const bool live = (int64_t)ts.at(k) * kTileRows + c32 < A.N;
-          const float* arow = &L.a1k[k][c32 * kLD + h * kKS];
+          const float* arow;
+          if constexpr (WIN)
+            arow = A.a1 + min((int64_t)ts.at(k) * kTileRows + c32, (int64_t)A.N - 1) * kD +
+                   h * kKS;
+          else
+            arow = &L.a1k[k][c32 * kLD + h * kKS];
           const float* wp = B.W2 + (size_t)col * kD + h * kKS;
           auto rv = [&](int kk) -> float {
             const int c = h * kKS + kk;
@@ -808,7 +1243,13 @@ int layer_capacity() {
                         (const void*)k_mp_fwd_layer<true, EPI_OUT_RES>,
                         (const void*)k_mp_fwd_layer<false, EPI_OUT>,
                         (const void*)k_mp_fwd_layer<false, EPI_OUT_RELU>,
-                        (const void*)k_mp_fwd_layer<false, EPI_OUT_RES>};
+                        (const void*)k_mp_fwd_layer<false, EPI_OUT_RES>,
+                        (const void*)k_mp_fwd_layer<true, EPI_OUT, true>,
+                        (const void*)k_mp_fwd_layer<true, EPI_OUT_RELU, true>,
+                        (const void*)k_mp_fwd_layer<true, EPI_OUT_RES, true>,
+                        (const void*)k_mp_fwd_layer<false, EPI_OUT, true>,
+                        (const void*)k_mp_fwd_layer<false, EPI_OUT_RELU, true>,
+                        (const void*)k_mp_fwd_layer<false, EPI_OUT_RES, true>};
     for (const void* k : ks) {
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kThreads, 0) != hipSuccess)
@@ -863,6 +1304,56 @@ extern "C" int gine_mp_fwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t
   return GINE_OK;
 }
 
+// One wave per 32-row tile: the window [lo, lo + rows) covering the tile's own rows and
+// every in-neighbour, and the maxima (window rows, in-edges) over the tiles.
+__global__ __launch_bounds__(64) void k_plan_layer_windows(const int32_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ src,
+                                                           int N, int tiles, int2* win,
+                                                           int32_t* maxima) {
+  const int T = blockIdx.x;
+  if (T >= tiles) return;
+  const int n0 = T * kTileRows, n1 = min(n0 + kTileRows, N);
+  const int e0 = rowptr[n0], e1 = rowptr[n1];
+  int lo = n0, hi = n1 - 1;
+  for (int e = e0 + (int)threadIdx.x; e < e1; e += 64) {
+    const int s = src[e];
+    lo = min(lo, s);
+    hi = max(hi, s);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, __shfl_xor(lo, o, 64));
+    hi = max(hi, __shfl_xor(hi, o, 64));
+  }
+  if (threadIdx.x == 0) {
+    win[T] = make_int2(lo, hi - lo + 1);
+    atomicMax(&maxima[0], hi - lo + 1);
+    atomicMax(&maxima[1], e1 - e0);
+  }
+}
+
+extern "C" int gine_graph_plan_layer_windows(const int32_t* in_rowptr, const int32_t* in_src,
+                                             int64_t num_nodes, int32_t* tile_windows,
+                                             int32_t* maxima, void* stream) {
+  if (num_nodes <= 0 || num_nodes >= (int64_t(1) << 31) || !in_rowptr || !in_src ||
+      !tile_windows || !maxima)
+    return GINE_ERR_INVALID;
+  const int tiles = (int)ceil_div(num_nodes, kTileRows);
+  hipStream_t s = as_stream(stream);
+  GINE_RETURN_IF_HIP(hipMemsetAsync(maxima, 0, 2 * sizeof(int32_t), s));
+  hipLaunchKernelGGL(k_plan_layer_windows, dim3((unsigned)tiles), dim3(64), 0, s, in_rowptr,
+                     in_src, (int)num_nodes, tiles, reinterpret_cast<int2*>(tile_windows),
+                     maxima);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+extern "C" int gine_mp_fwd_layer_windows_fit(int32_t window_rows, int32_t max_in_degree,
+                                             int32_t* ok) {
+  if (!ok) return GINE_ERR_INVALID;
+  *ok = lw_fits(window_rows, max_in_degree) ? 1 : 0;
+  return GINE_OK;
+}
+
 extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                                  const float* in_attr, const float* lin_w, const float* lin_b,
                                  const float* eps, const float* w1, const float* b1, float* z,
@@ -872,7 +1363,8 @@ extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const
                                  float bn_eps, int32_t update_running, const float* w2,
                                  const float* b2, float* y, uint8_t* mask, int64_t num_nodes,
                                  int32_t channels, int32_t max_in_degree, int32_t flags,
-                                 int32_t epilogue, void* stream) {
+                                 int32_t epilogue, const int32_t* tile_windows,
+                                 int32_t window_rows, void* stream) {
   if (channels != kD) return GINE_ERR_DIM;
   if ((flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
   if (!x || !in_rowptr || !in_src || !in_attr || !lin_w || !lin_b || !eps || !w1 || !b1 || !z ||
@@ -892,12 +1384,23 @@ extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const
   const FusedArgs A{x,  in_rowptr, in_src, in_attr, lin_w, lin_b,
                     eps, w1,       b1,     z,       a1,    nullptr,
                     reinterpret_cast<long long*>(bn_acc), (int)num_nodes, tiles};
+  const bool win = tile_windows != nullptr;
+  if (win && !lw_fits(window_rows, max_in_degree)) return GINE_ERR_INVALID;
   const LayerArgs B{w2, b2, y, mask,
                     BnFwdParams{gamma, beta, running_mean, running_var, num_batches_tracked,
-                                bn_save, num_nodes, momentum, bn_eps, update_running}};
+                                bn_save, num_nodes, momentum, bn_eps, update_running},
+                    reinterpret_cast<const int2*>(tile_windows), window_rows,
+                    lw_slots(max_in_degree)};
   const bool fma = !(flags & GINE_MP_LIN_MULADD);
-#define LAYER_LAUNCH(F_, E_) \
-  hipLaunchKernelGGL((k_mp_fwd_layer<F_, E_>), dim3((unsigned)grid), dim3(kThreads), 0, s, A, B)
+#define LAYER_LAUNCH(F_, E_)                                                                   \
+  do {                                                                                         \
+    if (win)                                                                                   \
+      hipLaunchKernelGGL((k_mp_fwd_layer<F_, E_, true>), dim3((unsigned)grid), dim3(kThreads), \
+                         0, s, A, B);                                                          \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_mp_fwd_layer<F_, E_>), dim3((unsigned)grid), dim3(kThreads), 0, s, \
+                         A, B);                                                                \
+  } while (0)
   switch (epilogue) {
     case GINE_EPI_NONE:
       if (fma) LAYER_LAUNCH(true, EPI_OUT); else LAYER_LAUNCH(false, EPI_OUT);

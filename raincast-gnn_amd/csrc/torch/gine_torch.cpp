@@ -61,13 +61,17 @@ enum IntOpt {
   // evicts the graph between forward and backward)
   kPlanIn,
   kPlanOut = kPlanIn + 5,
-  kIntOpts = kPlanOut + 5
+  // the layer window plan (gine_graph_plan_layer_windows): its largest window; its tile
+  // array is the graph list's last entry (undefined: the L2 gather)
+  kLayerWinRows = kPlanOut + 5,
+  kIntOpts
 };
 constexpr int kPlanFields = 5;
 // graph list: the two CSRs, then per plan (in, out) its device arrays
 enum GraphArg { kInRowptr = 0, kInSrc, kInAttr, kOutRowptr, kOutDst, kOutAttr, kGraphCsr };
 enum PlanArray { kTileBegin = 0, kWinLo, kWinRows, kSlot, kEdgeBegin, kPlanArrays };
-constexpr int kGraphArgs = kGraphCsr + 2 * kPlanArrays;
+constexpr int kLayerWinTiles = kGraphCsr + 2 * kPlanArrays;
+constexpr int kGraphArgs = kLayerWinTiles + 1;
 
 // The window plan of side `which` (0: in, 1: out) rebuilt from its scalars and its arrays
 // (a struct on the caller's stack: the library reads it only during the call).
@@ -196,7 +200,11 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
                              (const float*)P(bt), (float*)P(rmean), (float*)P(rvar),
                              (int64_t*)nbt_p, (float*)P(bn_save), momentum, bn_eps, upd,
                              (const float*)P(w2c), (const float*)P(b2c), (float*)P(y),
-                             (uint8_t*)P(mask), N, D, max_deg, lin_flag, epi, s),
+                             (uint8_t*)P(mask), N, D, max_deg, lin_flag, epi,
+                             graph[kLayerWinTiles].defined()
+                                 ? (const int32_t*)graph[kLayerWinTiles].data_ptr()
+                                 : nullptr,
+                             (int32_t)io[kLayerWinRows], s),
            "gine_mp_fwd_layer");
       } else {
         if (fused) {
@@ -436,7 +444,7 @@ Tensor gine_layer(Tensor x, Tensor lin_w, Tensor lin_b, Tensor eps, Tensor w1, T
   for (const auto& t : graph_opt) graph.push_back(opt(t));
   TORCH_CHECK(graph.size() == kGraphArgs, "graph: in_rowptr, in_src, in_attr, out_rowptr, "
               "out_dst, out_attr, then the in and out window plans' tile_begin, win_lo, "
-              "win_rows, slot, edge_begin");
+              "win_rows, slot, edge_begin, then the layer window plan's tiles");
   TORCH_CHECK(bn.size() == 5, "bn: running_mean, running_var, num_batches_tracked, acc, "
               "backward acc");
   TORCH_CHECK(io.size() == kIntOpts && fo.size() == kFloatOpts, "option vectors");

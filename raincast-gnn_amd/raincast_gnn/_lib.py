@@ -23,7 +23,7 @@ GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
-ABI_VERSION = 6
+ABI_VERSION = 7
 COUNT_PARTS = 64  # GINE_COUNT_PARTS
 
 _c_void_p = ctypes.c_void_p
@@ -91,7 +91,10 @@ _SIGNATURES = {
     "gine_mp_fwd_mlp1_acc": [_c_void_p] * 13 + [_i64, _i32, _i32, _i32, _c_void_p],
     "gine_mp_fwd_layer_ok": [_i64, _i32, _i32, ctypes.POINTER(_i32)],
     "gine_mp_fwd_layer": [_c_void_p] * 18 + [_f32, _f32, _i32] + [_c_void_p] * 4
-                         + [_i64, _i32, _i32, _i32, _i32, _c_void_p],
+                         + [_i64, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p],
+    "gine_graph_plan_layer_windows": [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                      _c_void_p],
+    "gine_mp_fwd_layer_windows_fit": [_i32, _i32, ctypes.POINTER(_i32)],
     "gine_mlp_fwd1_acc": [_c_void_p] * 6 + [_i64, _i32, _c_void_p],
     "gine_mlp_fwd2_bn": [_c_void_p] * 8 + [_f32, _f32, _i32] + [_c_void_p] * 5
                         + [_i64, _i32, _i32, _c_void_p],

@@ -258,6 +258,15 @@ def layer_policy_key():
     return distributed.device_shared()
 
 
+def layer_window_args(graph) -> tuple:
+    """(tile_windows, window_rows) for gine_mp_fwd_layer: the graph's layer window plan when
+    it has one and options.LAYER_WIN, else (None, 0) -- the L2 gather."""
+    lw = getattr(graph, "layer_windows", None)
+    if lw is None or not options.LAYER_WIN:
+        return None, 0
+    return ptr(lw[0]), lw[1]
+
+
 def layer_forward_ok(N: int, D: int, max_in_degree) -> bool:
     """gine_mp_fwd_layer applies (include/gine_hip.h: D = 128, in-degree <= 32, at most two row
     tiles per workgroup and the whole grid resident at once on this device).  Its grid
@@ -429,7 +438,8 @@ class GineLayer(torch.autograd.Function):
                      ptr(a1), ptr(acc), ptr(g), ptr(bt), ptr(bn.running_mean),
                      ptr(bn.running_var), nbt, ptr(bn_save), bn.momentum, bn.eps,
                      update_running, ptr(w2c), ptr(b2c), ptr(y), ptr(mask), N, D,
-                     graph.max_in_degree, edge_linear_flag(), epilogue, stream)
+                     graph.max_in_degree, edge_linear_flag(), epilogue,
+                     *layer_window_args(graph), stream)
             elif fused:
                 # gather of the next tile beside the matrix chain of this one: one launch
                 args = (ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),

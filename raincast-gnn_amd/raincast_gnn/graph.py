@@ -103,7 +103,7 @@ class GineGraph:
 
     __slots__ = ("num_nodes", "num_edges", "device", "in_rowptr", "in_src", "in_attr",
                  "out_rowptr", "out_dst", "out_attr", "_error", "_checked", "_windows",
-                 "max_in_degree", "_ext_opts")
+                 "max_in_degree", "_ext_opts", "layer_windows")
 
     def __init__(self, edge_index: torch.Tensor, edge_attr: torch.Tensor | None,
                  num_nodes: int, flow: str = "source_to_target"):
@@ -144,10 +144,33 @@ class GineGraph:
         self._checked = False
         self._windows = None
         self.max_in_degree = None  # host copy; None when built inside a stream capture
+        self.layer_windows = None  # (tile windows, max rows, max in-edges) or None
         if not torch.cuda.is_current_stream_capturing():
             self.check()
             self._plan_windows()
             self.max_in_degree = int(self.in_degree().max()) if self.num_nodes > 0 else 0
+            self._plan_layer_windows()
+
+    def _plan_layer_windows(self) -> None:
+        """The one-launch layer forward's per-tile windows (gine_graph_plan_layer_windows),
+        kept when they fit its LDS with this graph's in-degree (gine_mp_fwd_layer_windows_fit):
+        one small launch and one 8-byte readback per graph.  layer_windows = (tile windows
+        [T, 2], largest window, largest in-edges of a tile)."""
+        if self.num_nodes <= 0 or self.in_attr is None:
+            return
+        tiles = (self.num_nodes + 31) // 32
+        win = torch.empty(tiles, 2, dtype=torch.int32, device=self.device)
+        maxima = torch.empty(2, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.call("gine_graph_plan_layer_windows", _lib.ptr(self.in_rowptr),
+                      _lib.ptr(self.in_src), self.num_nodes, _lib.ptr(win), _lib.ptr(maxima),
+                      _lib.stream_handle(self.device))
+        rows, edges = (int(v) for v in maxima.tolist())
+        ok = _lib.ctypes.c_int32(0)
+        _lib.call("gine_mp_fwd_layer_windows_fit", rows, self.max_in_degree,
+                  _lib.ctypes.byref(ok))
+        if ok.value:
+            self.layer_windows = (win, rows, edges)
 
     def _plan_windows(self) -> None:
         mode, max_nodes = window_settings()

@@ -20,6 +20,10 @@ BN_ACC_BWD   the same for the BatchNorm backward sums.
 LAYER_FWD    True: where the fused forward and the accumulator apply and the grid fits the
              device at once, the whole layer forward in one launch (gine_mp_fwd_layer: the
              fused forward and the second GEMM separated by a grid barrier); False: the pair.
+LAYER_WIN    True: the one-launch layer forward stages each tile's neighbour rows (its window,
+             gine_graph_plan_layer_windows) in LDS where the graph's plan fits; False (the
+             measured-best default): it gathers them from L2.  Same bits either way; at cfg2
+             the window form runs 27.2 against 24.6 us per launch.
 LAYER_BWD    True: where the backward accumulator applies and the grid fits the device at
              once, the node-MLP backward in one launch (gine_mlp_bwd_layer: the dbn GEMM and
              the dz GEMM separated by a grid barrier); False: the pair.
@@ -33,4 +37,5 @@ ENGINE_IN_MP = True
 BN_ACC = True
 BN_ACC_BWD = True
 LAYER_FWD = True
+LAYER_WIN = False
 LAYER_BWD = True

@@ -91,7 +91,7 @@ def _graph_opts(graph, N: int, D: int, has_acc: bool) -> tuple:
     from . import functional as Fn
     from . import options
     key = (N, D, has_acc, options.MP_FUSED, options.LAYER_FWD, options.LAYER_BWD,
-           options.ENGINE_IN_MP, Fn.layer_policy_key())
+           options.LAYER_WIN, options.ENGINE_IN_MP, Fn.layer_policy_key())
     cache = graph._ext_opts
     got = cache.get(key)
     if got is None:
@@ -99,11 +99,14 @@ def _graph_opts(graph, N: int, D: int, has_acc: bool) -> tuple:
         lay = fused and has_acc and Fn.layer_forward_ok(N, D, graph.max_in_degree)
         pin, ain = _plan_args(graph, "in", D)
         pout, aout = _plan_args(graph, "out", D)
+        lw = graph.layer_windows if options.LAYER_WIN else None
         io = [int(fused), int(lay),
               int(graph.max_in_degree if graph.max_in_degree is not None else -1),
               int(Fn.engine_in_mp_ok(graph, D)), int(Fn.layer_backward_ok(N, D))] + pin + pout
+        io += [lw[1] if lw is not None else 0]
         tensors = [graph.in_rowptr, graph.in_src, graph.in_attr, graph.out_rowptr,
                    graph.out_dst, graph.out_attr] + ain + aout
+        tensors.append(lw[0] if lw is not None else None)
         got = cache[key] = (io, tensors)
     return got
 

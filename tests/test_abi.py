@@ -130,3 +130,17 @@ def test_deepset_group_layout_sizes(N, M, H):
     n = ctypes.c_int32(0)
     assert lib.gine_deepset_bwd_num_partials(N, H, ctypes.byref(n)) == 0
     assert n.value == min(groups, 512 if H >= 128 else 1024)
+
+
+def test_layer_window_fit_query():
+    """gine_mp_fwd_layer_windows_fit (host only): (rows + 1) x 512 B of window rows, a 32 x
+    round_up(in-degree, 4) slot table of 8-byte entries and 33 rowptr words within the
+    launch's 73,712-byte region; at most 144 rows (9 staging loads per gather thread) and
+    in-degree <= 32."""
+    lib = _lib.load()
+    ok = ctypes.c_int32(7)
+    for rows, deg, want in [(129, 11, 1), (136, 11, 1), (137, 11, 0), (120, 32, 1),
+                            (127, 32, 0), (126, 32, 1), (1, 33, 0), (0, 0, 0), (1, 0, 1),
+                            (144, 0, 0), (-1, 0, 0), (10, -1, 0)]:
+        assert lib.gine_mp_fwd_layer_windows_fit(rows, deg, ctypes.byref(ok)) == 0
+        assert ok.value == want, (rows, deg)

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-stamps", action="store_true", help="plain library: time only")
+    ap.add_argument("--no-win", action="store_true", help="gather from L2 (no layer windows)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     D = 128
@@ -52,12 +53,14 @@ def main():
     call, ptr = _lib.call, _lib.ptr
     s = _lib.stream_handle(dev)
     lin = Fn.edge_linear_flag()
+    win_args = (None, 0) if a.no_win else Fn.layer_window_args(g)
+    print(f"layer windows: {'off (L2 gather)' if win_args[0] is None else win_args[1:]}")
 
     def run():
         call("gine_mp_fwd_layer", ptr(x), ptr(g.in_rowptr), ptr(g.in_src), ptr(g.in_attr),
              ptr(lw), ptr(lb), ptr(ep), ptr(w1), ptr(b1), ptr(z), ptr(a1), ptr(acc), ptr(gam),
              ptr(bet), ptr(rm), ptr(rv), None, ptr(bsave), 0.1, 1e-5, 1, ptr(w2), ptr(b2),
-             ptr(y), ptr(mask), N, D, g.max_in_degree, lin, 2, s)
+             ptr(y), ptr(mask), N, D, g.max_in_degree, lin, 2, *win_args, s)
 
     lib = _lib.load()
     buf = (ctypes.c_longlong * (1024 * 24))()
@@ -103,11 +106,15 @@ def main():
         two = full[:, 11] > full[:, 0]
         print(f"  phase A detail (ticks after entry, median over workgroups; {int(two.sum())} "
               f"with two tiles):")
-        for i, nm in ((8, "W1 planes ready"), (14, "tile 1 gathered"), (20, "tile 1 z ready"),
-                      (9, "tile 1 chain"), (10, "tile 1 epilogue"), (15, "tile 2 gathered"),
-                      (21, "tile 2 z ready"), (11, "tile 2 chain"),
-                      (12, "tile 2 epilogue"), (13, "stats in acc"), (1, "matrix role end")):
-            sel = two if i in (11, 12, 15, 21) else np.ones_like(two)
+        marks = [(8, "W1 planes ready"), (14, "tile 1 gathered"), (20, "tile 1 z ready"),
+                 (9, "tile 1 chain"), (10, "tile 1 epilogue"), (15, "tile 2 gathered"),
+                 (21, "tile 2 z ready"), (11, "tile 2 chain"),
+                 (12, "tile 2 epilogue"), (13, "stats in acc"), (1, "matrix role end")]
+        if win_args[0] is not None:  # window form: tile k's window staged (after G_k)
+            marks[1:1] = [(22, "tile 1 staged")]
+            marks[6:6] = [(23, "tile 2 staged")]
+        for i, nm in marks:
+            sel = two if i in (11, 12, 15, 21, 23) else np.ones_like(two)
             d = full[sel, i] - full[sel, 0]
             print(f"    {nm:16s} median {np.median(d):8.0f}  p90 {np.percentile(d, 90):8.0f}")
     # a reference: HIP-event time of the launch
