@@ -372,7 +372,7 @@ def time_kernels(tr: Trainer, reps: int):
                  ptr(lw), ptr(lb), ptr(ep), ptr(w1), ptr(b1), ptr(z), ptr(a1), ptr(lacc),
                  ptr(bn.weight), ptr(bn.bias), ptr(rm_l), ptr(rv_l), None, ptr(bsave_l), 0.1,
                  1e-5, 1, ptr(w2), ptr(b2), ptr(y_l), ptr(mask), N, D, g.max_in_degree, lin, 2,
-                 S[0])
+                 *Fn.layer_window_args(g), S[0])
         # bytes: the message passing's B_f + a1 and y written, mask, x re-read for the residual
         kernels["gine_mp_fwd_layer"] = (mp_fwd_layer, {
             "flops": 4 * N * D * D,
