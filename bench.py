@@ -98,6 +98,9 @@ def parse():
                     help="time the drop-in path instead: the reference's model structure in "
                          "torch with raincast_gnn's GINEConv, train.py's loop (batch.to(device) "
                          "and loss.item() every step); 1 GPU")
+    ap.add_argument("--no-head-fold", action="store_true",
+                    help="A/B: the output head in a launch of its own instead of the last GINE "
+                         "layer's (options.HEAD_FOLD)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: ranks over gloo build their shards and time the gradient "
                          "all-reduce alone (launcher / rank / shard / JSON plumbing; no GPU "
@@ -372,7 +375,7 @@ def time_kernels(tr: Trainer, reps: int):
                  ptr(lw), ptr(lb), ptr(ep), ptr(w1), ptr(b1), ptr(z), ptr(a1), ptr(lacc),
                  ptr(bn.weight), ptr(bn.bias), ptr(rm_l), ptr(rv_l), None, ptr(bsave_l), 0.1,
                  1e-5, 1, ptr(w2), ptr(b2), ptr(y_l), ptr(mask), N, D, g.max_in_degree, lin, 2,
-                 *Fn.layer_window_args(g), S[0])
+                 *Fn.layer_window_args(g), None, S[0])
         # bytes: the message passing's B_f + a1 and y written, mask, x re-read for the residual
         kernels["gine_mp_fwd_layer"] = (mp_fwd_layer, {
             "flops": 4 * N * D * D,
@@ -1172,6 +1175,8 @@ def main():
     # barrier needs the whole chip (raincast_gnn.functional.layer_forward_ok)
     note_device_sharing()
     cfg = BENCH_CONFIGS[args.config].with_hidden(args.hidden)
+    if args.no_head_fold:
+        options.HEAD_FOLD = False
     if args.dropin:
         if world > 1:
             raise SystemExit("--dropin measures the single-GPU drop-in path (--gpus 1)")
@@ -1256,7 +1261,7 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": not args.no_graph,
                        "station_order": args.station_order,
                        "allreduce_in_graph": tr.allreduce_in_graph,
-                       "allreduce_overlap": tr.overlap},
+                       "allreduce_overlap": tr.overlap, "head_fold": options.HEAD_FOLD},
             "edges_aggregated_per_s": round(edges_per_s, 1),
             "step_ms_p10_p50_p90": [pct[10], pct[50], pct[90]],
             # N > 1 decomposition: the gradient all-reduce between the fwd+bwd and AdamW

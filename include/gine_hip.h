@@ -30,14 +30,15 @@
 extern "C" {
 #endif
 
-#define GINE_ABI_VERSION 7  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
+#define GINE_ABI_VERSION 8  /* 2: adamw step-state query, gine_count_valid, window plan slot/edge_begin;
                               3: gine_deepset_bwd_num_partials takes the hidden width;
                               4: bn_acc grows two grid-barrier words (gine_mp_fwd_layer);
                               5: grid-barrier failure count (gine_bn_acc_barrier_failures_index),
                                  gine_mlp_bwd_layer removed;
                               6: gine_mlp_bwd_layer again, in the forward layer's role-split form;
                               7: gine_mp_fwd_layer takes the layer window plan
-                                 (gine_graph_plan_layer_windows, gine_mp_fwd_layer_windows_fit) */
+                                 (gine_graph_plan_layer_windows, gine_mp_fwd_layer_windows_fit);
+                              8: gine_mp_fwd_layer can also run the output head (gine_layer_head) */
 
 #define GINE_OK 0
 #define GINE_ERR_INVALID 1    /* null pointer, negative size, bad flag */
@@ -398,12 +399,30 @@ int gine_mp_fwd_layer_ok(int64_t num_nodes, int32_t channels, int32_t max_in_deg
  * production), so a test can launch a grid the device cannot hold at once and check that the
  * barrier's failure reaches the host (gine_bn_acc_barrier_failures_index). */
 int gine_testing_layer_extra_workgroups(int32_t extra);
+/* Testing only: the output head's 32-lane butterfly sum (csrc/gine_headrow.hpp sum_32; mode 1)
+ * against the __shfl_xor butterfly it stands for (mode 0), on `waves` x 64 floats. */
+int gine_testing_sum_32(const float* in, float* out, int32_t waves, int32_t mode, void* stream);
 /* With a layer window plan (tile_windows != NULL; ABI 7) every workgroup stages each of its
  * 32-row tiles' neighbour rows -- the tile's window, one contiguous run of rows -- in LDS once
  * and sums the messages from there (per-destination LDS staging; same bits as the gather);
  * window_rows is the plan's largest window and (window_rows, max_in_degree) must pass
  * gine_mp_fwd_layer_windows_fit (GINE_ERR_INVALID otherwise).  NULL: neighbour rows are
  * gathered from L2 (any graph). */
+/* The output head folded into the last layer's launch (ABI 8; models/gnn.py:140-141,
+ * GNN.aggr + PostProcess): with head != NULL the epilogue also evaluates gine_head_fwd on the
+ * rows it writes -- raw = y W^T + b, pred = PostProcess(raw) -- with the same lane layout,
+ * fma order and butterfly as k_head_fwd (same bits), and, with y_target != NULL, the loss's
+ * GINE_COUNT_PARTS valid-target partial counts (gine_head_fwd_count).  One launch fewer
+ * and h is not read back.  kind: GINE_LOSS_* (K = 2..5 outputs per node). */
+typedef struct gine_layer_head {
+  const float* weight;    /* [K, 128] (GNN.aggr.weight) */
+  const float* bias;      /* [K] */
+  float* raw;             /* [N, K] pre-PostProcess output (what gine_head_bwd reads) */
+  float* pred;            /* [N, K] */
+  const float* y_target;  /* [N] batch targets, or NULL */
+  uint32_t* count_parts;  /* GINE_COUNT_PARTS partial counts (with y_target), or NULL */
+  int32_t kind;           /* GINE_LOSS_* */
+} gine_layer_head;
 int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* in_src,
                       const float* in_attr, const float* lin_w, const float* lin_b,
                       const float* eps, const float* w1, const float* b1, float* z, float* a1,
@@ -413,7 +432,7 @@ int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const int32_t* i
                       const float* w2, const float* b2, float* y, uint8_t* mask,
                       int64_t num_nodes, int32_t channels, int32_t max_in_degree, int32_t flags,
                       int32_t epilogue, const int32_t* tile_windows, int32_t window_rows,
-                      void* stream);
+                      const gine_layer_head* head, void* stream);
 /* The layer window plan of a graph (built once per graph, like its CSRs): for every 32-row
  * tile of destinations, tile_windows[2T] = first row and tile_windows[2T + 1] = number of rows
  * of the run [lo, lo + rows) holding the tile's own rows and all their in-neighbours (int32

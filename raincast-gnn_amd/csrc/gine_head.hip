@@ -9,7 +9,7 @@
 // and a concatenation each way.  K <= 5 outputs per node, so the head is a row-streaming
 // kernel bound by reading h [N, D] once: one 32-lane half-wave per node, lane t holding
 // float4 columns t, t+32, ... of the row; the K dot products are reduced across the
-// half-wave in a fixed butterfly order.  softplus / sigmoid and their derivatives follow
+// half-wave in a fixed order on VALU lane exchanges (gine_headrow.hpp sum4_32 / sum_32).  softplus / sigmoid and their derivatives follow
 // ATen's formulas (threshold 20 for softplus, sigmoid backward from the saved output).
 //
 // Backward: d raw = PostProcess'(raw) * d pred; dh = d raw W (written once); dW = d raw^T h
@@ -59,18 +59,23 @@ __global__ __launch_bounds__(kThreads) void k_head_fwd(const float* __restrict__
         }
       }
     }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-#pragma unroll
-      for (int m = 16; m >= 1; m >>= 1) acc[k] += __shfl_xor(acc[k], m, 32);
+    // outputs 0-3 reduce-scattered (sum4_32; output o at lanes 8 o .. 8 o + 7, finalised by
+    // lane 8 o), output 4 by a full butterfly (finalised by lane 1)
+    const float d = sum4_32(acc[0], K > 1 ? acc[1] : 0.f, K > 2 ? acc[2] : 0.f,
+                            K > 3 ? acc[3] : 0.f);
+    const int o = (t >> 3) & 3;
+    if ((t & 7) == 0 && o < K) {
+      const float v = d + b[o];
+      raw[n * K + o] = v;
+      pred[n * K + o] = post(role_of(kind, o), v);
     }
-    if (t < K) {  // lane k finalises output k
-      float v = 0.f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) v = (t == k) ? acc[k] : v;
-      v = v + b[t];
-      raw[n * K + t] = v;
-      pred[n * K + t] = post(role_of(kind, t), v);
+    if constexpr (K == 5) {
+      const float e = sum_32(acc[4]);
+      if (t == 1) {
+        const float v = e + b[4];
+        raw[n * K + 4] = v;
+        pred[n * K + 4] = post(role_of(kind, 4), v);
+      }
     }
   }
 }
@@ -92,6 +97,19 @@ __global__ __launch_bounds__(kThreads) void k_head_bwd(const float* __restrict__
       },
       (int64_t)blockIdx.x * kRowsPerBlock, (int64_t)gridDim.x * kRowsPerBlock, N, h, w, dh,
       slab + (size_t)blockIdx.x * (K * D + K), D, s_part);
+}
+
+// gine_testing_sum_32: sum_32 against the __shfl_xor butterfly it stands for, per lane
+__global__ __launch_bounds__(64) void k_testing_sum_32(const float* __restrict__ in,
+                                                       float* __restrict__ out, int mode) {
+  float a = in[blockIdx.x * 64 + threadIdx.x];
+  if (mode == 1) {
+    a = sum_32(a);
+  } else {
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) a += __shfl_xor(a, m, 32);
+  }
+  out[blockIdx.x * 64 + threadIdx.x] = a;
 }
 
 struct HeadOut {
@@ -160,6 +178,15 @@ int head_fwd(const float* h, const float* w, const float* b, float* raw, float* 
   return GINE_OK;
 }
 }  // namespace
+
+extern "C" int gine_testing_sum_32(const float* in, float* out, int32_t waves, int32_t mode,
+                                   void* stream) {
+  if (!in || !out || waves <= 0 || (mode != 0 && mode != 1)) return GINE_ERR_INVALID;
+  hipLaunchKernelGGL(k_testing_sum_32, dim3((unsigned)waves), dim3(64), 0, as_stream(stream), in,
+                     out, (int)mode);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
 
 extern "C" int gine_head_fwd(const float* h, const float* w, const float* b, float* raw,
                              float* pred, int64_t num_nodes, int32_t channels, int32_t kind,

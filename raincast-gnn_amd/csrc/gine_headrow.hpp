@@ -16,6 +16,51 @@ constexpr int kMaxK = 5;
 constexpr int kMaxChunks = 2;                  // D <= 256: two float4 per lane
 constexpr int kHeadBlocks = 256;               // backward grid (partials = one slab row each)
 
+// sum_32(a): the butterfly `for m = 16, 8, 4, 2, 1: a += __shfl_xor(a, m, 32)` with the same
+// partner, order and rounding at every lane (so the same bits), on VALU lane exchanges
+// instead of LDS-crossbar ds_bpermute round trips: xor 16 by v_permlane16_swap (odd and even
+// 16-lane rows of a half-wave exchanged), xor 8 by DPP row_ror:8, xor 4 by DPP row_half_mirror
+// (lane ^ 7) then quad_perm [3,2,1,0] (lane ^ 3), xor 2 / xor 1 by quad_perm.  Every partner
+// stays inside the lane's half-wave (a half-wave whose row is past N is inactive as a whole).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// the value of lane ^ 16 (v_permlane16_swap of v with itself: lanes 0-15 of the pair's first
+// result hold their own values, lanes 16-31 lanes 0-15's; the second result the other way)
+__device__ __forceinline__ float xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float sum_32(float a) {
+  a += xor16(a);
+  a += dpp_mov<0x128>(a);                     // row_ror:8       lane ^ 8
+  a += dpp_mov<0x1B>(dpp_mov<0x141>(a));      // half_mirror, quad_perm [3,2,1,0]: lane ^ 4
+  a += dpp_mov<0x4E>(a);                      // quad_perm [2,3,0,1]: lane ^ 2
+  a += dpp_mov<0xB1>(a);                      // quad_perm [1,0,3,2]: lane ^ 1
+  return a;
+}
+
+// The half-wave sums of four outputs a0..a3 at once, reduce-scattered: at xor 16 each lane
+// keeps the pair of outputs of its half of the half-wave ({0,1} for lanes 0-15, {2,3} for
+// 16-31) and receives its partner's values of that pair, at xor 8 it keeps one output
+// ((lane >> 3) & 3) and receives the partner's, then xor 4 / 2 / 1 sum the eight lanes of that
+// output.  Returns output ((lane >> 3) & 3)'s total, the same bits at all eight lanes of the
+// group (every step adds own + partner, and float addition commutes).  6 lane exchanges for
+// four outputs against 20 for four sum_32.  Every sum is own value + partner's, the same
+// order in the head kernel and in the layer epilogue that folds it (gine_mpmlp.hip).
+__device__ __forceinline__ float sum4_32(float a0, float a1, float a2, float a3) {
+  const bool b4 = threadIdx.x & 16, b3 = threadIdx.x & 8;
+  const float r0 = xor16(b4 ? a0 : a2), r1 = xor16(b4 ? a1 : a3);
+  const float c0 = (b4 ? a2 : a0) + r0, c1 = (b4 ? a3 : a1) + r1;
+  float d = (b3 ? c1 : c0) + dpp_mov<0x128>(b3 ? c0 : c1);  // lane ^ 8
+  d += dpp_mov<0x1B>(dpp_mov<0x141>(d));                     // lane ^ 4
+  d += dpp_mov<0x4E>(d);                                     // lane ^ 2
+  d += dpp_mov<0xB1>(d);                                     // lane ^ 1
+  return d;
+}
+
 // Column roles of the K outputs for each loss (models/model_utils.py:80-111).
 enum Role { R_ID = 0, R_SOFTPLUS = 1, R_SIGMOID = 2, R_SIGMOID_U = 3 };
 

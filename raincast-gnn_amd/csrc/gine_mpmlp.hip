@@ -29,6 +29,7 @@
 #include "gine_bnacc.hpp"
 #include "gine_edge.hpp"
 #include "gine_bf16x3.hpp"
+#include "gine_headrow.hpp"
 #include "gine_mlpsrc.hpp"
 
 #include <algorithm>
@@ -535,13 +536,25 @@ struct LayerArgs {
   const int2* win;     // WIN: per 32-row tile (first window row, window rows)
   int win_rows;        // WIN: max window rows over the tiles (the dummy row's index)
   int win_slots;       // WIN: slots per row of the padded slot table (lw_slots)
+  gine_layer_head hd;  // the output head folded into the epilogue (hk > 0)
+  int hk;              // head outputs per node (2..5), 0: no head
 };
+
+// The output head's LDS block (gine_layer_head): weights [kMaxK][kD] | bias [8] | raw outputs
+// of the workgroup's tiles [kLayerTiles][32][K] (PostProcess and the stores after the tile
+// loop, one element per thread) | valid-target counts per part [GINE_COUNT_PARTS] (uint32)
+constexpr int kHB = head::kMaxK * kD;
+constexpr int kHR = kHB + 8;
+constexpr int kHRTile = kTileRows * head::kMaxK;
+constexpr int kHC = kHR + kLayerTiles * kHRTile;
+constexpr int kHeadFloats = kHC + GINE_COUNT_PARTS;
 
 struct LayerLds {
   FusedLds f;
   float a1k[kLayerTiles][kTileRows * kLD];
   float bn[2 * kD];  // alpha | shift
   double tot[2 * kD];
+  float hd[kHeadFloats];  // the output head (gine_layer_head)
   int barrier_failed;  // this workgroup's grid barrier timed out (gine_bnacc.hpp)
 };
 
@@ -580,6 +593,10 @@ struct LayerWinLds {
 };
 static_assert(sizeof(LayerWinLds) <= 160 * 1024, "one workgroup per CU");
 static_assert(kD * kLD * 4 <= kLwRegion, "W2's image fits the window region");
+// phase B: the output head's weights and valid-target counts behind W2's image
+constexpr int kLwHeadOff = kD * kLD;  // floats into the window region
+static_assert((kLwHeadOff + kHeadFloats) * 4 <= kLwRegion,
+              "the head's weights and counts fit behind W2's image");
 static_assert(2 * kTileRows * kLD * 4 <= sizeof(float) * 4 * 32 * kTLD + sizeof(double) * 2 * 8 * kD,
               "phase B's output tiles fit the transposition + statistics region");
 // Slots per row of the padded slot table: the in-degree bound rounded up to whole groups.
@@ -923,7 +940,23 @@ __device__ __forceinline__ void gather_role_win(const FusedArgs& A, const LayerA
   w2r.load(reinterpret_cast<const float4*>(B.W2), p, kG);
   __syncthreads();  // G_nt: every gather wave is done with the last window
   w2r.store(reinterpret_cast<float*>(L.win), p, kG);
+  if (p < GINE_COUNT_PARTS)  // the head's valid-target counts (k_mp_fwd_layer)
+    reinterpret_cast<uint32_t*>(reinterpret_cast<float*>(L.win) + kLwHeadOff + kHC)[p] = 0;
   __syncthreads();  // S_nt+1
+}
+
+// Element e of the head's outputs of 32-row tile T from its raw values in LDS (rt: [32][K],
+// written by the epilogue's half-waves): raw stored and PostProcess applied once per element
+// after the tile loop (coalesced rows of raw / pred), instead of on the K lanes of every row's
+// half-wave inside it.
+__device__ __forceinline__ void head_finish(const LayerArgs& B, const float* rt, int T, int N,
+                                            int e) {
+  const int64_t base = (int64_t)T * kTileRows * B.hk;
+  if (base + e < (int64_t)N * B.hk) {
+    const float v = rt[e];
+    B.hd.raw[base + e] = v;
+    B.hd.pred[base + e] = head::post(head::role_of(B.hd.kind, e % B.hk), v);
+  }
 }
 
 template <bool FMA, int EPI, bool WIN = false>
@@ -938,6 +971,16 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   long long* phw = bnacc_phase(A.bnacc, 2 * kD);
   // written by earlier launches only (workgroup 0 moves them after the barrier)
   const long long ph = phw[0] + 1, consumed = phw[1 + ((ph - 1) & 1)];
+  // the output head's weights and valid-target counts (gine_layer_head)
+  float* hwl;
+  if constexpr (WIN) {
+    hwl = reinterpret_cast<float*>(L.win) + kLwHeadOff;  // counts zeroed by gather_role_win
+  } else {
+    hwl = L.hd;
+  }
+  uint32_t* const cwl = reinterpret_cast<uint32_t*>(hwl + kHC);
+  if constexpr (!WIN)
+    if (tid < GINE_COUNT_PARTS) cwl[tid] = 0;  // (phase A's barriers publish it)
 
   // ---- phase A ----
   LAYER_MARK(0);
@@ -991,6 +1034,29 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
   // p % 32 (p = tid - 256 < 512)
   const int p = tid - kMatThreads;
   const int eq = p & 31, er = p >> 5;
+  // the output head (gine_layer_head): its weights staged in LDS, and the loss's valid-target
+  // partial counts (count_valid_parts' parts: part q counts [q * chunk, min(N, q * chunk +
+  // chunk)), integer, any order) summed into L.cw -- gather waves, in the shadow of the grid
+  // barrier's wait
+  if (!mat && B.hk) {
+    if (p < B.hk * kD4)
+      *reinterpret_cast<float4*>(&hwl[4 * p]) =
+          *reinterpret_cast<const float4*>(B.hd.weight + 4 * p);
+    else if (p < B.hk * kD4 + B.hk)
+      hwl[kHB + p - B.hk * kD4] = B.hd.bias[p - B.hk * kD4];
+    if (B.hd.count_parts) {
+      const int64_t chunk = ((int64_t)A.N + GINE_COUNT_PARTS - 1) / GINE_COUNT_PARTS;
+      for (int q = blockIdx.x; q < GINE_COUNT_PARTS; q += gridDim.x) {
+        const int64_t lo = (int64_t)q * chunk, hi = min(lo + chunk, (int64_t)A.N);
+        uint32_t c = 0;
+        for (int64_t i = lo + p; i < hi; i += kThreads - kMatThreads)
+          c += B.hd.y_target[i] == B.hd.y_target[i];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+        if (lane == 0) atomicAdd(&cwl[q], c);
+      }
+    }
+  }
   LAYER_MARK(3);
   LAYER_RT(17);
   // the workgroup arrives as soon as phase A is done; W2's fragments are read after the
@@ -1041,6 +1107,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
           xres[k][i] = *reinterpret_cast<const float4*>(A.x + n * kD + 4 * eq);
         }
       }
+  }
+
+  // the loss's valid-target partial counts, summed above by the gather waves
+  if (!mat && B.hk && B.hd.count_parts) {
+    const int q = (int)blockIdx.x + p * (int)gridDim.x;
+    if (q < GINE_COUNT_PARTS) B.hd.count_parts[q] = cwl[q];
   }
 
   // ---- phase B: BatchNorm finish (the arithmetic of k_fwd2_bnacc's prologue) on the
@@ -1182,8 +1254,42 @@ __global__ __launch_bounds__(kThreads, 1) void k_mp_fwd_layer(FusedArgs A, Layer
           }
         }
         *reinterpret_cast<float4*>(B.y + off) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+        if (B.hk) {  // the head on this row: k_head_fwd's fma order and reduction
+          // (outputs 0-3 always -- independent chains; outputs past K are never stored --
+          // and output 4 when K = 5); raw into the LDS tile, finished after the tile loop
+          float a[4];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const float4 wk = *reinterpret_cast<const float4*>(&hwl[kk * kD + 4 * eq]);
+            a[kk] = 0.f;
+            a[kk] = __builtin_fmaf(o4[0], wk.x, a[kk]);
+            a[kk] = __builtin_fmaf(o4[1], wk.y, a[kk]);
+            a[kk] = __builtin_fmaf(o4[2], wk.z, a[kk]);
+            a[kk] = __builtin_fmaf(o4[3], wk.w, a[kk]);
+          }
+          const float d = head::sum4_32(a[0], a[1], a[2], a[3]);
+          const int o = (eq >> 3) & 3;
+          float* rt = hwl + kHR + k * kHRTile + r * B.hk;
+          if ((eq & 7) == 0 && o < B.hk) rt[o] = d + hwl[kHB + o];
+          if (B.hk == 5) {
+            const float4 wk = *reinterpret_cast<const float4*>(&hwl[4 * kD + 4 * eq]);
+            float a4 = 0.f;
+            a4 = __builtin_fmaf(o4[0], wk.x, a4);
+            a4 = __builtin_fmaf(o4[1], wk.y, a4);
+            a4 = __builtin_fmaf(o4[2], wk.z, a4);
+            a4 = __builtin_fmaf(o4[3], wk.w, a4);
+            a4 = head::sum_32(a4);
+            if (eq == 1) rt[4] = a4 + hwl[kHB + 4];
+          }
+        }
       }
     }
+  }
+  if (B.hk) {  // the head's PostProcess and stores of both tiles (nt <= kLayerTiles = 2)
+    __syncthreads();
+    static_assert(kLayerTiles * kHRTile <= kThreads - kMatThreads, "one element per thread");
+    const int kt = p / (kTileRows * B.hk), e = p - kt * kTileRows * B.hk;
+    if (!mat && kt < nt) head_finish(B, hwl + kHR + kt * kHRTile, ts.at(kt), A.N, e);
   }
   LAYER_MARK(7);
   LAYER_RT(19);
@@ -1364,7 +1470,8 @@ extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const
                                  const float* b2, float* y, uint8_t* mask, int64_t num_nodes,
                                  int32_t channels, int32_t max_in_degree, int32_t flags,
                                  int32_t epilogue, const int32_t* tile_windows,
-                                 int32_t window_rows, void* stream) {
+                                 int32_t window_rows, const gine_layer_head* head,
+                                 void* stream) {
   if (channels != kD) return GINE_ERR_DIM;
   if ((flags & ~GINE_MP_LIN_MULADD) != 0) return GINE_ERR_INVALID;
   if (!x || !in_rowptr || !in_src || !in_attr || !lin_w || !lin_b || !eps || !w1 || !b1 || !z ||
@@ -1375,6 +1482,19 @@ extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const
   if (epilogue < GINE_EPI_NONE || epilogue > GINE_EPI_RESIDUAL_RELU) return GINE_ERR_INVALID;
   if (epilogue == GINE_EPI_RESIDUAL_RELU && !mask) return GINE_ERR_INVALID;
   if (!layer_ok(num_nodes, channels, max_in_degree)) return GINE_ERR_INVALID;
+  int hk = 0;
+  if (head) {
+    switch (head->kind) {
+      case GINE_LOSS_NORMAL: hk = 2; break;
+      case GINE_LOSS_MIXED_NORMAL: hk = 3; break;
+      case GINE_LOSS_MIXED: hk = 4; break;
+      case GINE_LOSS_MIXED_U: hk = 5; break;
+      default: return GINE_ERR_INVALID;
+    }
+    if (!head->weight || !head->bias || !head->raw || !head->pred ||
+        (head->count_parts && !head->y_target))
+      return GINE_ERR_INVALID;
+  }
   int32_t grid = 0;
   const int st = gine_mlp_num_partials(num_nodes, channels, &grid);
   if (st != GINE_OK) return st;
@@ -1390,7 +1510,7 @@ extern "C" int gine_mp_fwd_layer(const float* x, const int32_t* in_rowptr, const
                     BnFwdParams{gamma, beta, running_mean, running_var, num_batches_tracked,
                                 bn_save, num_nodes, momentum, bn_eps, update_running},
                     reinterpret_cast<const int2*>(tile_windows), window_rows,
-                    lw_slots(max_in_degree)};
+                    lw_slots(max_in_degree), head ? *head : gine_layer_head{}, hk};
   const bool fma = !(flags & GINE_MP_LIN_MULADD);
 #define LAYER_LAUNCH(F_, E_)                                                                   \
   do {                                                                                         \

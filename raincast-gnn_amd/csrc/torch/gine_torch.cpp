@@ -204,7 +204,7 @@ class GineLayerFn : public torch::autograd::Function<GineLayerFn> {
                              graph[kLayerWinTiles].defined()
                                  ? (const int32_t*)graph[kLayerWinTiles].data_ptr()
                                  : nullptr,
-                             (int32_t)io[kLayerWinRows], s),
+                             (int32_t)io[kLayerWinRows], /*head=*/nullptr, s),
            "gine_mp_fwd_layer");
       } else {
         if (fused) {

@@ -23,7 +23,7 @@ GINE_MP_BWD_SELF = 1
 GINE_MP_LIN_MULADD = 2
 EPI_NONE, EPI_RELU, EPI_RESIDUAL_RELU = 0, 1, 2
 LOSS_NORMAL, LOSS_MIXED_NORMAL, LOSS_MIXED, LOSS_MIXED_U = 0, 1, 2, 3
-ABI_VERSION = 7
+ABI_VERSION = 8
 COUNT_PARTS = 64  # GINE_COUNT_PARTS
 
 _c_void_p = ctypes.c_void_p
@@ -49,6 +49,14 @@ class GradJob(ctypes.Structure):
                 ("nz", _i32), ("pad_", _i32), ("src", _c_void_p), ("cstride", _i64),
                 ("zstride", _i64), ("per", _i64 * 4), ("wsize", _i64 * 4),
                 ("bscale", _f32 * 4), ("w", _c_void_p * 4), ("b", _c_void_p * 4)]
+
+
+class LayerHead(ctypes.Structure):
+    """``gine_layer_head`` (include/gine_hip.h): the output head folded into the last layer's
+    gine_mp_fwd_layer launch."""
+    _fields_ = [("weight", _c_void_p), ("bias", _c_void_p), ("raw", _c_void_p),
+                ("pred", _c_void_p), ("y_target", _c_void_p), ("count_parts", _c_void_p),
+                ("kind", _i32)]
 
 
 GRAD_JOB_MP, GRAD_JOB_SLAB, GRAD_MAX_JOBS = 1, 2, 12
@@ -91,7 +99,8 @@ _SIGNATURES = {
     "gine_mp_fwd_mlp1_acc": [_c_void_p] * 13 + [_i64, _i32, _i32, _i32, _c_void_p],
     "gine_mp_fwd_layer_ok": [_i64, _i32, _i32, ctypes.POINTER(_i32)],
     "gine_mp_fwd_layer": [_c_void_p] * 18 + [_f32, _f32, _i32] + [_c_void_p] * 4
-                         + [_i64, _i32, _i32, _i32, _i32, _c_void_p, _i32, _c_void_p],
+                         + [_i64, _i32, _i32, _i32, _i32, _c_void_p, _i32,
+                            ctypes.POINTER(LayerHead), _c_void_p],
     "gine_graph_plan_layer_windows": [_c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                       _c_void_p],
     "gine_mp_fwd_layer_windows_fit": [_i32, _i32, ctypes.POINTER(_i32)],
@@ -101,6 +110,7 @@ _SIGNATURES = {
     "gine_bn_acc_words": [_i32, _c_void_p],
     "gine_bn_acc_barrier_failures_index": [_i32, _c_void_p],
     "gine_testing_layer_extra_workgroups": [_i32],
+    "gine_testing_sum_32": [_c_void_p, _c_void_p, _i32, _i32, _c_void_p],
     "gine_mlp_bwd2_acc": [_c_void_p] * 9 + [_i64, _i32, _i32, _c_void_p],
     "gine_mlp_bwd1_bn": [_c_void_p] * 10 + [_i64, _i32, _c_void_p],
     "gine_mlp_bwd_layer_ok": [_i64, _i32, ctypes.POINTER(_i32)],

@@ -394,10 +394,13 @@ class GineLayer(torch.autograd.Function):
     """y = epilogue( Linear2( ReLU( BN( Linear1( z ) ) ) ) ),  z = GINE message passing.
 
     epilogue: EPI_NONE -> o, EPI_RELU -> relu(o), EPI_RESIDUAL_RELU -> x + relu(o).
+    head: a head.HeadPlan for the output head that reads y (the stack's last layer), run by
+    the one-launch form's epilogue (gine_layer_head); other forms leave it to the head.
     """
 
     @staticmethod
-    def forward(ctx, x, lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2, graph, bn, epilogue):
+    def forward(ctx, x, lin_w, lin_b, eps, w1, b1, gamma, beta, w2, b2, graph, bn, epilogue,
+                head=None):
         x = x.contiguous()
         N, D = x.shape
         dev = x.device
@@ -430,6 +433,7 @@ class GineLayer(torch.autograd.Function):
         else:  # statistics summed by integer atomics, finished inside the second GEMM
             partials = None
         layer = fused and acc is not None and layer_forward_ok(N, D, graph.max_in_degree)
+        hargs = head.args(N, D, dev) if layer and head is not None else None
         with _paired(acc):
             if layer:
                 # the whole layer forward in one launch (grid barrier between its halves)
@@ -439,7 +443,10 @@ class GineLayer(torch.autograd.Function):
                      ptr(bn.running_var), nbt, ptr(bn_save), bn.momentum, bn.eps,
                      update_running, ptr(w2c), ptr(b2c), ptr(y), ptr(mask), N, D,
                      graph.max_in_degree, edge_linear_flag(), epilogue,
-                     *layer_window_args(graph), stream)
+                     *layer_window_args(graph),
+                     ctypes.byref(hargs) if hargs is not None else None, stream)
+                if hargs is not None:
+                    head.done = (y.data_ptr(), tuple(y.shape))
             elif fused:
                 # gather of the next tile beside the matrix chain of this one: one launch
                 args = (ptr(x), ptr(graph.in_rowptr), ptr(graph.in_src), ptr(graph.in_attr),
@@ -567,4 +574,4 @@ class GineLayer(torch.autograd.Function):
             call("gine_grad_finalize_batch", arr, len(jobs), stream)
         lin_w_shape, affine = ctx.shapes
         return (dx, dlw.view(lin_w_shape), dlb, deps.view_as(ep), dw1, db1, dgamma, dbeta,
-                dw2, db2, None, None, None)
+                dw2, db2, None, None, None, None)

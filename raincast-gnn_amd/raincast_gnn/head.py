@@ -74,18 +74,75 @@ def fusable(h: torch.Tensor, lin: torch.nn.Linear, kind) -> bool:
             and h.size(1) % 4 == 0 and h.size(1) <= MAX_CHANNELS)
 
 
+def _counts_y(y, N: int, dev) -> bool:
+    """The targets can be counted beside the head (gine_head_fwd_count / gine_layer_head)."""
+    return (y is not None and y.is_cuda and y.device == dev and y.dtype == torch.float32
+            and y.is_contiguous() and y.numel() == N)
+
+
+class HeadPlan:
+    """The head forward folded into the last GINE layer's launch (gine_layer_head,
+    csrc/gine_mpmlp.hip): the outputs are allocated here, handed to that launch
+    (functional.GineLayer) and taken by :func:`head` when its input is exactly the tensor
+    that launch wrote (``done`` = its data pointer); otherwise the head runs its own launch."""
+
+    __slots__ = ("params", "versions", "w", "b", "kind", "y", "raw", "pred", "parts", "done")
+
+    def __init__(self, N: int, D: int, lin: torch.nn.Linear, kind: int, y, dev):
+        self.params = (lin.weight, lin.bias)
+        self.versions = (lin.weight._version, lin.bias._version)
+        self.w, self.b = lin.weight.detach().contiguous(), lin.bias.detach().contiguous()
+        self.kind = kind
+        K = self.w.size(0)
+        self.raw = torch.empty(N, K, dtype=torch.float32, device=dev)
+        self.pred = torch.empty(N, K, dtype=torch.float32, device=dev)
+        self.y = y if _counts_y(y, N, dev) else None
+        self.parts = (torch.empty(_lib.COUNT_PARTS, dtype=torch.int32, device=dev)
+                      if self.y is not None else None)
+        self.done = None
+
+    def args(self, N: int, D: int, dev):
+        """The gine_layer_head of a launch writing [N, D] rows on ``dev``, or None."""
+        if self.raw.size(0) != N or self.w.size(1) != D or self.raw.device != dev:
+            return None
+        return _lib.LayerHead(_lib.ptr(self.w), _lib.ptr(self.b), _lib.ptr(self.raw),
+                              _lib.ptr(self.pred), _lib.ptr(self.y), _lib.ptr(self.parts),
+                              self.kind)
+
+    def take(self, h: torch.Tensor, weight, bias, kind: int, y):
+        """(raw, pred, parts | None) when the launch that wrote ``h`` also ran this head (the
+        same parameters, unchanged since, and kind), else None; one use."""
+        done, self.done = self.done, None
+        if (done is None or done != (h.data_ptr(), tuple(h.shape)) or kind != self.kind
+                or self.params[0] is not weight or self.params[1] is not bias
+                or self.versions != (weight._version, bias._version)):
+            return None
+        return self.raw, self.pred, (self.parts if y is self.y else None)
+
+
+def plan(h: torch.Tensor, lin: torch.nn.Linear, kind: int, y=None) -> HeadPlan:
+    """A HeadPlan for the head that follows the GINE stack whose input is ``h``."""
+    return HeadPlan(h.size(0), h.size(1), lin, kind, y, h.device)
+
+
 class _HeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, weight, bias, kind, y=None):
+    def forward(ctx, h, weight, bias, kind, y=None, hplan=None):
         h = h.contiguous()
         w, b = weight.detach().contiguous(), bias.detach().contiguous()
         N, D = h.shape
         K = w.size(0)
-        raw = torch.empty(N, K, dtype=torch.float32, device=h.device)
-        pred = torch.empty(N, K, dtype=torch.float32, device=h.device)
+        done = hplan.take(h, weight, bias, kind, y) if hplan is not None else None
+        if done is not None:  # computed by the last layer's launch
+            raw, pred, parts = done
+        else:
+            raw = torch.empty(N, K, dtype=torch.float32, device=h.device)
+            pred = torch.empty(N, K, dtype=torch.float32, device=h.device)
         rec = HeadRecord(h, w, raw, kind, (weight, bias))
-        if (y is not None and y.is_cuda and y.device == h.device and y.dtype == torch.float32
-                and y.is_contiguous() and y.numel() == N):
+        if done is not None:
+            if parts is not None:
+                rec.y, rec.y_version, rec.count_parts = y, y._version, parts
+        elif _counts_y(y, N, h.device):
             # the loss's valid-target count, computed beside the head (no launch of its own)
             parts = torch.empty(_lib.COUNT_PARTS, dtype=torch.int32, device=h.device)
             _lib.call("gine_head_fwd_count", _lib.ptr(h), _lib.ptr(w), _lib.ptr(b),
@@ -121,7 +178,7 @@ class _HeadFn(torch.autograd.Function):
             else:
                 arr = (_lib.GradJob * 1)(job)
                 _lib.call("gine_grad_finalize_batch", arr, 1, _lib.stream_handle(dev))
-            return dh, dw, db, None, None
+            return dh, dw, db, None, None, None
         gpred = gpred.float().contiguous()
         floats = ctypes.c_size_t(0)
         _lib.call("gine_head_bwd_slab_floats", N, D, ctx.kind, ctypes.byref(floats))
@@ -138,11 +195,13 @@ class _HeadFn(torch.autograd.Function):
             _lib.call("gine_head_bwd_grad_job", N, D, ctx.kind, _lib.ptr(slab), _lib.ptr(dw),
                       _lib.ptr(db), ctypes.byref(job))
             gradbuf.defer(job, dev, (slab,))
-        return dh, dw, db, None, None
+        return dh, dw, db, None, None, None
 
 
-def head(h: torch.Tensor, lin: torch.nn.Linear, kind: int, y: torch.Tensor | None = None
-         ) -> torch.Tensor:
+def head(h: torch.Tensor, lin: torch.nn.Linear, kind: int, y: torch.Tensor | None = None,
+         hplan: HeadPlan | None = None) -> torch.Tensor:
     """``PostProcess(lin(h))`` for the loss ``kind`` on the fused kernels.  ``y``: the
-    batch targets, whose non-NaN count the launch also takes for the loss that follows."""
-    return _HeadFn.apply(h, lin.weight, lin.bias, kind, y)
+    batch targets, whose non-NaN count the launch also takes for the loss that follows.
+    ``hplan``: the plan handed to the GINE stack (:func:`plan`); when its last layer's launch
+    ran the head on exactly ``h``, its outputs are used and no launch is made here."""
+    return _HeadFn.apply(h, lin.weight, lin.bias, kind, y, hplan)

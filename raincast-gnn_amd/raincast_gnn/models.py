@@ -14,6 +14,7 @@ from torch.nn import Linear, ModuleList, ReLU
 from . import chain as fused_chain
 from . import deepset
 from . import head as fused_head
+from . import options
 from .linear import Linear as RowLinear
 from .loss import MixedLoss, MixedNormalCRPS, NormalCRPS
 from .nn import GINEConv
@@ -39,14 +40,18 @@ class ResGnn(nn.Module):
         self.relu = ReLU()
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor,
-                edge_attr: torch.Tensor) -> torch.Tensor:
+                edge_attr: torch.Tensor, head=None) -> torch.Tensor:
+        """``head``: a head.HeadPlan for the output head that follows (GNN.forward), handed
+        to the last layer, whose launch runs it where it can."""
         x = x.float()
         edge_attr = edge_attr.float()
+        last = len(self.convolutions) - 1
         for i, conv in enumerate(self.convolutions):
+            hp = head if i == last else None
             if i == 0:
-                x = conv.forward_relu(x, edge_index, edge_attr)            # relu(conv(x))
+                x = conv.forward_relu(x, edge_index, edge_attr, head=hp)        # relu(conv(x))
             else:
-                x = conv.forward_residual_relu(x, edge_index, edge_attr)   # x + relu(conv(x))
+                x = conv.forward_residual_relu(x, edge_index, edge_attr, head=hp)  # x + relu(.)
         return x
 
 
@@ -140,11 +145,17 @@ class GNN(nn.Module):
 
     def forward(self, data):
         h = self._front(data)
-        h = self.conv(h, data.edge_index, data.edge_attr)
         kind = fused_head.loss_kind(self.postprocess.loss, self.postprocess.grad_u)
+        y = getattr(data, "y", None)
+        hplan = None
+        if (options.HEAD_FOLD and type(self.aggr) in (RowLinear, Linear)
+                and fused_head.fusable(h, self.aggr, kind)):
+            # the head's forward folded into the last GINE layer's launch (gine_layer_head)
+            hplan = fused_head.plan(h, self.aggr, kind, y)
+        h = self.conv(h, data.edge_index, data.edge_attr, head=hplan)
         if type(self.aggr) in (RowLinear, Linear) and fused_head.fusable(h, self.aggr, kind):
             # aggr + PostProcess in one kernel, which also counts the loss's valid targets
-            return fused_head.head(h, self.aggr, kind, getattr(data, "y", None))
+            return fused_head.head(h, self.aggr, kind, y, hplan)
         return self.postprocess(self.aggr(h))
 
     def configure_optimizers(self):

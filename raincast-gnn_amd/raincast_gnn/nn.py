@@ -145,7 +145,7 @@ class GINEConv(torch.nn.Module):
             raise ValueError(f"lin projects to {self.lin.out_features} channels, x has {x.size(1)}")
         return x
 
-    def _run(self, x, edge_index, edge_attr, size, epilogue):
+    def _run(self, x, edge_index, edge_attr, size, epilogue, head=None):
         x = self._check_inputs(x, edge_index, edge_attr, size)
         edge_attr = edge_attr.float()
         graph = get_graph(edge_index, edge_attr, x.size(0), self.flow)
@@ -158,7 +158,7 @@ class GINEConv(torch.nn.Module):
                 return torch_ext.layer(ext, x, self, graph, epilogue)
             return GineLayer.apply(x, self.lin.weight, self.lin.bias, self.eps, l1.weight,
                                    l1.bias, bn.weight, bn.bias, l2.weight, l2.bias, graph,
-                                   BnConfig(bn), epilogue)
+                                   BnConfig(bn), epilogue, head)
         z = GineMessagePassing.apply(x, self.lin.weight, self.lin.bias, self.eps, graph)
         out = self.nn(z)
         if epilogue == EPI_RELU:
@@ -171,13 +171,16 @@ class GINEConv(torch.nn.Module):
                 size=None) -> Tensor:
         return self._run(x, edge_index, edge_attr, size, EPI_NONE)
 
-    def forward_relu(self, x, edge_index, edge_attr=None):
-        """relu(self(x, ...)) with the ReLU fused into the last GEMM (ResGnn layer 0)."""
-        return self._run(x, edge_index, edge_attr, None, EPI_RELU)
+    def forward_relu(self, x, edge_index, edge_attr=None, head=None):
+        """relu(self(x, ...)) with the ReLU fused into the last GEMM (ResGnn layer 0).
+        ``head``: a head.HeadPlan when the output head reads this result (the stack's last
+        layer), run in the same launch where the one-launch layer forward applies."""
+        return self._run(x, edge_index, edge_attr, None, EPI_RELU, head)
 
-    def forward_residual_relu(self, x, edge_index, edge_attr=None):
-        """x + relu(self(x, ...)) fused (ResGnn layers >= 1, models/gnn.py:44)."""
-        return self._run(x, edge_index, edge_attr, None, EPI_RESIDUAL_RELU)
+    def forward_residual_relu(self, x, edge_index, edge_attr=None, head=None):
+        """x + relu(self(x, ...)) fused (ResGnn layers >= 1, models/gnn.py:44); ``head`` as
+        for forward_relu."""
+        return self._run(x, edge_index, edge_attr, None, EPI_RESIDUAL_RELU, head)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}(nn={self.nn})"

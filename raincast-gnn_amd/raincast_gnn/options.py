@@ -27,6 +27,9 @@ LAYER_WIN    True: the one-launch layer forward stages each tile's neighbour row
 LAYER_BWD    True: where the backward accumulator applies and the grid fits the device at
              once, the node-MLP backward in one launch (gine_mlp_bwd_layer: the dbn GEMM and
              the dz GEMM separated by a grid barrier); False: the pair.
+HEAD_FOLD    True: the output head's forward (GNN.aggr + PostProcess, and the loss's
+             valid-target count) runs in the last GINE layer's one-launch forward
+             (gine_layer_head) where that launch applies; False: its own launch.  Same bits.
 """
 from __future__ import annotations
 
@@ -39,3 +42,4 @@ BN_ACC_BWD = True
 LAYER_FWD = True
 LAYER_WIN = False
 LAYER_BWD = True
+HEAD_FOLD = True

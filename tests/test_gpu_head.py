@@ -110,3 +110,30 @@ def test_captured_step_recounts_valid_targets():
     torch.cuda.synchronize()
     assert torch.equal(l_graph, l_eager)
     assert torch.equal(g_graph, opt.flat_grad), (g_graph - opt.flat_grad).abs().max()
+
+
+def test_sum_32_same_bits_as_shfl_xor_butterfly():
+    """csrc/gine_headrow.hpp sum_32 (permlane16_swap + DPP lane exchanges) gives, at every
+    lane, the bits of the __shfl_xor butterfly it replaces: same partners, same order, same
+    rounding -- on values spread over many binades, with ties, signed zeros, inf and NaN."""
+    from raincast_gnn import _lib
+    g = torch.Generator().manual_seed(5)
+    waves = 4096
+    x = torch.randn(waves * 64, generator=g) * torch.exp2(torch.randint(-30, 30, (waves * 64,),
+                                                                         generator=g).float())
+    x[::97] = 0.0
+    x[1::101] = -0.0
+    x[5::1009] = float("inf")
+    x[7::1013] = float("-inf")
+    x[3::2003] = float("nan")
+    x = x.to(DEV)
+    outs = []
+    for mode in (0, 1):
+        o = torch.empty_like(x)
+        _lib.call("gine_testing_sum_32", _lib.ptr(x), _lib.ptr(o), waves, mode,
+                  _lib.stream_handle(DEV))
+        outs.append(o)
+    torch.cuda.synchronize()
+    num = ~torch.isnan(outs[0])
+    assert torch.equal(outs[0][num].view(torch.int32), outs[1][num].view(torch.int32))
+    assert torch.equal(torch.isnan(outs[0]), torch.isnan(outs[1]))

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-stamps", action="store_true", help="plain library: time only")
     ap.add_argument("--no-win", action="store_true", help="gather from L2 (no layer windows)")
+    ap.add_argument("--head", type=int, default=None, metavar="KIND",
+                    help="fold the output head (GINE_LOSS_* kind, with a valid-target count) "
+                         "into the launch (gine_layer_head)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     D = 128
@@ -51,16 +54,27 @@ def main():
     bsave = torch.empty(4, D, device=dev)
     acc = torch.zeros(Fn._count64("gine_bn_acc_words", D), dtype=torch.int64, device=dev)
     call, ptr = _lib.call, _lib.ptr
+    ptr_ = ptr
     s = _lib.stream_handle(dev)
     lin = Fn.edge_linear_flag()
     win_args = (None, 0) if a.no_win else Fn.layer_window_args(g)
     print(f"layer windows: {'off (L2 gather)' if win_args[0] is None else win_args[1:]}")
+    hargs = None
+    if a.head is not None:
+        K = {0: 2, 1: 3, 2: 4, 3: 5}[a.head]
+        hw, hb = torch.randn(K, D, device=dev) / D ** 0.5, torch.randn(K, device=dev)
+        raw, pred = torch.empty(N, K, device=dev), torch.empty(N, K, device=dev)
+        yt = torch.randn(N, device=dev)
+        parts = torch.empty(_lib.COUNT_PARTS, dtype=torch.int32, device=dev)
+        hargs = ctypes.byref(_lib.LayerHead(ptr_(hw), ptr_(hb), ptr_(raw), ptr_(pred), ptr_(yt),
+                                            ptr_(parts), a.head))
+        print(f"head folded in: kind {a.head} (K = {K}), valid-target count")
 
     def run():
         call("gine_mp_fwd_layer", ptr(x), ptr(g.in_rowptr), ptr(g.in_src), ptr(g.in_attr),
              ptr(lw), ptr(lb), ptr(ep), ptr(w1), ptr(b1), ptr(z), ptr(a1), ptr(acc), ptr(gam),
              ptr(bet), ptr(rm), ptr(rv), None, ptr(bsave), 0.1, 1e-5, 1, ptr(w2), ptr(b2),
-             ptr(y), ptr(mask), N, D, g.max_in_degree, lin, 2, *win_args, s)
+             ptr(y), ptr(mask), N, D, g.max_in_degree, lin, 2, *win_args, hargs, s)
 
     lib = _lib.load()
     buf = (ctypes.c_longlong * (1024 * 24))()
