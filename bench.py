@@ -98,6 +98,13 @@ def parse():
                     help="time the drop-in path instead: the reference's model structure in "
                          "torch with raincast_gnn's GINEConv, train.py's loop (batch.to(device) "
                          "and loss.item() every step); 1 GPU")
+    ap.add_argument("--settle-steps", type=int, default=100,
+                    help="replays of the captured step after capture, before the timed steps "
+                         "(same count on every rank): the GPU clock ramps for ~25 ms after the "
+                         "CPU-bound preparation (cfg2 step 0.474 -> 0.436 ms over the first 50 "
+                         "replays, profiles/r06_s18_clock_ramp.txt), so a 20-step region "
+                         "right after capture would time the ramp, not the training step; "
+                         "0 times the ramp")
     ap.add_argument("--no-head-fold", action="store_true",
                     help="A/B: the output head in a launch of its own instead of the last GINE "
                          "layer's (options.HEAD_FOLD)")
@@ -753,6 +760,10 @@ def measure(cfg, graphs_per_rank, args, device, rank, world):
         tr.capture()
         for _ in range(2):
             tr.step()
+    # clock settle (--settle-steps): untimed replays until the GPU runs at its training-steady
+    # clock; the same count on every rank (the N > 1 step holds a collective)
+    for _ in range(max(0, args.settle_steps)):
+        tr.step()
     torch.cuda.synchronize(device)
 
     if world > 1:
@@ -1245,6 +1256,8 @@ def main():
             "metric": "training graphs/s (24h_mixed GNN, full train step)",
             "value": round(value, 2), "unit": "graphs/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            # untimed replays between the warmup / capture and the timed steps (clock ramp)
+            "settle_steps": max(0, args.settle_steps),
             "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
             "dtype": "f32 (split-bf16x3 GEMM products, fp32 accumulate)",
             "data": "synthetic (k-NN station graphs, random-init weights)",
