@@ -367,6 +367,231 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The doubly folded chain's two row stages on the bf16 matrix cores (gine_bf16x3.hpp split
+// form, fp32-class products):
+//   FWD  (F2D): u  = relu(r Wf^T + bf)        -> h0 = [x | u] W'^T + b'
+//   !FWD (B2D): dt = (dh0 Wc) * 1[u > 0]      -> dr = dt Wf
+// k_chain's F2D / B2D ran both stages on v_mfma_f32_32x32x2_f32: at one wave per SIMD, K = 128
+// costs 64 x 64 = 4,096 MFMA cycles per 32x32 block, against 8 x 192 = 1,536 for the split
+// chain.  Both weights are split once per workgroup into register planes (BPlanes); every
+// A tile is split once, by the threads that stage it, into three bf16 planes in LDS (the
+// stage-1 input from HBM, x beside it; stage 1's output by the lanes that produce it, one
+// bf16 per plane), so the chains only read fragments (tools/chain_micro.py: a block with
+// pre-split planes 2,046 ticks, split in the loop 3,081).  x's columns are padded to a
+// multiple of 16 (FPX) so both stages run whole K = 16 blocks.  A wave whose accumulators
+// see a NaN (a non-finite input or weight) redoes its tile on the fp32 chain from memory:
+// non-finite values propagate as in the fp32 GEMM.  Same tile walk, grid and outputs as
+// k_chain.
+// Measured (profiles/r06_s21): correct (the chain, training and head tests green on it) but
+// SLOWER in the step -- forward 23.4 vs 20.4 us, backward 16.2 vs 16.4, step 0.4482 vs
+// 0.4432 ms interleaved: the fp32 chain is not MFMA-bound at one workgroup per CU (its
+// 2 x 9,472 MFMA cycles are ~8 of the 20 us), and the split form's 228 weight-plane
+// registers spill into AGPR copies and just-in-time fragment reads.  Off (GINE_CHAIN_X3=1
+// builds it into the dispatch).
+// ---------------------------------------------------------------------------------------
+#ifndef GINE_CHAIN_X3
+#define GINE_CHAIN_X3 0
+#endif
+
+template <int D, int FP, bool FWD>
+__global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int num_tiles) {
+  constexpr int NT = 2 * D, D4 = D / 4;
+  constexpr int FPX = FWD ? (FP + 15) / 16 * 16 : 0;  // stage 2's x columns, whole 16-k blocks
+  constexpr int K1 = D, K2 = FPX + D;
+  constexpr int KS1 = K1 / 2, KS2 = K2 / 2;
+  static_assert(KS1 % 8 == 0 && KS2 % 8 == 0, "whole split fragments per lane half");
+  constexpr int RS1 = K1 + 8, RS2 = K2 + 8;  // plane row strides (bf16): 16 x odd bytes
+  constexpr int P1 = kRowTile * RS1, P2 = kRowTile * RS2;
+  constexpr int ITEMS = kRowTile * D4 / NT;  // stage-1 A float4 per thread
+  constexpr int RSTEP = NT / D4;
+  constexpr int XP = FWD ? FPX / 2 : 1;  // x column pairs per row
+  constexpr int XITEMS = FWD ? (kRowTile * XP + NT - 1) / NT : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t pa[3 * P1];
+  __shared__ __attribute__((aligned(16))) uint16_t pb[3 * P2];
+
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int col = wave * 32 + c32;
+  const int q_me = threadIdx.x % D4, r_me = threadIdx.x / D4;
+  const int F = a.F;
+
+  // both weights as split register planes, once per workgroup (lane half h: k = h*KS + s)
+  BPlanes<KS1> b1;
+  BPlanes<KS2> b2;
+  {
+    float f[KS1];
+    if constexpr (FWD) frag_t<D>(f, a.w1, D, col, h);         // Wf
+    else frag_n<D>(f, a.w1, F + D, F, col, h);               // W' e-columns (Wc)
+    b1.from(f);
+  }
+  {
+    float f[KS2];
+    if constexpr (FWD) frag_dimred_t<FPX, D>(f, a.w3, F, col, h);  // W'^T, x columns padded
+    else frag_n<D>(f, a.w2, D, 0, col, h);                        // Wf
+    b2.from(f);
+  }
+  const float bias1 = FWD ? a.b1[col] * a.bias1_scale : 0.f;
+  const float bias2 = FWD ? a.b3[col] : 0.f;
+  float* out1 = a.out1;
+  float* out2 = FWD ? a.out3 : a.out2;
+
+  const TileRange tr = tile_range(num_tiles, gridDim.x);
+  float4 raw[ITEMS];
+  float xr[2 * XITEMS];
+  auto load_tile = [&](int tile) {
+    const int64_t n0 = (int64_t)tile * kRowTile;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+      int64_t n = n0 + r_me + i * RSTEP;
+      n = n < N ? n : N - 1;
+      raw[i] = reinterpret_cast<const float4*>(a.in + n * D)[q_me];
+    }
+    if constexpr (FWD) {
+#pragma unroll
+      for (int i = 0; i < XITEMS; ++i) {
+        const int idx = min((int)threadIdx.x + i * NT, kRowTile * XP - 1);
+        int64_t n = n0 + idx / XP;
+        n = n < N ? n : N - 1;
+        const int c = 2 * (idx % XP);
+        xr[2 * i] = a.x[n * F + min(c, F - 1)];  // padding columns zeroed at the store
+        xr[2 * i + 1] = a.x[n * F + min(c + 1, F - 1)];
+      }
+    }
+  };
+  if (tr.first < tr.end) load_tile(tr.first);
+  for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+    const int64_t n0 = (int64_t)tile * kRowTile;
+    __syncthreads();  // the previous tile's fragment reads are done
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {  // stage-1 A planes (rows past N: zero)
+      const int r = r_me + i * RSTEP;
+      const float4 v = (n0 + r < N) ? raw[i] : f4_zero();
+      uint32_t h0, m0, l0, h1, m1, l1;
+      split2(v.x, v.y, h0, m0, l0);
+      split2(v.z, v.w, h1, m1, l1);
+      uint16_t* d = pa + r * RS1 + 4 * q_me;
+      *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(d + P1) = make_uint2(m0, m1);
+      *reinterpret_cast<uint2*>(d + 2 * P1) = make_uint2(l0, l1);
+    }
+    if constexpr (FWD) {
+#pragma unroll
+      for (int i = 0; i < XITEMS; ++i) {  // x planes: columns [0, FPX) of stage 2's A
+        const int idx = threadIdx.x + i * NT;
+        if (idx < kRowTile * XP) {
+          const int r = idx / XP, c = 2 * (idx % XP);
+          const bool live = n0 + r < N;
+          const float v0 = live && c < F ? xr[2 * i] : 0.f;
+          const float v1 = live && c + 1 < F ? xr[2 * i + 1] : 0.f;
+          uint32_t hh, mm, ll;
+          split2(v0, v1, hh, mm, ll);
+          uint16_t* d = pb + r * RS2 + c;
+          *reinterpret_cast<uint32_t*>(d) = hh;
+          *reinterpret_cast<uint32_t*>(d + P2) = mm;
+          *reinterpret_cast<uint32_t*>(d + 2 * P2) = ll;
+        }
+      }
+    }
+    __syncthreads();
+    if (tile + tr.step < tr.end) load_tile(tile + tr.step);  // next tile in flight
+    float ep[FWD ? 1 : 16];
+    if constexpr (!FWD) {  // the ReLU mask of u, in flight under stage 1
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        n = n < N ? n : N - 1;
+        ep[r] = a.aux[n * D + col];
+      }
+    }
+
+    // stage 1
+    floatx16 acc = zero16();
+    {
+      const uint16_t* pr = pa + c32 * RS1 + h * KS1;
+#pragma unroll
+      for (int s8 = 0; s8 < KS1 / 8; ++s8) {
+        Bf16x3 f;
+        f.h = *reinterpret_cast<const bf16x8_t*>(pr + 8 * s8);
+        f.m = *reinterpret_cast<const bf16x8_t*>(pr + P1 + 8 * s8);
+        f.l = *reinterpret_cast<const bf16x8_t*>(pr + 2 * P1 + 8 * s8);
+        acc = mfma_bf16x3(f, b1.f[s8], acc);
+      }
+      if (wave_any_nan(acc)) {  // fp32 chain from memory (the fp32 GEMM's non-finite values)
+        const int64_t n = min(n0 + c32, N - 1);
+        acc = zero16();
+        if constexpr (FWD)
+          acc = mfma_f32_row_mem<KS1>(a.in + n * D + h * KS1, a.w1 + (size_t)col * D + h * KS1,
+                                      1, acc);
+        else
+          acc = mfma_f32_row_mem<KS1>(a.in + n * D + h * KS1,
+                                      a.w1 + (size_t)(h * KS1) * (F + D) + F + col, F + D, acc);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t n = n0 + rr;
+      float v;
+      if constexpr (FWD) v = relu_nan(acc[r] + bias1);   // u = relu(r Wf^T + bf)
+      else v = ep[r] > 0.f ? acc[r] : 0.f;               // dt = du * 1[u > 0]
+      if (n < N) out1[n * D + col] = v;
+      else v = 0.f;
+      uint32_t hh, mm, ll;
+      split2(v, 0.f, hh, mm, ll);
+      uint16_t* d = pb + rr * RS2 + FPX + col;
+      d[0] = (uint16_t)hh;
+      d[P2] = (uint16_t)mm;
+      d[2 * P2] = (uint16_t)ll;
+    }
+    __syncthreads();  // stage 2's A planes complete (and stage 1's outputs written)
+
+    // stage 2
+    acc = zero16();
+    {
+      const uint16_t* pr = pb + c32 * RS2 + h * KS2;
+#pragma unroll
+      for (int s8 = 0; s8 < KS2 / 8; ++s8) {
+        Bf16x3 f;
+        f.h = *reinterpret_cast<const bf16x8_t*>(pr + 8 * s8);
+        f.m = *reinterpret_cast<const bf16x8_t*>(pr + P2 + 8 * s8);
+        f.l = *reinterpret_cast<const bf16x8_t*>(pr + 2 * P2 + 8 * s8);
+        acc = mfma_bf16x3(f, b2.f[s8], acc);
+      }
+      if (wave_any_nan(acc)) {
+        const int64_t n = min(n0 + c32, N - 1);
+        acc = zero16();
+        if constexpr (FWD) {  // A = [x | 0 | u] of row n, B = W'^T on the same padded k axis
+#pragma unroll 1
+          for (int s = 0; s < KS2; ++s) {
+            const int k = h * KS2 + s;
+            float av, bv;
+            if (k < FPX) {
+              av = k < F ? a.x[n * F + k] : 0.f;
+              bv = k < F ? a.w3[(size_t)k * D + col] : 0.f;
+            } else {
+              av = out1[n * D + (k - FPX)];
+              bv = a.w3[(size_t)(k - FPX + F) * D + col];
+            }
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+          }
+        } else {
+          acc = mfma_f32_row_mem<KS2>(out1 + n * D + h * KS2, a.w2 + (size_t)(h * KS2) * D + col,
+                                      D, acc);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (n < N) out2[n * D + col] = acc[r] + bias2;
+    }
+  }
+}
+
+template <int D, int FP, bool FWD>
+int launch_chain2_x3(const ChainArgs& a, int64_t N, hipStream_t s);
+
 // Persistent grid, one workgroup per CU (two per CU measured slower at cfg2: 0.614 vs
 // 0.589 ms per step).
 inline int chain_grid(int64_t N) {
@@ -380,6 +605,15 @@ int launch_chain(const ChainArgs& a, int64_t N, hipStream_t s) {
   const int fold = (KIND == CH_F1 && a.wfold != nullptr) ? kFoldBlocks<D> : 0;
   hipLaunchKernelGGL((k_chain<D, FP, KIND>), dim3(chain_grid(N) + fold), dim3(2 * D), 0, s, a,
                      N, tiles);
+  GINE_LAUNCH_STATUS();
+  return GINE_OK;
+}
+
+template <int D, int FP, bool FWD>
+int launch_chain2_x3(const ChainArgs& a, int64_t N, hipStream_t s) {
+  const int tiles = (int)ceil_div(N, kRowTile);
+  hipLaunchKernelGGL((k_chain2_x3<D, FP, FWD>), dim3(chain_grid(N)), dim3(2 * D), 0, s, a, N,
+                     tiles);
   GINE_LAUNCH_STATUS();
   return GINE_OK;
 }
@@ -906,7 +1140,9 @@ extern "C" int gine_chain_fwd_folded2(const float* r, const float* x, const floa
   f.b3 = bfold;
   f.out3 = h0;
   int rc = GINE_OK;
-#define CALL_F(DD, FF) rc = launch_chain<DD, FF, CH_F2D>(f, num_nodes, st)
+#define CALL_F(DD, FF)                                                                  \
+  rc = GINE_CHAIN_X3 ? launch_chain2_x3<DD, FF, true>(f, num_nodes, st)                   \
+                     : launch_chain<DD, FF, CH_F2D>(f, num_nodes, st)
   GINE_CHAIN_DISPATCH(D, F, CALL_F);
 #undef CALL_F
   return rc;
@@ -924,7 +1160,9 @@ extern "C" int gine_chain_bwd_folded2(const float* dh0, const float* u, const fl
   const int F = in_features;
   const ChainArgs b{dh0, nullptr, u, wfold, nullptr, wfold2, nullptr, dt, dr, 1.f, F};
   int rc = GINE_OK;
-#define CALL_B(DD, FF) rc = launch_chain<DD, FF, CH_B2D>(b, num_nodes, st)
+#define CALL_B(DD, FF)                                                                  \
+  rc = GINE_CHAIN_X3 ? launch_chain2_x3<DD, FF, false>(b, num_nodes, st)                  \
+                     : launch_chain<DD, FF, CH_B2D>(b, num_nodes, st)
   GINE_CHAIN_DISPATCH(hidden, F, CALL_B);
 #undef CALL_B
   return rc;
