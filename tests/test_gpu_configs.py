@@ -81,6 +81,23 @@ def test_training_step_matches_oracle_at_config(cfg, graphs, relabel):
     print(f"{c.name} x{graphs} relabel={relabel}: worst scaled grad err {worst:.2e}")
 
 
+@pytest.mark.skipif(not os.environ.get("GINE_FULL_PARITY"),
+                    reason="full-size oracle steps take minutes of host time: set "
+                           "GINE_FULL_PARITY=1 (run by tools/sessions, tables in profiles/)")
+@pytest.mark.timeout(1800)
+@pytest.mark.parametrize("cfg,graphs", [(5, 8), (3, 64)], ids=["cfg5-full", "cfg3-full"])
+def test_training_step_matches_oracle_at_full_config(cfg, graphs):
+    """The same oracle parity at the configs' full sizes (cfg5: 8 x 10,000 stations, 80,000
+    nodes, 3 layers; cfg3: 64 x 2,000 stations, 128,000 nodes), in the locality order the
+    benchmark runs: opt-in (GINE_FULL_PARITY=1), its tables committed under profiles/."""
+    c = BENCH_CONFIGS[cfg]
+    assert graphs == c.graphs_per_gpu
+    batch = synthetic_batch(c.num_stations, graphs, k=c.k, seed=100 + cfg)
+    worst = check_training_step(c.params(), batch, DEV, TOL, relabel=True,
+                                report=_report(f"cfg{cfg}_b{graphs}_locality"))
+    print(f"{c.name} x{graphs} full size: worst scaled grad err {worst:.2e}")
+
+
 @pytest.mark.parametrize("relabel", [False, True], ids=["dataset-order", "relabel"])
 def test_training_step_matches_oracle_at_cfg2_d64(relabel):
     """The D = 64 sweep point of the 24h_mixed benchmark (BASELINE.md:47, the north star's
