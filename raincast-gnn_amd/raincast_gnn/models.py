@@ -148,9 +148,10 @@ class GNN(nn.Module):
         kind = fused_head.loss_kind(self.postprocess.loss, self.postprocess.grad_u)
         y = getattr(data, "y", None)
         hplan = None
-        if (options.HEAD_FOLD and type(self.aggr) in (RowLinear, Linear)
+        if (options.HEAD_FOLD and self.training and type(self.aggr) in (RowLinear, Linear)
                 and fused_head.fusable(h, self.aggr, kind)):
-            # the head's forward folded into the last GINE layer's launch (gine_layer_head)
+            # the head's forward folded into the last GINE layer's launch (gine_layer_head;
+            # training mode: the one-launch layer runs on batch statistics only)
             hplan = fused_head.plan(h, self.aggr, kind, y)
         h = self.conv(h, data.edge_index, data.edge_attr, head=hplan)
         if type(self.aggr) in (RowLinear, Linear) and fused_head.fusable(h, self.aggr, kind):
