@@ -111,6 +111,17 @@ class FlatGradReducer:
             return False
         return dist.get_world_size(self.group) > 1 or self.force
 
+    def _mean(self, t: torch.Tensor, world: int) -> None:
+        """t <- the mean of t over the ranks.  RCCL: one ReduceOp.AVG collective (its
+        scaling by 1/world is exact for the power-of-two worlds the benchmark runs, so the
+        bits are those of the sum divided by world, without the division's extra kernel);
+        gloo (no AVG): the sum, then the division."""
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t.div_(world)
+
     def all_reduce_(self) -> None:
         if not self._collective():
             return
@@ -122,19 +133,16 @@ class FlatGradReducer:
                 # other ranks may have started their tail: keep the collective sequence every
                 # rank issues -- tail, then front -- independent of the rank
                 tail, head = self.flat[self._tail_lo:], self.flat[:self._tail_lo]
-                dist.all_reduce(tail, op=dist.ReduceOp.SUM, group=self.group)
-                dist.all_reduce(head, op=dist.ReduceOp.SUM, group=self.group)
-                self.flat.div_(world)
+                self._mean(tail, world)
+                self._mean(head, world)
                 return
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-            self.flat.div_(world)
+            self._mean(self.flat, world)
             return
         # the tail's collective is in flight (overlap_after): the rest of the buffer now,
         # then join the tail's stream (or wait for its work object on CPU tensors)
         self._tail_started = False
         head = self.flat[:self._tail_lo]
-        dist.all_reduce(head, op=dist.ReduceOp.SUM, group=self.group)
-        head.div_(world)
+        self._mean(head, world)
         if self._tail_work is not None:
             self._tail_work.wait()
             self._tail_work = None
@@ -194,8 +202,7 @@ class FlatGradReducer:
             cur = torch.cuda.current_stream(flat.device)
             self._side.wait_stream(cur)
             with torch.cuda.stream(self._side):
-                dist.all_reduce(tail, op=dist.ReduceOp.SUM, group=self.group)
-                tail.div_(world)
+                self._mean(tail, world)
             # (the backward keeps writing the front of the buffer on ``cur`` meanwhile; the
             # flat buffer outlives the step, so no allocator bookkeeping is needed)
         else:
