@@ -34,6 +34,28 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kRowTile = 32;
 
+#ifdef GINE_CHAIN_PROFILE
+// Debug build only (make variant V=chainprof VSRC=gine_chain.hip VDEFS=-DGINE_CHAIN_PROFILE,
+// tools/chain_prof.py): thread 0 of every workgroup of the two-stage chain kernels stamps
+// s_memtime: 0 entry, 1 weight fragments issued, then per tile k < 2 at 2 + 4k: A tile
+// staged (after the barrier), 3 + 4k: stage 1 done, 4 + 4k: stage-2 A tile complete (after
+// the barrier), 5 + 4k: stage 2 done; 10 end; 11 / 12: s_memrealtime at entry / end.
+__device__ long long g_chain_prof[1024][16];
+#define CHAIN_MARK(i)                                                          \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 1024)                                 \
+      g_chain_prof[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memtime();  \
+  } while (0)
+#define CHAIN_RT(i)                                                            \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 1024)                                 \
+      g_chain_prof[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define CHAIN_MARK(i) do {} while (0)
+#define CHAIN_RT(i) do {} while (0)
+#endif
+
 // F2F / B1F: the one-stage kernels of the folded chain (rho[2] folded into dim_red, see
 // gine_chain_fwd_folded): F2F h0 = [x | u] W'^T + b', B1F dt = (dh0 Wc) * 1[u > 0].
 // B3: the folded chain's whole input-gradient backward in one launch (B1F's stage, then B2's
@@ -195,6 +217,8 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   const int h = lane >> 5, c32 = lane & 31;
   const int col = wave * 32 + c32;
   const int q_me = threadIdx.x % D4, r_me = threadIdx.x / D4;
+  CHAIN_RT(11);
+  CHAIN_MARK(0);
   int nb = gridDim.x;  // chain workgroups
   if constexpr (KIND == CH_F1) {
     if (a.wfold != nullptr) {
@@ -243,6 +267,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   if constexpr (KIND == CH_F1 || KIND == CH_F2 || kLast) bias1 = a.b1[col] * a.bias1_scale;
   if constexpr (KIND == CH_F1 || kDimRed || kF3) bias2 = a.b2[col];
   if constexpr (kLast) bias3 = a.b3[col];
+  CHAIN_MARK(1);
 
   auto load_tile = [&](int tile, float4 (&raw)[ITEMS], float (&xr)[XITEMS]) {
     const int64_t n0 = (int64_t)tile * kRowTile;
@@ -270,7 +295,8 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   float4 raw[ITEMS];
   float xr[XITEMS];
   if (tr.first < tr.end) load_tile(tr.first, raw, xr);
-  for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+  int kt = 0;  // (profile stamps) tile index of this workgroup
+  for (int tile = tr.first; tile < tr.end; tile += tr.step, ++kt) {
     const int64_t n0 = (int64_t)tile * kRowTile;
     __syncthreads();  // previous tile's reads of sA / sB are done
 #pragma unroll
@@ -290,6 +316,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
       }
     }
     __syncthreads();
+    if (kt < 2) CHAIN_MARK(2 + 4 * kt);
     if (tile + tr.step < tr.end) load_tile(tile + tr.step, raw, xr);  // next tile in flight
     float ep[16];
     if constexpr (KIND == CH_B1 || KIND == CH_B1F || kMaskIn) {  // ReLU mask, in flight
@@ -328,7 +355,9 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
         }
         if (n < N) a.out1[n * D + col] = v;
       }
+      if (kt < 2) CHAIN_MARK(3 + 4 * kt);
       __syncthreads();
+      if (kt < 2) CHAIN_MARK(4 + 4 * kt);
     }
 
     // stage 2
@@ -354,6 +383,7 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
         const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (n < N) a.out3[n * D + col] = acc[r] + bias3;
       }
+      if (kt < 2) CHAIN_MARK(5 + 4 * kt);
     }
     if constexpr (KIND == CH_B3) {  // stage 3: dr = ds Wp2 (sA: every wave is past stage 1)
       __syncthreads();
@@ -364,7 +394,11 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
         if (n < N) a.out3[n * D + col] = acc[r];
       }
     }
+    if constexpr (!kLast)
+      if (kt < 2) CHAIN_MARK(5 + 4 * kt);
   }
+  CHAIN_MARK(10);
+  CHAIN_RT(12);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -387,12 +421,26 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
 // SLOWER in the step -- forward 23.4 vs 20.4 us, backward 16.2 vs 16.4, step 0.4482 vs
 // 0.4432 ms interleaved: the fp32 chain is not MFMA-bound at one workgroup per CU (its
 // 2 x 9,472 MFMA cycles are ~8 of the 20 us), and the split form's 228 weight-plane
-// registers spill into AGPR copies and just-in-time fragment reads.  Off (GINE_CHAIN_X3=1
-// builds it into the dispatch).
+// registers spill into AGPR copies and just-in-time fragment reads.  With the weights split
+// in the loop instead (fp32 fragments, as k_chain; the split hidden from loop-invariant code
+// motion) and two accumulators per stage: forward 22.0-25.5 vs 20.8 us standalone
+// (profiles/r06_s28-s30, tools/chain_prof.py stamps: the stages take as long as the fp32
+// ones -- the chain is bound by more than its MFMA issue).  Off (GINE_CHAIN_X3=1 builds it
+// into the dispatch).
 // ---------------------------------------------------------------------------------------
 #ifndef GINE_CHAIN_X3
 #define GINE_CHAIN_X3 0
 #endif
+
+// The split planes of eight fp32 weights, computed where they are used: the (empty) asm
+// hides the values' loop invariance, so the split is not hoisted out of the tile loop into
+// 228 live plane registers.
+__device__ __forceinline__ Bf16x3 split_w8(const float* w) {
+  float w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5], w6 = w[6], w7 = w[7];
+  asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3), "+v"(w4), "+v"(w5), "+v"(w6),
+               "+v"(w7));
+  return split8(make_float4(w0, w1, w2, w3), make_float4(w4, w5, w6, w7));
+}
 
 template <int D, int FP, bool FWD>
 __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int num_tiles) {
@@ -415,26 +463,8 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
   const int col = wave * 32 + c32;
   const int q_me = threadIdx.x % D4, r_me = threadIdx.x / D4;
   const int F = a.F;
-
-  // both weights as split register planes, once per workgroup (lane half h: k = h*KS + s)
-  BPlanes<KS1> b1;
-  BPlanes<KS2> b2;
-  {
-    float f[KS1];
-    if constexpr (FWD) frag_t<D>(f, a.w1, D, col, h);         // Wf
-    else frag_n<D>(f, a.w1, F + D, F, col, h);               // W' e-columns (Wc)
-    b1.from(f);
-  }
-  {
-    float f[KS2];
-    if constexpr (FWD) frag_dimred_t<FPX, D>(f, a.w3, F, col, h);  // W'^T, x columns padded
-    else frag_n<D>(f, a.w2, D, 0, col, h);                        // Wf
-    b2.from(f);
-  }
-  const float bias1 = FWD ? a.b1[col] * a.bias1_scale : 0.f;
-  const float bias2 = FWD ? a.b3[col] : 0.f;
-  float* out1 = a.out1;
-  float* out2 = FWD ? a.out3 : a.out2;
+  CHAIN_RT(11);
+  CHAIN_MARK(0);
 
   const TileRange tr = tile_range(num_tiles, gridDim.x);
   float4 raw[ITEMS];
@@ -459,8 +489,26 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
       }
     }
   };
+  // the first tile's rows first (its staging waits for them only), then both weights' fp32
+  // fragments (lane half h: k = h*KS + s), split per K = 16 block inside the chains: held
+  // as split planes (228 registers at D = 128) they spilled into AGPR copies
   if (tr.first < tr.end) load_tile(tr.first);
-  for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+  float bf1[KS1], bf2[KS2];
+  if constexpr (FWD) {
+    frag_t4<D>(bf1, a.w1, D, col, h);              // Wf
+    frag_dimred_t<FPX, D>(bf2, a.w3, F, col, h);   // W'^T, x columns padded to FPX
+  } else {
+    frag_n<D>(bf1, a.w1, F + D, F, col, h);        // W' e-columns (Wc)
+    frag_n<D>(bf2, a.w2, D, 0, col, h);            // Wf
+  }
+  const float bias1 = FWD ? a.b1[col] * a.bias1_scale : 0.f;
+  const float bias2 = FWD ? a.b3[col] : 0.f;
+  float* out1 = a.out1;
+  float* out2 = FWD ? a.out3 : a.out2;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) before the loop (see k_chain)
+  CHAIN_MARK(1);
+  int kt = 0;
+  for (int tile = tr.first; tile < tr.end; tile += tr.step, ++kt) {
     const int64_t n0 = (int64_t)tile * kRowTile;
     __syncthreads();  // the previous tile's fragment reads are done
 #pragma unroll
@@ -494,6 +542,7 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
       }
     }
     __syncthreads();
+    if (kt < 2) CHAIN_MARK(2 + 4 * kt);
     if (tile + tr.step < tr.end) load_tile(tile + tr.step);  // next tile in flight
     float ep[FWD ? 1 : 16];
     if constexpr (!FWD) {  // the ReLU mask of u, in flight under stage 1
@@ -505,9 +554,10 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
       }
     }
 
-    // stage 1
+    // stage 1 (two accumulators over alternate K = 16 blocks: independent MFMA chains)
     floatx16 acc = zero16();
     {
+      floatx16 acc2 = zero16();
       const uint16_t* pr = pa + c32 * RS1 + h * KS1;
 #pragma unroll
       for (int s8 = 0; s8 < KS1 / 8; ++s8) {
@@ -515,8 +565,11 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
         f.h = *reinterpret_cast<const bf16x8_t*>(pr + 8 * s8);
         f.m = *reinterpret_cast<const bf16x8_t*>(pr + P1 + 8 * s8);
         f.l = *reinterpret_cast<const bf16x8_t*>(pr + 2 * P1 + 8 * s8);
-        acc = mfma_bf16x3(f, b1.f[s8], acc);
+        const Bf16x3 b = split_w8(bf1 + 8 * s8);
+        if (s8 & 1) acc2 = mfma_bf16x3(f, b, acc2);
+        else acc = mfma_bf16x3(f, b, acc);
       }
+      acc = acc + acc2;
       if (wave_any_nan(acc)) {  // fp32 chain from memory (the fp32 GEMM's non-finite values)
         const int64_t n = min(n0 + c32, N - 1);
         acc = zero16();
@@ -544,11 +597,14 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
       d[P2] = (uint16_t)mm;
       d[2 * P2] = (uint16_t)ll;
     }
+    if (kt < 2) CHAIN_MARK(3 + 4 * kt);
     __syncthreads();  // stage 2's A planes complete (and stage 1's outputs written)
+    if (kt < 2) CHAIN_MARK(4 + 4 * kt);
 
-    // stage 2
+    // stage 2 (two accumulators, as stage 1)
     acc = zero16();
     {
+      floatx16 acc2 = zero16();
       const uint16_t* pr = pb + c32 * RS2 + h * KS2;
 #pragma unroll
       for (int s8 = 0; s8 < KS2 / 8; ++s8) {
@@ -556,8 +612,11 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
         f.h = *reinterpret_cast<const bf16x8_t*>(pr + 8 * s8);
         f.m = *reinterpret_cast<const bf16x8_t*>(pr + P2 + 8 * s8);
         f.l = *reinterpret_cast<const bf16x8_t*>(pr + 2 * P2 + 8 * s8);
-        acc = mfma_bf16x3(f, b2.f[s8], acc);
+        const Bf16x3 b = split_w8(bf2 + 8 * s8);
+        if (s8 & 1) acc2 = mfma_bf16x3(f, b, acc2);
+        else acc = mfma_bf16x3(f, b, acc);
       }
+      acc = acc + acc2;
       if (wave_any_nan(acc)) {
         const int64_t n = min(n0 + c32, N - 1);
         acc = zero16();
@@ -586,7 +645,10 @@ __global__ __launch_bounds__(2 * D) void k_chain2_x3(ChainArgs a, int64_t N, int
       const int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (n < N) out2[n * D + col] = acc[r] + bias2;
     }
+    if (kt < 2) CHAIN_MARK(5 + 4 * kt);
   }
+  CHAIN_MARK(10);
+  CHAIN_RT(12);
 }
 
 template <int D, int FP, bool FWD>
@@ -1221,3 +1283,11 @@ extern "C" int gine_chain_unfold_grads2(const float* gfold, const float* wr1, co
                        UnfoldJob{gfold, wr1, br1, wdr, dwdr, dbdr, dwr1, dbr1, in_features, 1.f},
                        &j1, as_stream(stream));
 }
+
+#ifdef GINE_CHAIN_PROFILE
+extern "C" int gine_debug_chain_prof(long long* out) {  // [1024][16] host buffer
+  GINE_RETURN_IF_HIP(hipDeviceSynchronize());
+  GINE_RETURN_IF_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_prof), sizeof(g_chain_prof)));
+  return GINE_OK;
+}
+#endif
