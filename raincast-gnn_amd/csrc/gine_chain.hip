@@ -33,6 +33,9 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kRowTile = 32;
+#ifndef GINE_CHAIN_EP_EARLY
+#define GINE_CHAIN_EP_EARLY 1
+#endif
 
 #ifdef GINE_CHAIN_PROFILE
 // Debug build only (make variant V=chainprof VSRC=gine_chain.hip VDEFS=-DGINE_CHAIN_PROFILE,
@@ -298,6 +301,18 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
   int kt = 0;  // (profile stamps) tile index of this workgroup
   for (int tile = tr.first; tile < tr.end; tile += tr.step, ++kt) {
     const int64_t n0 = (int64_t)tile * kRowTile;
+    float ep[16];
+    if constexpr ((KIND == CH_B1 || KIND == CH_B1F || kMaskIn) && GINE_CHAIN_EP_EARLY) {
+      // the ReLU mask, in flight under the staging and stage 1 -- issued before the next
+      // tile's rows, so the epilogue's wait for it (vector-memory counts retire in order)
+      // does not also wait for that prefetch
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        n = n < N ? n : N - 1;
+        ep[r] = a.aux[n * D + col];
+      }
+    }
     __syncthreads();  // previous tile's reads of sA / sB are done
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
@@ -318,10 +333,9 @@ __global__ __launch_bounds__(2 * D) void k_chain(ChainArgs a, int64_t N, int num
     __syncthreads();
     if (kt < 2) CHAIN_MARK(2 + 4 * kt);
     if (tile + tr.step < tr.end) load_tile(tile + tr.step, raw, xr);  // next tile in flight
-    float ep[16];
-    if constexpr (KIND == CH_B1 || KIND == CH_B1F || kMaskIn) {  // ReLU mask, in flight
+    if constexpr ((KIND == CH_B1 || KIND == CH_B1F || kMaskIn) && !GINE_CHAIN_EP_EARLY) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+      for (int r = 0; r < 16; ++r) {  // (A/B builds: the mask behind the prefetch)
         int64_t n = n0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         n = n < N ? n : N - 1;
         ep[r] = a.aux[n * D + col];
